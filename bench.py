@@ -1,0 +1,256 @@
+"""Benchmark: env-steps/s of the HIP boat env (BASELINE.json metric).
+
+Workload (BASELINE.json configs[2] at N=1, configs[3] at N>1): boat_env
+experiment 6 (random wind in all directions), 65 536 envs per GPU,
+test_mode 0 (actions drive the rudder), actions U(-1,1) f32 pre-generated as
+a [500, N] table in HBM, episodes truncated at 500 steps and auto-reset in
+the step kernel (early terminations too). One "step" = one BoatEnv.step
+over all envs of the rank (+ at N>1 the packed (obs, reward, done, term)
+all-gather over RCCL that pools transitions for a shared replay buffer).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+Timing: W untimed steps, then exactly K steps bracketed by barrier +
+synchronize; value = all envs x K / max-over-ranks time. At N=1 the steps
+are replayed from hipGraphs of 100 step launches (launch-bound otherwise).
+Roofline: SURVEY.md §8(d) algorithmic 222 B per boat env-step over the
+k_step launch duration (HIP events around launches on the env's stream).
+cpu_baseline: the numpy float64 oracle (oracle/boat_oracle.py, a port of the
+reference step) on the same workload shape, one core, bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "sac-agent_amd"))
+
+METRIC = "env-steps/sec (whole node), boat_env exp-6, 65 536 envs/GPU at 1/2/4/8 MI355X"
+BYTES_PER_ENV_STEP = 222      # state r+w 152, action 4, wind 16, obs 44, reward 4, done+term 2
+HBM_PEAK = 8.0e12             # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+EPISODE_STEPS = 500
+GRAPH_STEPS = 100
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=500)
+    ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--experiment", type=int, default=6)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--kernel-launches", type=int, default=200)
+    return ap.parse_args()
+
+
+def init_dist(n_gpus: int):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != n_gpus:
+        raise SystemExit(f"--gpus {n_gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return rank, world, torch.device("cuda", local)
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def cpu_baseline(n_envs: int, seconds: float, experiment: int) -> dict:
+    """The oracle (numpy port of BoatEnv.step) on the bench workload, 1 thread."""
+    try:
+        from threadpoolctl import threadpool_limits
+    except Exception:  # noqa: BLE001
+        threadpool_limits = None
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from boat_oracle import OracleConfig, OracleVecBoat
+
+    import contextlib
+    ctx = threadpool_limits(limits=1) if threadpool_limits else contextlib.nullcontext()
+    with ctx:
+        seeds = np.arange(n_envs, dtype=np.uint64)
+        # the constructor builds every env's first Boat (boat_env.py:15), untimed
+        ora = OracleVecBoat(OracleConfig(experiment=experiment, test_mode=0), seeds,
+                            max_episode_steps=EPISODE_STEPS)
+        acts = np.random.default_rng(0).uniform(-1, 1, (64, n_envs)).astype(np.float32)
+        ora.step(acts[0])  # warm
+        steps, t0 = 0, time.perf_counter()
+        while True:
+            ora.step(acts[steps % 64])
+            steps += 1
+            el = time.perf_counter() - t0
+            if el >= seconds and steps >= 3:
+                break
+    return {"value": n_envs * steps / el, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/boat_oracle.py numpy f64, exp {experiment}, {n_envs} envs x "
+                      f"{steps} steps ({el:.1f} s), auto-reset + 500-step truncation, 1 thread",
+            "note": "reference BoatEnv itself (pure Python, 1 env, 1 core) measured 12 584 "
+                    "env-steps/s for exp 6 in the survey container (BASELINE.md)"}
+
+
+def load_traffic(n_envs: int):
+    """Per-launch HBM bytes of k_step from the committed rocprofv3 PMC summary, if any."""
+    path = os.path.join(ROOT, "profiles", "pmc_k_step.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+        if int(d.get("envs", -1)) == n_envs:
+            return float(d["hbm_bytes_per_launch"])
+    except Exception:  # noqa: BLE001
+        return None
+    return None
+
+
+def main():
+    args = parse()
+    rank, world, dev = init_dist(args.gpus)
+    from sacenv import VecBoatEnv
+
+    N = args.envs
+    env = VecBoatEnv({"base_settings": {"experiment": args.experiment, "test_mode": 0}}, N,
+                     seed=0, device=dev, autoreset=True, max_episode_steps=EPISODE_STEPS,
+                     env_id_offset=rank * N)
+    env.reset()
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+    actions = (torch.rand((EPISODE_STEPS, N), generator=g, device=dev, dtype=torch.float32) * 2 - 1)
+    gathered = None
+    if world > 1:
+        import torch.distributed as dist
+        gathered = torch.empty(world * env.record.numel(), dtype=torch.uint8, device=dev)
+
+    def step_eager(k: int):
+        env.step_async(actions[k % EPISODE_STEPS])
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, env.record)
+
+    use_graph = world == 1 and not args.no_graph
+    graphs = []
+    if use_graph:
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            for k in range(3):
+                step_eager(k)
+        torch.cuda.current_stream(dev).wait_stream(s)
+        torch.cuda.synchronize(dev)
+        for base in range(0, EPISODE_STEPS, GRAPH_STEPS):
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr):
+                for k in range(base, base + GRAPH_STEPS):
+                    env.step_async(actions[k])
+            graphs.append(gr)
+
+    def run(n_steps: int, k0: int) -> int:
+        k = k0
+        done = 0
+        while done < n_steps:
+            if use_graph and k % GRAPH_STEPS == 0 and n_steps - done >= GRAPH_STEPS:
+                graphs[(k % EPISODE_STEPS) // GRAPH_STEPS].replay()
+                k += GRAPH_STEPS
+                done += GRAPH_STEPS
+            else:
+                step_eager(k)
+                k += 1
+                done += 1
+        return k
+
+    k = run(args.warmup, 0)
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    k = run(args.steps, k)
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el_max = float(t.item())
+
+    # k_step launch duration: HIP events around individual launches on env's stream
+    st = torch.cuda.current_stream(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.kernel_launches)]
+    torch.cuda.synchronize(dev)
+    for i, (a, b) in enumerate(evs):
+        a.record(st)
+        env.step_async(actions[(k + i) % EPISODE_STEPS])
+        b.record(st)
+    torch.cuda.synchronize(dev)
+    durs = np.array([a.elapsed_time(b) for a, b in evs]) * 1e-3  # s
+    kern_s = float(np.median(durs))
+    kern_mean = float(durs.mean())
+    # graph-paced per-step time (kernels back to back, no host in the loop)
+    graph_step_s = None
+    if use_graph:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for gr in graphs:
+            gr.replay()
+        e1.record(st)
+        torch.cuda.synchronize(dev)
+        graph_step_s = e0.elapsed_time(e1) * 1e-3 / (len(graphs) * GRAPH_STEPS)
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    bytes_launch = BYTES_PER_ENV_STEP * N
+    achieved = bytes_launch / kern_s
+    traffic = load_traffic(N)
+    out = {
+        "metric": METRIC,
+        "value": world * N * args.steps / el_max,
+        "unit": "env-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": el_max / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: U(-1,1) f32 actions, per-env MT19937 wind/start draws (seeds 0..N-1)",
+        "config": {"workload": f"boat_env exp {args.experiment}, {N} envs/GPU, "
+                               f"{EPISODE_STEPS}-step episodes, in-kernel auto-reset",
+                   "experiment": args.experiment, "envs_per_gpu": N, "global_envs": world * N,
+                   "episode_steps": EPISODE_STEPS, "parallelism": f"env-dp{world}",
+                   "collective": "all_gather (obs,reward,done,term) 50 B/env/step" if world > 1 else None,
+                   "launch": "hipGraph x100 steps" if use_graph else "eager"},
+        "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK,
+                     "traffic": traffic,
+                     "kernel": "k_step", "bytes_per_launch": bytes_launch,
+                     "kernel_us_median": kern_s * 1e6, "kernel_us_mean": kern_mean * 1e6,
+                     "graph_step_us": None if graph_step_s is None else graph_step_s * 1e6},
+        "cpu_baseline": None,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(N, args.cpu_seconds, args.experiment)
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

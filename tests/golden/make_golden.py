@@ -1,0 +1,222 @@
+"""Generate the golden fixtures under tests/golden/ from the reference itself.
+
+Runs ONLY in the build container (needs /root/reference); the outputs are
+plain ``.npz`` data committed next to this script. Nothing here is imported
+by the product package, by smoke() or by bench.py.
+
+Fixture kinds
+-------------
+``seeded_<name>.npz``
+    The reference ``BoatEnv`` (``environment/boat_env.py:9-140``) driven the
+    way ``main.py:70-91`` drives it: ``np.random.seed(seed)`` -> ``BoatEnv(cfg)``
+    (constructor draws one ``Boat``, ``boat_env.py:15``) -> ``reset()`` -> ``step``
+    with float32-valued actions, ``reset()`` again whenever ``done``.
+    One independent reference env (one global-RNG seed) per fixture env.
+``wind_exp<k>.npz``
+    ``Wind`` tables (``wind.py:26-99``) for many seeds, sampled at fixed
+    indices, plus each table's min/max (pins the spline and the min-max
+    renormalisation, ``wind.py:87-89``).
+``recorded_exp<k>.npz``
+    The reference's own recorded runs under
+    ``ressources/settings_visualized/experiment_setting_<k>/`` converted from
+    CSV (data files the reference ships).
+
+Usage: ``python tests/golden/make_golden.py`` (writes into tests/golden/).
+"""
+from __future__ import annotations
+
+import csv
+import os
+import tempfile
+import types
+
+import numpy as np
+
+import _refharness as H
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+# term codes: order of the info-dict keys, boat_env.py:24-32
+TERM_CODES = {"": 0, "reached_goal": 1, "out_of_bounds": 2, "out_of_fuel": 3,
+              "rudder_broken": 4, "timeout": 5}
+
+STATE_FIELDS = ("s_x", "s_y", "s_r", "v_x", "v_y", "v_r", "a_x", "a_y", "a_r",
+                "rudder_angle", "t", "fuel", "index")
+
+SEEDS = np.array([0, 1, 7, 12345, 2**31 + 11, 2**32 - 1], dtype=np.uint64)
+
+
+def _state(boat) -> list[float]:
+    return [float(getattr(boat, f)) for f in STATE_FIELDS]
+
+
+def run_seeded(name, overrides, n_steps, action_kind, seeds=SEEDS, action_seed=0):
+    be = H.boat_env_module()
+    cfg = H.load_config(overrides)
+    E, S = len(seeds), n_steps
+    rng = np.random.default_rng(action_seed)
+    if action_kind == "uniform":
+        actions = rng.uniform(-1.0, 1.0, size=(E, S)).astype(np.float32)
+    elif action_kind == "zero":
+        actions = np.zeros((E, S), np.float32)
+    elif action_kind == "big":
+        actions = rng.choice(np.array([-5.0, 5.0, 0.3], np.float32), size=(E, S))
+    else:
+        raise ValueError(action_kind)
+
+    out = {k: [] for k in ("obs", "reward", "done", "term", "state", "ep_reward",
+                           "wind", "reset_obs", "reset_state", "start_y",
+                           "init_obs", "init_state", "init_start_y", "counters")}
+    for e, seed in enumerate(seeds):
+        np.random.seed(int(seed))
+        env = be.BoatEnv(cfg, types.SimpleNamespace(experiment_dir=tempfile.mkdtemp()))
+        # main.py:72 - reset before the first step
+        obs0 = env.reset()
+        out["init_obs"].append(np.asarray(obs0, np.float64))
+        out["init_state"].append(_state(env.boat))
+        out["init_start_y"].append(int(env.boat.s_y_start))
+        rows = {k: [] for k in ("obs", "reward", "done", "term", "state", "ep_reward",
+                                "wind", "reset_obs", "reset_state", "start_y")}
+        for k in range(S):
+            idx = env.boat.index
+            wv, wa = env.boat.wind.get_wind(idx)
+            a = np.array([float(actions[e, k])], dtype=np.float64)
+            o, r, d, info = env.step(a)
+            rows["wind"].append([float(wv), float(wa)])
+            rows["obs"].append(np.asarray(o, np.float64))
+            rows["reward"].append(float(r))
+            rows["done"].append(bool(d))
+            rows["term"].append(TERM_CODES[info["termination"]] if d else 0)
+            rows["state"].append(_state(env.boat))
+            rows["ep_reward"].append(float(info["episode_reward"]))
+            if d:
+                ro = env.reset()
+                rows["reset_obs"].append(np.asarray(ro, np.float64))
+                rows["reset_state"].append(_state(env.boat))
+                rows["start_y"].append(int(env.boat.s_y_start))
+            else:
+                rows["reset_obs"].append(np.full(11, np.nan))
+                rows["reset_state"].append([np.nan] * len(STATE_FIELDS))
+                rows["start_y"].append(0)
+        for kk, v in rows.items():
+            out[kk].append(v)
+        out["counters"].append([env.info[k] for k in
+                                ("reached_goal", "out_of_bounds", "out_of_fuel",
+                                 "rudder_broken", "timeout")])
+
+    flat = {k: np.asarray(v) for k, v in out.items()}
+    flat["obs"] = flat["obs"].astype(np.float64)
+    flat["done"] = flat["done"].astype(np.uint8)
+    flat["term"] = flat["term"].astype(np.uint8)
+    flat["start_y"] = flat["start_y"].astype(np.int32)
+    flat["seeds"] = np.asarray(seeds, np.uint64)
+    flat["actions"] = actions
+    flat["state_fields"] = np.array(STATE_FIELDS)
+    cfg_vals = _cfg_vector(cfg)
+    flat.update(cfg_vals)
+    path = os.path.join(HERE, f"seeded_{name}.npz")
+    np.savez_compressed(path, **flat)
+    n_done = int(flat["done"].sum())
+    print(f"{path}: E={E} S={S} episodes_ended={n_done} "
+          f"terms={np.bincount(flat['term'].ravel(), minlength=6).tolist()}")
+
+
+def _cfg_vector(cfg):
+    """Config values the fixture was produced with (flat, for the tests)."""
+    return {
+        "cfg_experiment": np.int32(int(cfg.base_settings.experiment)),
+        "cfg_test_mode": np.int32(int(cfg.base_settings.test_mode)),
+        "cfg_dt": np.float64(cfg.base_settings.dt),
+        "cfg_t_max": np.float64(cfg.base_settings.t_max),
+        "cfg_fuel": np.int64(cfg.boat.fuel),
+        "cfg_track_width": np.float64(cfg.boat_env.track_width),
+        "cfg_goal_line": np.float64(cfg.boat_env.goal_line),
+        "cfg_oob_offset": np.float64(cfg.boat_env.boat_out_of_bounds_offset),
+    }
+
+
+WIND_IDX = np.unique(np.concatenate([np.arange(0, 10000, 97), [9998, 9999]]))
+
+
+def run_wind(exp, n_seeds=64, t_max=None):
+    be = H.boat_env_module()
+    over = {"base_settings": {"experiment": exp}}
+    if t_max is not None:
+        over["base_settings"]["t_max"] = t_max
+    cfg = H.load_config(over)
+    L = int(cfg.base_settings.t_max / cfg.base_settings.dt)
+    idx = WIND_IDX[WIND_IDX < L] if t_max is None else np.arange(L)
+    vel, ang, vmin, vmax, amin, amax, sy = [], [], [], [], [], [], []
+    seeds = np.arange(1000, 1000 + n_seeds, dtype=np.uint64)
+    for s in seeds:
+        np.random.seed(int(s))
+        boat = be.Boat(cfg)       # randint then Wind draws (boat_env.py:147-156)
+        wv = np.asarray(boat.wind.wind_velocity, np.float64)
+        wa = np.asarray(boat.wind.wind_angle, np.float64)
+        vel.append(wv[idx]); ang.append(wa[idx])
+        vmin.append(wv.min()); vmax.append(wv.max()); amin.append(wa.min()); amax.append(wa.max())
+        sy.append(int(boat.s_y_start))
+    suffix = "" if t_max is None else f"_tmax{t_max:g}"
+    path = os.path.join(HERE, f"wind_exp{exp}{suffix}.npz")
+    np.savez_compressed(path, seeds=seeds, idx=idx.astype(np.int32), L=np.int32(L),
+                        vel=np.asarray(vel), ang=np.asarray(ang),
+                        vmin=np.asarray(vmin), vmax=np.asarray(vmax),
+                        amin=np.asarray(amin), amax=np.asarray(amax),
+                        start_y=np.asarray(sy, np.int32),
+                        experiment=np.int32(exp),
+                        max_velocity=np.float64(cfg.wind.max_velocity),
+                        direction=np.float64(cfg.wind.direction))
+    print(f"{path}: seeds={n_seeds} L={L}")
+
+
+def convert_recorded(exp):
+    d = os.path.join(H.REF_ROOT, "ressources", "settings_visualized",
+                     f"experiment_setting_{exp}")
+
+    def read(p):
+        with open(p) as f:
+            rows = list(csv.reader(f, delimiter=";"))
+        return rows[0], rows[1:]
+
+    hdr, rows = read(os.path.join(d, "episodes", "episode_0_data.csv"))
+    data = np.array([[float(x) for x in r] for r in rows], np.float64)
+    whdr, wrows = read(os.path.join(d, "episodes", "wind.csv"))
+    wind = np.array([[float(x) for x in r] for r in wrows], np.float64)
+    thdr, trows = read(os.path.join(d, "terminations.csv"))
+    term = dict(zip(thdr, trows[0]))
+    path = os.path.join(HERE, f"recorded_exp{exp}.npz")
+    np.savez_compressed(path, columns=np.array(hdr), trace=data,
+                        wind_velocity=wind[:, 0], wind_angle=wind[:, 1],
+                        termination=np.array(term["termination"]),
+                        episode_reward=np.float64(term["episode_reward"]),
+                        experiment=np.int32(exp))
+    print(f"{path}: rows={len(data)} term={term['termination']}")
+
+
+def main():
+    for exp in range(1, 7):
+        run_seeded(f"exp{exp}_uniform", {"base_settings": {"experiment": exp, "test_mode": 0}},
+                   400, "uniform", action_seed=100 + exp)
+    run_seeded("exp6_narrow", {"base_settings": {"experiment": 6, "test_mode": 0},
+                               "boat_env": {"track_width": 20}}, 700, "uniform", action_seed=7)
+    run_seeded("exp2_narrow", {"base_settings": {"experiment": 2, "test_mode": 0},
+                               "boat_env": {"track_width": 20}}, 500, "uniform", action_seed=8)
+    run_seeded("exp6_fuel", {"base_settings": {"experiment": 6, "test_mode": 1},
+                             "boat": {"fuel": 30}}, 100, "zero")
+    run_seeded("exp6_timeout", {"base_settings": {"experiment": 6, "test_mode": 1, "t_max": 5}},
+               60, "zero")
+    run_seeded("exp5_timeout", {"base_settings": {"experiment": 5, "test_mode": 0, "t_max": 5}},
+               60, "uniform", action_seed=9)
+    run_seeded("exp6_goal", {"base_settings": {"experiment": 6, "test_mode": 1},
+                             "boat_env": {"goal_line": 100}}, 400, "zero")
+    run_seeded("exp3_big", {"base_settings": {"experiment": 3, "test_mode": 0}},
+               60, "big", action_seed=10)
+    for exp in (4, 5, 6):
+        run_wind(exp)
+    run_wind(6, n_seeds=32, t_max=5)
+    for exp in range(1, 7):
+        convert_recorded(exp)
+
+
+if __name__ == "__main__":
+    main()

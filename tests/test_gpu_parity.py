@@ -1,0 +1,248 @@
+"""GPU parity: the HIP engine vs the reference's fixtures and the CPU oracle.
+
+Bar (BASELINE.json north_star): done/termination codes bit-exact, float64
+state within STATE_TOL = 1e-5 of the CPU reference for identical seeds.
+Observations are float32 outputs: compared within f32 rounding of the
+reference's float64 values (OBS_TOL). RNG draws (start y, knot values) are
+compared bit-exactly.
+"""
+import numpy as np
+import pytest
+import torch
+
+from boat_oracle import OracleConfig, OracleVecBoat, config_from_fixture
+from conftest import golden, seeded_fixtures
+
+pytestmark = pytest.mark.gpu
+
+STATE_TOL = 1e-5
+OBS_TOL = 1e-6
+STATE_KEYS = ("s_x", "s_y", "s_r", "v_x", "v_y", "v_r", "a_x", "a_y", "a_r",
+              "rudder_angle", "t", "fuel", "index")
+
+
+def _cfg_dict(z):
+    c = config_from_fixture(z)
+    return {"base_settings": {"experiment": c.experiment, "test_mode": c.test_mode,
+                              "dt": c.dt, "t_max": c.t_max},
+            "boat_env": {"track_width": c.track_width, "goal_line": c.goal_line,
+                         "boat_out_of_bounds_offset": c.oob_offset},
+            "boat": {"fuel": c.fuel}}
+
+
+def _state_matrix(env):
+    d = env.state_dict()
+    d["rudder_angle"] = d["rudder"]
+    return np.stack([np.asarray(d[k], np.float64) for k in STATE_KEYS], 1)
+
+
+@pytest.mark.parametrize("name", seeded_fixtures())
+def test_seeded_fixture_explicit_reset(name, gpu, built_lib):
+    """Step the reference's seeded runs; reset ended envs via reset(ids)."""
+    from sacenv import VecBoatEnv
+    z = golden(name)
+    E, S = z["reward"].shape
+    env = VecBoatEnv(_cfg_dict(z), E, seeds=z["seeds"], device=gpu, autoreset=False,
+                     record_knots=True)
+    obs = env.reset().cpu().numpy()
+    np.testing.assert_allclose(obs, z["init_obs"], rtol=0, atol=OBS_TOL)
+    np.testing.assert_array_equal(env.start_y.cpu().numpy(), z["init_start_y"])
+    worst = 0.0
+    for k in range(S):
+        a = torch.from_numpy(np.ascontiguousarray(z["actions"][:, k])).to(gpu)
+        o, r, d, info = env.step(a)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(info["term"].cpu().numpy(), z["term"][:, k], err_msg=f"{k}")
+        np.testing.assert_array_equal(d.cpu().numpy(), z["done"][:, k], err_msg=f"{k}")
+        st = _state_matrix(env)
+        err = np.abs(st - z["state"][:, k]).max()
+        worst = max(worst, err)
+        assert err <= STATE_TOL, f"state off by {err} at step {k}"
+        np.testing.assert_allclose(o.cpu().numpy(), z["obs"][:, k], rtol=OBS_TOL, atol=OBS_TOL)
+        np.testing.assert_allclose(env.reward64.cpu().numpy(), z["reward"][:, k], rtol=0,
+                                   atol=STATE_TOL)
+        ended = np.flatnonzero(z["done"][:, k])
+        if ended.size:
+            np.testing.assert_allclose(info["final_ep_reward"].cpu().numpy()[ended],
+                                       z["ep_reward"][ended, k], rtol=0, atol=1e-4)
+            ro = env.reset(ended).cpu().numpy()
+            torch.cuda.synchronize()
+            np.testing.assert_allclose(ro[ended], z["reset_obs"][ended, k], rtol=0, atol=OBS_TOL)
+            np.testing.assert_array_equal(env.start_y.cpu().numpy()[ended], z["start_y"][ended, k])
+    np.testing.assert_array_equal(env.counters.cpu().numpy().T, z["counters"])
+    print(f"{name}: worst state err {worst:.3e}")
+
+
+@pytest.mark.parametrize("name", ["seeded_exp6_uniform.npz", "seeded_exp3_big.npz",
+                                  "seeded_exp6_fuel.npz", "seeded_exp6_narrow.npz"])
+def test_seeded_fixture_autoreset(name, gpu, built_lib):
+    """In-kernel auto-reset: obs row = new episode's obs, final_obs = terminal obs."""
+    from sacenv import VecBoatEnv
+    z = golden(name)
+    E, S = z["reward"].shape
+    env = VecBoatEnv(_cfg_dict(z), E, seeds=z["seeds"], device=gpu, autoreset=True)
+    env.reset()
+    for k in range(S):
+        a = torch.from_numpy(np.ascontiguousarray(z["actions"][:, k])).to(gpu)
+        o, r, d, info = env.step(a)
+        torch.cuda.synchronize()
+        done = z["done"][:, k].astype(bool)
+        np.testing.assert_array_equal(info["term"].cpu().numpy(), z["term"][:, k])
+        o = o.cpu().numpy()
+        np.testing.assert_allclose(o[~done], z["obs"][~done, k], rtol=OBS_TOL, atol=OBS_TOL)
+        if done.any():
+            fo = info["final_obs"].cpu().numpy()
+            np.testing.assert_allclose(fo[done], z["obs"][done, k], rtol=OBS_TOL, atol=OBS_TOL)
+            np.testing.assert_allclose(o[done], z["reset_obs"][done, k], rtol=0, atol=OBS_TOL)
+            np.testing.assert_array_equal(env.start_y.cpu().numpy()[done], z["start_y"][done, k])
+        st = _state_matrix(env)
+        live = ~done
+        assert np.abs(st[live] - z["state"][live, k]).max(initial=0) <= STATE_TOL
+    np.testing.assert_array_equal(env.counters.cpu().numpy().T, z["counters"])
+
+
+@pytest.mark.parametrize("name", ["wind_exp4.npz", "wind_exp5.npz", "wind_exp6.npz",
+                                  "wind_exp6_tmax5.npz"])
+def test_wind_tables_vs_reference(name, gpu, built_lib):
+    """GPU wind curves vs the reference's interp1d tables (wind.py:69-99)."""
+    from sacenv import VecBoatEnv
+    z = golden(name)
+    exp, L = int(z["experiment"]), int(z["L"])
+    n = len(z["seeds"])
+    env = VecBoatEnv({"base_settings": {"experiment": exp, "t_max": L * 0.25}}, n,
+                     seeds=z["seeds"], device=gpu)
+    np.testing.assert_array_equal(env.start_y.cpu().numpy(), z["start_y"])
+    idx = z["idx"]
+    ids = np.repeat(np.arange(n, dtype=np.int32), len(idx))
+    ix = np.tile(idx.astype(np.int32), n)
+    v, a = env.wind_eval(ids, ix)
+    torch.cuda.synchronize()
+    v = v.cpu().numpy().reshape(n, len(idx))
+    a = a.cpu().numpy().reshape(n, len(idx))
+    np.testing.assert_allclose(v, z["vel"], rtol=0, atol=1e-12)
+    np.testing.assert_allclose(a, z["ang"], rtol=0, atol=1e-12)
+
+
+def test_rng_draws_bit_exact_across_many_resets(gpu, built_lib):
+    """Knots/start-y of 150 consecutive resets per env == numpy RandomState (crosses
+    many 624-word MT blocks, incl. windows straddling a block end)."""
+    from sacenv import VecBoatEnv
+    seeds = np.array([0, 5, 99, 2**32 - 1], np.uint64)
+    env = VecBoatEnv({"base_settings": {"experiment": 6}}, len(seeds), seeds=seeds, device=gpu,
+                     record_knots=True)
+    rs = [np.random.RandomState(int(s)) for s in seeds]
+    for r in range(150):
+        if r > 0:
+            env.reset()
+        torch.cuda.synchronize()
+        kn = env.knots_raw.cpu().numpy()       # [2, 8, E]
+        sy = env.start_y.cpu().numpy()
+        for e, g in enumerate(rs):
+            assert sy[e] == g.randint(-640, 640), (r, e)
+            assert np.array_equal(kn[0, :, e], g.random_sample(8)), (r, e)
+            assert np.array_equal(kn[1, :, e], g.random_sample(8)), (r, e)
+    for e, g in enumerate(rs):   # the device MT state is numpy's state
+        st = g.get_state()
+        assert int(env.mt_pos[e]) == st[2] or (int(env.mt_pos[e]) == 0 and st[2] == 624)
+
+
+@pytest.mark.parametrize("exp", [1, 2, 3, 4, 5, 6])
+def test_recorded_episode_replay(exp, gpu, built_lib):
+    """The reference's own recorded episodes (4 959 / 4 963 steps, goal reached)."""
+    from sacenv import VecBoatEnv
+    z = golden(f"recorded_exp{exp}.npz")
+    tr = z["trace"]
+    cols = [str(c) for c in z["columns"]]
+    c = {n: cols.index(n) for n in cols}
+    table = np.stack([z["wind_velocity"], z["wind_angle"]])
+    env = VecBoatEnv({"base_settings": {"experiment": exp, "test_mode": 1}}, 1, device=gpu,
+                     autoreset=False, wind_table=table)
+    env.reset_explicit([0], [int(tr[0, c["boat_position_y"]])])
+    n = len(tr) - 1
+    act = torch.zeros(1, dtype=torch.float32, device=gpu)
+    hist = []
+    for k in range(n + 1):
+        env.step(act)
+        hist.append(torch.stack([env.s_x, env.s_y, env.v_x, env.v_y, env.s_r]).clone())
+    torch.cuda.synchronize()
+    h = torch.cat(hist, 1).cpu().numpy().T       # [n+1, 5]
+    ref = tr[1:, [c["boat_position_x"], c["boat_position_y"], c["boat_velocity_x"],
+                  c["boat_velocity_y"], c["boat_angle"]]]
+    err = np.abs(h[:n] - ref).max()
+    assert err <= STATE_TOL, err
+    assert int(env.term[0]) == 1                 # reached_goal on the last step
+    if exp == 6:
+        assert abs(float(env.ep_reward[0]) - float(z["episode_reward"])) < 1e-6
+
+
+def test_full_size_subsample_vs_oracle(gpu, built_lib):
+    """65 536 envs (the bench config) with auto-reset and 500-step truncation:
+    envs are independent, so a random subset is checked against the oracle
+    run on just those seeds."""
+    from sacenv import VecBoatEnv
+    N, S = 65536, 120
+    rng = np.random.default_rng(1)
+    seeds = np.arange(N, dtype=np.uint64) + 1000
+    env = VecBoatEnv({"base_settings": {"experiment": 6, "test_mode": 0}}, N, seeds=seeds,
+                     device=gpu, autoreset=True, max_episode_steps=50)
+    env.reset()
+    pick = np.sort(rng.choice(N, 256, replace=False))
+    ora = OracleVecBoat(OracleConfig(experiment=6), seeds[pick], max_episode_steps=50)
+    ora.reset()
+    acts = rng.uniform(-1, 1, (S, N)).astype(np.float32)
+    acts_d = torch.from_numpy(acts).to(gpu)
+    n_trunc = 0
+    for k in range(S):
+        o, r, d, info = env.step(acts_d[k])
+        ro = ora.step(acts[k, pick])
+        torch.cuda.synchronize()
+        term = info["term"].cpu().numpy()[pick]
+        np.testing.assert_array_equal(term, ro["term"], err_msg=f"step {k}")
+        np.testing.assert_allclose(o.cpu().numpy()[pick], ro["reset_obs"], rtol=OBS_TOL,
+                                   atol=OBS_TOL)
+        n_trunc += int((term == 6).sum())
+        sx = env.s_x.cpu().numpy()[pick]
+        assert np.abs(sx - ora.s_x).max() <= STATE_TOL
+    assert n_trunc > 0
+
+
+def test_dropin_boatenv_shares_global_rng(gpu, built_lib):
+    """BoatEnv shim driven like main.py:70-91 reproduces the seeded reference run,
+    and leaves numpy's global stream exactly where the reference would."""
+    from sacenv import BoatEnv
+    z = golden("seeded_exp6_uniform.npz")
+    e = 1
+    np.random.seed(int(z["seeds"][e]))
+    env = BoatEnv(_cfg_dict(z), None, device=gpu)
+    obs = env.reset()
+    np.testing.assert_allclose(obs, z["init_obs"][e], atol=OBS_TOL)
+    assert env.action_space.shape == (1,) and env.observation_space.shape == (11,)
+    S = z["reward"].shape[1]
+    for k in range(S):
+        o, r, d, info = env.step(np.array([z["actions"][e, k]], np.float32))
+        assert d == bool(z["done"][e, k])
+        assert abs(env.boat.s_x - z["state"][e, k, 0]) <= STATE_TOL
+        assert abs(r - z["reward"][e, k]) <= STATE_TOL
+        assert info is env.info
+        if d:
+            assert info["termination"] == "rudder_broken"
+            env.reset()
+            assert env.info["episode_reward"] == 0
+    ora = OracleVecBoat(OracleConfig(experiment=6), z["seeds"][e:e + 1])
+    ora.reset()
+    for k in range(S):
+        ro = ora.step(z["actions"][e:e + 1, k])
+    assert np.random.random_sample() == ora.rngs[0].random_sample()
+    row = env.return_all_data()
+    assert set(row) == {"boat_position_x", "boat_position_y", "boat_velocity_x",
+                        "boat_velocity_y", "boat_angle", "action_rudder", "reward",
+                        "rudder_angle", "n"}
+    assert len(env.boat.wind.wind_velocity) == 10000
+
+
+def test_bad_config_raises(gpu, built_lib):
+    from sacenv import VecBoatEnv
+    with pytest.raises(ValueError):
+        VecBoatEnv({"base_settings": {"experiment": 7}}, 4, device=gpu)
+    with pytest.raises(ValueError):
+        VecBoatEnv({"base_settings": {"experiment": 6}, "wind": {"fixed_points": 3}}, 4, device=gpu)

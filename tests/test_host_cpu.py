@@ -1,0 +1,271 @@
+"""CPU-only checks of the host side and of the algorithms the kernels implement.
+
+* the C-ABI library loads and exports every entry point include/sacenv.h
+  declares; the ctypes mirrors have the C layout (gcc offsetof probe);
+* the numpy-legacy MT19937 algorithm the reset kernel implements — seeding,
+  the four-phase lane-parallel twist, tempering, masked-rejection randint,
+  53-bit doubles — reproduces ``np.random.RandomState`` word for word;
+* the not-a-knot spline in second-derivative form (config.spline_g) equals
+  scipy's interp1d basis the reference uses (wind.py:82-84), and the
+  critical-point grid min/max rule the reset kernel uses finds the exact
+  grid extrema.
+No compute call is made into the library here (no GPU in this container).
+"""
+import ctypes
+import math
+import os
+import re
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "sacenv.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(sacenv_\w+)\s*\(", src)))
+
+
+def test_library_exports_header(built_lib):
+    from sacenv import _lib
+    names = declared_functions()
+    assert len(names) == 7
+    assert set(names) == set(_lib.EXPORTS)
+    for n in names:
+        assert hasattr(built_lib, n), n
+    assert built_lib.sacenv_abi_version() == _lib.ABI_VERSION
+    assert built_lib.sacenv_error_string(-2).decode().startswith("Well someone")
+
+
+def test_argument_errors_without_gpu(built_lib):
+    """Argument validation runs on the host and never launches."""
+    from sacenv import _lib
+    from sacenv.config import BoatConfig, make_params
+    p = make_params(BoatConfig(experiment=6), 4)
+    p.experiment = 7
+    s = _lib.BoatState()
+    rc = built_lib.sacenv_boat_step(ctypes.byref(p), ctypes.byref(s), None, None, None)
+    assert rc == -2
+    p.experiment = 6
+    rc = built_lib.sacenv_boat_step(ctypes.byref(p), ctypes.byref(s), None, None, None)
+    assert rc == -1  # NULL state pointers
+
+
+def test_struct_layout_matches_c(tmp_path):
+    from sacenv import _lib
+    probe = tmp_path / "probe.c"
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "sacenv.h"', 'int main(void){']
+    for cname, cls in (("SacenvBoatParams", _lib.BoatParams), ("SacenvBoatState", _lib.BoatState),
+                       ("SacenvBoatStepOut", _lib.BoatStepOut)):
+        lines.append(f'printf("{cname} sizeof %zu\\n", sizeof({cname}));')
+        for f, _ in cls._fields_:
+            lines.append(f'printf("{cname} {f} %zu\\n", offsetof({cname}, {f}));')
+    lines.append("return 0;}")
+    probe.write_text("\n".join(lines))
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-std=c99", "-I", os.path.join(ROOT, "include"), str(probe), "-o", str(exe)],
+                   check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    got = {}
+    for ln in out:
+        if ln:
+            a, b, c = ln.split()
+            got[(a, b)] = int(c)
+    for cname, cls in (("SacenvBoatParams", _lib.BoatParams), ("SacenvBoatState", _lib.BoatState),
+                       ("SacenvBoatStepOut", _lib.BoatStepOut)):
+        assert got[(cname, "sizeof")] == ctypes.sizeof(cls), cname
+        for f, _ in cls._fields_:
+            assert got[(cname, f)] == getattr(cls, f).offset, (cname, f)
+
+
+# ---------------------------------------------------------------- MT19937
+M32 = 0xFFFFFFFF
+
+
+def mt_seed(seed):
+    key = [0] * 624
+    x = seed & M32
+    for i in range(624):
+        key[i] = x
+        x = (1812433253 * (x ^ (x >> 30)) + i + 1) & M32
+    return key, 624
+
+
+def mix(a, b, c):
+    y = (a & 0x80000000) | (b & 0x7FFFFFFF)
+    return c ^ (y >> 1) ^ (0x9908B0DF if y & 1 else 0)
+
+
+def twist_phased(o):
+    """Exactly the kernel's mt_twist_wave phase split (lane-parallel phases)."""
+    n = [None] * 624
+    for i in range(0, 227):
+        n[i] = mix(o[i], o[i + 1], o[i + 397])
+    for i in range(227, 454):
+        n[i] = mix(o[i], o[i + 1], n[i - 227])
+    for i in range(454, 623):
+        n[i] = mix(o[i], o[i + 1], n[i - 227])
+    n[623] = mix(o[623], n[0], n[396])
+    return n
+
+
+def temper(y):
+    y ^= y >> 11
+    y ^= (y << 7) & 0x9D2C5680
+    y ^= (y << 15) & 0xEFC60000
+    y ^= y >> 18
+    return y & M32
+
+
+class PyMT:
+    def __init__(self, seed):
+        self.key, self.pos = mt_seed(seed)
+
+    def next32(self):
+        if self.pos >= 624:
+            self.key, self.pos = twist_phased(self.key), 0
+        w = self.key[self.pos]
+        self.pos += 1
+        return temper(w)
+
+    def randint(self, lo, hi):
+        rng = hi - 1 - lo
+        mask = rng
+        for s in (1, 2, 4, 8, 16):
+            mask |= mask >> s
+        while True:
+            v = self.next32() & mask
+            if v <= rng:
+                return lo + v
+
+    def sample(self):
+        a, b = self.next32() >> 5, self.next32() >> 6
+        return (a * 67108864.0 + b) / 9007199254740992.0
+
+
+@pytest.mark.parametrize("seed", [0, 1, 12345, 2**31 + 11, 2**32 - 1])
+def test_mt19937_matches_numpy_legacy(seed):
+    ref = np.random.RandomState(seed)
+    me = PyMT(seed)
+    for _ in range(40):  # 40 Boat resets of exp 6: crosses several 624-word blocks
+        assert me.randint(-640, 640) == ref.randint(-640, 640)
+        kv = [me.sample() for _ in range(16)]
+        assert kv == list(ref.random_sample(16))
+    st = ref.get_state()
+    assert list(st[1]) == me.key and st[2] == me.pos
+
+
+# ---------------------------------------------------------------- spline
+def test_spline_g_equals_scipy_basis():
+    from boat_oracle import spline_basis
+    from sacenv.config import spline_g
+    for L, n in ((10000, 8), (20, 8), (500, 4), (10000, 16)):
+        B = spline_basis(L, n)
+        G = spline_g(n)
+        r = (n - 1) / (L - 1)
+        i = np.arange(L)
+        s = i * r
+        j = np.minimum(s.astype(int), n - 2)
+        t = s - j
+        u = 1 - t
+        E = np.eye(n)
+        # basis functions through the second-derivative form
+        M = G @ E
+        val = (u[:, None] * E[j] + t[:, None] * E[j + 1]
+               + (u ** 3 - u)[:, None] * M[j] + (t ** 3 - t)[:, None] * M[j + 1])
+        np.testing.assert_allclose(val, B, rtol=0, atol=2e-14)
+
+
+def _interval_extrema_py(y, m, n, L, j):
+    """Python mirror of the kernel's interval_extrema candidate rule -> grid indices."""
+    step = (n - 1) / (L - 1)
+    jf = lambda i: min(int(i * step), n - 2)
+
+    inv = 1 / step
+    lo = max(math.ceil(j * inv) - 2, 0)
+    while lo < L and jf(lo) < j:
+        lo += 1
+    hi = min(math.floor((j + 1) * inv) + 2, L - 1)
+    while hi >= 0 and jf(hi) > j:
+        hi -= 1
+    if lo > hi:
+        return [], []
+    cand = [lo, hi]
+    a, b = m[j], m[j + 1]
+    qa, qb, qc = 3 * (b - a), 6 * a, y[j + 1] - y[j] - 2 * a - b
+    roots = []
+    scale = abs(qa) + abs(qb) + abs(qc)
+    if abs(qa) <= 1e-14 * scale:
+        if qb != 0:
+            roots.append(-qc / qb)
+    else:
+        disc = qb * qb - 4 * qa * qc
+        if disc >= 0:
+            q = -0.5 * (qb + math.copysign(math.sqrt(disc), qb if qb != 0 else 1.0))
+            roots.append(q / qa)
+            if q != 0:
+                roots.append(qc / q)
+    for tr in roots:
+        if not (-0.01 < tr < 1.01):
+            continue
+        i0 = math.floor((j + tr) * inv)
+        for d in (-1, 0, 1, 2):
+            cand.append(min(max(i0 + d, lo), hi))
+    return cand, (lo, hi)
+
+
+@pytest.mark.parametrize("L", [10000, 20, 37])
+def test_grid_extrema_rule_is_exact(L):
+    from sacenv.config import spline_g
+    rng = np.random.RandomState(3)
+    n = 8
+    G = spline_g(n)
+    step = (n - 1) / (L - 1)
+    for _ in range(300):
+        y = rng.random_sample(n)
+        m = G @ y
+        i = np.arange(L)
+        s = i * step
+        jj = np.minimum(s.astype(int), n - 2)
+        t = s - jj
+        u = 1 - t
+        full = u * y[jj] + t * y[jj + 1] + (u * u * u - u) * m[jj] + (t * t * t - t) * m[jj + 1]
+        cands, cover = [], 0
+        for j in range(n - 1):
+            cand, rng_ = _interval_extrema_py(y, m, n, L, j)
+            cands += cand
+            if rng_:
+                cover += rng_[1] - rng_[0] + 1
+        assert cover == L  # intervals partition the grid
+        # the candidate grid points contain the exact grid argmin/argmax
+        assert full[cands].min() == full.min()
+        assert full[cands].max() == full.max()
+
+
+def test_config_from_reference_yaml_shape():
+    from sacenv.config import BoatConfig
+    raw = {"base_settings": {"experiment": 6, "test_mode": 1, "dt": 0.25, "t_max": 2500},
+           "boat": {"fuel": 30}, "wind": {"max_velocity": 0.5}}
+    c = BoatConfig.from_any(raw)
+    assert (c.experiment, c.test_mode, c.fuel, c.wind_len) == (6, 1, 30, 10000)
+
+    class Dot(dict):
+        __getattr__ = dict.__getitem__
+    d = Dot(base_settings=Dot(experiment=2, test_mode=0, dt=0.25, t_max=5))
+    c2 = BoatConfig.from_any(d)
+    assert (c2.experiment, c2.wind_len) == (2, 20)
+    with pytest.raises(ValueError):
+        BoatConfig(experiment=7).validate()
+    with pytest.raises(ValueError):
+        BoatConfig(experiment=6, fixed_points=3).validate()
+
+
+def test_package_imports_without_gpu():
+    import sacenv
+    assert sacenv.BoatConfig is not None
+    assert "oracle" not in sys.modules.get("sacenv").__dict__
