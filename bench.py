@@ -50,6 +50,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--kernel-launches", type=int, default=200)
+    ap.add_argument("--test-mode", type=int, default=0, help="1 = rudder frozen (no terminations)")
+    ap.add_argument("--episode-steps", type=int, default=EPISODE_STEPS,
+                    help="truncation length (0 = none)")
     return ap.parse_args()
 
 
@@ -125,8 +128,8 @@ def main():
     from sacenv import VecBoatEnv
 
     N = args.envs
-    env = VecBoatEnv({"base_settings": {"experiment": args.experiment, "test_mode": 0}}, N,
-                     seed=0, device=dev, autoreset=True, max_episode_steps=EPISODE_STEPS,
+    env = VecBoatEnv({"base_settings": {"experiment": args.experiment, "test_mode": args.test_mode}},
+                     N, seed=0, device=dev, autoreset=True, max_episode_steps=args.episode_steps,
                      env_id_offset=rank * N)
     env.reset()
     g = torch.Generator(device=dev)
