@@ -6,22 +6,25 @@
  * call (Boat dynamics boat_env.py:143-326, Wind wind.py:5-99, RewardFunction
  * reward_functions.py:9-57, Integrator control_theory/control_blocks.py:5-36).
  * The reference has no FFI; its boundary is the Python Gym surface. This
- * library replaces that surface's compute with gfx950 HIP kernels over N
- * envs held as structure-of-arrays in HBM; the Python package
- * `sac-agent_amd/sacenv` re-exposes the Gym surface on top.
+ * library runs that surface's compute as gfx950 HIP kernels over N envs held
+ * in one caller-owned device ARENA; the Python package `sac-agent_amd/sacenv`
+ * re-exposes the Gym surface on top (INTEGRATION.md shows the bindings).
  *
  * Conventions
- *   - Every pointer inside the structs and every array argument is a DEVICE
- *     pointer owned by the caller (torch tensors in the Python host).
- *   - The params / state / out structs themselves are HOST memory; they are
- *     read during the call only (captured by value into the launch).
+ *   - The arena is a DEVICE buffer of sacenv_boat_layout()->total_bytes
+ *     bytes owned by the caller (a torch uint8 tensor in the Python host),
+ *     zero-filled before sacenv_boat_init(). Its fields are SoA arrays whose
+ *     byte offsets sacenv_boat_layout() reports, so an FFI user can view them.
+ *   - `params` is HOST memory, read during the call (captured by value into
+ *     the launch). It must not change after sacenv_boat_init().
  *   - `stream` is a hipStream_t (void* here so the header needs no HIP
- *     headers); NULL = the default stream. Every call only enqueues work on
- *     `stream`: no host synchronisation, no allocation, graph-capturable.
+ *     headers); NULL = the default stream. Apart from sacenv_boat_init (one
+ *     small host->device copy), every call only enqueues kernels on `stream`:
+ *     no host synchronisation, no allocation, graph-capturable.
  *   - Return value: 0 on success, otherwise an SACENV_E_* code (argument
- *     errors) or a hipError_t from the launch (> 0). No exception crosses
- *     the ABI. sacenv_error_string() names the code.
- *   - Bit-for-bit the reference's float64 arithmetic order; state is f64.
+ *     errors) or a hipError_t from the launch (> 0). No exception crosses the
+ *     ABI; sacenv_error_string() names the code.
+ *   - Float64 arithmetic in the reference's expression order; state is f64.
  */
 #ifndef SACENV_H
 #define SACENV_H
@@ -32,11 +35,13 @@
 extern "C" {
 #endif
 
-#define SACENV_ABI_VERSION 1
+#define SACENV_ABI_VERSION 2
 #define SACENV_OBS_DIM 11      /* Boat.return_state, boat_env.py:308-323 */
 #define SACENV_MT_N 624        /* MT19937 words per env (numpy legacy RNG) */
 #define SACENV_MAX_KNOTS 16    /* wind.fixed_points upper bound */
 #define SACENV_N_COUNTERS 5    /* info-dict termination counters, boat_env.py:24-32 */
+#define SACENV_SLOTS 3         /* pre-drawn episode slots per env in autoreset mode */
+#define SACENV_RECORD_BYTES 50 /* packed per-env step record (see layout.record) */
 
 /* termination codes; 1..5 follow the info-dict key order boat_env.py:24-32,
  * the chain's priority stays goal > oob > fuel > timeout > rudder (:84-105). */
@@ -55,101 +60,128 @@ enum {
   SACENV_E_NULL = -1,        /* required pointer is NULL */
   SACENV_E_EXPERIMENT = -2,  /* experiment not in 1..6  (wind.py:65-67 ValueError) */
   SACENV_E_KNOTS = -3,       /* fixed_points < 4 or > SACENV_MAX_KNOTS (wind.py:73-75) */
-  SACENV_E_SIZE = -4,        /* n_envs / n_ids / wind_len out of range */
-  SACENV_E_RANGE = -5        /* start-y half width < 1 (np.random.randint low >= high) */
+  SACENV_E_SIZE = -4,        /* n_envs / n_ids / wind_len / n_helpers out of range */
+  SACENV_E_RANGE = -5,       /* start-y half width < 1 (np.random.randint low >= high) */
+  SACENV_E_MODE = -6         /* call not valid in this autoreset mode */
+};
+
+/* optional outputs (params.out_flags) */
+enum {
+  SACENV_OUT_ACCEL = 1,      /* layout.accel: a_x, a_y, a_r of the step (f64) */
+  SACENV_OUT_REWARD64 = 2,   /* layout.reward64: reward in f64 */
+  SACENV_OUT_KNOTS = 4       /* layout.knots_raw: drawn knot values per slot */
 };
 
 /* Everything the hot path reads from the reference config
- * (configs/original_config.yaml:2-65), plus derived launch constants. */
+ * (configs/original_config.yaml:2-65), plus launch constants. Sums and
+ * differences the reference forms from config values are passed pre-formed
+ * (the same single IEEE operation). */
 typedef struct SacenvBoatParams {
-  int32_t n_envs;             /* envs held by this state (per GPU / rank) */
+  int32_t n_envs;             /* envs in this arena (per GPU / rank) */
   int32_t experiment;         /* base_settings.experiment, 1..6 (wind.py:26-67) */
-  int32_t test_mode;          /* base_settings.test_mode; 0 => action drives rudder (boat_env.py:72-73) */
+  int32_t test_mode;          /* 0 => action drives rudder (boat_env.py:72-73) */
   int32_t wind_len;           /* L = int(t_max/dt) (wind.py:14-15) */
   int32_t n_knots;            /* wind.fixed_points (wind.py:76-78) */
   int32_t fuel0;              /* boat.fuel (boat_env.py:180) */
   int32_t start_y_half;       /* int(0.8*track_width) (boat_env.py:147-150) */
   int32_t max_episode_steps;  /* > 0: truncate (term 6) after this many steps; 0: off */
-  int32_t autoreset;          /* 1: envs that end are reset inside step (obs row = reset obs) */
-  int32_t reserved0;
+  int32_t autoreset;          /* 1: envs that end start their next episode inside step */
+  int32_t n_helpers;          /* autoreset: helper waves per step launch (1..4096) */
+  int32_t out_flags;          /* SACENV_OUT_* bitmask */
+  int32_t use_wind_table;     /* 1: wind from layout.wind_table [2][L] for every env */
   double dt, t_max, goal_line, oob_limit, track_width;  /* oob = width + offset (:200-201) */
-  double boat_m, boat_m_x, boat_m_y, boat_I, boat_Iz;
-  double propeller_diameter, wake_friction, c_r_front, c_r_side, thrust_deduction, rho;
-  double boat_area_front, boat_area_side, boat_l, boat_b, rudder_area;
-  double n_rpm;               /* 20, boat_env.py:178 */
+  double c_r_front, c_r_side, rho, boat_area_front, boat_area_side, boat_l, boat_b, rudder_area;
+  double m_plus_mx;           /* (boat_m + boat_m_x) :239 */
+  double m_plus_my;           /* (boat_m + boat_m_y) :230, :265 */
+  double i_plus_iz;           /* (boat_I + boat_Iz)  :281 */
+  double one_minus_wf;        /* (1 - wake_friction) :221 */
+  double one_minus_td;        /* (1 - thrust_deduction) :227 */
+  double n_rpm;               /* self.n = 20 (:178) */
+  double n_times_d;           /* self.n * propeller_diameter (:224) */
+  double n_squared;           /* np.square(self.n) (:226) */
+  double d_pow4;              /* np.power(propeller_diameter, 4) (:226) */
   double max_velocity;        /* wind.max_velocity */
   double wind_dir_rad;        /* float(wind.direction) * (pi/180) (wind.py:370) */
-  double reward_k;            /* (-y_a / y_b) with y_a=0.03, y_b=3.4 (reward_functions.py:53) */
-  double reward_center;       /* track_width * 0.2 */
+  double reward_k;            /* (-y_a / y_b), y_a=0.03, y_b=3.4 (reward_functions.py:53) */
+  double reward_center;       /* track_width * 0.2 (reward_functions.py:53) */
   double knot_step;           /* (n_knots-1)/(wind_len-1): grid index -> knot coordinate */
-  double obs_lo[SACENV_OBS_DIM], obs_hi[SACENV_OBS_DIM]; /* normalize() bounds, :310-321 */
-  const double *spline_g;     /* [n_knots*n_knots]: (m/6) = G @ knots, not-a-knot cubic */
-  const double *wind_table;   /* NULL, or [2][wind_len] (velocity, angle) shared by all envs */
 } SacenvBoatParams;
 
-/* Per-env carried state, SoA, length n_envs unless noted. */
-typedef struct SacenvBoatState {
-  double *s_x, *s_y, *s_r;    /* position integrator outputs (get_kinematics :297-306) */
-  double *v_x, *v_y, *v_r;    /* velocity integrator outputs (run_model_step :205-209) */
-  double *rudder;             /* Boat.rudder_angle (f64, pinned-numpy semantics) */
-  double *t;                  /* Boat.t, accumulated t += dt (:69) */
-  double *ep_reward;          /* info['episode_reward'] (:113, :122) */
-  int32_t *index;             /* Boat.index == steps since reset (:155, :211); fuel = fuel0 - index */
-  int32_t *start_y;           /* Boat.s_y_start (:147-150) */
-  double *wind_y;             /* [2][n_knots][n_envs] folded knot values of the wind curves */
-  double *wind_m;             /* [2][n_knots][n_envs] folded second derivatives / 6 */
-  double *knots_raw;          /* NULL, or [2][n_knots][n_envs]: the drawn knot values (debug) */
-  uint32_t *mt_key;           /* [n_envs][624] per-env MT19937 state (np.random legacy) */
-  int32_t *mt_pos;            /* [n_envs] next word index in mt_key, 624 => twist first */
-  uint32_t *counters;         /* [5][n_envs] cumulative termination counters (never reset) */
-} SacenvBoatState;
-
-/* Step outputs. obs/reward/done/term are required; the rest may be NULL. */
-typedef struct SacenvBoatStepOut {
-  float *obs;                 /* [n_envs][11] (reset obs for envs auto-reset this step) */
-  float *reward;              /* [n_envs] */
-  uint8_t *done;              /* [n_envs] 1 if term != 0 */
-  uint8_t *term;              /* [n_envs] SACENV_TERM_* */
-  float *final_obs;           /* [n_envs][11] terminal obs, written only where done && autoreset */
-  double *final_ep_reward;    /* [n_envs] episode reward, written only where done */
-  double *accel;              /* [3][n_envs] a_x, a_y, a_r of this step */
-  double *reward64;           /* [n_envs] reward in float64 */
-} SacenvBoatStepOut;
+/* Byte offsets of the arena fields. n_pad = n_envs rounded up to 64; per-env
+ * arrays have n_pad entries (entries >= n_envs are padding). */
+typedef struct SacenvBoatLayout {
+  int64_t total_bytes;
+  int64_t n_pad;
+  int64_t s_x, s_y, s_r, v_x, v_y, v_r, rudder, t, ep_reward; /* f64 [n_pad] */
+  int64_t index;              /* i32 [n_pad] steps since reset; fuel = fuel0 - index */
+  int64_t cons;               /* i32 [n_pad] episodes started (active slot = cons % 3) */
+  int64_t fill;               /* i32 [n_pad] episodes drawn (autoreset) */
+  int64_t mt_pos;             /* i32 [n_pad] next MT word index, 624 => twist first */
+  int64_t start_y;            /* i32 [3][n_pad] Boat.s_y_start per slot */
+  int64_t counters;           /* u32 [5][n_pad] cumulative termination counters */
+  int64_t refill_list;        /* i32 [3][n_pad] envs whose slot awaits a refill */
+  int64_t wind_y;             /* f64 [3][2][n_knots][n_pad] folded knot values per slot, curve */
+  int64_t wind_m;             /* f64 [3][2][n_knots][n_pad] folded 2nd derivatives / 6 */
+  int64_t knots_raw;          /* f64 [3][2][n_knots][n_pad] drawn knots (SACENV_OUT_KNOTS) */
+  int64_t mt_key;             /* u32 [n_pad][624] per-env MT19937 state */
+  int64_t record;             /* u8 [50 n_pad]: obs f32 [n_pad][11] | reward f32 [n_pad]
+                                 | done u8 [n_pad] | term u8 [n_pad]  (the all-gather payload) */
+  int64_t obs, reward, done, term; /* the four parts of `record` */
+  int64_t final_obs;          /* f32 [n_pad][11] terminal obs of envs that auto-reset */
+  int64_t final_ep_reward;    /* f64 [n_pad] episode reward of envs that ended */
+  int64_t accel;              /* f64 [3][n_pad] a_x, a_y, a_r */
+  int64_t reward64;           /* f64 [n_pad] */
+  int64_t refill_count;       /* i32 [4] */
+  int64_t owner_epoch;        /* i32 [n_pad/64] per owner-block launch counter */
+  int64_t helper_epoch;       /* i32 [n_helpers] per helper-block launch counter */
+  int64_t spline_g;           /* f64 [n_knots][n_knots]: (m/6) = G @ knots (written by init) */
+  int64_t wind_table;         /* f64 [2][wind_len] (velocity, angle), if use_wind_table */
+} SacenvBoatLayout;
 
 int sacenv_abi_version(void);
 const char *sacenv_error_string(int code);
 
-/* np.random.seed(seeds[e]) for every env: legacy MT19937 init_genrand.
- * Replaces the global-RNG seeding the reference relies on (boat_env.py:147,
- * wind.py:78; numpy RandomState._legacy_seeding). */
-int sacenv_boat_seed(const SacenvBoatParams *p, const SacenvBoatState *s,
-                     const uint32_t *seeds, void *stream);
+/* Validate params and compute the arena layout (host only, no device work). */
+int sacenv_boat_layout(const SacenvBoatParams *p, SacenvBoatLayout *out);
 
-/* Boat(config) for envs ids[0..n_ids) (ids == NULL: all n_envs), consuming
- * each env's RNG in the reference's order (randint, then 8 knots per random
- * wind curve), info['episode_reward'] = 0, and writes their obs rows.
- * Replaces BoatEnv.reset (boat_env.py:120-126) / Boat.__init__ (:144-201)
- * and Wind.generate_wind (wind.py:26-99). obs may be NULL. */
-int sacenv_boat_reset(const SacenvBoatParams *p, const SacenvBoatState *s,
-                      const int32_t *ids, int32_t n_ids, float *obs, void *stream);
+/* Seed every env's RNG exactly like np.random.seed(seeds[e]) (legacy MT19937
+ * init_genrand; numpy RandomState._legacy_seeding), upload the spline
+ * constants, and build every env's first Boat — BoatEnv.__init__ constructs
+ * one (boat_env.py:15; Boat.__init__ :144-201, Wind wind.py:26-99) — drawing
+ * in the reference's order (randint :147, then 8 knot values per random
+ * curve wind.py:78). In autoreset mode the next two episodes are pre-drawn
+ * too (same per-env stream, same order). `seeds` is a DEVICE u32 [n_envs];
+ * `obs` (nullable) receives the first observations [n_envs][11] f32. */
+int sacenv_boat_init(const SacenvBoatParams *p, void *arena, const uint32_t *seeds, void *stream);
 
-/* As sacenv_boat_reset but with the draws supplied by the caller (no RNG):
- * start_y[n_ids], knots[n_ids][2][n_knots] (knots may be NULL for
- * experiments 1-3). For replaying recorded episodes. */
-int sacenv_boat_reset_explicit(const SacenvBoatParams *p, const SacenvBoatState *s,
-                               const int32_t *ids, int32_t n_ids, const int32_t *start_y,
-                               const double *knots, float *obs, void *stream);
+/* BoatEnv.reset (boat_env.py:120-126) for envs ids[0..n_ids) (device i32;
+ * ids == NULL: all envs): a new Boat, info['episode_reward'] = 0, obs rows
+ * written to layout.obs. Draw order per env is the reference's. */
+int sacenv_boat_reset(const SacenvBoatParams *p, void *arena, const int32_t *ids, int32_t n_ids,
+                      void *stream);
 
-/* One BoatEnv.step for every env (boat_env.py:67-115): action[n_envs] f32.
- * With p->autoreset, envs that end are reset in the same launch. */
-int sacenv_boat_step(const SacenvBoatParams *p, const SacenvBoatState *s,
-                     const float *action, const SacenvBoatStepOut *out, void *stream);
+/* Non-autoreset mode only: reset with caller-supplied draws (no RNG):
+ * start_y[n_ids] (device i32), knots[n_ids][2][n_knots] (device f64,
+ * nullable for experiments 1-3 or with the wind table). For replaying
+ * recorded episodes. */
+int sacenv_boat_reset_explicit(const SacenvBoatParams *p, void *arena, const int32_t *ids,
+                               int32_t n_ids, const int32_t *start_y, const double *knots,
+                               void *stream);
 
-/* Wind.get_wind for n (env, index) pairs (wind.py:20-24); used to expose
- * env.boat.wind.wind_velocity / wind_angle tables (recorder.py:45-56). */
-int sacenv_boat_wind_eval(const SacenvBoatParams *p, const SacenvBoatState *s,
-                          const int32_t *env_ids, const int32_t *idx, int32_t n,
-                          double *out_velocity, double *out_angle, void *stream);
+/* One BoatEnv.step for every env (boat_env.py:67-115); action: device f32
+ * [n_envs]. Outputs go to the arena's record (+ optional outputs). With
+ * autoreset, an env that ends starts its next (pre-drawn) episode in the same
+ * launch: its obs row is the new episode's, the terminal obs is in
+ * final_obs; helper waves of the same launch draw replacement episodes for
+ * the envs that ended in the previous launch. */
+int sacenv_boat_step(const SacenvBoatParams *p, void *arena, const float *action, void *stream);
+
+/* Wind.get_wind(index) (wind.py:20-24) of each env's CURRENT episode for n
+ * (env, index) pairs (device i32 arrays) -> device f64 out arrays. Exposes
+ * env.boat.wind.wind_velocity / wind_angle (recorder.py:45-56). */
+int sacenv_boat_wind_eval(const SacenvBoatParams *p, const void *arena, const int32_t *env_ids,
+                          const int32_t *idx, int32_t n, double *out_velocity, double *out_angle,
+                          void *stream);
 
 #ifdef __cplusplus
 }

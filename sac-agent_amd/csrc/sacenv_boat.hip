@@ -1,16 +1,27 @@
 // sacenv_boat.hip — gfx950 kernels + C ABI for the vectorised boat env.
 //
-// One wave64 workgroup owns 64 consecutive envs. Per step each lane runs one
-// env's BoatEnv.step (boat_env.py:67-115) on float64 SoA state; envs that end
-// are then reset by the WHOLE wave, one env at a time (Boat.__init__,
-// boat_env.py:144-201): the per-env MT19937 twist, the randint rejection
-// loop, the knot draws and the not-a-knot spline's grid min/max are spread
-// across the 64 lanes, so a reset costs a few hundred cycles instead of the
-// 10 000-sample scan the reference does (wind.py:80-89).
+// Work split of one step launch (autoreset mode):
+//   * owner blocks: one wave64 = 64 consecutive envs, one lane per env. Each
+//     lane runs BoatEnv.step (boat_env.py:67-115) on float64 SoA state. An env
+//     that ends (terminated or truncated) starts its next episode at once from
+//     a PRE-DRAWN slot (3 slots/env: active + 2 ahead), so no RNG or spline
+//     work ever sits on the step's critical path. The env id is appended to
+//     the launch's refill list (wave-aggregated atomic).
+//   * helper blocks: one wave per env listed by the PREVIOUS launch draws the
+//     replacement episode (Boat.__init__ draws, boat_env.py:144-201; Wind,
+//     wind.py:26-99) into the freed slot, cooperatively across 64 lanes: the
+//     MT19937 twist, the randint rejection, the 53-bit knot values and the
+//     not-a-knot spline's exact grid min/max via critical points (instead of
+//     the reference's 10 000-sample scan, wind.py:80-89).
+// Owners and helpers of one launch never touch the same bytes: a slot freed
+// in launch k is refilled in launch k+1 and consumed no earlier than k+1
+// (three slots cover an env that ends in every launch). Lists are triple-
+// buffered by a per-block launch counter, so no inter-block hand-off happens
+// inside a launch and graph replay needs no per-launch arguments.
 //
 // Floating-point order follows the reference expression by expression
-// (left-to-right products, no FMA contraction: -ffp-contract=off), so the
-// only differences from the CPU step are the libm/ocml transcendentals.
+// (left-to-right products, no FMA contraction: -ffp-contract=off); the only
+// differences from the CPU step are the libm/ocml transcendentals.
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -28,12 +39,115 @@ constexpr uint32_t kMtUpper = 0x80000000u;
 constexpr uint32_t kMtLower = 0x7fffffffu;
 constexpr uint32_t kMtMatrixA = 0x9908b0dfu;
 constexpr int kMaxK = SACENV_MAX_KNOTS;
+constexpr int kSlots = SACENV_SLOTS;
 constexpr double kPi = 3.141592653589793;  // np.pi
 
-struct ResetLds {
-  uint32_t blk[2][kMtN];          // current MT block, next (twisted) block
-  double y[2][kMaxK];             // knot values per curve (unfolded)
-  double m[2][kMaxK];             // second derivatives / 6 per curve (unfolded)
+// ---------------------------------------------------------------- arena
+// Per-env byte widths; a field's offset is (sum of widths before it) * n_pad.
+// n_pad is a multiple of 64, so every array is 64-byte aligned.
+constexpr int U_SX = 0, U_SY = 8, U_SR = 16, U_VX = 24, U_VY = 32, U_VR = 40, U_RUD = 48,
+              U_T = 56, U_EP = 64, U_IDX = 72, U_CONS = 76, U_FILL = 80, U_MTPOS = 84,
+              U_STARTY = 88, U_CNT = 100, U_LIST = 120, U_WIND = 132;
+constexpr int U_MT_BYTES = 4 * kMtN;
+
+__host__ __device__ inline int64_t pad64(int64_t n) { return (n + 63) / 64 * 64; }
+__host__ __device__ inline int64_t align256(int64_t x) { return (x + 255) / 256 * 256; }
+
+__host__ __device__ inline void compute_layout(int n, int nk, int nh, int L, int use_table,
+                                               SacenvBoatLayout* o) {
+  const int64_t np = pad64(n);
+  o->n_pad = np;
+  o->s_x = U_SX * np;
+  o->s_y = U_SY * np;
+  o->s_r = U_SR * np;
+  o->v_x = U_VX * np;
+  o->v_y = U_VY * np;
+  o->v_r = U_VR * np;
+  o->rudder = U_RUD * np;
+  o->t = U_T * np;
+  o->ep_reward = U_EP * np;
+  o->index = U_IDX * np;
+  o->cons = U_CONS * np;
+  o->fill = U_FILL * np;
+  o->mt_pos = U_MTPOS * np;
+  o->start_y = U_STARTY * np;
+  o->counters = U_CNT * np;
+  o->refill_list = U_LIST * np;
+  const int64_t uw = U_WIND, wk = 48LL * nk;
+  o->wind_y = uw * np;
+  o->wind_m = (uw + wk) * np;
+  o->knots_raw = (uw + 2 * wk) * np;
+  o->mt_key = (uw + 3 * wk) * np;
+  const int64_t ur = uw + 3 * wk + U_MT_BYTES;
+  o->record = ur * np;
+  o->obs = ur * np;
+  o->reward = (ur + 44) * np;
+  o->done = (ur + 48) * np;
+  o->term = (ur + 49) * np;
+  o->final_obs = (ur + 50) * np;
+  o->final_ep_reward = (ur + 94) * np;
+  o->accel = (ur + 102) * np;
+  o->reward64 = (ur + 126) * np;
+  int64_t off = align256((ur + 134) * np);
+  o->refill_count = off;
+  off += 256;
+  o->owner_epoch = off;
+  off += align256(4 * (np / 64));
+  o->helper_epoch = off;
+  off += align256(4LL * (nh > 0 ? nh : 1));
+  o->spline_g = off;
+  off += align256(8LL * kMaxK * kMaxK);
+  o->wind_table = off;
+  off += use_table ? align256(16LL * L) : 0;
+  o->total_bytes = off;
+}
+
+// Device view: pointers are recomputed from (base, n_pad, n_knots) at use,
+// which keeps the kernels' scalar-register footprint small.
+struct Arena {
+  char* b;
+  int64_t np;
+  int nk;
+  template <class T>
+  __device__ __forceinline__ T* at(int64_t units) const { return reinterpret_cast<T*>(b + units * np); }
+  __device__ __forceinline__ double* f64(int u) const { return at<double>(u); }
+  __device__ __forceinline__ int32_t* i32(int u) const { return at<int32_t>(u); }
+  __device__ __forceinline__ int64_t uw() const { return U_WIND; }
+  __device__ __forceinline__ int64_t wk() const { return 48LL * nk; }
+  __device__ __forceinline__ double* wind_y() const { return at<double>(uw()); }
+  __device__ __forceinline__ double* wind_m() const { return at<double>(uw() + wk()); }
+  __device__ __forceinline__ double* knots_raw() const { return at<double>(uw() + 2 * wk()); }
+  __device__ __forceinline__ uint32_t* mt_key() const { return at<uint32_t>(uw() + 3 * wk()); }
+  __device__ __forceinline__ int64_t ur() const { return uw() + 3 * wk() + U_MT_BYTES; }
+  __device__ __forceinline__ float* obs() const { return at<float>(ur()); }
+  __device__ __forceinline__ float* reward() const { return at<float>(ur() + 44); }
+  __device__ __forceinline__ uint8_t* done() const { return at<uint8_t>(ur() + 48); }
+  __device__ __forceinline__ uint8_t* term() const { return at<uint8_t>(ur() + 49); }
+  __device__ __forceinline__ float* final_obs() const { return at<float>(ur() + 50); }
+  __device__ __forceinline__ double* final_ep() const { return at<double>(ur() + 94); }
+  __device__ __forceinline__ double* accel() const { return at<double>(ur() + 102); }
+  __device__ __forceinline__ double* reward64() const { return at<double>(ur() + 126); }
+  __device__ __forceinline__ char* tail() const { return b + align256((ur() + 134) * np); }
+  __device__ __forceinline__ int32_t* refill_count() const { return reinterpret_cast<int32_t*>(tail()); }
+  __device__ __forceinline__ int32_t* owner_epoch() const {
+    return reinterpret_cast<int32_t*>(tail() + 256);
+  }
+  __device__ __forceinline__ int32_t* helper_epoch() const {
+    return reinterpret_cast<int32_t*>(tail() + 256 + align256(4 * (np / 64)));
+  }
+  // slot-major wind coefficient of (slot, curve, knot) for env e
+  __device__ __forceinline__ int64_t wix(int slot, int c, int k, int e) const {
+    return ((int64_t)(slot * 2 + c) * nk + k) * np + e;
+  }
+};
+
+__host__ inline Arena make_arena(const SacenvBoatParams& p, void* base) {
+  return Arena{static_cast<char*>(base), pad64(p.n_envs), p.n_knots};
+}
+
+struct Tail {  // small tables whose offsets depend on n_helpers / wind_len
+  const double* g;
+  const double* table;
 };
 
 // ---------------------------------------------------------------- MT19937
@@ -51,6 +165,13 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t c) {
   const uint32_t y = (a & kMtUpper) | (b & kMtLower);
   return c ^ (y >> 1) ^ ((y & 1u) ? kMtMatrixA : 0u);
 }
+
+struct DrawLds {
+  uint32_t blk[2][kMtN];  // current MT block, next (twisted) block
+  double y[2][kMaxK];     // knot values per curve (unfolded)
+  double m[2][kMaxK];     // second derivatives / 6 per curve (unfolded)
+  double g[kMaxK * kMaxK];
+};
 
 // mt19937_gen as four lane-parallel phases: word i depends on old[i],
 // old[i+1] and either old[i+397] (i < 227) or new[i-227].
@@ -72,14 +193,14 @@ __device__ void mt_twist_wave(const uint32_t* __restrict__ o, uint32_t* __restri
 // when a window crosses the block end.
 struct MtStream {
   uint32_t* gkey;
-  int pos;        // offset of the next unconsumed word in the current block
-  int cur;        // which ResetLds::blk holds the current block (when loaded)
+  int pos;   // offset of the next unconsumed word in the current block
+  int cur;   // which DrawLds::blk holds the current block (when loaded)
   bool loaded;
   bool nxt_valid;
   bool advanced;  // current block differs from gkey
 };
 
-__device__ uint32_t mt_fetch(MtStream& st, ResetLds& l, int lane) {
+__device__ uint32_t mt_fetch(MtStream& st, DrawLds& l, int lane) {
   if (!st.loaded) {
     if (st.pos + kWave <= kMtN) return mt_temper(st.gkey[st.pos + lane]);
     for (int i = lane; i < kMtN; i += kWave) l.blk[0][i] = st.gkey[i];
@@ -104,7 +225,7 @@ __device__ uint32_t mt_fetch(MtStream& st, ResetLds& l, int lane) {
   return mt_temper(w);
 }
 
-__device__ void mt_finish(MtStream& st, ResetLds& l, int32_t* gpos, int lane) {
+__device__ void mt_finish(MtStream& st, DrawLds& l, int32_t* gpos, int lane) {
   // words consumed past the block end came from the twisted block: make it current
   while (st.loaded && (st.pos > kMtN || (st.pos == kMtN && st.nxt_valid))) {
     if (!st.nxt_valid) mt_twist_wave(l.blk[st.cur], l.blk[st.cur ^ 1], lane);
@@ -138,17 +259,18 @@ __device__ __forceinline__ double spline_piece(double y0, double y1, double m0, 
   return u * y0 + t * y1 + (u * u * u - u) * m0 + (t * t * t - t) * m1;
 }
 
-__device__ __forceinline__ double curve_lds(const SacenvBoatParams& p, const ResetLds& l, int c, int i) {
+__device__ __forceinline__ double curve_lds(const SacenvBoatParams& p, const DrawLds& l, int c, int i) {
   const Knot k = knot_coord(p, i);
   return spline_piece(l.y[c][k.j], l.y[c][k.j + 1], l.m[c][k.j], l.m[c][k.j + 1], k.t);
 }
 
-__device__ __forceinline__ double curve_env(const SacenvBoatParams& p, const SacenvBoatState& s,
-                                            int c, int e, int i) {
+__device__ __forceinline__ double curve_env(const SacenvBoatParams& p, const Arena& A, int slot, int c,
+                                            int e, int i) {
   const Knot k = knot_coord(p, i);
-  const size_t n = (size_t)p.n_envs;
-  const size_t base = ((size_t)c * p.n_knots + k.j) * n + e;
-  return spline_piece(s.wind_y[base], s.wind_y[base + n], s.wind_m[base], s.wind_m[base + n], k.t);
+  const int64_t o = A.wix(slot, c, k.j, e);
+  const double* wy = A.wind_y();
+  const double* wm = A.wind_m();
+  return spline_piece(wy[o], wy[o + A.np], wm[o], wm[o + A.np], k.t);
 }
 
 __host__ __device__ __forceinline__ int n_curves(int experiment) {
@@ -156,13 +278,13 @@ __host__ __device__ __forceinline__ int n_curves(int experiment) {
 }
 
 // Wind.get_wind(index) (wind.py:20-24) for the tables of wind.py:26-99.
-__device__ __forceinline__ void wind_at(const SacenvBoatParams& p, const SacenvBoatState& s, int e,
-                                        int idx, double& wv, double& wa) {
+__device__ __forceinline__ void wind_at(const SacenvBoatParams& p, const Arena& A, const double* table,
+                                        int slot, int e, int idx, double& wv, double& wa) {
   if (idx > p.wind_len - 1) idx = p.wind_len - 1;  // reference: IndexError
   if (idx < 0) idx = 0;
-  if (p.wind_table != nullptr) {
-    wv = p.wind_table[idx];
-    wa = p.wind_table[p.wind_len + idx];
+  if (p.use_wind_table) {
+    wv = table[idx];
+    wa = table[p.wind_len + idx];
     return;
   }
   switch (p.experiment) {
@@ -171,18 +293,18 @@ __device__ __forceinline__ void wind_at(const SacenvBoatParams& p, const SacenvB
       wa = p.wind_dir_rad;
       return;
     case 4:
-      wv = curve_env(p, s, 0, e, idx);
+      wv = curve_env(p, A, slot, 0, e, idx);
       wa = p.wind_dir_rad;
       return;
     case 5: {
       wv = p.max_velocity;
-      const double r = curve_env(p, s, 0, e, idx) <= 0.5 / 2 ? 0.0 : 1.0;  // wind.py:92-99
+      const double r = curve_env(p, A, slot, 0, e, idx) <= 0.5 / 2 ? 0.0 : 1.0;  // wind.py:92-99
       wa = (r * kPi) + kPi / 2;
       return;
     }
     case 6:
-      wv = curve_env(p, s, 0, e, idx);
-      wa = curve_env(p, s, 1, e, idx);
+      wv = curve_env(p, A, slot, 0, e, idx);
+      wa = curve_env(p, A, slot, 1, e, idx);
       return;
     default:  // 1, 2: no wind
       wv = 0.0;
@@ -192,11 +314,9 @@ __device__ __forceinline__ void wind_at(const SacenvBoatParams& p, const SacenvB
 }
 
 // ---------------------------------------------------------------- observation
-
-__device__ __forceinline__ double norm(const SacenvBoatParams& p, int k, double v) {
-  return (v - p.obs_lo[k]) / (p.obs_hi[k] - p.obs_lo[k]);  // Boat.normalize, :325-326
-}
-
+// Boat.return_state / normalize (boat_env.py:308-326): (v - lo) / (hi - lo);
+// the constant spans are the reference's literals, applied as reciprocals
+// (the float32 observation is the output; state itself is untouched).
 struct Obs {
   float v[SACENV_OBS_DIM];
 };
@@ -205,17 +325,17 @@ __device__ __forceinline__ Obs make_obs(const SacenvBoatParams& p, double s_x, d
                                         double s_y, double v_y, double a_y, double s_r, double v_r,
                                         double a_r, double rudder, double fuel) {
   Obs o;
-  o.v[0] = (float)norm(p, 0, s_x);
-  o.v[1] = (float)norm(p, 1, v_x);
-  o.v[2] = (float)norm(p, 2, a_x);
-  o.v[3] = (float)norm(p, 3, s_y);
-  o.v[4] = (float)norm(p, 4, v_y);
-  o.v[5] = (float)norm(p, 5, a_y);
-  o.v[6] = (float)norm(p, 6, s_r);
-  o.v[7] = (float)norm(p, 7, v_r);
-  o.v[8] = (float)norm(p, 8, a_r);
-  o.v[9] = (float)norm(p, 9, rudder);
-  o.v[10] = (float)norm(p, 10, fuel);
+  o.v[0] = (float)(s_x / p.goal_line);
+  o.v[1] = (float)(v_x * (1.0 / 5.0));
+  o.v[2] = (float)(a_x * (1.0 / 0.025));
+  o.v[3] = (float)((s_y + p.track_width) / (p.track_width + p.track_width));
+  o.v[4] = (float)(v_y * (1.0 / 2.0));
+  o.v[5] = (float)(a_y * (1.0 / 0.37));
+  o.v[6] = (float)(s_r * (1.0 / (2 * kPi)));
+  o.v[7] = (float)(v_r * (1.0 / 8.5e-3));
+  o.v[8] = (float)(a_r * (1.0 / 1.4e-5));
+  o.v[9] = (float)((rudder + kPi / 3) * (1.0 / (kPi / 3 - (-kPi / 3))));
+  o.v[10] = (float)(fuel / (double)p.fuel0);
   return o;
 }
 
@@ -224,7 +344,7 @@ __device__ __forceinline__ void store_obs(float* dst, const Obs& o) {
   for (int k = 0; k < SACENV_OBS_DIM; ++k) dst[k] = o.v[k];
 }
 
-// ---------------------------------------------------------------- reset
+// ---------------------------------------------------------------- episode draw
 
 __device__ __forceinline__ double wave_min16(double v) {
 #pragma unroll
@@ -239,9 +359,10 @@ __device__ __forceinline__ double wave_max16(double v) {
 
 // Grid-sample min/max of one spline interval: the cubic is monotone between
 // its critical points, so the extreme grid samples of interval j are its
-// first/last grid points and the neighbours of each critical point.
-__device__ void interval_extrema(const SacenvBoatParams& p, const ResetLds& l, int c, int j,
-                                 double& mn, double& mx) {
+// first/last grid points and the neighbours of each critical point
+// (tests/test_host_cpu.py::test_grid_extrema_rule_is_exact).
+__device__ void interval_extrema(const SacenvBoatParams& p, const DrawLds& l, int c, int j, double& mn,
+                                 double& mx) {
   mn = INFINITY;
   mx = -INFINITY;
   const int L = p.wind_len;
@@ -292,19 +413,25 @@ __device__ void interval_extrema(const SacenvBoatParams& p, const ResetLds& l, i
   }
 }
 
-// Boat(config) for env `e`, executed by all 64 lanes of the wave (e uniform).
-// Draws (unless explicit) in the reference order: randint (boat_env.py:147),
-// then 8 knot values per random curve (wind.py:78; velocity first in exp 6).
-// Writes the wind coefficients and the RNG state; returns start_y in all
-// lanes. The caller writes the scalar state and the obs row.
-__device__ int32_t reset_env_wave(const SacenvBoatParams& p, const SacenvBoatState& s, ResetLds& l,
-                                  int e, int lane, const int32_t* ex_start_y,
-                                  const double* ex_knots) {
+__device__ __forceinline__ void load_g(const SacenvBoatParams& p, const double* g, DrawLds& l, int lane) {
+  for (int i = lane; i < p.n_knots * p.n_knots; i += kWave) l.g[i] = g[i];
+  __syncthreads();
+}
+
+// One Boat(config) draw for env `e` into `slot`, by all 64 lanes of the wave
+// (e, slot uniform; l.g loaded). Draws (unless explicit) in the reference
+// order: randint (boat_env.py:147), then n knot values per random curve
+// (wind.py:78; velocity first in exp 6). Fits the curves, applies the grid
+// min-max renormalisation (wind.py:87-89) and the table scaling, stores the
+// slot. Returns start_y in all lanes.
+__device__ int32_t draw_episode_wave(const SacenvBoatParams& p, const Arena& A, DrawLds& l, int e,
+                                     int slot, int lane, const int32_t* ex_start_y,
+                                     const double* ex_knots) {
   const int nk = p.n_knots;
   // draws follow the reference even when a recorded wind table overrides the
   // curves; only the spline fit is skipped then
   const int ndraw = n_curves(p.experiment);
-  const int ncurves = p.wind_table != nullptr ? 0 : ndraw;
+  const int ncurves = p.use_wind_table ? 0 : ndraw;
   int32_t start_y;
   if (ex_start_y != nullptr) {
     start_y = *ex_start_y;
@@ -312,8 +439,8 @@ __device__ int32_t reset_env_wave(const SacenvBoatParams& p, const SacenvBoatSta
       if (lane < nk) l.y[c][lane] = ex_knots[c * nk + lane];
   } else {
     MtStream st;
-    st.gkey = s.mt_key + (size_t)e * kMtN;
-    st.pos = s.mt_pos[e];
+    st.gkey = A.mt_key() + (int64_t)e * kMtN;
+    st.pos = A.i32(U_MTPOS)[e];
     st.cur = 0;
     st.loaded = false;
     st.nxt_valid = false;
@@ -352,18 +479,18 @@ __device__ int32_t reset_env_wave(const SacenvBoatParams& p, const SacenvBoatSta
       }
       st.pos += 2 * nk;
     }
-    mt_finish(st, l, s.mt_pos + e, lane);
+    mt_finish(st, l, A.i32(U_MTPOS) + e, lane);
   }
+  if (lane == 0) A.i32(U_STARTY)[(int64_t)slot * A.np + e] = start_y;
   if (ncurves > 0) {
     __syncthreads();
-    const size_t n = (size_t)p.n_envs;
     // second derivatives / 6 of the not-a-knot spline: m = G @ y
     for (int c = 0; c < ncurves; ++c) {
       if (lane < nk) {
         double acc = 0.0;
-        for (int k = 0; k < nk; ++k) acc += p.spline_g[lane * nk + k] * l.y[c][k];
+        for (int k = 0; k < nk; ++k) acc += l.g[lane * nk + k] * l.y[c][k];
         l.m[c][lane] = acc;
-        if (s.knots_raw != nullptr) s.knots_raw[((size_t)c * nk + lane) * n + e] = l.y[c][lane];
+        if (p.out_flags & SACENV_OUT_KNOTS) A.knots_raw()[A.wix(slot, c, lane, e)] = l.y[c][lane];
       }
     }
     __syncthreads();
@@ -391,83 +518,196 @@ __device__ int32_t reset_env_wave(const SacenvBoatParams& p, const SacenvBoatSta
           yv = yv * kPi * 2;
           mv = mv * kPi * 2;
         }
-        const size_t o = ((size_t)cc * nk + lane) * n + e;
-        s.wind_y[o] = yv;
-        s.wind_m[o] = mv;
+        const int64_t o = A.wix(slot, cc, lane, e);
+        A.wind_y()[o] = yv;
+        A.wind_m()[o] = mv;
       }
     }
+    __syncthreads();
   }
   return start_y;
 }
 
-// scalar state + obs of a fresh Boat (boat_env.py:152-198), written by one lane
-__device__ __forceinline__ void write_fresh_state(const SacenvBoatParams& p, const SacenvBoatState& s,
-                                                  int e, int32_t start_y, float* obs_row) {
+// scalar state of a fresh Boat (boat_env.py:152-198) and its observation
+__device__ __forceinline__ Obs fresh_state(const SacenvBoatParams& p, const Arena& A, int e,
+                                           int32_t start_y) {
   const double s_y = p.experiment == 2 ? (double)start_y : 0.0;  // :166-169
-  s.s_x[e] = 0.0;
-  s.s_y[e] = s_y;
-  s.s_r[e] = 0.0;
-  s.v_x[e] = 0.0;
-  s.v_y[e] = 0.0;
-  s.v_r[e] = 0.0;
-  s.rudder[e] = 0.0;
-  s.t[e] = 0.0;
-  s.ep_reward[e] = 0.0;  // :122
-  s.index[e] = 0;
-  s.start_y[e] = start_y;
-  if (obs_row != nullptr)
-    store_obs(obs_row, make_obs(p, 0.0, 0.0, 0.0, s_y, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, (double)p.fuel0));
+  A.f64(U_SX)[e] = 0.0;
+  A.f64(U_SY)[e] = s_y;
+  A.f64(U_SR)[e] = 0.0;
+  A.f64(U_VX)[e] = 0.0;
+  A.f64(U_VY)[e] = 0.0;
+  A.f64(U_VR)[e] = 0.0;
+  A.f64(U_RUD)[e] = 0.0;
+  A.f64(U_T)[e] = 0.0;
+  A.f64(U_EP)[e] = 0.0;  // :122
+  A.i32(U_IDX)[e] = 0;
+  return make_obs(p, 0.0, 0.0, 0.0, s_y, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, (double)p.fuel0);
 }
 
 // ---------------------------------------------------------------- kernels
 
-__global__ void __launch_bounds__(kWave) k_seed(SacenvBoatParams p, SacenvBoatState s,
-                                                const uint32_t* __restrict__ seeds) {
+__global__ void k_spline_g(SacenvBoatParams p, double* __restrict__ g) {
+  // (m/6) = G @ y for the not-a-knot cubic on uniform knots (knot coordinate):
+  // rows 1..n-2: m[j-1] + 4 m[j] + m[j+1] = 6 (y[j-1] - 2 y[j] + y[j+1]);
+  // rows 0, n-1: m[0] - 2 m[1] + m[2] = 0, m[n-3] - 2 m[n-2] + m[n-1] = 0.
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const int n = p.n_knots;
+  double a[kMaxK][kMaxK], r[kMaxK][kMaxK];
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) a[i][j] = r[i][j] = 0.0;
+  a[0][0] = 1.0, a[0][1] = -2.0, a[0][2] = 1.0;
+  a[n - 1][n - 3] = 1.0, a[n - 1][n - 2] = -2.0, a[n - 1][n - 1] = 1.0;
+  for (int j = 1; j < n - 1; ++j) {
+    a[j][j - 1] = 1.0, a[j][j] = 4.0, a[j][j + 1] = 1.0;
+    r[j][j - 1] = 1.0, r[j][j] = -2.0, r[j][j + 1] = 1.0;  // (6 * rhs) / 6
+  }
+  for (int c = 0; c < n; ++c) {  // Gauss-Jordan, partial pivoting
+    int piv = c;
+    for (int i = c + 1; i < n; ++i)
+      if (fabs(a[i][c]) > fabs(a[piv][c])) piv = i;
+    for (int j = 0; j < n; ++j) {
+      double t = a[c][j]; a[c][j] = a[piv][j]; a[piv][j] = t;
+      t = r[c][j]; r[c][j] = r[piv][j]; r[piv][j] = t;
+    }
+    const double d = a[c][c];
+    for (int j = 0; j < n; ++j) a[c][j] /= d, r[c][j] /= d;
+    for (int i = 0; i < n; ++i) {
+      if (i == c) continue;
+      const double f = a[i][c];
+      if (f == 0.0) continue;
+      for (int j = 0; j < n; ++j) a[i][j] -= f * a[c][j], r[i][j] -= f * r[c][j];
+    }
+  }
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) g[i * n + j] = r[i][j];
+}
+
+__global__ void __launch_bounds__(kWave) k_seed(SacenvBoatParams p, Arena A, const uint32_t* __restrict__ seeds) {
   const int e = blockIdx.x * kWave + threadIdx.x;
   if (e >= p.n_envs) return;
   // mt19937_seed (init_genrand), numpy RandomState._legacy_seeding(int)
   uint32_t x = seeds[e];
-  uint32_t* key = s.mt_key + (size_t)e * kMtN;
+  uint32_t* key = A.mt_key() + (int64_t)e * kMtN;
   for (int i = 0; i < kMtN; ++i) {
     key[i] = x;
     x = 1812433253u * (x ^ (x >> 30)) + (uint32_t)(i + 1);
   }
-  s.mt_pos[e] = kMtN;
+  A.i32(U_MTPOS)[e] = kMtN;
+  A.i32(U_CONS)[e] = 0;
+  A.i32(U_FILL)[e] = 0;
 }
 
-__global__ void __launch_bounds__(kWave) k_reset(SacenvBoatParams p, SacenvBoatState s,
-                                                 const int32_t* __restrict__ ids,
-                                                 const int32_t* __restrict__ ex_start_y,
-                                                 const double* __restrict__ ex_knots,
-                                                 float* __restrict__ obs) {
-  __shared__ ResetLds lds;
+// mode 0: first Boat (init). autoreset: slots 0,1,2 <- episodes 1,2,3.
+// mode 1: reset listed envs. non-autoreset: slot 0 <- a new draw;
+//         autoreset: start the next pre-drawn slot, then refill the freed one.
+// mode 2: explicit draws (non-autoreset), slot 0.
+__global__ void __launch_bounds__(kWave) k_draw(SacenvBoatParams p, Arena A, Tail T, int mode,
+                                                const int32_t* __restrict__ ids,
+                                                const int32_t* __restrict__ ex_start_y,
+                                                const double* __restrict__ ex_knots) {
+  __shared__ DrawLds lds;
   const int b = blockIdx.x;
   const int lane = threadIdx.x;
   const int e = ids != nullptr ? ids[b] : b;
   if (e < 0 || e >= p.n_envs) return;  // uniform per block
-  const int32_t* sy = ex_start_y != nullptr ? ex_start_y + b : nullptr;
-  const double* kn = ex_knots != nullptr ? ex_knots + (size_t)b * 2 * p.n_knots : nullptr;
-  const int32_t start_y = reset_env_wave(p, s, lds, e, lane, sy, kn);
-  if (lane == 0)
-    write_fresh_state(p, s, e, start_y, obs != nullptr ? obs + (size_t)e * SACENV_OBS_DIM : nullptr);
+  load_g(p, T.g, lds, lane);
+  int32_t start_y;
+  int slot = 0;
+  if (mode == 2) {
+    start_y = draw_episode_wave(p, A, lds, e, 0, lane, ex_start_y + b,
+                                ex_knots != nullptr ? ex_knots + (int64_t)b * 2 * p.n_knots : nullptr);
+  } else if (!p.autoreset) {
+    start_y = draw_episode_wave(p, A, lds, e, 0, lane, nullptr, nullptr);
+  } else if (mode == 0) {
+    start_y = draw_episode_wave(p, A, lds, e, 0, lane, nullptr, nullptr);
+    for (int s = 1; s < kSlots; ++s) draw_episode_wave(p, A, lds, e, s, lane, nullptr, nullptr);
+    if (lane == 0) {
+      A.i32(U_CONS)[e] = 0;
+      A.i32(U_FILL)[e] = kSlots;
+    }
+  } else {
+    const int c = A.i32(U_CONS)[e] + 1;
+    slot = c % kSlots;
+    start_y = A.i32(U_STARTY)[(int64_t)slot * A.np + e];
+    if (lane == 0) A.i32(U_CONS)[e] = c;
+    const int f = A.i32(U_FILL)[e];
+    draw_episode_wave(p, A, lds, e, f % kSlots, lane, nullptr, nullptr);
+    if (lane == 0) A.i32(U_FILL)[e] = f + 1;
+  }
+  if (lane == 0) {
+    const Obs o = fresh_state(p, A, e, start_y);
+    store_obs(A.obs() + (int64_t)e * SACENV_OBS_DIM, o);
+  }
 }
 
-__global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, SacenvBoatState s,
-                                                const float* __restrict__ action,
-                                                SacenvBoatStepOut out) {
-  __shared__ ResetLds lds;
+// Helper work outside a step launch: refill the slots freed by the last step
+// launch (before a host-driven reset consumes more slots), then clear the list.
+__global__ void __launch_bounds__(kWave) k_drain(SacenvBoatParams p, Arena A, Tail T) {
+  __shared__ DrawLds lds;
   const int lane = threadIdx.x;
+  const int k = A.helper_epoch()[0];
+  const int prev = (k + 2) % 3;
+  const int cnt = A.refill_count()[prev];
+  if ((int)blockIdx.x >= cnt) return;
+  load_g(p, T.g, lds, lane);
+  const int32_t* list = A.i32(U_LIST) + (int64_t)prev * A.np;
+  for (int i = blockIdx.x; i < cnt; i += gridDim.x) {
+    const int e = list[i];
+    const int f = A.i32(U_FILL)[e];
+    draw_episode_wave(p, A, lds, e, f % kSlots, lane, nullptr, nullptr);
+    if (lane == 0) A.i32(U_FILL)[e] = f + 1;
+  }
+}
+
+__global__ void k_drain_done(Arena A) {
+  const int k = A.helper_epoch()[0];
+  A.refill_count()[(k + 2) % 3] = 0;
+}
+
+__global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, Arena A, Tail T,
+                                                const float* __restrict__ action) {
+  __shared__ DrawLds lds;
+  __shared__ __attribute__((aligned(16))) float obs_stage[kWave * SACENV_OBS_DIM];
+  const int lane = threadIdx.x;
+  const int nb_owner = (int)(A.np / kWave);
+
+  if ((int)blockIdx.x >= nb_owner) {
+    // ---------------- helper: refill slots freed by the previous launch
+    const int h = blockIdx.x - nb_owner;
+    const int k = A.helper_epoch()[h];
+    if (h == 0 && lane == 0) A.refill_count()[(k + 1) % 3] = 0;  // list of launch k+1
+    const int prev = (k + 2) % 3;                                   // list of launch k-1
+    const int cnt = A.refill_count()[prev];
+    if (h < cnt) {
+      load_g(p, T.g, lds, lane);
+      const int32_t* list = A.i32(U_LIST) + (int64_t)prev * A.np;
+      for (int i = h; i < cnt; i += p.n_helpers) {
+        const int e = list[i];
+        const int f = A.i32(U_FILL)[e];
+        draw_episode_wave(p, A, lds, e, f % kSlots, lane, nullptr, nullptr);
+        if (lane == 0) A.i32(U_FILL)[e] = f + 1;
+      }
+    }
+    if (lane == 0) A.helper_epoch()[h] = k + 1;
+    return;
+  }
+
+  // ---------------- owner: one env per lane
   const int e = blockIdx.x * kWave + lane;
   const bool active = e < p.n_envs;
+  const int kepoch = A.owner_epoch()[blockIdx.x];
+  Obs o;
   bool ended = false;
   if (active) {
-    double s_x = s.s_x[e], s_y = s.s_y[e], s_r = s.s_r[e];
-    double v_x = s.v_x[e], v_y = s.v_y[e], v_r = s.v_r[e];
-    double rudder = s.rudder[e], t = s.t[e], ep = s.ep_reward[e];
-    int32_t index = s.index[e];
+    double s_x = A.f64(U_SX)[e], s_y = A.f64(U_SY)[e], s_r = A.f64(U_SR)[e];
+    double v_x = A.f64(U_VX)[e], v_y = A.f64(U_VY)[e], v_r = A.f64(U_VR)[e];
+    double rudder = A.f64(U_RUD)[e], t = A.f64(U_T)[e], ep = A.f64(U_EP)[e];
+    int32_t index = A.i32(U_IDX)[e];
+    const int cons = p.autoreset ? A.i32(U_CONS)[e] : 0;
     const float act = action[e];
     double wv, wa;
-    wind_at(p, s, e, index, wv, wa);
+    wind_at(p, A, T.table, cons % kSlots, e, index, wv, wa);
 
     // BoatEnv.step :69-73
     t = t + p.dt;
@@ -475,18 +715,17 @@ __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, SacenvBoatSt
     if (p.test_mode == 0) rudder = rudder + (double)act / 10;
     const bool first = index == 0;  // integrator counter == 0 (control_blocks.py:21-22)
     const double wsign = (double)((wv > 0.0) - (wv < 0.0));
-    const double cwa = cos(wa), swa = sin(wa);
+    double swa, cwa;
+    sincos(wa, &swa, &cwa);
 
     // eom_longitudinal :213-239
     const double F_R = v_x * v_x * p.c_r_front * 0.5 * p.rho * p.boat_area_front;
-    const double v_x_w = v_x * (1.0 - p.wake_friction);
-    const double nD = p.n_rpm * p.propeller_diameter;
-    const double J = p.n_rpm != 0.0 ? v_x_w / nD : 0.0;  // :222-224
-    const double D = p.propeller_diameter;
-    const double F_T = sin(J) * (p.n_rpm * p.n_rpm) * p.rho * (D * D * D * D) * (1.0 - p.thrust_deduction);
-    const double F_C = v_y * (p.boat_m + p.boat_m_y) * v_r;
+    const double v_x_w = v_x * p.one_minus_wf;
+    const double J = p.n_rpm != 0.0 ? v_x_w / p.n_times_d : 0.0;  // :222-224
+    const double F_T = sin(J) * p.n_squared * p.rho * p.d_pow4 * p.one_minus_td;
+    const double F_C = v_y * p.m_plus_my * v_r;
     const double F_W = (wv * wv * wsign * p.c_r_front * 0.5 * p.rho * p.boat_area_front) * cwa;
-    const double a_x = (-F_R + F_T + F_C + F_W) / (p.boat_m + p.boat_m_x);
+    const double a_x = (-F_R + F_T + F_C + F_W) / p.m_plus_mx;
     v_x = first ? 3.0 : a_x * p.dt + v_x;
 
     // eom_transverse :241-265 (new v_x)
@@ -494,9 +733,9 @@ __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, SacenvBoatSt
     const double F_R2 = v_y * v_y * p.c_r_side * 0.5 * p.rho * p.boat_area_side * vys;
     const double sin_rud = sin(rudder);
     const double F_RU = sin_rud * (v_x * v_x * p.c_r_front * 0.5 * p.rho * p.rudder_area);
-    const double F_C2 = v_x * (p.boat_m + p.boat_m_x) * v_r;
+    const double F_C2 = v_x * p.m_plus_mx * v_r;
     const double F_W2 = (wv * wv * wsign * p.c_r_side * 0.5 * p.rho * p.boat_area_side) * swa;
-    const double a_y = (-F_R2 + F_RU + F_C2 + F_W2) / (p.boat_m + p.boat_m_y);
+    const double a_y = (-F_R2 + F_RU + F_C2 + F_W2) / p.m_plus_my;
     v_y = first ? 0.0 : a_y * p.dt + v_y;
 
     // eom_yawning :267-281
@@ -504,7 +743,7 @@ __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, SacenvBoatSt
     const double vxs = (double)((v_x > 0.0) - (v_x < 0.0));
     const double M_hull = v_r * v_r * p.c_r_side * 0.5 * p.rho * p.boat_area_side * p.boat_l * 5.0 * vrs;
     const double M_rud = v_x * v_x * p.c_r_side * 0.5 * p.rho * p.rudder_area * sin_rud * (p.boat_b / 2) * vxs;
-    const double a_r = (-M_hull + M_rud) / (p.boat_I + p.boat_Iz);
+    const double a_r = (-M_hull + M_rud) / p.i_plus_iz;
     v_r = first ? 0.0 : a_r * p.dt + v_r;
 
     // get_kinematics :283-306
@@ -518,9 +757,9 @@ __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, SacenvBoatSt
     s_y = (cd * v) * p.dt + s_y;
     index = index + 1;
 
-    const Obs o = make_obs(p, s_x, v_x, a_x, s_y, v_y, a_y, s_r, v_r, a_r, rudder, (double)fuel);
+    o = make_obs(p, s_x, v_x, a_x, s_y, v_y, a_y, s_r, v_r, a_r, rudder, (double)fuel);
 
-    // exponential_reward (reward_functions.py:42-57)
+    // exponential_reward (reward_functions.py:42-57), f_x = 0
     const double ay = fabs(s_y);
     const double f_y = (ay / p.track_width) / (1.0 + exp(p.reward_k * (ay - p.reward_center)));
     double reward = 0.0 - f_y;
@@ -544,61 +783,77 @@ __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, SacenvBoatSt
     if (fabs(s_r) > kPi / 2) reward = reward - 1.0;
     ep = ep + reward;
 
-    if (term != SACENV_TERM_NONE) s.counters[(size_t)(term - 1) * p.n_envs + e] += 1u;
+    if (term != SACENV_TERM_NONE) A.at<uint32_t>(U_CNT)[(int64_t)(term - 1) * A.np + e] += 1u;
     if (term == SACENV_TERM_NONE && p.max_episode_steps > 0 && index >= p.max_episode_steps)
       term = SACENV_TERM_TRUNCATED;
     ended = term != SACENV_TERM_NONE;
 
-    out.reward[e] = (float)reward;
-    out.done[e] = ended ? 1 : 0;
-    out.term[e] = term;
-    if (out.reward64 != nullptr) out.reward64[e] = reward;
-    if (out.accel != nullptr) {
-      out.accel[e] = a_x;
-      out.accel[(size_t)p.n_envs + e] = a_y;
-      out.accel[2 * (size_t)p.n_envs + e] = a_r;
+    A.reward()[e] = (float)reward;
+    A.done()[e] = ended ? 1 : 0;
+    A.term()[e] = term;
+    if (p.out_flags & SACENV_OUT_REWARD64) A.reward64()[e] = reward;
+    if (p.out_flags & SACENV_OUT_ACCEL) {
+      A.accel()[e] = a_x;
+      A.accel()[A.np + e] = a_y;
+      A.accel()[2 * A.np + e] = a_r;
     }
-    if (ended && out.final_ep_reward != nullptr) out.final_ep_reward[e] = ep;
+    if (ended) A.final_ep()[e] = ep;
     if (ended && p.autoreset) {
-      if (out.final_obs != nullptr) store_obs(out.final_obs + (size_t)e * SACENV_OBS_DIM, o);
+      // next episode from its pre-drawn slot (main.py:72 reset, boat_env.py:121)
+      store_obs(A.final_obs() + (int64_t)e * SACENV_OBS_DIM, o);
+      const int c = cons + 1;
+      const int32_t sy = A.i32(U_STARTY)[(int64_t)(c % kSlots) * A.np + e];
+      A.i32(U_CONS)[e] = c;
+      o = fresh_state(p, A, e, sy);
     } else {
-      store_obs(out.obs + (size_t)e * SACENV_OBS_DIM, o);
-      s.s_x[e] = s_x;
-      s.s_y[e] = s_y;
-      s.s_r[e] = s_r;
-      s.v_x[e] = v_x;
-      s.v_y[e] = v_y;
-      s.v_r[e] = v_r;
-      s.rudder[e] = rudder;
-      s.t[e] = t;
-      s.ep_reward[e] = ep;
-      s.index[e] = index;
+      A.f64(U_SX)[e] = s_x;
+      A.f64(U_SY)[e] = s_y;
+      A.f64(U_SR)[e] = s_r;
+      A.f64(U_VX)[e] = v_x;
+      A.f64(U_VY)[e] = v_y;
+      A.f64(U_VR)[e] = v_r;
+      A.f64(U_RUD)[e] = rudder;
+      A.f64(U_T)[e] = t;
+      A.f64(U_EP)[e] = ep;
+      A.i32(U_IDX)[e] = index;
     }
   }
-  if (!p.autoreset) return;
-  // auto-reset: the whole wave resets each ended env in turn
-  unsigned long long pending = __ballot(ended);
-  while (pending) {
-    const int owner = __ffsll((long long)pending) - 1;
-    pending &= pending - 1;
-    const int er = blockIdx.x * kWave + owner;
-    const int32_t start_y = reset_env_wave(p, s, lds, er, lane, nullptr, nullptr);
-    if (lane == owner) write_fresh_state(p, s, er, start_y, out.obs + (size_t)er * SACENV_OBS_DIM);
-    __syncthreads();
+  // obs rows through LDS: 64 rows x 44 B = 2816 B stored as 176 float4
+#pragma unroll
+  for (int k = 0; k < SACENV_OBS_DIM; ++k) obs_stage[lane * SACENV_OBS_DIM + k] = active ? o.v[k] : 0.0f;
+  __syncthreads();
+  {
+    const float4* src = reinterpret_cast<const float4*>(obs_stage);
+    float4* dst = reinterpret_cast<float4*>(A.obs() + (int64_t)blockIdx.x * kWave * SACENV_OBS_DIM);
+    for (int i = lane; i < kWave * SACENV_OBS_DIM / 4; i += kWave) dst[i] = src[i];
   }
+  if (p.autoreset) {
+    // refill list of this launch (wave-aggregated append)
+    const unsigned long long m = __ballot(ended);
+    if (m) {
+      int base = 0;
+      if (lane == 0) base = atomicAdd(A.refill_count() + kepoch % 3, __popcll(m));
+      base = __shfl(base, 0);
+      if (ended) {
+        const int rank = __popcll(m & ((1ull << lane) - 1ull));
+        A.i32(U_LIST)[(int64_t)(kepoch % 3) * A.np + base + rank] = e;
+      }
+    }
+  }
+  if (lane == 0) A.owner_epoch()[blockIdx.x] = kepoch + 1;
 }
 
-__global__ void __launch_bounds__(256) k_wind_eval(SacenvBoatParams p, SacenvBoatState s,
+__global__ void __launch_bounds__(256) k_wind_eval(SacenvBoatParams p, Arena A, Tail T,
                                                    const int32_t* __restrict__ env_ids,
                                                    const int32_t* __restrict__ idx, int n,
-                                                   double* __restrict__ out_v,
-                                                   double* __restrict__ out_a) {
+                                                   double* __restrict__ out_v, double* __restrict__ out_a) {
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= n) return;
   const int e = env_ids[q];
   if (e < 0 || e >= p.n_envs) return;
+  const int slot = p.autoreset ? A.i32(U_CONS)[e] % kSlots : 0;
   double wv, wa;
-  wind_at(p, s, e, idx[q], wv, wa);
+  wind_at(p, A, T.table, slot, e, idx[q], wv, wa);
   out_v[q] = wv;
   out_a[q] = wa;
 }
@@ -609,22 +864,22 @@ int check_params(const SacenvBoatParams* p) {
   if (p == nullptr) return SACENV_E_NULL;
   if (p->experiment < 1 || p->experiment > 6) return SACENV_E_EXPERIMENT;
   if (p->n_envs <= 0 || p->wind_len <= 0) return SACENV_E_SIZE;
-  if (n_curves(p->experiment) > 0 && p->wind_table == nullptr) {
-    if (p->n_knots < 4 || p->n_knots > kMaxK) return SACENV_E_KNOTS;
-    if (p->wind_len < 2) return SACENV_E_SIZE;
-    if (p->spline_g == nullptr) return SACENV_E_NULL;
+  if (p->n_knots < 4 || p->n_knots > kMaxK) {
+    if (n_curves(p->experiment) > 0) return SACENV_E_KNOTS;
   }
+  if (p->n_knots < 2 || p->n_knots > kMaxK) return SACENV_E_KNOTS;
+  if (n_curves(p->experiment) > 0 && !p->use_wind_table && p->wind_len < 2) return SACENV_E_SIZE;
   if (p->start_y_half < 1) return SACENV_E_RANGE;
+  if (p->autoreset && (p->n_helpers < 1 || p->n_helpers > 4096)) return SACENV_E_SIZE;
   return SACENV_OK;
 }
 
-int check_state(const SacenvBoatParams* p, const SacenvBoatState* s) {
-  if (s == nullptr) return SACENV_E_NULL;
-  if (!s->s_x || !s->s_y || !s->s_r || !s->v_x || !s->v_y || !s->v_r || !s->rudder || !s->t ||
-      !s->ep_reward || !s->index || !s->start_y || !s->mt_key || !s->mt_pos || !s->counters)
-    return SACENV_E_NULL;
-  if (n_curves(p->experiment) > 0 && (!s->wind_y || !s->wind_m)) return SACENV_E_NULL;
-  return SACENV_OK;
+Tail make_tail(const SacenvBoatParams& p, void* arena) {
+  SacenvBoatLayout L;
+  compute_layout(p.n_envs, p.n_knots, p.n_helpers, p.wind_len, p.use_wind_table, &L);
+  char* b = static_cast<char*>(arena);
+  return Tail{reinterpret_cast<const double*>(b + L.spline_g),
+              reinterpret_cast<const double*>(b + L.wind_table)};
 }
 
 int launch_status() {
@@ -645,75 +900,98 @@ const char* sacenv_error_string(int code) {
     case SACENV_OK: return "ok";
     case SACENV_E_NULL: return "required pointer is NULL";
     case SACENV_E_EXPERIMENT: return "Well someone tried to use an experiment that doesnt exist!";
-    case SACENV_E_KNOTS: return "Please select at least 4 fixed_points in your config (max 16).";
+    case SACENV_E_KNOTS:
+      return "Please select at least 4 fixed_points in your config. The interpolation doesn't work "
+             "otherwise! (max 16)";
     case SACENV_E_SIZE: return "size out of range";
-    case SACENV_E_RANGE: return "start-y range empty: int(0.8*track_width) must be >= 1";
+    case SACENV_E_RANGE: return "low >= high: int(0.8*track_width) must be >= 1";
+    case SACENV_E_MODE: return "call not valid in this autoreset mode";
     default: return code > 0 ? hipGetErrorString((hipError_t)code) : "unknown sacenv error";
   }
 }
 
-int sacenv_boat_seed(const SacenvBoatParams* p, const SacenvBoatState* s, const uint32_t* seeds,
-                     void* stream) {
+int sacenv_boat_layout(const SacenvBoatParams* p, SacenvBoatLayout* out) {
+  const int rc = check_params(p);
+  if (rc) return rc;
+  if (out == nullptr) return SACENV_E_NULL;
+  compute_layout(p->n_envs, p->n_knots, p->n_helpers, p->wind_len, p->use_wind_table, out);
+  return SACENV_OK;
+}
+
+int sacenv_boat_init(const SacenvBoatParams* p, void* arena, const uint32_t* seeds, void* stream) {
   int rc = check_params(p);
   if (rc) return rc;
-  if ((rc = check_state(p, s))) return rc;
-  if (seeds == nullptr) return SACENV_E_NULL;
-  hipLaunchKernelGGL(k_seed, dim3(blocks_for(p->n_envs, kWave)), dim3(kWave), 0, (hipStream_t)stream,
-                     *p, *s, seeds);
+  if (arena == nullptr || seeds == nullptr) return SACENV_E_NULL;
+  const hipStream_t s = (hipStream_t)stream;
+  const Arena A = make_arena(*p, arena);
+  const Tail T = make_tail(*p, arena);
+  hipLaunchKernelGGL(k_spline_g, dim3(1), dim3(1), 0, s, *p, const_cast<double*>(T.g));
+  if ((rc = launch_status())) return rc;
+  hipLaunchKernelGGL(k_seed, dim3(blocks_for(p->n_envs, kWave)), dim3(kWave), 0, s, *p, A, seeds);
+  if ((rc = launch_status())) return rc;
+  hipLaunchKernelGGL(k_draw, dim3(p->n_envs), dim3(kWave), 0, s, *p, A, T, 0, (const int32_t*)nullptr,
+                     (const int32_t*)nullptr, (const double*)nullptr);
   return launch_status();
 }
 
-int sacenv_boat_reset(const SacenvBoatParams* p, const SacenvBoatState* s, const int32_t* ids,
-                      int32_t n_ids, float* obs, void* stream) {
+int sacenv_boat_reset(const SacenvBoatParams* p, void* arena, const int32_t* ids, int32_t n_ids,
+                      void* stream) {
   int rc = check_params(p);
   if (rc) return rc;
-  if ((rc = check_state(p, s))) return rc;
+  if (arena == nullptr) return SACENV_E_NULL;
   const int nb = ids != nullptr ? n_ids : p->n_envs;
   if (nb < 0) return SACENV_E_SIZE;
   if (nb == 0) return SACENV_OK;
-  hipLaunchKernelGGL(k_reset, dim3(nb), dim3(kWave), 0, (hipStream_t)stream, *p, *s, ids,
-                     (const int32_t*)nullptr, (const double*)nullptr, obs);
+  const hipStream_t s = (hipStream_t)stream;
+  const Arena A = make_arena(*p, arena);
+  const Tail T = make_tail(*p, arena);
+  if (p->autoreset) {
+    // slots freed by the last step are refilled first: per-env draw order
+    hipLaunchKernelGGL(k_drain, dim3(p->n_helpers), dim3(kWave), 0, s, *p, A, T);
+    if ((rc = launch_status())) return rc;
+    hipLaunchKernelGGL(k_drain_done, dim3(1), dim3(1), 0, s, A);
+    if ((rc = launch_status())) return rc;
+  }
+  hipLaunchKernelGGL(k_draw, dim3(nb), dim3(kWave), 0, s, *p, A, T, 1, ids, (const int32_t*)nullptr,
+                     (const double*)nullptr);
   return launch_status();
 }
 
-int sacenv_boat_reset_explicit(const SacenvBoatParams* p, const SacenvBoatState* s,
-                               const int32_t* ids, int32_t n_ids, const int32_t* start_y,
-                               const double* knots, float* obs, void* stream) {
+int sacenv_boat_reset_explicit(const SacenvBoatParams* p, void* arena, const int32_t* ids, int32_t n_ids,
+                               const int32_t* start_y, const double* knots, void* stream) {
   int rc = check_params(p);
   if (rc) return rc;
-  if ((rc = check_state(p, s))) return rc;
-  if (ids == nullptr || start_y == nullptr) return SACENV_E_NULL;
-  if (n_curves(p->experiment) > 0 && p->wind_table == nullptr && knots == nullptr) return SACENV_E_NULL;
+  if (p->autoreset) return SACENV_E_MODE;
+  if (arena == nullptr || ids == nullptr || start_y == nullptr) return SACENV_E_NULL;
+  if (n_curves(p->experiment) > 0 && !p->use_wind_table && knots == nullptr) return SACENV_E_NULL;
   if (n_ids < 0) return SACENV_E_SIZE;
   if (n_ids == 0) return SACENV_OK;
-  hipLaunchKernelGGL(k_reset, dim3(n_ids), dim3(kWave), 0, (hipStream_t)stream, *p, *s, ids, start_y,
-                     knots, obs);
+  hipLaunchKernelGGL(k_draw, dim3(n_ids), dim3(kWave), 0, (hipStream_t)stream, *p, make_arena(*p, arena),
+                     make_tail(*p, arena), 2, ids, start_y, knots);
   return launch_status();
 }
 
-int sacenv_boat_step(const SacenvBoatParams* p, const SacenvBoatState* s, const float* action,
-                     const SacenvBoatStepOut* out, void* stream) {
+int sacenv_boat_step(const SacenvBoatParams* p, void* arena, const float* action, void* stream) {
   int rc = check_params(p);
   if (rc) return rc;
-  if ((rc = check_state(p, s))) return rc;
-  if (action == nullptr || out == nullptr || !out->obs || !out->reward || !out->done || !out->term)
-    return SACENV_E_NULL;
-  hipLaunchKernelGGL(k_step, dim3(blocks_for(p->n_envs, kWave)), dim3(kWave), 0, (hipStream_t)stream,
-                     *p, *s, action, *out);
+  if (arena == nullptr || action == nullptr) return SACENV_E_NULL;
+  const int nb = (int)(pad64(p->n_envs) / kWave) + (p->autoreset ? p->n_helpers : 0);
+  hipLaunchKernelGGL(k_step, dim3(nb), dim3(kWave), 0, (hipStream_t)stream, *p, make_arena(*p, arena),
+                     make_tail(*p, arena), action);
   return launch_status();
 }
 
-int sacenv_boat_wind_eval(const SacenvBoatParams* p, const SacenvBoatState* s, const int32_t* env_ids,
+int sacenv_boat_wind_eval(const SacenvBoatParams* p, const void* arena, const int32_t* env_ids,
                           const int32_t* idx, int32_t n, double* out_velocity, double* out_angle,
                           void* stream) {
   int rc = check_params(p);
   if (rc) return rc;
-  if ((rc = check_state(p, s))) return rc;
-  if (!env_ids || !idx || !out_velocity || !out_angle) return SACENV_E_NULL;
+  if (!arena || !env_ids || !idx || !out_velocity || !out_angle) return SACENV_E_NULL;
   if (n < 0) return SACENV_E_SIZE;
   if (n == 0) return SACENV_OK;
-  hipLaunchKernelGGL(k_wind_eval, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, *p, *s,
-                     env_ids, idx, n, out_velocity, out_angle);
+  void* a = const_cast<void*>(arena);
+  hipLaunchKernelGGL(k_wind_eval, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, *p,
+                     make_arena(*p, a), make_tail(*p, a), env_ids, idx, n, out_velocity, out_angle);
   return launch_status();
 }
 

@@ -11,11 +11,13 @@ import os
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # .../sac-agent_amd
 LIB_PATH = os.environ.get("SACENV_LIB", os.path.join(PKG_ROOT, "build", "libsacenv.so"))
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 OBS_DIM = 11
 MT_N = 624
 MAX_KNOTS = 16
 N_COUNTERS = 5
+SLOTS = 3
+RECORD_BYTES = 50
 
 TERM_NONE, TERM_REACHED_GOAL, TERM_OUT_OF_BOUNDS, TERM_OUT_OF_FUEL, \
     TERM_RUDDER_BROKEN, TERM_TIMEOUT, TERM_TRUNCATED = range(7)
@@ -23,43 +25,46 @@ TERM_NONE, TERM_REACHED_GOAL, TERM_OUT_OF_BOUNDS, TERM_OUT_OF_FUEL, \
 TERM_NAMES = ("", "reached_goal", "out_of_bounds", "out_of_fuel", "rudder_broken",
               "timeout", "truncated")
 
+OUT_ACCEL, OUT_REWARD64, OUT_KNOTS = 1, 2, 4
+
 _d = C.c_double
 _i32 = C.c_int32
-_pd = C.c_void_p
+_i64 = C.c_int64
+_p = C.c_void_p
 
 
 class BoatParams(C.Structure):
     _fields_ = [
         ("n_envs", _i32), ("experiment", _i32), ("test_mode", _i32), ("wind_len", _i32),
         ("n_knots", _i32), ("fuel0", _i32), ("start_y_half", _i32),
-        ("max_episode_steps", _i32), ("autoreset", _i32), ("reserved0", _i32),
+        ("max_episode_steps", _i32), ("autoreset", _i32), ("n_helpers", _i32),
+        ("out_flags", _i32), ("use_wind_table", _i32),
         ("dt", _d), ("t_max", _d), ("goal_line", _d), ("oob_limit", _d), ("track_width", _d),
-        ("boat_m", _d), ("boat_m_x", _d), ("boat_m_y", _d), ("boat_I", _d), ("boat_Iz", _d),
-        ("propeller_diameter", _d), ("wake_friction", _d), ("c_r_front", _d), ("c_r_side", _d),
-        ("thrust_deduction", _d), ("rho", _d),
-        ("boat_area_front", _d), ("boat_area_side", _d), ("boat_l", _d), ("boat_b", _d),
-        ("rudder_area", _d),
-        ("n_rpm", _d), ("max_velocity", _d), ("wind_dir_rad", _d), ("reward_k", _d),
-        ("reward_center", _d), ("knot_step", _d),
-        ("obs_lo", _d * OBS_DIM), ("obs_hi", _d * OBS_DIM),
-        ("spline_g", _pd), ("wind_table", _pd),
+        ("c_r_front", _d), ("c_r_side", _d), ("rho", _d), ("boat_area_front", _d),
+        ("boat_area_side", _d), ("boat_l", _d), ("boat_b", _d), ("rudder_area", _d),
+        ("m_plus_mx", _d), ("m_plus_my", _d), ("i_plus_iz", _d),
+        ("one_minus_wf", _d), ("one_minus_td", _d),
+        ("n_rpm", _d), ("n_times_d", _d), ("n_squared", _d), ("d_pow4", _d),
+        ("max_velocity", _d), ("wind_dir_rad", _d), ("reward_k", _d), ("reward_center", _d),
+        ("knot_step", _d),
     ]
 
 
-class BoatState(C.Structure):
-    _fields_ = [(n, _pd) for n in (
-        "s_x", "s_y", "s_r", "v_x", "v_y", "v_r", "rudder", "t", "ep_reward",
-        "index", "start_y", "wind_y", "wind_m", "knots_raw", "mt_key", "mt_pos", "counters")]
+LAYOUT_FIELDS = (
+    "total_bytes", "n_pad", "s_x", "s_y", "s_r", "v_x", "v_y", "v_r", "rudder", "t",
+    "ep_reward", "index", "cons", "fill", "mt_pos", "start_y", "counters", "refill_list",
+    "wind_y", "wind_m", "knots_raw", "mt_key", "record", "obs", "reward", "done", "term",
+    "final_obs", "final_ep_reward", "accel", "reward64", "refill_count", "owner_epoch",
+    "helper_epoch", "spline_g", "wind_table")
 
 
-class BoatStepOut(C.Structure):
-    _fields_ = [(n, _pd) for n in (
-        "obs", "reward", "done", "term", "final_obs", "final_ep_reward", "accel", "reward64")]
+class BoatLayout(C.Structure):
+    _fields_ = [(n, _i64) for n in LAYOUT_FIELDS]
 
 
-EXPORTS = ("sacenv_abi_version", "sacenv_error_string", "sacenv_boat_seed",
-           "sacenv_boat_reset", "sacenv_boat_reset_explicit", "sacenv_boat_step",
-           "sacenv_boat_wind_eval")
+EXPORTS = ("sacenv_abi_version", "sacenv_error_string", "sacenv_boat_layout",
+           "sacenv_boat_init", "sacenv_boat_reset", "sacenv_boat_reset_explicit",
+           "sacenv_boat_step", "sacenv_boat_wind_eval")
 
 _LIB = None
 
@@ -79,21 +84,20 @@ def load(path: str | None = None):
             f"libsacenv.so not found at {p}: build it with `python __graft_entry__.py build` "
             "(hipcc --offload-arch=gfx950). The env has no CPU fallback.")
     lib = C.CDLL(p)
-    P, S, O = C.POINTER(BoatParams), C.POINTER(BoatState), C.POINTER(BoatStepOut)
-    lib.sacenv_abi_version.restype = C.c_int
-    lib.sacenv_abi_version.argtypes = []
-    lib.sacenv_error_string.restype = C.c_char_p
-    lib.sacenv_error_string.argtypes = [C.c_int]
-    lib.sacenv_boat_seed.restype = C.c_int
-    lib.sacenv_boat_seed.argtypes = [P, S, _pd, _pd]
-    lib.sacenv_boat_reset.restype = C.c_int
-    lib.sacenv_boat_reset.argtypes = [P, S, _pd, _i32, _pd, _pd]
-    lib.sacenv_boat_reset_explicit.restype = C.c_int
-    lib.sacenv_boat_reset_explicit.argtypes = [P, S, _pd, _i32, _pd, _pd, _pd, _pd]
-    lib.sacenv_boat_step.restype = C.c_int
-    lib.sacenv_boat_step.argtypes = [P, S, _pd, O, _pd]
-    lib.sacenv_boat_wind_eval.restype = C.c_int
-    lib.sacenv_boat_wind_eval.argtypes = [P, S, _pd, _pd, _i32, _pd, _pd, _pd]
+    P = C.POINTER(BoatParams)
+    sig = {
+        "sacenv_abi_version": (C.c_int, []),
+        "sacenv_error_string": (C.c_char_p, [C.c_int]),
+        "sacenv_boat_layout": (C.c_int, [P, C.POINTER(BoatLayout)]),
+        "sacenv_boat_init": (C.c_int, [P, _p, _p, _p]),
+        "sacenv_boat_reset": (C.c_int, [P, _p, _p, _i32, _p]),
+        "sacenv_boat_reset_explicit": (C.c_int, [P, _p, _p, _i32, _p, _p, _p]),
+        "sacenv_boat_step": (C.c_int, [P, _p, _p, _p]),
+        "sacenv_boat_wind_eval": (C.c_int, [P, _p, _p, _p, _i32, _p, _p, _p]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype, f.argtypes = res, args
     v = lib.sacenv_abi_version()
     if v != ABI_VERSION:
         raise SacenvError(f"libsacenv ABI {v} != expected {ABI_VERSION}")
@@ -105,8 +109,12 @@ def load(path: str | None = None):
 def check(rc: int) -> None:
     if rc != 0:
         msg = load().sacenv_error_string(rc).decode()
-        if rc == -2:
-            raise ValueError(msg)
-        if rc in (-3, -5):
+        if rc in (-2, -3, -5):
             raise ValueError(msg)
         raise SacenvError(f"sacenv call failed ({rc}): {msg}")
+
+
+def layout(params: BoatParams) -> BoatLayout:
+    out = BoatLayout()
+    check(load().sacenv_boat_layout(C.byref(params), C.byref(out)))
+    return out

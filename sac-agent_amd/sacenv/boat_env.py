@@ -98,8 +98,9 @@ class BoatEnv:
         self.reward = 0
         self._global_rng = rng == "global"
         seed = 0 if self._global_rng else int(rng)
+        # the arena's own init draw is replaced by _new_boat() below
         self._vec = VecBoatEnv(self._cfg, 1, seed=seed, device=device, autoreset=False,
-                               _skip_init_reset=True)
+                               record_accel=True, record_reward64=True)
         self._episode = 0
         self._hs = None
         self.info = {"termination": "", "reached_goal": 0, "out_of_bounds": 0,

@@ -128,7 +128,8 @@ def spline_g(n: int) -> np.ndarray:
 
 
 def make_params(cfg: BoatConfig, n_envs: int, *, max_episode_steps: int = 0,
-                autoreset: bool = True) -> _lib.BoatParams:
+                autoreset: bool = True, n_helpers: int = 256, out_flags: int = 0,
+                use_wind_table: bool = False) -> _lib.BoatParams:
     cfg.validate()
     p = _lib.BoatParams()
     p.n_envs = int(n_envs)
@@ -140,27 +141,33 @@ def make_params(cfg: BoatConfig, n_envs: int, *, max_episode_steps: int = 0,
     p.start_y_half = int(cfg.track_width * 0.8)     # boat_env.py:147-150
     p.max_episode_steps = int(max_episode_steps)
     p.autoreset = 1 if autoreset else 0
+    p.n_helpers = int(n_helpers)
+    p.out_flags = int(out_flags)
+    p.use_wind_table = 1 if use_wind_table else 0
     p.dt = float(cfg.dt)
     p.t_max = float(cfg.t_max)
     p.goal_line = float(cfg.goal_line)
     p.oob_limit = float(cfg.track_width + cfg.boat_out_of_bounds_offset)  # :200-201
     p.track_width = float(cfg.track_width)
-    for f in ("boat_m", "boat_m_x", "boat_m_y", "boat_I", "boat_Iz", "propeller_diameter",
-              "wake_friction", "c_r_front", "c_r_side", "thrust_deduction", "rho",
-              "boat_area_front", "boat_area_side", "boat_l", "boat_b", "rudder_area"):
+    for f in ("c_r_front", "c_r_side", "rho", "boat_area_front", "boat_area_side", "boat_l",
+              "boat_b", "rudder_area"):
         setattr(p, f, float(getattr(cfg, f)))
-    p.n_rpm = 20.0                                   # boat_env.py:178
+    # sums/differences the reference forms from config values (one IEEE op each)
+    p.m_plus_mx = float(cfg.boat_m + cfg.boat_m_x)              # boat_env.py:239
+    p.m_plus_my = float(cfg.boat_m + cfg.boat_m_y)              # :230, :265
+    p.i_plus_iz = float(cfg.boat_I + cfg.boat_Iz)               # :281
+    p.one_minus_wf = float(1 - cfg.wake_friction)               # :221
+    p.one_minus_td = float(1 - cfg.thrust_deduction)            # :227
+    n, D = 20, cfg.propeller_diameter                           # :178
+    p.n_rpm = float(n)
+    p.n_times_d = float(n * D)                                  # :224
+    p.n_squared = float(np.square(n))                           # :226
+    p.d_pow4 = float(np.power(D, 4))                            # :226
     p.max_velocity = float(cfg.max_velocity)
-    p.wind_dir_rad = float(cfg.direction) * (math.pi / 180)   # wind.py:370
-    p.reward_k = (-0.03) / 3.4                       # (-y_a/y_b), boat_env.py:21-22
-    p.reward_center = float(cfg.track_width) * 0.2   # reward_functions.py:53
+    p.wind_dir_rad = float(cfg.direction) * (math.pi / 180)     # wind.py:370
+    p.reward_k = (-0.03) / 3.4                                  # (-y_a/y_b), boat_env.py:21-22
+    p.reward_center = float(cfg.track_width) * 0.2              # reward_functions.py:53
     p.knot_step = (cfg.fixed_points - 1) / (cfg.wind_len - 1)
-    W, pi = float(cfg.track_width), math.pi
-    lo = (0, 0, 0, -W, 0, 0, 0, 0, 0, -pi / 3, 0)    # boat_env.py:310-321
-    hi = (cfg.goal_line, 5, 0.025, W, 2, 0.37, 2 * pi, 8.5e-3, 1.4e-5, pi / 3, cfg.fuel)
-    for k in range(_lib.OBS_DIM):
-        p.obs_lo[k] = float(lo[k])
-        p.obs_hi[k] = float(hi[k])
     return p
 
 

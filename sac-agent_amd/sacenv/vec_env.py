@@ -6,9 +6,10 @@ stream: env ``e`` seeded with ``s`` behaves exactly like
 ``np.random.seed(s); env = BoatEnv(cfg)`` in the reference — the constructor
 builds one Boat (boat_env.py:15) and every ``reset`` another (:121).
 
-All compute runs in libsacenv.so (gfx950 HIP); tensors here are device
-memory plumbing. ``step`` enqueues one kernel on the current torch stream and
-never synchronises.
+All compute runs in libsacenv.so (gfx950 HIP). The env's whole state lives in
+one device arena (a uint8 tensor) whose fields are exposed here as tensor
+views; ``step`` enqueues one kernel on the current torch stream and never
+synchronises.
 """
 from __future__ import annotations
 
@@ -18,14 +19,10 @@ import numpy as np
 import torch
 
 from . import _lib
-from .config import BoatConfig, make_params, observation_bounds, spline_g
+from .config import BoatConfig, make_params, observation_bounds
 from .spaces import Box
 
-RECORD_BYTES = 50  # packed per-env record: obs f32x11 | reward f32 | done u8 | term u8
-
-
-def _ptr(t: torch.Tensor | None) -> int | None:
-    return None if t is None else t.data_ptr()
+RECORD_BYTES = _lib.RECORD_BYTES  # packed per-env record: obs f32x11 | reward f32 | done u8 | term u8
 
 
 class VecBoatEnv:
@@ -38,17 +35,21 @@ class VecBoatEnv:
     seed : base seed; env ``e`` gets ``seeds[e] = (seed + env_id_offset + e) mod 2**32``
         unless ``seeds`` is given explicitly.
     max_episode_steps : >0 truncates episodes (term code 6) after that many steps.
-    autoreset : reset ended envs inside ``step`` (gym vector-env semantics:
-        the returned obs row is the new episode's first obs, the terminal obs
-        is in ``info['final_obs']``).
+    autoreset : start the next episode inside ``step`` for envs that end
+        (gym vector-env semantics: the returned obs row is the new episode's
+        first obs, the terminal obs is ``info['final_obs']``). Episodes are
+        pre-drawn two ahead per env, from the env's own RNG stream in the
+        reference's order, so draws match the reference exactly.
     env_id_offset : global id of this rank's first env (multi-GPU sharding).
-    record_knots : also keep the raw drawn knot values (parity tests).
+    record_knots / record_accel / record_reward64 : extra outputs (tests, shim).
+    wind_table : [2, int(t_max/dt)] recorded wind (velocity, angle) for all envs.
+    n_helpers : autoreset helper waves per step launch (slot refills).
     """
 
     def __init__(self, config=None, num_envs: int = 1, *, seed: int = 0, seeds=None,
                  device=None, max_episode_steps: int = 0, autoreset: bool = True,
-                 env_id_offset: int = 0, record_knots: bool = False, wind_table=None,
-                 _skip_init_reset: bool = False):
+                 env_id_offset: int = 0, record_knots: bool = False, record_accel: bool = False,
+                 record_reward64: bool = False, wind_table=None, n_helpers: int = 256):
         self.lib = _lib.load()
         self.cfg = BoatConfig.from_any(config)
         self.num_envs = N = int(num_envs)
@@ -58,59 +59,52 @@ class VecBoatEnv:
         if self.device.type != "cuda":
             raise RuntimeError("VecBoatEnv runs on a GPU (HIP); no CPU path")
         self.env_id_offset = int(env_id_offset)
+        self.autoreset = bool(autoreset)
+        flags = ((_lib.OUT_KNOTS if record_knots else 0) | (_lib.OUT_ACCEL if record_accel else 0)
+                 | (_lib.OUT_REWARD64 if record_reward64 else 0))
         self.params = make_params(self.cfg, N, max_episode_steps=max_episode_steps,
-                                  autoreset=autoreset)
-        dev, f64, i32 = self.device, torch.float64, torch.int32
+                                  autoreset=autoreset, n_helpers=n_helpers, out_flags=flags,
+                                  use_wind_table=wind_table is not None)
+        self._pp = C.byref(self.params)
+        self.layout = L = _lib.layout(self.params)
+        self.n_pad = NP = int(L.n_pad)
+        self.arena = torch.zeros(int(L.total_bytes), dtype=torch.uint8, device=self.device)
         nk = int(self.cfg.fixed_points)
 
-        def z(dtype, *shape):
-            return torch.zeros(*shape, dtype=dtype, device=dev)
+        def view(off, dtype, *shape):
+            esz = torch.empty((), dtype=dtype).element_size()
+            cnt = int(np.prod(shape))
+            return self.arena[off: off + cnt * esz].view(dtype).view(*shape)
 
-        # carried state, SoA
-        self.s_x, self.s_y, self.s_r = z(f64, N), z(f64, N), z(f64, N)
-        self.v_x, self.v_y, self.v_r = z(f64, N), z(f64, N), z(f64, N)
-        self.rudder, self.t, self.ep_reward = z(f64, N), z(f64, N), z(f64, N)
-        self.index, self.start_y = z(i32, N), z(i32, N)
-        self.wind_y = z(f64, 2, nk, N)
-        self.wind_m = z(f64, 2, nk, N)
-        self.knots_raw = z(f64, 2, nk, N) if record_knots else None
-        self.mt_key = z(i32, N, _lib.MT_N)
-        self.mt_pos = z(i32, N)
-        self.counters = z(i32, _lib.N_COUNTERS, N)
-        self._spline_g = torch.as_tensor(spline_g(nk), dtype=f64, device=dev).contiguous()
-        self.params.spline_g = self._spline_g.data_ptr()
-        self._wind_table = None
+        f64, i32 = torch.float64, torch.int32
+        # carried state (SoA views, first N entries of each n_pad array)
+        for name in ("s_x", "s_y", "s_r", "v_x", "v_y", "v_r", "rudder", "t", "ep_reward"):
+            setattr(self, name, view(getattr(L, name), f64, NP)[:N])
+        self.index = view(L.index, i32, NP)[:N]
+        self.cons = view(L.cons, i32, NP)[:N]
+        self.mt_pos = view(L.mt_pos, i32, NP)[:N]
+        self.start_y_slots = view(L.start_y, i32, _lib.SLOTS, NP)[:, :N]
+        self.counters = view(L.counters, i32, _lib.N_COUNTERS, NP)[:, :N]
+        self.wind_y = view(L.wind_y, f64, _lib.SLOTS, 2, nk, NP)
+        self.wind_m = view(L.wind_m, f64, _lib.SLOTS, 2, nk, NP)
+        self.knots_raw_slots = view(L.knots_raw, f64, _lib.SLOTS, 2, nk, NP)
+        self.mt_key = view(L.mt_key, i32, NP, _lib.MT_N)[:N]
+        self.spline_g = view(L.spline_g, f64, nk, nk)
+        # outputs: the packed record (the all-gather payload) and extras
+        self.record = self.arena[L.record: L.record + RECORD_BYTES * NP]
+        self.obs = view(L.obs, torch.float32, NP, _lib.OBS_DIM)[:N]
+        self.reward = view(L.reward, torch.float32, NP)[:N]
+        self.done = view(L.done, torch.uint8, NP)[:N]
+        self.term = view(L.term, torch.uint8, NP)[:N]
+        self.final_obs = view(L.final_obs, torch.float32, NP, _lib.OBS_DIM)[:N]
+        self.final_ep_reward = view(L.final_ep_reward, f64, NP)[:N]
+        self.accel = view(L.accel, f64, 3, NP)[:, :N]
+        self.reward64 = view(L.reward64, f64, NP)[:N]
         if wind_table is not None:
-            wt = torch.as_tensor(np.asarray(wind_table, np.float64).reshape(2, -1), device=dev)
+            wt = torch.as_tensor(np.asarray(wind_table, np.float64).reshape(2, -1))
             if wt.shape[1] != self.cfg.wind_len:
                 raise ValueError("wind_table must be [2, int(t_max/dt)]")
-            self._wind_table = wt.contiguous()
-            self.params.wind_table = self._wind_table.data_ptr()
-
-        # outputs: one packed record buffer (the all-gather payload), plus extras
-        self.record = z(torch.uint8, N * RECORD_BYTES)
-        self.obs = self.record[: 44 * N].view(torch.float32).view(N, _lib.OBS_DIM)
-        self.reward = self.record[44 * N: 48 * N].view(torch.float32)
-        self.done = self.record[48 * N: 49 * N]
-        self.term = self.record[49 * N: 50 * N]
-        self.final_obs = z(torch.float32, N, _lib.OBS_DIM)
-        self.final_ep_reward = z(f64, N)
-        self.accel = z(f64, 3, N)
-        self.reward64 = z(f64, N)
-
-        self.state = _lib.BoatState(
-            s_x=_ptr(self.s_x), s_y=_ptr(self.s_y), s_r=_ptr(self.s_r),
-            v_x=_ptr(self.v_x), v_y=_ptr(self.v_y), v_r=_ptr(self.v_r),
-            rudder=_ptr(self.rudder), t=_ptr(self.t), ep_reward=_ptr(self.ep_reward),
-            index=_ptr(self.index), start_y=_ptr(self.start_y),
-            wind_y=_ptr(self.wind_y), wind_m=_ptr(self.wind_m), knots_raw=_ptr(self.knots_raw),
-            mt_key=_ptr(self.mt_key), mt_pos=_ptr(self.mt_pos), counters=_ptr(self.counters))
-        self.out = _lib.BoatStepOut(
-            obs=_ptr(self.obs), reward=_ptr(self.reward), done=_ptr(self.done),
-            term=_ptr(self.term), final_obs=_ptr(self.final_obs),
-            final_ep_reward=_ptr(self.final_ep_reward), accel=_ptr(self.accel),
-            reward64=_ptr(self.reward64))
-        self._pp, self._ps, self._po = C.byref(self.params), C.byref(self.state), C.byref(self.out)
+            view(L.wind_table, f64, 2, self.cfg.wind_len).copy_(wt)
 
         # Gym surface (boat_env.py:37-65)
         self.action_space = Box(low=-1, high=1, dtype=np.float32)
@@ -126,56 +120,63 @@ class VecBoatEnv:
         if np.any(seeds > 0xFFFFFFFF):
             raise ValueError("Seed must be between 0 and 2**32 - 1")
         self.seeds = seeds
-        self.seed(seeds)
-        if not _skip_init_reset:
-            self._reset_all()   # BoatEnv.__init__ builds a Boat (boat_env.py:15)
+        self._seeds_dev = torch.from_numpy(seeds.astype(np.uint32).view(np.int32)).to(self.device)
+        # np.random.seed + BoatEnv.__init__'s Boat (boat_env.py:15)
+        _lib.check(self.lib.sacenv_boat_init(self._pp, self._ptr, self._seeds_dev.data_ptr(),
+                                             self.stream))
 
     # ------------------------------------------------------------------ plumbing
+    @property
+    def _ptr(self) -> int:
+        return self.arena.data_ptr()
+
     @property
     def stream(self) -> int:
         return torch.cuda.current_stream(self.device).cuda_stream
 
-    def seed(self, seeds) -> None:
-        """np.random.seed(seeds[e]) for every env (legacy MT19937 init)."""
-        s = torch.from_numpy(np.asarray(seeds, np.uint64).astype(np.uint32).view(np.int32))
-        self._seeds_dev = s.to(self.device)
-        _lib.check(self.lib.sacenv_boat_seed(self._pp, self._ps, self._seeds_dev.data_ptr(),
-                                             self.stream))
+    @property
+    def start_y(self) -> torch.Tensor:
+        """Boat.s_y_start of each env's current episode."""
+        slot = (self.cons % _lib.SLOTS).long() if self.autoreset else torch.zeros_like(self.cons).long()
+        return self.start_y_slots.gather(0, slot[None, :])[0]
 
-    def _reset_all(self) -> None:
-        _lib.check(self.lib.sacenv_boat_reset(self._pp, self._ps, None, 0,
-                                              self.obs.data_ptr(), self.stream))
+    @property
+    def knots_raw(self) -> torch.Tensor:
+        """Knot values [2, n_knots, N] of each env's current episode (record_knots)."""
+        slot = (self.cons % _lib.SLOTS).long() if self.autoreset else torch.zeros_like(self.cons).long()
+        k = self.knots_raw_slots[:, :, :, : self.num_envs]            # [3, 2, nk, N]
+        idx = slot.view(1, 1, 1, -1).expand(1, k.shape[1], k.shape[2], -1)
+        return k.gather(0, idx)[0]
 
     # ------------------------------------------------------------------ gym API
     def reset(self, env_ids=None) -> torch.Tensor:
         """BoatEnv.reset for all envs, or for ``env_ids`` (boat_env.py:120-126)."""
         if env_ids is None:
-            self._reset_all()
+            _lib.check(self.lib.sacenv_boat_reset(self._pp, self._ptr, None, 0, self.stream))
         else:
             ids = torch.as_tensor(env_ids, dtype=torch.int32, device=self.device).contiguous()
             if ids.numel():
-                _lib.check(self.lib.sacenv_boat_reset(self._pp, self._ps, ids.data_ptr(),
-                                                      ids.numel(), self.obs.data_ptr(),
-                                                      self.stream))
+                _lib.check(self.lib.sacenv_boat_reset(self._pp, self._ptr, ids.data_ptr(),
+                                                      ids.numel(), self.stream))
+                self._keep = ids
         return self.obs
 
     def reset_explicit(self, env_ids, start_y, knots=None) -> torch.Tensor:
-        """Reset with caller-supplied draws (replaying recorded episodes)."""
+        """Reset with caller-supplied draws (replaying recorded episodes; autoreset=False)."""
         ids = torch.as_tensor(env_ids, dtype=torch.int32, device=self.device).contiguous()
         sy = torch.as_tensor(start_y, dtype=torch.int32, device=self.device).contiguous()
         kn = None
         if knots is not None:
             kn = torch.as_tensor(knots, dtype=torch.float64, device=self.device).contiguous()
         _lib.check(self.lib.sacenv_boat_reset_explicit(
-            self._pp, self._ps, ids.data_ptr(), ids.numel(), sy.data_ptr(),
-            None if kn is None else kn.data_ptr(), self.obs.data_ptr(), self.stream))
+            self._pp, self._ptr, ids.data_ptr(), ids.numel(), sy.data_ptr(),
+            None if kn is None else kn.data_ptr(), self.stream))
         self._keep = (ids, sy, kn)  # alive until the stream has consumed them
         return self.obs
 
     def step_async(self, actions: torch.Tensor) -> None:
-        """Enqueue one step; ``actions`` is a contiguous f32 device tensor [N] or [N, 1]."""
-        _lib.check(self.lib.sacenv_boat_step(self._pp, self._ps, actions.data_ptr(),
-                                             self._po, self.stream))
+        """Enqueue one step; ``actions`` is a contiguous f32 device tensor of N values."""
+        _lib.check(self.lib.sacenv_boat_step(self._pp, self._ptr, actions.data_ptr(), self.stream))
 
     def step(self, actions):
         """BoatEnv.step for all envs (boat_env.py:67-115).
@@ -184,7 +185,7 @@ class VecBoatEnv:
         env's output buffers (overwritten by the next step; clone to keep).
         ``info`` holds ``term`` (SACENV_TERM_* codes; 1..5 in the order of the
         reference info-dict keys), ``final_obs`` and ``final_ep_reward``
-        (valid where done) and the cumulative ``counters``.
+        (valid where done) and the cumulative ``counters`` [5, N].
         """
         a = torch.as_tensor(actions, device=self.device)
         if a.dtype != torch.float32:
@@ -197,24 +198,25 @@ class VecBoatEnv:
         return self.obs, self.reward, self.done, info
 
     def wind_eval(self, env_ids, idx):
-        """Wind.get_wind(index) for (env, index) pairs -> (velocity, angle) f64."""
+        """Wind.get_wind(index) of each env's current episode -> (velocity, angle) f64."""
         ids = torch.as_tensor(env_ids, dtype=torch.int32, device=self.device).contiguous()
         ix = torch.as_tensor(idx, dtype=torch.int32, device=self.device).contiguous()
         if ids.shape != ix.shape:
             raise ValueError("env_ids and idx must have the same shape")
         v = torch.empty(ids.shape, dtype=torch.float64, device=self.device)
         a = torch.empty_like(v)
-        _lib.check(self.lib.sacenv_boat_wind_eval(self._pp, self._ps, ids.data_ptr(),
+        _lib.check(self.lib.sacenv_boat_wind_eval(self._pp, self._ptr, ids.data_ptr(),
                                                   ix.data_ptr(), ids.numel(), v.data_ptr(),
                                                   a.data_ptr(), self.stream))
+        self._keep = (ids, ix)
         return v, a
 
     def state_dict(self) -> dict:
         """Host copy of the carried state (parity tests / checkpoints)."""
         torch.cuda.synchronize(self.device)
         d = {k: getattr(self, k).cpu().numpy() for k in
-             ("s_x", "s_y", "s_r", "v_x", "v_y", "v_r", "rudder", "t", "ep_reward",
-              "index", "start_y")}
+             ("s_x", "s_y", "s_r", "v_x", "v_y", "v_r", "rudder", "t", "ep_reward", "index")}
+        d["start_y"] = self.start_y.cpu().numpy()
         d["fuel"] = int(self.cfg.fuel) - d["index"].astype(np.int64)
         d["a_x"], d["a_y"], d["a_r"] = self.accel.cpu().numpy()
         return d

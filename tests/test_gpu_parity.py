@@ -43,7 +43,7 @@ def test_seeded_fixture_explicit_reset(name, gpu, built_lib):
     z = golden(name)
     E, S = z["reward"].shape
     env = VecBoatEnv(_cfg_dict(z), E, seeds=z["seeds"], device=gpu, autoreset=False,
-                     record_knots=True)
+                     record_knots=True, record_accel=True, record_reward64=True)
     obs = env.reset().cpu().numpy()
     np.testing.assert_allclose(obs, z["init_obs"], rtol=0, atol=OBS_TOL)
     np.testing.assert_array_equal(env.start_y.cpu().numpy(), z["init_start_y"])
@@ -80,7 +80,8 @@ def test_seeded_fixture_autoreset(name, gpu, built_lib):
     from sacenv import VecBoatEnv
     z = golden(name)
     E, S = z["reward"].shape
-    env = VecBoatEnv(_cfg_dict(z), E, seeds=z["seeds"], device=gpu, autoreset=True)
+    env = VecBoatEnv(_cfg_dict(z), E, seeds=z["seeds"], device=gpu, autoreset=True,
+                     record_accel=True, n_helpers=4)
     env.reset()
     for k in range(S):
         a = torch.from_numpy(np.ascontiguousarray(z["actions"][:, k])).to(gpu)
@@ -123,13 +124,15 @@ def test_wind_tables_vs_reference(name, gpu, built_lib):
     np.testing.assert_allclose(a, z["ang"], rtol=0, atol=1e-12)
 
 
-def test_rng_draws_bit_exact_across_many_resets(gpu, built_lib):
-    """Knots/start-y of 150 consecutive resets per env == numpy RandomState (crosses
-    many 624-word MT blocks, incl. windows straddling a block end)."""
+@pytest.mark.parametrize("autoreset", [False, True])
+def test_rng_draws_bit_exact_across_many_resets(autoreset, gpu, built_lib):
+    """Knots/start-y of 150 consecutive Boats per env == numpy RandomState (crosses
+    many 624-word MT blocks, incl. windows straddling a block end). In autoreset
+    mode the draws happen two episodes ahead; the sequence is the same."""
     from sacenv import VecBoatEnv
     seeds = np.array([0, 5, 99, 2**32 - 1], np.uint64)
     env = VecBoatEnv({"base_settings": {"experiment": 6}}, len(seeds), seeds=seeds, device=gpu,
-                     record_knots=True)
+                     record_knots=True, autoreset=autoreset, n_helpers=3)
     rs = [np.random.RandomState(int(s)) for s in seeds]
     for r in range(150):
         if r > 0:
@@ -141,9 +144,48 @@ def test_rng_draws_bit_exact_across_many_resets(gpu, built_lib):
             assert sy[e] == g.randint(-640, 640), (r, e)
             assert np.array_equal(kn[0, :, e], g.random_sample(8)), (r, e)
             assert np.array_equal(kn[1, :, e], g.random_sample(8)), (r, e)
-    for e, g in enumerate(rs):   # the device MT state is numpy's state
-        st = g.get_state()
-        assert int(env.mt_pos[e]) == st[2] or (int(env.mt_pos[e]) == 0 and st[2] == 624)
+    if not autoreset:   # the device MT state is numpy's state
+        key = env.mt_key.cpu().numpy().view(np.uint32)
+        for e, g in enumerate(rs):
+            st = g.get_state()
+            pos = int(env.mt_pos[e])
+            if pos == st[2]:
+                assert np.array_equal(key[e], st[1])
+            else:   # block exhausted: numpy twists lazily, the device may have already
+                assert pos == 0 and st[2] == 624
+
+
+def test_spline_g_on_device(gpu, built_lib):
+    from sacenv import VecBoatEnv
+    from sacenv.config import spline_g
+    for nk in (4, 8, 16):
+        env = VecBoatEnv({"base_settings": {"experiment": 6}, "wind": {"fixed_points": nk}}, 2,
+                         device=gpu)
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(env.spline_g.cpu().numpy(), spline_g(nk), rtol=0, atol=1e-15)
+
+
+def test_autoreset_every_step_one_step_episodes(gpu, built_lib):
+    """|action| > 10.5 breaks the rudder on the first step: every env ends in every
+    launch, the worst case for the 3-slot pipeline. Draws must stay exact."""
+    from sacenv import VecBoatEnv
+    E, S = 70, 12
+    seeds = np.arange(E, dtype=np.uint64) * 7 + 3
+    env = VecBoatEnv({"base_settings": {"experiment": 6, "test_mode": 0}}, E, seeds=seeds,
+                     device=gpu, autoreset=True, n_helpers=5, record_knots=True)
+    ora = OracleVecBoat(OracleConfig(experiment=6), seeds)
+    acts = np.full(E, 20.0, np.float32)
+    for k in range(S):
+        o, r, d, info = env.step(torch.from_numpy(acts).to(gpu))
+        ro = ora.step(acts)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(info["term"].cpu().numpy(), ro["term"])
+        assert (ro["term"] == 4).all()
+        np.testing.assert_allclose(o.cpu().numpy(), ro["reset_obs"], rtol=OBS_TOL, atol=OBS_TOL)
+        np.testing.assert_allclose(info["final_obs"].cpu().numpy(), ro["obs"], rtol=OBS_TOL,
+                                   atol=OBS_TOL)
+        np.testing.assert_array_equal(env.start_y.cpu().numpy(), ora.start_y)
+        np.testing.assert_array_equal(env.knots_raw.cpu().numpy().transpose(2, 0, 1), ora.knots)
 
 
 @pytest.mark.parametrize("exp", [1, 2, 3, 4, 5, 6])
@@ -156,7 +198,7 @@ def test_recorded_episode_replay(exp, gpu, built_lib):
     c = {n: cols.index(n) for n in cols}
     table = np.stack([z["wind_velocity"], z["wind_angle"]])
     env = VecBoatEnv({"base_settings": {"experiment": exp, "test_mode": 1}}, 1, device=gpu,
-                     autoreset=False, wind_table=table)
+                     autoreset=False, wind_table=table, record_reward64=True)
     env.reset_explicit([0], [int(tr[0, c["boat_position_y"]])])
     n = len(tr) - 1
     act = torch.zeros(1, dtype=torch.float32, device=gpu)

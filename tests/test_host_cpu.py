@@ -34,7 +34,7 @@ def declared_functions():
 def test_library_exports_header(built_lib):
     from sacenv import _lib
     names = declared_functions()
-    assert len(names) == 7
+    assert len(names) == 8
     assert set(names) == set(_lib.EXPORTS)
     for n in names:
         assert hasattr(built_lib, n), n
@@ -44,43 +44,55 @@ def test_library_exports_header(built_lib):
 
 def test_argument_errors_without_gpu(built_lib):
     """Argument validation runs on the host and never launches."""
-    from sacenv import _lib
     from sacenv.config import BoatConfig, make_params
     p = make_params(BoatConfig(experiment=6), 4)
     p.experiment = 7
-    s = _lib.BoatState()
-    rc = built_lib.sacenv_boat_step(ctypes.byref(p), ctypes.byref(s), None, None, None)
-    assert rc == -2
+    assert built_lib.sacenv_boat_step(ctypes.byref(p), None, None, None) == -2
     p.experiment = 6
-    rc = built_lib.sacenv_boat_step(ctypes.byref(p), ctypes.byref(s), None, None, None)
-    assert rc == -1  # NULL state pointers
+    assert built_lib.sacenv_boat_step(ctypes.byref(p), None, None, None) == -1
+    p.n_knots = 3
+    assert built_lib.sacenv_boat_step(ctypes.byref(p), None, None, None) == -3
+    p.n_knots = 8
+    p.start_y_half = 0
+    assert built_lib.sacenv_boat_step(ctypes.byref(p), None, None, None) == -5
+    p.start_y_half = 640
+    p.autoreset = 1
+    p.n_helpers = 0
+    assert built_lib.sacenv_boat_step(ctypes.byref(p), None, None, None) == -4
+    p.n_helpers = 256
+    p.autoreset = 1
+    assert built_lib.sacenv_boat_reset_explicit(ctypes.byref(p), 1, 1, 1, 1, None, None) == -6
 
 
-def test_struct_layout_matches_c(tmp_path):
+@pytest.mark.parametrize("n", [1, 63, 64, 65536, 100000])
+def test_arena_layout(built_lib, n):
+    """Fields are aligned, disjoint and inside total_bytes; record is contiguous."""
     from sacenv import _lib
-    probe = tmp_path / "probe.c"
-    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "sacenv.h"', 'int main(void){']
-    for cname, cls in (("SacenvBoatParams", _lib.BoatParams), ("SacenvBoatState", _lib.BoatState),
-                       ("SacenvBoatStepOut", _lib.BoatStepOut)):
-        lines.append(f'printf("{cname} sizeof %zu\\n", sizeof({cname}));')
-        for f, _ in cls._fields_:
-            lines.append(f'printf("{cname} {f} %zu\\n", offsetof({cname}, {f}));')
-    lines.append("return 0;}")
-    probe.write_text("\n".join(lines))
-    exe = tmp_path / "probe"
-    subprocess.run(["gcc", "-std=c99", "-I", os.path.join(ROOT, "include"), str(probe), "-o", str(exe)],
-                   check=True)
-    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
-    got = {}
-    for ln in out:
-        if ln:
-            a, b, c = ln.split()
-            got[(a, b)] = int(c)
-    for cname, cls in (("SacenvBoatParams", _lib.BoatParams), ("SacenvBoatState", _lib.BoatState),
-                       ("SacenvBoatStepOut", _lib.BoatStepOut)):
-        assert got[(cname, "sizeof")] == ctypes.sizeof(cls), cname
-        for f, _ in cls._fields_:
-            assert got[(cname, f)] == getattr(cls, f).offset, (cname, f)
+    from sacenv.config import BoatConfig, make_params
+    p = make_params(BoatConfig(experiment=6), n, n_helpers=256, use_wind_table=True)
+    L = _lib.layout(p)
+    np_ = L.n_pad
+    assert np_ % 64 == 0 and n <= np_ < n + 64
+    nk = 8
+    sizes = {"s_x": 8, "s_y": 8, "s_r": 8, "v_x": 8, "v_y": 8, "v_r": 8, "rudder": 8, "t": 8,
+             "ep_reward": 8, "index": 4, "cons": 4, "fill": 4, "mt_pos": 4, "start_y": 12,
+             "counters": 20, "refill_list": 12, "wind_y": 48 * nk, "wind_m": 48 * nk,
+             "knots_raw": 48 * nk, "mt_key": 2496, "obs": 44, "reward": 4, "done": 1, "term": 1,
+             "final_obs": 44, "final_ep_reward": 8, "accel": 24, "reward64": 8}
+    spans = sorted((getattr(L, f), getattr(L, f) + w * np_, f) for f, w in sizes.items())
+    for (a0, a1, f), (b0, b1, g) in zip(spans, spans[1:]):
+        assert a1 <= b0, (f, g)
+    for a0, a1, f in spans:
+        assert a0 % 64 == 0, f
+    assert L.record == L.obs and L.term + np_ == L.record + 50 * np_
+    tail = [("refill_count", 16), ("owner_epoch", 4 * np_ // 64), ("helper_epoch", 4 * 256),
+            ("spline_g", 8 * 256), ("wind_table", 16 * 10000)]
+    end = spans[-1][1]
+    for f, w in tail:
+        off = getattr(L, f)
+        assert off >= end and off % 256 == 0, f
+        end = off + w
+    assert end <= L.total_bytes
 
 
 # ---------------------------------------------------------------- MT19937
