@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--kernel-launches", type=int, default=200)
     ap.add_argument("--test-mode", type=int, default=0, help="1 = rudder frozen (no terminations)")
+    ap.add_argument("--helpers", type=int, default=256, help="helper waves per step launch")
     ap.add_argument("--episode-steps", type=int, default=EPISODE_STEPS,
                     help="truncation length (0 = none)")
     return ap.parse_args()
@@ -130,7 +131,7 @@ def main():
     N = args.envs
     env = VecBoatEnv({"base_settings": {"experiment": args.experiment, "test_mode": args.test_mode}},
                      N, seed=0, device=dev, autoreset=True, max_episode_steps=args.episode_steps,
-                     env_id_offset=rank * N)
+                     env_id_offset=rank * N, n_helpers=args.helpers)
     env.reset()
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)

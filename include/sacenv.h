@@ -35,12 +35,12 @@
 extern "C" {
 #endif
 
-#define SACENV_ABI_VERSION 2
+#define SACENV_ABI_VERSION 3
 #define SACENV_OBS_DIM 11      /* Boat.return_state, boat_env.py:308-323 */
 #define SACENV_MT_N 624        /* MT19937 words per env (numpy legacy RNG) */
 #define SACENV_MAX_KNOTS 16    /* wind.fixed_points upper bound */
 #define SACENV_N_COUNTERS 5    /* info-dict termination counters, boat_env.py:24-32 */
-#define SACENV_SLOTS 3         /* pre-drawn episode slots per env in autoreset mode */
+#define SACENV_SLOTS 4         /* episode slots per env in autoreset mode (active + 3 ahead) */
 #define SACENV_RECORD_BYTES 50 /* packed per-env step record (see layout.record) */
 
 /* termination codes; 1..5 follow the info-dict key order boat_env.py:24-32,
@@ -105,6 +105,7 @@ typedef struct SacenvBoatParams {
   double reward_k;            /* (-y_a / y_b), y_a=0.03, y_b=3.4 (reward_functions.py:53) */
   double reward_center;       /* track_width * 0.2 (reward_functions.py:53) */
   double knot_step;           /* (n_knots-1)/(wind_len-1): grid index -> knot coordinate */
+  double knot_inv;            /* (wind_len-1)/(n_knots-1): knot coordinate -> grid index */
 } SacenvBoatParams;
 
 /* Byte offsets of the arena fields. n_pad = n_envs rounded up to 64; per-env
@@ -113,16 +114,18 @@ typedef struct SacenvBoatLayout {
   int64_t total_bytes;
   int64_t n_pad;
   int64_t s_x, s_y, s_r, v_x, v_y, v_r, rudder, t, ep_reward; /* f64 [n_pad] */
+  int64_t wind_next;          /* f64 [2][n_pad] Wind.get_wind(index) for the NEXT step (v, angle) */
   int64_t index;              /* i32 [n_pad] steps since reset; fuel = fuel0 - index */
-  int64_t cons;               /* i32 [n_pad] episodes started (active slot = cons % 3) */
+  int64_t cons;               /* i32 [n_pad] episodes started (active slot = cons % 4) */
   int64_t fill;               /* i32 [n_pad] episodes drawn (autoreset) */
   int64_t mt_pos;             /* i32 [n_pad] next MT word index, 624 => twist first */
-  int64_t start_y;            /* i32 [3][n_pad] Boat.s_y_start per slot */
+  int64_t start_y;            /* i32 [4][n_pad] Boat.s_y_start per slot */
   int64_t counters;           /* u32 [5][n_pad] cumulative termination counters */
-  int64_t refill_list;        /* i32 [3][n_pad] envs whose slot awaits a refill */
-  int64_t wind_y;             /* f64 [3][2][n_knots][n_pad] folded knot values per slot, curve */
-  int64_t wind_m;             /* f64 [3][2][n_knots][n_pad] folded 2nd derivatives / 6 */
-  int64_t knots_raw;          /* f64 [3][2][n_knots][n_pad] drawn knots (SACENV_OUT_KNOTS) */
+  int64_t refill_list;        /* i32 [3][n_pad] ranked (env*4 + slot) drawn by phase A of launch k
+                                 (ring k % 3), spline-fitted by phase B of launch k+1 */
+  int64_t wind_y;             /* f64 [4][2][n_knots][n_pad] folded knot values per slot, curve */
+  int64_t wind_m;             /* f64 [4][2][n_knots][n_pad] folded 2nd derivatives / 6 */
+  int64_t knots_raw;          /* f64 [4][2][n_knots][n_pad] drawn knots (SACENV_OUT_KNOTS) */
   int64_t mt_key;             /* u32 [n_pad][624] per-env MT19937 state */
   int64_t record;             /* u8 [50 n_pad]: obs f32 [n_pad][11] | reward f32 [n_pad]
                                  | done u8 [n_pad] | term u8 [n_pad]  (the all-gather payload) */
@@ -131,9 +134,11 @@ typedef struct SacenvBoatLayout {
   int64_t final_ep_reward;    /* f64 [n_pad] episode reward of envs that ended */
   int64_t accel;              /* f64 [3][n_pad] a_x, a_y, a_r */
   int64_t reward64;           /* f64 [n_pad] */
-  int64_t refill_count;       /* i32 [4] */
+  int64_t refill_mask;        /* u64 [3][n_pad/64] per owner wave: envs that ended in launch k
+                                 (ring index k % 3), i.e. whose freed slot awaits a refill */
+  int64_t refill_count;       /* i32 [3] (256 B): entries of refill_list per ring index */
   int64_t owner_epoch;        /* i32 [n_pad/64] per owner-block launch counter */
-  int64_t helper_epoch;       /* i32 [n_helpers] per helper-block launch counter */
+  int64_t helper_epoch;       /* i32 [2 n_helpers] per helper-block launch counter (phase A, B) */
   int64_t spline_g;           /* f64 [n_knots][n_knots]: (m/6) = G @ knots (written by init) */
   int64_t wind_table;         /* f64 [2][wind_len] (velocity, angle), if use_wind_table */
 } SacenvBoatLayout;
@@ -149,7 +154,7 @@ int sacenv_boat_layout(const SacenvBoatParams *p, SacenvBoatLayout *out);
  * constants, and build every env's first Boat — BoatEnv.__init__ constructs
  * one (boat_env.py:15; Boat.__init__ :144-201, Wind wind.py:26-99) — drawing
  * in the reference's order (randint :147, then 8 knot values per random
- * curve wind.py:78). In autoreset mode the next two episodes are pre-drawn
+ * curve wind.py:78). In autoreset mode the next three episodes are pre-drawn
  * too (same per-env stream, same order). `seeds` is a DEVICE u32 [n_envs];
  * `obs` (nullable) receives the first observations [n_envs][11] f32. */
 int sacenv_boat_init(const SacenvBoatParams *p, void *arena, const uint32_t *seeds, void *stream);
@@ -172,8 +177,11 @@ int sacenv_boat_reset_explicit(const SacenvBoatParams *p, void *arena, const int
  * [n_envs]. Outputs go to the arena's record (+ optional outputs). With
  * autoreset, an env that ends starts its next (pre-drawn) episode in the same
  * launch: its obs row is the new episode's, the terminal obs is in
- * final_obs; helper waves of the same launch draw replacement episodes for
- * the envs that ended in the previous launch. */
+ * final_obs. Helper waves of the same launch refill freed slots in two
+ * phases: phase A draws (RNG) the replacement episodes of the envs that ended
+ * in launch k-1, phase B fits the wind splines of the episodes phase A drew
+ * in launch k-1. A freed slot is thus ready two launches after it is freed,
+ * and four slots keep an env that ends every step supplied. */
 int sacenv_boat_step(const SacenvBoatParams *p, void *arena, const float *action, void *stream);
 
 /* Wind.get_wind(index) (wind.py:20-24) of each env's CURRENT episode for n

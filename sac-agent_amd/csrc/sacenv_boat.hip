@@ -1,23 +1,26 @@
 // sacenv_boat.hip — gfx950 kernels + C ABI for the vectorised boat env.
 //
-// Work split of one step launch (autoreset mode):
-//   * owner blocks: one wave64 = 64 consecutive envs, one lane per env. Each
-//     lane runs BoatEnv.step (boat_env.py:67-115) on float64 SoA state. An env
-//     that ends (terminated or truncated) starts its next episode at once from
-//     a PRE-DRAWN slot (3 slots/env: active + 2 ahead), so no RNG or spline
-//     work ever sits on the step's critical path. The env id is appended to
-//     the launch's refill list (wave-aggregated atomic).
-//   * helper blocks: one wave per env listed by the PREVIOUS launch draws the
-//     replacement episode (Boat.__init__ draws, boat_env.py:144-201; Wind,
-//     wind.py:26-99) into the freed slot, cooperatively across 64 lanes: the
-//     MT19937 twist, the randint rejection, the 53-bit knot values and the
-//     not-a-knot spline's exact grid min/max via critical points (instead of
-//     the reference's 10 000-sample scan, wind.py:80-89).
-// Owners and helpers of one launch never touch the same bytes: a slot freed
-// in launch k is refilled in launch k+1 and consumed no earlier than k+1
-// (three slots cover an env that ends in every launch). Lists are triple-
-// buffered by a per-block launch counter, so no inter-block hand-off happens
-// inside a launch and graph replay needs no per-launch arguments.
+// One step launch (autoreset mode) runs three kinds of wave64 workgroups:
+//   * owner waves (one lane per env, 64 consecutive envs): BoatEnv.step
+//     (boat_env.py:67-115) on float64 SoA state. An env that ends (terminated
+//     or truncated) starts its next episode at once from a PRE-DRAWN slot
+//     (4 slots/env: the active episode + 3 ahead), so no RNG or spline work
+//     ever sits on the step's critical path. Each owner wave publishes a
+//     64-bit mask of its ended envs (one plain store, no atomics).
+//   * phase-A helpers: for the envs that ended in the PREVIOUS launch, draw
+//     the replacement episode from the env's own numpy-legacy MT19937 stream
+//     (Boat.__init__ boat_env.py:144-201: randint, then the wind knots,
+//     wind.py:69-90) into the freed slot, one wave per env.
+//   * phase-B helpers: for the envs drawn by the previous launch's phase A,
+//     fit the not-a-knot spline, find its exact grid-sample min/max from the
+//     critical points (instead of the reference's 10 000-sample scan,
+//     wind.py:80-89), renormalise and scale the curve (wind.py:86-99).
+// Helpers rank the flagged envs from the masks (DPP scans, no atomics), so
+// the work is balanced exactly. Nothing is handed between workgroups inside a
+// launch: a slot freed in launch k is drawn in k+1, fitted in k+2 and used no
+// earlier than k+3, which four slots guarantee even for an env that ends in
+// every launch. Masks/lists are ring-buffered by per-block launch counters,
+// so graph replay needs no per-launch arguments.
 //
 // Floating-point order follows the reference expression by expression
 // (left-to-right products, no FMA contraction: -ffp-contract=off); the only
@@ -40,22 +43,26 @@ constexpr uint32_t kMtLower = 0x7fffffffu;
 constexpr uint32_t kMtMatrixA = 0x9908b0dfu;
 constexpr int kMaxK = SACENV_MAX_KNOTS;
 constexpr int kSlots = SACENV_SLOTS;
+constexpr int kRing = 3;          // ring depth of masks / lists (written k, read k+1, k+2)
+constexpr int kMaskLds = 1024;    // refill masks staged in LDS (owner waves <= 1024)
 constexpr double kPi = 3.141592653589793;  // np.pi
 
 // ---------------------------------------------------------------- arena
 // Per-env byte widths; a field's offset is (sum of widths before it) * n_pad.
 // n_pad is a multiple of 64, so every array is 64-byte aligned.
 constexpr int U_SX = 0, U_SY = 8, U_SR = 16, U_VX = 24, U_VY = 32, U_VR = 40, U_RUD = 48,
-              U_T = 56, U_EP = 64, U_IDX = 72, U_CONS = 76, U_FILL = 80, U_MTPOS = 84,
-              U_STARTY = 88, U_CNT = 100, U_LIST = 120, U_WIND = 132;
+              U_T = 56, U_EP = 64, U_WNX = 72, U_IDX = 88, U_CONS = 92, U_FILL = 96,
+              U_MTPOS = 100, U_STARTY = 104, U_CNT = 104 + 4 * kSlots,
+              U_LIST = U_CNT + 4 * SACENV_N_COUNTERS, U_WIND = U_LIST + 4 * kRing;
 constexpr int U_MT_BYTES = 4 * kMtN;
+constexpr int64_t kWindUnits = 16LL * kSlots;  // f64 x 2 curves x slots, per knot
 
 __host__ __device__ inline int64_t pad64(int64_t n) { return (n + 63) / 64 * 64; }
 __host__ __device__ inline int64_t align256(int64_t x) { return (x + 255) / 256 * 256; }
 
 __host__ __device__ inline void compute_layout(int n, int nk, int nh, int L, int use_table,
                                                SacenvBoatLayout* o) {
-  const int64_t np = pad64(n);
+  const int64_t np = pad64(n), nw = np / 64;
   o->n_pad = np;
   o->s_x = U_SX * np;
   o->s_y = U_SY * np;
@@ -66,6 +73,7 @@ __host__ __device__ inline void compute_layout(int n, int nk, int nh, int L, int
   o->rudder = U_RUD * np;
   o->t = U_T * np;
   o->ep_reward = U_EP * np;
+  o->wind_next = U_WNX * np;
   o->index = U_IDX * np;
   o->cons = U_CONS * np;
   o->fill = U_FILL * np;
@@ -73,7 +81,7 @@ __host__ __device__ inline void compute_layout(int n, int nk, int nh, int L, int
   o->start_y = U_STARTY * np;
   o->counters = U_CNT * np;
   o->refill_list = U_LIST * np;
-  const int64_t uw = U_WIND, wk = 48LL * nk;
+  const int64_t uw = U_WIND, wk = kWindUnits * nk;
   o->wind_y = uw * np;
   o->wind_m = (uw + wk) * np;
   o->knots_raw = (uw + 2 * wk) * np;
@@ -89,12 +97,14 @@ __host__ __device__ inline void compute_layout(int n, int nk, int nh, int L, int
   o->accel = (ur + 102) * np;
   o->reward64 = (ur + 126) * np;
   int64_t off = align256((ur + 134) * np);
+  o->refill_mask = off;
+  off += align256(8 * kRing * nw);
   o->refill_count = off;
   off += 256;
   o->owner_epoch = off;
-  off += align256(4 * (np / 64));
+  off += align256(4 * nw);
   o->helper_epoch = off;
-  off += align256(4LL * (nh > 0 ? nh : 1));
+  off += align256(4LL * 2 * (nh > 0 ? nh : 1));
   o->spline_g = off;
   off += align256(8LL * kMaxK * kMaxK);
   o->wind_table = off;
@@ -112,13 +122,13 @@ struct Arena {
   __device__ __forceinline__ T* at(int64_t units) const { return reinterpret_cast<T*>(b + units * np); }
   __device__ __forceinline__ double* f64(int u) const { return at<double>(u); }
   __device__ __forceinline__ int32_t* i32(int u) const { return at<int32_t>(u); }
-  __device__ __forceinline__ int64_t uw() const { return U_WIND; }
-  __device__ __forceinline__ int64_t wk() const { return 48LL * nk; }
-  __device__ __forceinline__ double* wind_y() const { return at<double>(uw()); }
-  __device__ __forceinline__ double* wind_m() const { return at<double>(uw() + wk()); }
-  __device__ __forceinline__ double* knots_raw() const { return at<double>(uw() + 2 * wk()); }
-  __device__ __forceinline__ uint32_t* mt_key() const { return at<uint32_t>(uw() + 3 * wk()); }
-  __device__ __forceinline__ int64_t ur() const { return uw() + 3 * wk() + U_MT_BYTES; }
+  __device__ __forceinline__ int nwaves() const { return (int)(np / 64); }
+  __device__ __forceinline__ int64_t wk() const { return kWindUnits * nk; }
+  __device__ __forceinline__ double* wind_y() const { return at<double>(U_WIND); }
+  __device__ __forceinline__ double* wind_m() const { return at<double>(U_WIND + wk()); }
+  __device__ __forceinline__ double* knots_raw() const { return at<double>(U_WIND + 2 * wk()); }
+  __device__ __forceinline__ uint32_t* mt_key() const { return at<uint32_t>(U_WIND + 3 * wk()); }
+  __device__ __forceinline__ int64_t ur() const { return U_WIND + 3 * wk() + U_MT_BYTES; }
   __device__ __forceinline__ float* obs() const { return at<float>(ur()); }
   __device__ __forceinline__ float* reward() const { return at<float>(ur() + 44); }
   __device__ __forceinline__ uint8_t* done() const { return at<uint8_t>(ur() + 48); }
@@ -128,12 +138,22 @@ struct Arena {
   __device__ __forceinline__ double* accel() const { return at<double>(ur() + 102); }
   __device__ __forceinline__ double* reward64() const { return at<double>(ur() + 126); }
   __device__ __forceinline__ char* tail() const { return b + align256((ur() + 134) * np); }
-  __device__ __forceinline__ int32_t* refill_count() const { return reinterpret_cast<int32_t*>(tail()); }
+  // ended-env mask of owner wave w, ring slot r (written by launch k, r = k % 3)
+  __device__ __forceinline__ unsigned long long* refill_mask(int r) const {
+    return reinterpret_cast<unsigned long long*>(tail()) + (int64_t)r * nwaves();
+  }
+  __device__ __forceinline__ int32_t* refill_count() const {
+    return reinterpret_cast<int32_t*>(tail() + align256(8 * kRing * nwaves()));
+  }
+  __device__ __forceinline__ int32_t* refill_list(int r) const {
+    return i32(U_LIST) + (int64_t)r * np;
+  }
   __device__ __forceinline__ int32_t* owner_epoch() const {
-    return reinterpret_cast<int32_t*>(tail() + 256);
+    return reinterpret_cast<int32_t*>(tail() + align256(8 * kRing * nwaves()) + 256);
   }
   __device__ __forceinline__ int32_t* helper_epoch() const {
-    return reinterpret_cast<int32_t*>(tail() + 256 + align256(4 * (np / 64)));
+    return reinterpret_cast<int32_t*>(tail() + align256(8 * kRing * nwaves()) + 256 +
+                                      align256(4 * nwaves()));
   }
   // slot-major wind coefficient of (slot, curve, knot) for env e
   __device__ __forceinline__ int64_t wix(int slot, int c, int k, int e) const {
@@ -150,6 +170,33 @@ struct Tail {  // small tables whose offsets depend on n_helpers / wind_len
   const double* table;
 };
 
+// ---------------------------------------------------------------- LDS of a drawing wave
+
+struct DrawLds {
+  unsigned long long masks[kMaskLds];
+  uint32_t win[kWave];    // MT window (tempered words pos .. pos+63)
+  uint32_t blk[2][kMtN];  // current MT block, next (twisted) block
+  double y[2][kMaxK];     // knot values per curve (unfolded)
+  double m[2][kMaxK];     // second derivatives / 6 per curve (unfolded)
+  double g[kMaxK * kMaxK];
+#ifdef SACENV_STAMPS
+  uint64_t stamp[8];
+#endif
+};
+
+// diagnostic phase clocks (tools/stamps.py; -DSACENV_STAMPS builds only)
+#ifdef SACENV_STAMPS
+#define DRAW_STAMP(l, i)                                                   \
+  do {                                                                     \
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");            \
+    (l).stamp[i] = __builtin_amdgcn_s_memrealtime();                       \
+  } while (0)
+#else
+#define DRAW_STAMP(l, i) \
+  do {                   \
+  } while (0)
+#endif
+
 // ---------------------------------------------------------------- MT19937
 // numpy legacy RandomState (numpy/random/src/mt19937), pinned numpy 1.23.5.
 
@@ -165,13 +212,6 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t c) {
   const uint32_t y = (a & kMtUpper) | (b & kMtLower);
   return c ^ (y >> 1) ^ ((y & 1u) ? kMtMatrixA : 0u);
 }
-
-struct DrawLds {
-  uint32_t blk[2][kMtN];  // current MT block, next (twisted) block
-  double y[2][kMaxK];     // knot values per curve (unfolded)
-  double m[2][kMaxK];     // second derivatives / 6 per curve (unfolded)
-  double g[kMaxK * kMaxK];
-};
 
 // mt19937_gen as four lane-parallel phases: word i depends on old[i],
 // old[i+1] and either old[i+397] (i < 227) or new[i-227].
@@ -313,29 +353,83 @@ __device__ __forceinline__ void wind_at(const SacenvBoatParams& p, const Arena& 
   }
 }
 
+// Wind.get_wind(0) of a slot's episode: at grid index 0 the spline is exactly
+// its first (folded) knot value, so no curve evaluation is needed.
+__device__ __forceinline__ void wind0_of_slot(const SacenvBoatParams& p, const Arena& A,
+                                              const double* table, int slot, int e, double& wv,
+                                              double& wa) {
+  if (p.use_wind_table) {
+    wv = table[0];
+    wa = table[p.wind_len];
+    return;
+  }
+  switch (p.experiment) {
+    case 3:
+      wv = p.max_velocity;
+      wa = p.wind_dir_rad;
+      return;
+    case 4:
+      wv = A.wind_y()[A.wix(slot, 0, 0, e)];
+      wa = p.wind_dir_rad;
+      return;
+    case 5: {
+      wv = p.max_velocity;
+      const double r = A.wind_y()[A.wix(slot, 0, 0, e)] <= 0.5 / 2 ? 0.0 : 1.0;
+      wa = (r * kPi) + kPi / 2;
+      return;
+    }
+    case 6:
+      wv = A.wind_y()[A.wix(slot, 0, 0, e)];
+      wa = A.wind_y()[A.wix(slot, 1, 0, e)];
+      return;
+    default:
+      wv = 0.0;
+      wa = 0.0;
+      return;
+  }
+}
+
+// x / c for a per-launch constant c, from r = RN(1/c): Markstein's correction
+// step returns the correctly rounded quotient, i.e. the same double as IEEE
+// division, in 3 dependent FLOPs instead of the ~10 of a full fp64 divide.
+__device__ __forceinline__ double div_c(double x, double c, double r) {
+  const double q = x * r;
+  const double err = fma(-q, c, x);
+  return fma(err, r, q);
+}
+
 // ---------------------------------------------------------------- observation
-// Boat.return_state / normalize (boat_env.py:308-326): (v - lo) / (hi - lo);
-// the constant spans are the reference's literals, applied as reciprocals
-// (the float32 observation is the output; state itself is untouched).
+// Boat.return_state / normalize (boat_env.py:308-326): (v - lo) / (hi - lo).
+// Config-dependent spans divide exactly (div_c); the reference's literal
+// spans are applied as reciprocals (the float32 observation is the output).
 struct Obs {
   float v[SACENV_OBS_DIM];
 };
 
-__device__ __forceinline__ Obs make_obs(const SacenvBoatParams& p, double s_x, double v_x, double a_x,
-                                        double s_y, double v_y, double a_y, double s_r, double v_r,
-                                        double a_r, double rudder, double fuel) {
+struct ObsConst {  // per-launch reciprocals of the config-dependent spans
+  double goal, two_w, fuel;
+};
+
+__device__ __forceinline__ ObsConst obs_const(const SacenvBoatParams& p) {
+  return ObsConst{1.0 / p.goal_line, 1.0 / (p.track_width + p.track_width), 1.0 / (double)p.fuel0};
+}
+
+__device__ __forceinline__ Obs make_obs(const SacenvBoatParams& p, const ObsConst& oc, double s_x,
+                                        double v_x, double a_x, double s_y, double v_y, double a_y,
+                                        double s_r, double v_r, double a_r, double rudder,
+                                        double fuel) {
   Obs o;
-  o.v[0] = (float)(s_x / p.goal_line);
+  o.v[0] = (float)div_c(s_x, p.goal_line, oc.goal);
   o.v[1] = (float)(v_x * (1.0 / 5.0));
   o.v[2] = (float)(a_x * (1.0 / 0.025));
-  o.v[3] = (float)((s_y + p.track_width) / (p.track_width + p.track_width));
+  o.v[3] = (float)div_c(s_y + p.track_width, p.track_width + p.track_width, oc.two_w);
   o.v[4] = (float)(v_y * (1.0 / 2.0));
   o.v[5] = (float)(a_y * (1.0 / 0.37));
   o.v[6] = (float)(s_r * (1.0 / (2 * kPi)));
   o.v[7] = (float)(v_r * (1.0 / 8.5e-3));
   o.v[8] = (float)(a_r * (1.0 / 1.4e-5));
   o.v[9] = (float)((rudder + kPi / 3) * (1.0 / (kPi / 3 - (-kPi / 3))));
-  o.v[10] = (float)(fuel / (double)p.fuel0);
+  o.v[10] = (float)div_c(fuel, (double)p.fuel0, oc.fuel);
   return o;
 }
 
@@ -344,29 +438,57 @@ __device__ __forceinline__ void store_obs(float* dst, const Obs& o) {
   for (int k = 0; k < SACENV_OBS_DIM; ++k) dst[k] = o.v[k];
 }
 
-// ---------------------------------------------------------------- episode draw
+// ---------------------------------------------------------------- cross-lane helpers
 
-__device__ __forceinline__ double wave_min16(double v) {
-#pragma unroll
-  for (int off = 8; off >= 1; off >>= 1) v = fmin(v, __shfl_xor(v, off));
-  return v;
+// DPP lane permutes (gfx9 dpp_ctrl): register-to-register, no LDS round trip.
+template <int kCtrl>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), kCtrl, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), kCtrl, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
 }
-__device__ __forceinline__ double wave_max16(double v) {
-#pragma unroll
-  for (int off = 8; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off));
-  return v;
+__device__ __forceinline__ double row16_min(double v) {
+  v = fmin(v, dpp_f64<0xB1>(v));      // quad_perm [1,0,3,2]
+  v = fmin(v, dpp_f64<0x4E>(v));      // quad_perm [2,3,0,1]
+  v = fmin(v, dpp_f64<0x141>(v));     // row_half_mirror
+  return fmin(v, dpp_f64<0x140>(v));  // row_mirror
 }
+__device__ __forceinline__ double row16_max(double v) {
+  v = fmax(v, dpp_f64<0xB1>(v));
+  v = fmax(v, dpp_f64<0x4E>(v));
+  v = fmax(v, dpp_f64<0x141>(v));
+  return fmax(v, dpp_f64<0x140>(v));
+}
+__device__ __forceinline__ double readlane_f64(double v, int src) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), src),
+                          __builtin_amdgcn_readlane(__double2loint(v), src));
+}
+// Wave-wide inclusive prefix sum: row shifts, then row_bcast15/31 carry rows.
+__device__ __forceinline__ int wave_incl_scan(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, true);   // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, true);   // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, true);   // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, true);   // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+  return x;
+}
+
+// ---------------------------------------------------------------- spline extrema
 
 // Grid-sample min/max of one spline interval: the cubic is monotone between
 // its critical points, so the extreme grid samples of interval j are its
 // first/last grid points and the neighbours of each critical point
-// (tests/test_host_cpu.py::test_grid_extrema_rule_is_exact).
-__device__ void interval_extrema(const SacenvBoatParams& p, const DrawLds& l, int c, int j, double& mn,
-                                 double& mx) {
+// (tests/test_host_cpu.py::test_grid_extrema_rule_is_exact). The ten
+// candidates are split over S lanes (lane s evaluates candidates s, s+S, ...);
+// critical points need only grid-point accuracy, so approximate rcp/rsq do.
+template <int S>
+__device__ void interval_extrema(const SacenvBoatParams& p, const DrawLds& l, int c, int j, int s,
+                                 double& mn, double& mx) {
   mn = INFINITY;
   mx = -INFINITY;
   const int L = p.wind_len;
-  const double inv = 1.0 / p.knot_step;
+  const double inv = p.knot_inv;
   int lo = (int)ceil((double)j * inv) - 2;
   if (lo < 0) lo = 0;
   while (lo < L && knot_coord(p, lo).j < j) ++lo;
@@ -374,164 +496,385 @@ __device__ void interval_extrema(const SacenvBoatParams& p, const DrawLds& l, in
   if (hi > L - 1) hi = L - 1;
   while (hi >= 0 && knot_coord(p, hi).j > j) --hi;
   if (lo > hi) return;
-  int cand[10];
-  int nc = 0;
-  cand[nc++] = lo;
-  cand[nc++] = hi;
   const double a = l.m[c][j], b = l.m[c][j + 1];
   const double y0 = l.y[c][j], y1 = l.y[c][j + 1];
   const double qa = 3.0 * (b - a), qb = 6.0 * a, qc = y1 - y0 - 2.0 * a - b;
-  double roots[2];
-  int nr = 0;
+  double r0 = -1.0, r1 = -1.0;  // roots of the derivative in [0,1]; -1 = none
   const double scale = fabs(qa) + fabs(qb) + fabs(qc);
   if (fabs(qa) <= 1e-14 * scale) {
-    if (qb != 0.0) roots[nr++] = -qc / qb;
+    if (qb != 0.0) r0 = -qc * __builtin_amdgcn_rcp(qb);
   } else {
     const double disc = qb * qb - 4.0 * qa * qc;
     if (disc >= 0.0) {
-      const double sq = sqrt(disc);
-      const double q = -0.5 * (qb + (qb >= 0.0 ? sq : -sq));
-      roots[nr++] = q / qa;
-      if (q != 0.0) roots[nr++] = qc / q;
+      const double sq = disc > 0.0 ? disc * __builtin_amdgcn_rsq(disc) : 0.0;
+      const double q = -0.5 * (qb + copysign(sq, qb));
+      r0 = q * __builtin_amdgcn_rcp(qa);
+      if (q != 0.0) r1 = qc * __builtin_amdgcn_rcp(q);
     }
   }
-  for (int r = 0; r < nr; ++r) {
-    const double tr = roots[r];
-    if (!(tr > -0.01 && tr < 1.01)) continue;
-    const double ic = ((double)j + tr) * inv;
-    const int i0 = (int)floor(ic);
-    for (int d = -1; d <= 2; ++d) {
-      int i = i0 + d;
+  const bool ok0 = r0 > -0.01 && r0 < 1.01, ok1 = r1 > -0.01 && r1 < 1.01;
+  const int i0 = ok0 ? (int)floor(((double)j + r0) * inv) : lo;
+  const int i1 = ok1 ? (int)floor(((double)j + r1) * inv) : lo;
+#pragma unroll
+  for (int t = 0; t < (10 + S - 1) / S; ++t) {
+    const int q = s + S * t;  // candidate number 0..9
+    int i;
+    if (q == 0) {
+      i = lo;
+    } else if (q == 1) {
+      i = hi;
+    } else {
+      const bool first = q < 6;
+      const int d = (first ? q - 2 : q - 6) - 1;
+      const bool ok = first ? ok0 : ok1;
+      i = (first ? i0 : i1) + d;
       i = i < lo ? lo : (i > hi ? hi : i);
-      cand[nc++] = i;
+      i = ok ? i : lo;
     }
-  }
-  for (int q = 0; q < nc; ++q) {
-    const double v = curve_lds(p, l, c, cand[q]);
-    mn = fmin(mn, v);
-    mx = fmax(mx, v);
+    if (q < 10) {
+      const double v = curve_lds(p, l, c, i);
+      mn = fmin(mn, v);
+      mx = fmax(mx, v);
+    }
   }
 }
+
+// ---------------------------------------------------------------- spline constants
 
 __device__ __forceinline__ void load_g(const SacenvBoatParams& p, const double* g, DrawLds& l, int lane) {
   for (int i = lane; i < p.n_knots * p.n_knots; i += kWave) l.g[i] = g[i];
   __syncthreads();
 }
 
-// One Boat(config) draw for env `e` into `slot`, by all 64 lanes of the wave
-// (e, slot uniform; l.g loaded). Draws (unless explicit) in the reference
-// order: randint (boat_env.py:147), then n knot values per random curve
-// (wind.py:78; velocity first in exp 6). Fits the curves, applies the grid
-// min-max renormalisation (wind.py:87-89) and the table scaling, stores the
-// slot. Returns start_y in all lanes.
-__device__ int32_t draw_episode_wave(const SacenvBoatParams& p, const Arena& A, DrawLds& l, int e,
-                                     int slot, int lane, const int32_t* ex_start_y,
-                                     const double* ex_knots) {
+// G split in two so its global load overlaps other loads: fetch to registers
+// first, publish to LDS once the wave knows it has work.
+struct GRegs {
+  double v[kMaxK * kMaxK / kWave];
+};
+__device__ __forceinline__ GRegs fetch_g(const SacenvBoatParams& p, const double* g, int lane) {
+  GRegs r;
+  const int nn = p.n_knots * p.n_knots;
+#pragma unroll
+  for (int k = 0; k < kMaxK * kMaxK / kWave; ++k) {  // clamped: no branch per load
+    const int i = lane + kWave * k;
+    r.v[k] = g[i < nn ? i : nn - 1];
+  }
+  return r;
+}
+__device__ __forceinline__ void publish_g(const GRegs& r, DrawLds& l, int lane) {
+#pragma unroll
+  for (int k = 0; k < kMaxK * kMaxK / kWave; ++k) l.g[lane + kWave * k] = r.v[k];
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------- episode draw
+
+// The RNG half of Boat(config) for env `e`, by all 64 lanes (e uniform):
+// np.random.randint(-hw, hw) (boat_env.py:147-150), then n knot values per
+// random curve (wind.py:78; velocity first in exp 6) into l.y. Explicit
+// draws (replays) bypass the RNG. Returns start_y in all lanes.
+__device__ int32_t draw_knots_wave(const SacenvBoatParams& p, const Arena& A, DrawLds& l, int e,
+                                   int lane, const int32_t* ex_start_y, const double* ex_knots) {
   const int nk = p.n_knots;
   // draws follow the reference even when a recorded wind table overrides the
   // curves; only the spline fit is skipped then
   const int ndraw = n_curves(p.experiment);
   const int ncurves = p.use_wind_table ? 0 : ndraw;
-  int32_t start_y;
   if (ex_start_y != nullptr) {
-    start_y = *ex_start_y;
     for (int c = 0; c < ncurves; ++c)
       if (lane < nk) l.y[c][lane] = ex_knots[c * nk + lane];
+    return *ex_start_y;
+  }
+  MtStream st;
+  st.gkey = A.mt_key() + (int64_t)e * kMtN;
+  st.pos = A.i32(U_MTPOS)[e];
+  st.cur = 0;
+  st.loaded = false;
+  st.nxt_valid = false;
+  st.advanced = false;
+  // masked rejection on 32-bit words (numpy random_bounded_uint64_fill ->
+  // buffered_bounded_masked_uint32)
+  const uint32_t rng = (uint32_t)(2 * p.start_y_half - 1);
+  uint32_t mask = rng;
+  mask |= mask >> 1;
+  mask |= mask >> 2;
+  mask |= mask >> 4;
+  mask |= mask >> 8;
+  mask |= mask >> 16;
+  uint32_t val = 0;
+  const int need = 2 * nk * ndraw;  // words of the knot values after the randint
+  const uint32_t w0 = mt_fetch(st, l, lane);
+  const unsigned long long acc0 = __ballot(((w0 & mask) <= rng) && lane < kWave - need);
+  if (acc0) {
+    // fast path: one 64-word window holds the randint draw and every knot
+    const int k = __ffsll((long long)acc0) - 1;
+    val = (uint32_t)__builtin_amdgcn_readlane((int)w0, k) & mask;
+    if (ndraw > 0) {  // window through LDS: per-lane gathers without bpermute
+      l.win[lane] = w0;
+      __syncthreads();
+    }
+    for (int c = 0; c < ndraw; ++c) {
+      const int src = k + 1 + c * 2 * nk + ((2 * lane) & 31);
+      const uint32_t wa = l.win[src & (kWave - 1)];
+      const uint32_t wb = l.win[(src + 1) & (kWave - 1)];
+      if (lane < nk) {  // np.random.sample: legacy_double = genrand_res53 on two words
+        const double a = (double)(wa >> 5), b = (double)(wb >> 6);
+        l.y[c][lane] = (a * 67108864.0 + b) / 9007199254740992.0;
+      }
+    }
+    st.pos += k + 1 + need;
   } else {
-    MtStream st;
-    st.gkey = A.mt_key() + (int64_t)e * kMtN;
-    st.pos = A.i32(U_MTPOS)[e];
-    st.cur = 0;
-    st.loaded = false;
-    st.nxt_valid = false;
-    st.advanced = false;
-    // np.random.randint(-hw, hw): masked rejection on 32-bit words
-    // (numpy random_bounded_uint64_fill -> buffered_bounded_masked_uint32).
-    const uint32_t rng = (uint32_t)(2 * p.start_y_half - 1);
-    uint32_t mask = rng;
-    mask |= mask >> 1;
-    mask |= mask >> 2;
-    mask |= mask >> 4;
-    mask |= mask >> 8;
-    mask |= mask >> 16;
-    uint32_t val = 0;
+    // general path: rejection runs past the window, or the knots do
     for (;;) {
       const uint32_t w = mt_fetch(st, l, lane);
       const unsigned long long acc = __ballot((w & mask) <= rng);
       if (acc) {
         const int k = __ffsll((long long)acc) - 1;
-        val = (uint32_t)__shfl((int)w, k) & mask;
+        val = (uint32_t)__builtin_amdgcn_readlane((int)w, k) & mask;
         st.pos += k + 1;
         break;
       }
       st.pos += kWave;
     }
-    start_y = -p.start_y_half + (int32_t)val;
-    // np.random.sample(n): legacy_double = genrand_res53 on two words.
     for (int c = 0; c < ndraw; ++c) {
       const uint32_t w = mt_fetch(st, l, lane);
-      const int src = (2 * lane) & (kWave - 1);
-      const uint32_t wa = (uint32_t)__shfl((int)w, src);
-      const uint32_t wb = (uint32_t)__shfl((int)w, src + 1);
+      l.win[lane] = w;
+      __syncthreads();
+      const uint32_t wa = l.win[(2 * lane) & (kWave - 1)];
+      const uint32_t wb = l.win[(2 * lane + 1) & (kWave - 1)];
       if (lane < nk) {
         const double a = (double)(wa >> 5), b = (double)(wb >> 6);
         l.y[c][lane] = (a * 67108864.0 + b) / 9007199254740992.0;
       }
+      __syncthreads();
       st.pos += 2 * nk;
     }
-    mt_finish(st, l, A.i32(U_MTPOS) + e, lane);
   }
+  mt_finish(st, l, A.i32(U_MTPOS) + e, lane);
+  return -p.start_y_half + (int32_t)val;
+}
+
+// The spline half: from the knot values in l.y (lanes 16c + j hold knot j of
+// curve c), second derivatives m = G @ y, exact grid min/max, the min-max
+// renormalisation (wind.py:87-89) and the table scaling (wind.py:86-99);
+// stores the folded coefficients of `slot`. l.g must be loaded.
+__device__ void fit_store_wave(const SacenvBoatParams& p, const Arena& A, DrawLds& l, int e, int slot,
+                               int lane) {
+  const int nk = p.n_knots;
+  const int ncurves = p.use_wind_table ? 0 : n_curves(p.experiment);
+  if (ncurves == 0) return;
+  __syncthreads();
+  const int c = lane >> 4, j = lane & 15;
+  const bool knot_lane = c < ncurves && j < nk;
+  double yv = 0.0, mv = 0.0;
+  if (knot_lane) {
+    yv = l.y[c][j];
+#pragma unroll
+    for (int k = 0; k < kMaxK; ++k)
+      if (k < nk) mv += l.g[j * nk + k] * l.y[c][k];
+    l.m[c][j] = mv;
+  }
+  __syncthreads();
+  // lanes 32c + u work on curve c: S lanes per interval (4 if <= 8 intervals)
+  double mn = INFINITY, mx = -INFINITY;
+  {
+    const int cc = lane >> 5, u = lane & 31;
+    if (nk - 1 <= 8) {
+      if (cc < ncurves && (u >> 2) < nk - 1) interval_extrema<4>(p, l, cc, u >> 2, u & 3, mn, mx);
+    } else {
+      if (cc < ncurves && u < nk - 1) interval_extrema<1>(p, l, cc, u, 0, mn, mx);
+    }
+  }
+  mn = row16_min(mn);
+  mx = row16_max(mx);
+  // curve c's extremes are the two rows of its half-wave: uniform values
+  const double cmn0 = fmin(readlane_f64(mn, 0), readlane_f64(mn, 16));
+  const double cmx0 = fmax(readlane_f64(mx, 0), readlane_f64(mx, 16));
+  const double cmn1 = fmin(readlane_f64(mn, 32), readlane_f64(mn, 48));
+  const double cmx1 = fmax(readlane_f64(mx, 32), readlane_f64(mx, 48));
+  mn = c == 0 ? cmn0 : cmn1;
+  mx = c == 0 ? cmx0 : cmx1;
+  if (knot_lane) {
+    if (mn < 0.0 || mx > 1.0) {  // wind.py:87-89 min-max renormalisation
+      const double span = mx - mn;
+      yv = (yv - mn) / span;
+      mv = mv / span;
+    }
+    // table scaling of wind.py:86-89: velocity * max_v, angle * pi * 2;
+    // exp 5 keeps the unit curve for the rectifier (wind.py:92-99).
+    if (p.experiment == 4 || (p.experiment == 6 && c == 0)) {
+      yv = yv * p.max_velocity;
+      mv = mv * p.max_velocity;
+    } else if (p.experiment == 6 && c == 1) {
+      yv = yv * kPi * 2;
+      mv = mv * kPi * 2;
+    }
+    const int64_t o = A.wix(slot, c, j, e);
+    A.wind_y()[o] = yv;
+    A.wind_m()[o] = mv;
+  }
+  __syncthreads();
+}
+
+// knot values -> per-curve rows of l.y (lanes 16c + j), used before a fit
+__device__ __forceinline__ void store_draw(const SacenvBoatParams& p, const Arena& A, const DrawLds& l,
+                                           int e, int slot, int32_t start_y, bool raw_to_wind,
+                                           int lane) {
+  const int nk = p.n_knots;
+  const int ncurves = p.use_wind_table ? 0 : n_curves(p.experiment);
   if (lane == 0) A.i32(U_STARTY)[(int64_t)slot * A.np + e] = start_y;
-  if (ncurves > 0) {
-    __syncthreads();
-    // second derivatives / 6 of the not-a-knot spline: m = G @ y
-    for (int c = 0; c < ncurves; ++c) {
-      if (lane < nk) {
-        double acc = 0.0;
-        for (int k = 0; k < nk; ++k) acc += l.g[lane * nk + k] * l.y[c][k];
-        l.m[c][lane] = acc;
-        if (p.out_flags & SACENV_OUT_KNOTS) A.knots_raw()[A.wix(slot, c, lane, e)] = l.y[c][lane];
-      }
-    }
-    __syncthreads();
-    // grid min/max per curve: lanes c*16 + j own interval j of curve c
-    const int c = lane >> 4, j = lane & 15;
-    double mn = INFINITY, mx = -INFINITY;
-    if (c < ncurves && j < nk - 1) interval_extrema(p, l, c, j, mn, mx);
-    mn = wave_min16(mn);
-    mx = wave_max16(mx);
-    for (int cc = 0; cc < ncurves; ++cc) {
-      const double cmn = __shfl(mn, cc * 16), cmx = __shfl(mx, cc * 16);
-      if (lane < nk) {
-        double yv = l.y[cc][lane], mv = l.m[cc][lane];
-        if (cmn < 0.0 || cmx > 1.0) {  // wind.py:87-89 min-max renormalisation
-          const double span = cmx - cmn;
-          yv = (yv - cmn) / span;
-          mv = mv / span;
-        }
-        // table scaling of wind.py:86-89: velocity * max_v, angle * pi * 2;
-        // exp 5 keeps the unit curve for the rectifier (wind.py:92-99).
-        if (p.experiment == 4 || (p.experiment == 6 && cc == 0)) {
-          yv = yv * p.max_velocity;
-          mv = mv * p.max_velocity;
-        } else if (p.experiment == 6 && cc == 1) {
-          yv = yv * kPi * 2;
-          mv = mv * kPi * 2;
-        }
-        const int64_t o = A.wix(slot, cc, lane, e);
-        A.wind_y()[o] = yv;
-        A.wind_m()[o] = mv;
-      }
-    }
-    __syncthreads();
+  const int c = lane >> 4, j = lane & 15;
+  if (c < ncurves && j < nk) {
+    const int64_t o = A.wix(slot, c, j, e);
+    if (p.out_flags & SACENV_OUT_KNOTS) A.knots_raw()[o] = l.y[c][j];
+    if (raw_to_wind) A.wind_y()[o] = l.y[c][j];  // phase A: unfolded, fitted by phase B
   }
+}
+
+// Boat(config) in one go (init / host-driven resets): draw + fit into slot.
+__device__ int32_t draw_episode_wave(const SacenvBoatParams& p, const Arena& A, DrawLds& l, int e,
+                                     int slot, int lane, const int32_t* ex_start_y,
+                                     const double* ex_knots) {
+  const int32_t start_y = draw_knots_wave(p, A, l, e, lane, ex_start_y, ex_knots);
+  __syncthreads();
+  store_draw(p, A, l, e, slot, start_y, false, lane);
+  fit_store_wave(p, A, l, e, slot, lane);
   return start_y;
 }
 
-// scalar state of a fresh Boat (boat_env.py:152-198) and its observation
+// ---------------------------------------------------------------- refill ranking
+
+// Owner wave w flagged its ended envs in one 64-bit mask. Every helper ranks
+// the flagged envs the same way (lane l owns the masks of waves l, l+64, ...;
+// envs ordered by lane, then mask, then bit) with DPP scans, so rank rr maps
+// to one env without atomics or cross-lane shuffles.
+struct Ranking {
+  int incl, cnt, total, R;
+};
+
+__device__ Ranking rank_masks(const Arena& A, DrawLds& l, int r, int lane) {
+  const int nw = A.nwaves();
+  const unsigned long long* masks = A.refill_mask(r);
+  Ranking k;
+  k.R = (nw + kWave - 1) / kWave;  // masks per lane
+  int cnt = 0;
+  // fixed trip count and clamped (branch-free) addresses, so all 16 loads
+  // are in flight at once before the first wait; then staged in LDS
+  unsigned long long mv[kMaskLds / kWave];
+#pragma unroll
+  for (int i = 0; i < kMaskLds / kWave; ++i) {
+    const int w = lane + kWave * i;
+    mv[i] = masks[w < nw ? w : nw - 1];
+  }
+#pragma unroll
+  for (int i = 0; i < kMaskLds / kWave; ++i) {
+    const int w = lane + kWave * i;
+    const unsigned long long m = w < nw ? mv[i] : 0ull;
+    l.masks[w] = m;
+    cnt += __popcll(m);
+  }
+  for (int i = kMaskLds / kWave; i < k.R; ++i) {
+    const int w = lane + kWave * i;
+    cnt += w < nw ? __popcll(masks[w]) : 0;
+  }
+  k.cnt = cnt;
+  k.incl = wave_incl_scan(cnt);
+  k.total = __builtin_amdgcn_readlane(k.incl, kWave - 1);
+  return k;
+}
+
+// env of rank rr (l.masks published by a barrier after rank_masks)
+__device__ int ranked_env(const Arena& A, const DrawLds& l, const Ranking& k, int r, int rr, int lane) {
+  const int nw = A.nwaves();
+  const unsigned long long* masks = A.refill_mask(r);
+  const int L = __ffsll((long long)__ballot(k.incl > rr)) - 1;  // owning lane
+  int rem = rr - __builtin_amdgcn_readlane(k.incl - k.cnt, L);
+  int e = -1;
+  for (int i0 = 0; i0 < k.R && e < 0; i0 += kWave) {  // lane q takes L's mask i0 + q
+    const int w = L + kWave * (i0 + lane);
+    const unsigned long long v =
+        (i0 + lane < k.R && w < nw) ? (k.R <= kMaskLds / kWave ? l.masks[w] : masks[w]) : 0ull;
+    const int pc = __popcll(v);
+    const int ip = wave_incl_scan(pc);
+    const int chunk = __builtin_amdgcn_readlane(ip, kWave - 1);
+    if (rem < chunk) {
+      const int q = __ffsll((long long)__ballot(ip > rem)) - 1;
+      const int within = rem - __builtin_amdgcn_readlane(ip - pc, q);
+      const unsigned long long m =
+          ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), q) << 32) |
+          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, q);
+      // the within-th set bit of m: each lane tests its own bit, one ballot
+      const bool is_bit = ((m >> lane) & 1ull) && __popcll(m & ((1ull << lane) - 1ull)) == within;
+      e = (L + kWave * (i0 + q)) * kWave + (__ffsll((long long)__ballot(is_bit)) - 1);
+    }
+    rem -= chunk;
+  }
+  return e;
+}
+
+// Phase A for the envs flagged in mask ring r: draw each replacement episode
+// into the env's next free slot (raw knots), and record (env, slot) at its
+// rank for phase B. `fit` also fits at once (host-driven drains).
+__device__ int phase_a(const SacenvBoatParams& p, const Arena& A, const Tail& T, DrawLds& l, int r,
+                       int h, int H, bool fit, int lane) {
+  const GRegs g = fetch_g(p, T.g, lane);  // in flight together with the masks
+  const Ranking k = rank_masks(A, l, r, lane);
+  DRAW_STAMP(l, 1);
+  const bool curves = !p.use_wind_table && n_curves(p.experiment) > 0;
+  if (h == 0 && lane == 0) A.refill_count()[r] = (curves && !fit) ? k.total : 0;
+  if (h >= k.total) return 0;
+  publish_g(g, l, lane);  // its barrier also publishes l.masks
+  int done = 0;
+  for (int rr = h; rr < k.total; rr += H) {
+    const int e = ranked_env(A, l, k, r, rr, lane);
+    DRAW_STAMP(l, 2);
+    const int f = A.i32(U_FILL)[e];
+    const int slot = f % kSlots;
+    const int32_t start_y = draw_knots_wave(p, A, l, e, lane, nullptr, nullptr);
+    __syncthreads();
+    DRAW_STAMP(l, 3);
+    store_draw(p, A, l, e, slot, start_y, !fit, lane);
+    if (fit) fit_store_wave(p, A, l, e, slot, lane);
+    if (lane == 0) {
+      A.i32(U_FILL)[e] = f + 1;
+      if (curves && !fit) A.refill_list(r)[rr] = e * kSlots + slot;
+    }
+    __syncthreads();
+    ++done;
+  }
+  return done;
+}
+
+// Phase B for list ring r: fit the raw knots phase A stored.
+__device__ int phase_b(const SacenvBoatParams& p, const Arena& A, const Tail& T, DrawLds& l, int r,
+                       int h, int H, int lane) {
+  const GRegs g = fetch_g(p, T.g, lane);
+  const int cnt = A.refill_count()[r];
+  DRAW_STAMP(l, 1);
+  if (h >= cnt) return 0;
+  publish_g(g, l, lane);
+  const int nk = p.n_knots;
+  const int ncurves = n_curves(p.experiment);
+  int done = 0;
+  for (int rr = h; rr < cnt; rr += H) {
+    const int v = A.refill_list(r)[rr];
+    const int e = v / kSlots, slot = v % kSlots;
+    const int c = lane >> 4, j = lane & 15;
+    if (c < ncurves && j < nk) l.y[c][j] = A.wind_y()[A.wix(slot, c, j, e)];
+    DRAW_STAMP(l, 2);
+    fit_store_wave(p, A, l, e, slot, lane);
+    ++done;
+  }
+  return done;
+}
+
+// scalar state of a fresh Boat (boat_env.py:152-198) and its observation;
+// (wv0, wa0) = Wind.get_wind(0) of the new episode, the first step's wind
 __device__ __forceinline__ Obs fresh_state(const SacenvBoatParams& p, const Arena& A, int e,
-                                           int32_t start_y) {
+                                           int32_t start_y, double wv0, double wa0) {
   const double s_y = p.experiment == 2 ? (double)start_y : 0.0;  // :166-169
+  A.f64(U_WNX)[e] = wv0;
+  A.f64(U_WNX)[A.np + e] = wa0;
   A.f64(U_SX)[e] = 0.0;
   A.f64(U_SY)[e] = s_y;
   A.f64(U_SR)[e] = 0.0;
@@ -542,7 +885,7 @@ __device__ __forceinline__ Obs fresh_state(const SacenvBoatParams& p, const Aren
   A.f64(U_T)[e] = 0.0;
   A.f64(U_EP)[e] = 0.0;  // :122
   A.i32(U_IDX)[e] = 0;
-  return make_obs(p, 0.0, 0.0, 0.0, s_y, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, (double)p.fuel0);
+  return make_obs(p, obs_const(p), 0.0, 0.0, 0.0, s_y, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, (double)p.fuel0);
 }
 
 // ---------------------------------------------------------------- kernels
@@ -598,7 +941,7 @@ __global__ void __launch_bounds__(kWave) k_seed(SacenvBoatParams p, Arena A, con
   A.i32(U_FILL)[e] = 0;
 }
 
-// mode 0: first Boat (init). autoreset: slots 0,1,2 <- episodes 1,2,3.
+// mode 0: first Boat (init). autoreset: slots 0..3 <- episodes 1..4.
 // mode 1: reset listed envs. non-autoreset: slot 0 <- a new draw;
 //         autoreset: start the next pre-drawn slot, then refill the freed one.
 // mode 2: explicit draws (non-autoreset), slot 0.
@@ -636,33 +979,30 @@ __global__ void __launch_bounds__(kWave) k_draw(SacenvBoatParams p, Arena A, Tai
     if (lane == 0) A.i32(U_FILL)[e] = f + 1;
   }
   if (lane == 0) {
-    const Obs o = fresh_state(p, A, e, start_y);
+    double wv0, wa0;
+    wind0_of_slot(p, A, T.table, slot, e, wv0, wa0);
+    const Obs o = fresh_state(p, A, e, start_y, wv0, wa0);
     store_obs(A.obs() + (int64_t)e * SACENV_OBS_DIM, o);
   }
 }
 
-// Helper work outside a step launch: refill the slots freed by the last step
-// launch (before a host-driven reset consumes more slots), then clear the list.
+// Refill work pending after the last step launch (k-1), done before a
+// host-driven reset consumes more slots (per-env draw order): phase B of
+// the list phase A built in launch k-1, and phase A+B of launch k-1's masks.
 __global__ void __launch_bounds__(kWave) k_drain(SacenvBoatParams p, Arena A, Tail T) {
   __shared__ DrawLds lds;
   const int lane = threadIdx.x;
   const int k = A.helper_epoch()[0];
-  const int prev = (k + 2) % 3;
-  const int cnt = A.refill_count()[prev];
-  if ((int)blockIdx.x >= cnt) return;
-  load_g(p, T.g, lds, lane);
-  const int32_t* list = A.i32(U_LIST) + (int64_t)prev * A.np;
-  for (int i = blockIdx.x; i < cnt; i += gridDim.x) {
-    const int e = list[i];
-    const int f = A.i32(U_FILL)[e];
-    draw_episode_wave(p, A, lds, e, f % kSlots, lane, nullptr, nullptr);
-    if (lane == 0) A.i32(U_FILL)[e] = f + 1;
-  }
+  phase_b(p, A, T, lds, (k + 1) % kRing, blockIdx.x, gridDim.x, lane);
+  __syncthreads();
+  phase_a(p, A, T, lds, (k + 2) % kRing, blockIdx.x, gridDim.x, true, lane);
 }
 
 __global__ void k_drain_done(Arena A) {
   const int k = A.helper_epoch()[0];
-  A.refill_count()[(k + 2) % 3] = 0;
+  const int w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w == 0) A.refill_count()[(k + 1) % kRing] = 0;
+  if (w < A.nwaves()) A.refill_mask((k + 2) % kRing)[w] = 0ull;
 }
 
 __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, Arena A, Tail T,
@@ -670,33 +1010,49 @@ __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, Arena A, Tai
   __shared__ DrawLds lds;
   __shared__ __attribute__((aligned(16))) float obs_stage[kWave * SACENV_OBS_DIM];
   const int lane = threadIdx.x;
-  const int nb_owner = (int)(A.np / kWave);
+  const int nh = p.autoreset ? p.n_helpers : 0;
 
-  if ((int)blockIdx.x >= nb_owner) {
-    // ---------------- helper: refill slots freed by the previous launch
-    const int h = blockIdx.x - nb_owner;
-    const int k = A.helper_epoch()[h];
-    if (h == 0 && lane == 0) A.refill_count()[(k + 1) % 3] = 0;  // list of launch k+1
-    const int prev = (k + 2) % 3;                                   // list of launch k-1
-    const int cnt = A.refill_count()[prev];
-    if (h < cnt) {
-      load_g(p, T.g, lds, lane);
-      const int32_t* list = A.i32(U_LIST) + (int64_t)prev * A.np;
-      for (int i = h; i < cnt; i += p.n_helpers) {
-        const int e = list[i];
-        const int f = A.i32(U_FILL)[e];
-        draw_episode_wave(p, A, lds, e, f % kSlots, lane, nullptr, nullptr);
-        if (lane == 0) A.i32(U_FILL)[e] = f + 1;
-      }
+  if ((int)blockIdx.x < 2 * nh) {
+    // ---------------- helpers (first in the grid, so they start first)
+#ifdef SACENV_STAMPS
+    const uint64_t hs_real0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    const int hb = blockIdx.x;
+    const int k = A.helper_epoch()[hb];
+#ifdef SACENV_STAMPS
+    for (int i = 0; i < 8; ++i) lds.stamp[i] = 0;
+    DRAW_STAMP(lds, 0);
+#endif
+    int nd;
+    if (hb < nh)  // phase A on launch k-1's masks (ring (k-1) % 3)
+      nd = phase_a(p, A, T, lds, (k + 2) % kRing, hb, nh, false, lane);
+    else          // phase B on the list phase A built in launch k-1 (ring (k-2) % 3)
+      nd = phase_b(p, A, T, lds, (k + 1) % kRing, hb - nh, nh, lane);
+    if (lane == 0) A.helper_epoch()[hb] = k + 1;
+#ifdef SACENV_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) {
+      double* d = A.reward64() + (int64_t)hb * 12;
+      d[0] = (double)hs_real0;
+      d[1] = (double)__builtin_amdgcn_s_memrealtime();
+      d[2] = (double)nd;
+      d[3] = hb < nh ? 0.0 : 1.0;
+      for (int i = 0; i < 8; ++i) d[4 + i] = (double)lds.stamp[i];
     }
-    if (lane == 0) A.helper_epoch()[h] = k + 1;
+#else
+    (void)nd;
+#endif
     return;
   }
 
   // ---------------- owner: one env per lane
-  const int e = blockIdx.x * kWave + lane;
+  const int ob = blockIdx.x - 2 * nh;
+#ifdef SACENV_STAMPS
+  const uint64_t st_real0 = __builtin_amdgcn_s_memrealtime();
+#endif
+  const int e = ob * kWave + lane;
   const bool active = e < p.n_envs;
-  const int kepoch = A.owner_epoch()[blockIdx.x];
+  const int kepoch = A.owner_epoch()[ob];
   Obs o;
   bool ended = false;
   if (active) {
@@ -706,8 +1062,21 @@ __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, Arena A, Tai
     int32_t index = A.i32(U_IDX)[e];
     const int cons = p.autoreset ? A.i32(U_CONS)[e] : 0;
     const float act = action[e];
-    double wv, wa;
-    wind_at(p, A, T.table, cons % kSlots, e, index, wv, wa);
+    // this step's wind was evaluated one step ahead (no index-dependent load
+    // on the critical path); the next step's is fetched now, used at the end
+    const double wv = A.f64(U_WNX)[e], wa = A.f64(U_WNX)[A.np + e];
+    double nwv, nwa;
+    wind_at(p, A, T.table, cons % kSlots, e, index + 1, nwv, nwa);
+    // autoreset: the next pre-drawn episode's first wind and start y, speculatively
+    double w0v = 0.0, w0a = 0.0;
+    int32_t sy_next = 0;
+    if (p.autoreset) {
+      wind0_of_slot(p, A, T.table, (cons + 1) % kSlots, e, w0v, w0a);
+      if (p.experiment == 2) sy_next = A.i32(U_STARTY)[(int64_t)((cons + 1) % kSlots) * A.np + e];
+    }
+    const double r_mx = 1.0 / p.m_plus_mx, r_my = 1.0 / p.m_plus_my, r_iz = 1.0 / p.i_plus_iz;
+    const double r_nd = 1.0 / p.n_times_d, r_w = 1.0 / p.track_width;
+    const ObsConst oc = obs_const(p);
 
     // BoatEnv.step :69-73
     t = t + p.dt;
@@ -721,11 +1090,11 @@ __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, Arena A, Tai
     // eom_longitudinal :213-239
     const double F_R = v_x * v_x * p.c_r_front * 0.5 * p.rho * p.boat_area_front;
     const double v_x_w = v_x * p.one_minus_wf;
-    const double J = p.n_rpm != 0.0 ? v_x_w / p.n_times_d : 0.0;  // :222-224
+    const double J = p.n_rpm != 0.0 ? div_c(v_x_w, p.n_times_d, r_nd) : 0.0;  // :222-224
     const double F_T = sin(J) * p.n_squared * p.rho * p.d_pow4 * p.one_minus_td;
     const double F_C = v_y * p.m_plus_my * v_r;
     const double F_W = (wv * wv * wsign * p.c_r_front * 0.5 * p.rho * p.boat_area_front) * cwa;
-    const double a_x = (-F_R + F_T + F_C + F_W) / p.m_plus_mx;
+    const double a_x = div_c(-F_R + F_T + F_C + F_W, p.m_plus_mx, r_mx);
     v_x = first ? 3.0 : a_x * p.dt + v_x;
 
     // eom_transverse :241-265 (new v_x)
@@ -735,7 +1104,7 @@ __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, Arena A, Tai
     const double F_RU = sin_rud * (v_x * v_x * p.c_r_front * 0.5 * p.rho * p.rudder_area);
     const double F_C2 = v_x * p.m_plus_mx * v_r;
     const double F_W2 = (wv * wv * wsign * p.c_r_side * 0.5 * p.rho * p.boat_area_side) * swa;
-    const double a_y = (-F_R2 + F_RU + F_C2 + F_W2) / p.m_plus_my;
+    const double a_y = div_c(-F_R2 + F_RU + F_C2 + F_W2, p.m_plus_my, r_my);
     v_y = first ? 0.0 : a_y * p.dt + v_y;
 
     // eom_yawning :267-281
@@ -743,7 +1112,7 @@ __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, Arena A, Tai
     const double vxs = (double)((v_x > 0.0) - (v_x < 0.0));
     const double M_hull = v_r * v_r * p.c_r_side * 0.5 * p.rho * p.boat_area_side * p.boat_l * 5.0 * vrs;
     const double M_rud = v_x * v_x * p.c_r_side * 0.5 * p.rho * p.rudder_area * sin_rud * (p.boat_b / 2) * vxs;
-    const double a_r = (-M_hull + M_rud) / p.i_plus_iz;
+    const double a_r = div_c(-M_hull + M_rud, p.i_plus_iz, r_iz);
     v_r = first ? 0.0 : a_r * p.dt + v_r;
 
     // get_kinematics :283-306
@@ -757,11 +1126,11 @@ __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, Arena A, Tai
     s_y = (cd * v) * p.dt + s_y;
     index = index + 1;
 
-    o = make_obs(p, s_x, v_x, a_x, s_y, v_y, a_y, s_r, v_r, a_r, rudder, (double)fuel);
+    o = make_obs(p, oc, s_x, v_x, a_x, s_y, v_y, a_y, s_r, v_r, a_r, rudder, (double)fuel);
 
     // exponential_reward (reward_functions.py:42-57), f_x = 0
     const double ay = fabs(s_y);
-    const double f_y = (ay / p.track_width) / (1.0 + exp(p.reward_k * (ay - p.reward_center)));
+    const double f_y = div_c(ay, p.track_width, r_w) / (1.0 + exp(p.reward_k * (ay - p.reward_center)));
     double reward = 0.0 - f_y;
 
     // termination chain :84-105
@@ -783,7 +1152,9 @@ __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, Arena A, Tai
     if (fabs(s_r) > kPi / 2) reward = reward - 1.0;
     ep = ep + reward;
 
-    if (term != SACENV_TERM_NONE) A.at<uint32_t>(U_CNT)[(int64_t)(term - 1) * A.np + e] += 1u;
+    if (term != SACENV_TERM_NONE)  // no-return atomic: nothing on the critical path waits
+      __hip_atomic_fetch_add(A.at<uint32_t>(U_CNT) + (int64_t)(term - 1) * A.np + e, 1u,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (term == SACENV_TERM_NONE && p.max_episode_steps > 0 && index >= p.max_episode_steps)
       term = SACENV_TERM_TRUNCATED;
     ended = term != SACENV_TERM_NONE;
@@ -801,11 +1172,11 @@ __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, Arena A, Tai
     if (ended && p.autoreset) {
       // next episode from its pre-drawn slot (main.py:72 reset, boat_env.py:121)
       store_obs(A.final_obs() + (int64_t)e * SACENV_OBS_DIM, o);
-      const int c = cons + 1;
-      const int32_t sy = A.i32(U_STARTY)[(int64_t)(c % kSlots) * A.np + e];
-      A.i32(U_CONS)[e] = c;
-      o = fresh_state(p, A, e, sy);
+      A.i32(U_CONS)[e] = cons + 1;
+      o = fresh_state(p, A, e, sy_next, w0v, w0a);
     } else {
+      A.f64(U_WNX)[e] = nwv;
+      A.f64(U_WNX)[A.np + e] = nwa;
       A.f64(U_SX)[e] = s_x;
       A.f64(U_SY)[e] = s_y;
       A.f64(U_SR)[e] = s_r;
@@ -824,23 +1195,24 @@ __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, Arena A, Tai
   __syncthreads();
   {
     const float4* src = reinterpret_cast<const float4*>(obs_stage);
-    float4* dst = reinterpret_cast<float4*>(A.obs() + (int64_t)blockIdx.x * kWave * SACENV_OBS_DIM);
+    float4* dst = reinterpret_cast<float4*>(A.obs() + (int64_t)ob * kWave * SACENV_OBS_DIM);
     for (int i = lane; i < kWave * SACENV_OBS_DIM / 4; i += kWave) dst[i] = src[i];
   }
   if (p.autoreset) {
-    // refill list of this launch (wave-aggregated append)
+    // this launch's ended envs, for the next launch's helpers (every wave
+    // rewrites its word each launch, so the ring needs no clearing)
     const unsigned long long m = __ballot(ended);
-    if (m) {
-      int base = 0;
-      if (lane == 0) base = atomicAdd(A.refill_count() + kepoch % 3, __popcll(m));
-      base = __shfl(base, 0);
-      if (ended) {
-        const int rank = __popcll(m & ((1ull << lane) - 1ull));
-        A.i32(U_LIST)[(int64_t)(kepoch % 3) * A.np + base + rank] = e;
-      }
-    }
+    if (lane == 0) A.refill_mask(kepoch % kRing)[ob] = m;
   }
-  if (lane == 0) A.owner_epoch()[blockIdx.x] = kepoch + 1;
+  if (lane == 0) A.owner_epoch()[ob] = kepoch + 1;
+#ifdef SACENV_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (lane == 0) {
+    double* d = A.accel() + (int64_t)ob * 2;
+    d[0] = (double)st_real0;
+    d[1] = (double)__builtin_amdgcn_s_memrealtime();
+  }
+#endif
 }
 
 __global__ void __launch_bounds__(256) k_wind_eval(SacenvBoatParams p, Arena A, Tail T,
@@ -864,9 +1236,7 @@ int check_params(const SacenvBoatParams* p) {
   if (p == nullptr) return SACENV_E_NULL;
   if (p->experiment < 1 || p->experiment > 6) return SACENV_E_EXPERIMENT;
   if (p->n_envs <= 0 || p->wind_len <= 0) return SACENV_E_SIZE;
-  if (p->n_knots < 4 || p->n_knots > kMaxK) {
-    if (n_curves(p->experiment) > 0) return SACENV_E_KNOTS;
-  }
+  if (n_curves(p->experiment) > 0 && (p->n_knots < 4 || p->n_knots > kMaxK)) return SACENV_E_KNOTS;
   if (p->n_knots < 2 || p->n_knots > kMaxK) return SACENV_E_KNOTS;
   if (n_curves(p->experiment) > 0 && !p->use_wind_table && p->wind_len < 2) return SACENV_E_SIZE;
   if (p->start_y_half < 1) return SACENV_E_RANGE;
@@ -946,10 +1316,10 @@ int sacenv_boat_reset(const SacenvBoatParams* p, void* arena, const int32_t* ids
   const Arena A = make_arena(*p, arena);
   const Tail T = make_tail(*p, arena);
   if (p->autoreset) {
-    // slots freed by the last step are refilled first: per-env draw order
+    // slots freed by the last step launches are refilled first: per-env draw order
     hipLaunchKernelGGL(k_drain, dim3(p->n_helpers), dim3(kWave), 0, s, *p, A, T);
     if ((rc = launch_status())) return rc;
-    hipLaunchKernelGGL(k_drain_done, dim3(1), dim3(1), 0, s, A);
+    hipLaunchKernelGGL(k_drain_done, dim3(blocks_for((int)(A.np / kWave), 256)), dim3(256), 0, s, A);
     if ((rc = launch_status())) return rc;
   }
   hipLaunchKernelGGL(k_draw, dim3(nb), dim3(kWave), 0, s, *p, A, T, 1, ids, (const int32_t*)nullptr,
@@ -975,7 +1345,7 @@ int sacenv_boat_step(const SacenvBoatParams* p, void* arena, const float* action
   int rc = check_params(p);
   if (rc) return rc;
   if (arena == nullptr || action == nullptr) return SACENV_E_NULL;
-  const int nb = (int)(pad64(p->n_envs) / kWave) + (p->autoreset ? p->n_helpers : 0);
+  const int nb = (int)(pad64(p->n_envs) / kWave) + (p->autoreset ? 2 * p->n_helpers : 0);
   hipLaunchKernelGGL(k_step, dim3(nb), dim3(kWave), 0, (hipStream_t)stream, *p, make_arena(*p, arena),
                      make_tail(*p, arena), action);
   return launch_status();

@@ -11,12 +11,12 @@ import os
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # .../sac-agent_amd
 LIB_PATH = os.environ.get("SACENV_LIB", os.path.join(PKG_ROOT, "build", "libsacenv.so"))
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 OBS_DIM = 11
 MT_N = 624
 MAX_KNOTS = 16
 N_COUNTERS = 5
-SLOTS = 3
+SLOTS = 4
 RECORD_BYTES = 50
 
 TERM_NONE, TERM_REACHED_GOAL, TERM_OUT_OF_BOUNDS, TERM_OUT_OF_FUEL, \
@@ -46,15 +46,16 @@ class BoatParams(C.Structure):
         ("one_minus_wf", _d), ("one_minus_td", _d),
         ("n_rpm", _d), ("n_times_d", _d), ("n_squared", _d), ("d_pow4", _d),
         ("max_velocity", _d), ("wind_dir_rad", _d), ("reward_k", _d), ("reward_center", _d),
-        ("knot_step", _d),
+        ("knot_step", _d), ("knot_inv", _d),
     ]
 
 
 LAYOUT_FIELDS = (
     "total_bytes", "n_pad", "s_x", "s_y", "s_r", "v_x", "v_y", "v_r", "rudder", "t",
-    "ep_reward", "index", "cons", "fill", "mt_pos", "start_y", "counters", "refill_list",
+    "ep_reward", "wind_next", "index", "cons", "fill", "mt_pos", "start_y", "counters",
+    "refill_list",
     "wind_y", "wind_m", "knots_raw", "mt_key", "record", "obs", "reward", "done", "term",
-    "final_obs", "final_ep_reward", "accel", "reward64", "refill_count", "owner_epoch",
+    "final_obs", "final_ep_reward", "accel", "reward64", "refill_mask", "refill_count", "owner_epoch",
     "helper_epoch", "spline_g", "wind_table")
 
 

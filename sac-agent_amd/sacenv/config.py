@@ -168,6 +168,7 @@ def make_params(cfg: BoatConfig, n_envs: int, *, max_episode_steps: int = 0,
     p.reward_k = (-0.03) / 3.4                                  # (-y_a/y_b), boat_env.py:21-22
     p.reward_center = float(cfg.track_width) * 0.2              # reward_functions.py:53
     p.knot_step = (cfg.fixed_points - 1) / (cfg.wind_len - 1)
+    p.knot_inv = (cfg.wind_len - 1) / (cfg.fixed_points - 1)
     return p
 
 

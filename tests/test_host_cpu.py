@@ -75,9 +75,9 @@ def test_arena_layout(built_lib, n):
     assert np_ % 64 == 0 and n <= np_ < n + 64
     nk = 8
     sizes = {"s_x": 8, "s_y": 8, "s_r": 8, "v_x": 8, "v_y": 8, "v_r": 8, "rudder": 8, "t": 8,
-             "ep_reward": 8, "index": 4, "cons": 4, "fill": 4, "mt_pos": 4, "start_y": 12,
-             "counters": 20, "refill_list": 12, "wind_y": 48 * nk, "wind_m": 48 * nk,
-             "knots_raw": 48 * nk, "mt_key": 2496, "obs": 44, "reward": 4, "done": 1, "term": 1,
+             "ep_reward": 8, "wind_next": 16, "index": 4, "cons": 4, "fill": 4, "mt_pos": 4, "start_y": 16,
+             "counters": 20, "refill_list": 12, "wind_y": 64 * nk, "wind_m": 64 * nk,
+             "knots_raw": 64 * nk, "mt_key": 2496, "obs": 44, "reward": 4, "done": 1, "term": 1,
              "final_obs": 44, "final_ep_reward": 8, "accel": 24, "reward64": 8}
     spans = sorted((getattr(L, f), getattr(L, f) + w * np_, f) for f, w in sizes.items())
     for (a0, a1, f), (b0, b1, g) in zip(spans, spans[1:]):
@@ -85,7 +85,8 @@ def test_arena_layout(built_lib, n):
     for a0, a1, f in spans:
         assert a0 % 64 == 0, f
     assert L.record == L.obs and L.term + np_ == L.record + 50 * np_
-    tail = [("refill_count", 16), ("owner_epoch", 4 * np_ // 64), ("helper_epoch", 4 * 256),
+    tail = [("refill_mask", 24 * np_ // 64), ("refill_count", 12), ("owner_epoch", 4 * np_ // 64),
+            ("helper_epoch", 4 * 2 * 256),
             ("spline_g", 8 * 256), ("wind_table", 16 * 10000)]
     end = spans[-1][1]
     for f, w in tail:
