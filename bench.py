@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--kernel-launches", type=int, default=200)
     ap.add_argument("--test-mode", type=int, default=0, help="1 = rudder frozen (no terminations)")
     ap.add_argument("--helpers", type=int, default=256, help="helper waves per step launch")
+    ap.add_argument("--no-autoreset", action="store_true",
+                    help="diagnostic: no in-kernel auto-reset (ended envs keep stepping)")
     ap.add_argument("--episode-steps", type=int, default=EPISODE_STEPS,
                     help="truncation length (0 = none)")
     return ap.parse_args()
@@ -130,7 +132,8 @@ def main():
 
     N = args.envs
     env = VecBoatEnv({"base_settings": {"experiment": args.experiment, "test_mode": args.test_mode}},
-                     N, seed=0, device=dev, autoreset=True, max_episode_steps=args.episode_steps,
+                     N, seed=0, device=dev, autoreset=not args.no_autoreset,
+                     max_episode_steps=args.episode_steps,
                      env_id_offset=rank * N, n_helpers=args.helpers)
     env.reset()
     g = torch.Generator(device=dev)

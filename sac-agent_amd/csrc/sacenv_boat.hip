@@ -165,9 +165,15 @@ __host__ inline Arena make_arena(const SacenvBoatParams& p, void* base) {
   return Arena{static_cast<char*>(base), pad64(p.n_envs), p.n_knots};
 }
 
-struct Tail {  // small tables whose offsets depend on n_helpers / wind_len
+// Launch constants built on the host: the small tables whose offsets depend
+// on n_helpers / wind_len, and the reciprocals of the config divisors (IEEE
+// 1/x on the host is the same double as on the device; computing them here
+// keeps eight uniform fp64 divisions out of every lane).
+struct Tail {
   const double* g;
   const double* table;
+  double r_mx, r_my, r_iz, r_nd, r_w;  // 1/(m+m_x), 1/(m+m_y), 1/(I+I_z), 1/(n D), 1/width
+  double r_goal, r_two_w, r_fuel;      // observation spans: 1/goal, 1/(2 width), 1/fuel
 };
 
 // ---------------------------------------------------------------- LDS of a drawing wave
@@ -410,8 +416,8 @@ struct ObsConst {  // per-launch reciprocals of the config-dependent spans
   double goal, two_w, fuel;
 };
 
-__device__ __forceinline__ ObsConst obs_const(const SacenvBoatParams& p) {
-  return ObsConst{1.0 / p.goal_line, 1.0 / (p.track_width + p.track_width), 1.0 / (double)p.fuel0};
+__device__ __forceinline__ ObsConst obs_const(const Tail& T) {
+  return ObsConst{T.r_goal, T.r_two_w, T.r_fuel};
 }
 
 __device__ __forceinline__ Obs make_obs(const SacenvBoatParams& p, const ObsConst& oc, double s_x,
@@ -432,6 +438,8 @@ __device__ __forceinline__ Obs make_obs(const SacenvBoatParams& p, const ObsCons
   o.v[10] = (float)div_c(fuel, (double)p.fuel0, oc.fuel);
   return o;
 }
+
+typedef float f4v __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void store_obs(float* dst, const Obs& o) {
 #pragma unroll
@@ -870,7 +878,7 @@ __device__ int phase_b(const SacenvBoatParams& p, const Arena& A, const Tail& T,
 
 // scalar state of a fresh Boat (boat_env.py:152-198) and its observation;
 // (wv0, wa0) = Wind.get_wind(0) of the new episode, the first step's wind
-__device__ __forceinline__ Obs fresh_state(const SacenvBoatParams& p, const Arena& A, int e,
+__device__ __forceinline__ Obs fresh_state(const SacenvBoatParams& p, const Arena& A, const Tail& T, int e,
                                            int32_t start_y, double wv0, double wa0) {
   const double s_y = p.experiment == 2 ? (double)start_y : 0.0;  // :166-169
   A.f64(U_WNX)[e] = wv0;
@@ -885,7 +893,7 @@ __device__ __forceinline__ Obs fresh_state(const SacenvBoatParams& p, const Aren
   A.f64(U_T)[e] = 0.0;
   A.f64(U_EP)[e] = 0.0;  // :122
   A.i32(U_IDX)[e] = 0;
-  return make_obs(p, obs_const(p), 0.0, 0.0, 0.0, s_y, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, (double)p.fuel0);
+  return make_obs(p, obs_const(T), 0.0, 0.0, 0.0, s_y, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, (double)p.fuel0);
 }
 
 // ---------------------------------------------------------------- kernels
@@ -981,7 +989,7 @@ __global__ void __launch_bounds__(kWave) k_draw(SacenvBoatParams p, Arena A, Tai
   if (lane == 0) {
     double wv0, wa0;
     wind0_of_slot(p, A, T.table, slot, e, wv0, wa0);
-    const Obs o = fresh_state(p, A, e, start_y, wv0, wa0);
+    const Obs o = fresh_state(p, A, T, e, start_y, wv0, wa0);
     store_obs(A.obs() + (int64_t)e * SACENV_OBS_DIM, o);
   }
 }
@@ -1005,10 +1013,310 @@ __global__ void k_drain_done(Arena A) {
   if (w < A.nwaves()) A.refill_mask((k + 2) % kRing)[w] = 0ull;
 }
 
+// Uniform fp64 constants as VGPR copies: the step reads ~40 config doubles,
+// more than the SGPR file holds next to the addresses, and SGPR spills
+// (v_writelane/v_readlane pairs) cost more than VGPR operands; the owner
+// wave has VGPRs to spare (LDS, not registers, bounds occupancy).
+__device__ __forceinline__ double vreg(double x) {
+  double r;
+  asm volatile("v_mov_b64 %0, %1" : "=v"(r) : "s"(x));
+  return r;
+}
+__device__ __forceinline__ SacenvBoatParams vreg_params(SacenvBoatParams q) {
+  q.dt = vreg(q.dt), q.t_max = vreg(q.t_max), q.goal_line = vreg(q.goal_line);
+  q.oob_limit = vreg(q.oob_limit), q.track_width = vreg(q.track_width);
+  q.c_r_front = vreg(q.c_r_front), q.c_r_side = vreg(q.c_r_side), q.rho = vreg(q.rho);
+  q.boat_area_front = vreg(q.boat_area_front), q.boat_area_side = vreg(q.boat_area_side);
+  q.boat_l = vreg(q.boat_l), q.boat_b = vreg(q.boat_b), q.rudder_area = vreg(q.rudder_area);
+  q.m_plus_mx = vreg(q.m_plus_mx), q.m_plus_my = vreg(q.m_plus_my), q.i_plus_iz = vreg(q.i_plus_iz);
+  q.one_minus_wf = vreg(q.one_minus_wf), q.one_minus_td = vreg(q.one_minus_td);
+  q.n_times_d = vreg(q.n_times_d), q.n_squared = vreg(q.n_squared), q.d_pow4 = vreg(q.d_pow4);
+  q.reward_k = vreg(q.reward_k), q.reward_center = vreg(q.reward_center);
+  q.knot_step = vreg(q.knot_step);
+  return q;
+}
+__device__ __forceinline__ Tail vreg_tail(Tail t) {
+  t.r_mx = vreg(t.r_mx), t.r_my = vreg(t.r_my), t.r_iz = vreg(t.r_iz), t.r_nd = vreg(t.r_nd);
+  t.r_w = vreg(t.r_w), t.r_goal = vreg(t.r_goal), t.r_two_w = vreg(t.r_two_w), t.r_fuel = vreg(t.r_fuel);
+  return t;
+}
+
+// ---------------------------------------------------------------- owner wave
+
+// Per-step SoA traffic of one owner wave goes through LDS so that every
+// global access is 16 B per lane: lanes 0-31 move 512 contiguous bytes of one
+// field, lanes 32-63 of the next. Per-lane 8-byte accesses are issue-bound on
+// gfx950 (twice the instructions for the same bytes), and the step is
+// dominated by its memory instructions, not its arithmetic.
+constexpr int kF64 = 11;  // s_x s_y s_r v_x v_y v_r rudder t ep_reward wind_next[2]
+struct OwnerLds {
+  double f[kF64][kWave];
+  int32_t idx[kWave], cons[kWave];
+  float reward[kWave];
+  uint8_t done[kWave], term[kWave];
+  float obs[kWave * SACENV_OBS_DIM];
+};
+union StepLds {
+  DrawLds draw;
+  OwnerLds own;
+};
+
+// byte address of (f64 field k, env e); fields 0..8 are U_SX..U_EP, 9/10 are wind_next
+__device__ __forceinline__ char* f64_field(const Arena& A, int k, int64_t e) {
+  return A.b + (int64_t)(8 * k) * A.np + 8 * e;
+}
+
+// wave-wide 16-B gathers of the owner's SoA inputs into LDS: 6 load instructions
+__device__ __forceinline__ void owner_load(const Arena& A, OwnerLds& l, int ob, int lane) {
+  const int half = lane >> 5, c = lane & 31;
+  const int64_t e0 = (int64_t)ob * kWave;
+  f4v v[6];
+#pragma unroll
+  for (int q = 0; q < 5; ++q)
+    v[q] = *reinterpret_cast<const f4v*>(f64_field(A, 2 * q + half, e0 + 2 * c));
+  {  // lanes 0-31: wind_next angle; 32-47: index; 48-63: cons (4 envs per lane)
+    const char* src = lane < 32 ? f64_field(A, 10, e0 + 2 * c)
+                                : reinterpret_cast<const char*>(A.i32(lane < 48 ? U_IDX : U_CONS) + e0 +
+                                                                4 * (lane & 15));
+    v[5] = *reinterpret_cast<const f4v*>(src);
+  }
+#pragma unroll
+  for (int q = 0; q < 5; ++q) *reinterpret_cast<f4v*>(&l.f[2 * q + half][2 * c]) = v[q];
+  if (lane < 32)
+    *reinterpret_cast<f4v*>(&l.f[10][2 * c]) = v[5];
+  else
+    *reinterpret_cast<f4v*>((lane < 48 ? l.idx : l.cons) + 4 * (lane & 15)) = v[5];
+  __syncthreads();
+}
+
+// 16-B store (plain: write-through sc1 and nt measured no faster here)
+__device__ __forceinline__ void st16(void* dst, f4v v) { *reinterpret_cast<f4v*>(dst) = v; }
+
+// the mirror image for the outputs: 7 store instructions + 3 for the obs rows
+__device__ __forceinline__ void owner_store(const Arena& A, const OwnerLds& l, int ob, int lane) {
+  const int half = lane >> 5, c = lane & 31;
+  const int64_t e0 = (int64_t)ob * kWave;
+#pragma unroll
+  for (int q = 0; q < 5; ++q)
+    st16(f64_field(A, 2 * q + half, e0 + 2 * c), *reinterpret_cast<const f4v*>(&l.f[2 * q + half][2 * c]));
+  {  // lanes 0-31: wind_next angle; 32-47: index; 48-63: reward
+    const int j = lane & 15;
+    char* dst = lane < 32   ? f64_field(A, 10, e0 + 2 * c)
+                : lane < 48 ? reinterpret_cast<char*>(A.i32(U_IDX) + e0 + 4 * j)
+                            : reinterpret_cast<char*>(A.reward() + e0 + 4 * j);
+    const f4v* src = lane < 32   ? reinterpret_cast<const f4v*>(&l.f[10][2 * c])
+                     : lane < 48 ? reinterpret_cast<const f4v*>(l.idx + 4 * j)
+                                 : reinterpret_cast<const f4v*>(l.reward + 4 * j);
+    st16(dst, *src);
+  }
+  if (lane < 24) {  // lanes 0-15: cons; 16-19: done; 20-23: term
+    char* dst;
+    const f4v* src;
+    if (lane < 16) {
+      dst = reinterpret_cast<char*>(A.i32(U_CONS) + e0 + 4 * lane);
+      src = reinterpret_cast<const f4v*>(l.cons + 4 * lane);
+    } else if (lane < 20) {
+      dst = reinterpret_cast<char*>(A.done() + e0 + 16 * (lane - 16));
+      src = reinterpret_cast<const f4v*>(l.done + 16 * (lane - 16));
+    } else {
+      dst = reinterpret_cast<char*>(A.term() + e0 + 16 * (lane - 20));
+      src = reinterpret_cast<const f4v*>(l.term + 16 * (lane - 20));
+    }
+    st16(dst, *src);
+  }
+  // obs rows: 64 rows x 44 B = 2816 B = 176 float4
+  const f4v* src = reinterpret_cast<const f4v*>(l.obs);
+  f4v* dst = reinterpret_cast<f4v*>(A.obs() + e0 * SACENV_OBS_DIM);
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    if (lane + kWave * i < kWave * SACENV_OBS_DIM / 4) st16(dst + lane + kWave * i, src[lane + kWave * i]);
+}
+
+// One owner wave: BoatEnv.step for 64 consecutive envs, one per lane.
+__device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Arena& A, const Tail& T,
+                                           const float* __restrict__ action, OwnerLds& l, int ob,
+                                           int lane) {
+#ifdef SACENV_STAMPS
+  const uint64_t st_real0 = __builtin_amdgcn_s_memrealtime();
+  uint64_t st_loaded = 0, st_computed = 0;
+#define OWNER_STAMP(v)                                          \
+  do {                                                          \
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); \
+    v = __builtin_amdgcn_s_memrealtime();                       \
+  } while (0)
+#else
+#define OWNER_STAMP(v) \
+  do {                 \
+  } while (0)
+#endif
+  const int e = ob * kWave + lane;
+  const bool active = e < p.n_envs;
+  const int kepoch = A.owner_epoch()[ob];
+  const float act = action[active ? e : 0];
+  owner_load(A, l, ob, lane);
+  double s_x = l.f[0][lane], s_y = l.f[1][lane], s_r = l.f[2][lane];
+  double v_x = l.f[3][lane], v_y = l.f[4][lane], v_r = l.f[5][lane];
+  double rudder = l.f[6][lane], t = l.f[7][lane], ep = l.f[8][lane];
+  // this step's wind was evaluated one step ahead (no index-dependent load
+  // on the critical path); the next step's is fetched now, used at the end
+  const double wv = l.f[9][lane], wa = l.f[10][lane];
+  int32_t index = l.idx[lane];
+  const int cons = p.autoreset ? l.cons[lane] : 0;
+  double nwv, nwa;
+  wind_at(p, A, T.table, cons % kSlots, e, index + 1, nwv, nwa);
+  // autoreset: the next pre-drawn episode's first wind and start y, speculatively
+  double w0v = 0.0, w0a = 0.0;
+  int32_t sy_next = 0;
+  if (p.autoreset) {
+    wind0_of_slot(p, A, T.table, (cons + 1) % kSlots, e, w0v, w0a);
+    if (p.experiment == 2) sy_next = A.i32(U_STARTY)[(int64_t)((cons + 1) % kSlots) * A.np + e];
+  }
+  OWNER_STAMP(st_loaded);
+  const double r_mx = T.r_mx, r_my = T.r_my, r_iz = T.r_iz, r_nd = T.r_nd, r_w = T.r_w;
+  const ObsConst oc = obs_const(T);
+
+  // BoatEnv.step :69-73
+  t = t + p.dt;
+  const int32_t fuel = p.fuel0 - (index + 1);
+  if (p.test_mode == 0) rudder = rudder + div_c((double)act, 10.0, 0.1);  // action / 10
+  const bool first = index == 0;  // integrator counter == 0 (control_blocks.py:21-22)
+  const double wsign = (double)((wv > 0.0) - (wv < 0.0));
+  double swa, cwa;
+  sincos(wa, &swa, &cwa);
+
+  // eom_longitudinal :213-239
+  const double F_R = v_x * v_x * p.c_r_front * 0.5 * p.rho * p.boat_area_front;
+  const double v_x_w = v_x * p.one_minus_wf;
+  const double J = p.n_rpm != 0.0 ? div_c(v_x_w, p.n_times_d, r_nd) : 0.0;  // :222-224
+  const double F_T = sin(J) * p.n_squared * p.rho * p.d_pow4 * p.one_minus_td;
+  const double F_C = v_y * p.m_plus_my * v_r;
+  const double F_W = (wv * wv * wsign * p.c_r_front * 0.5 * p.rho * p.boat_area_front) * cwa;
+  const double a_x = div_c(-F_R + F_T + F_C + F_W, p.m_plus_mx, r_mx);
+  v_x = first ? 3.0 : a_x * p.dt + v_x;
+
+  // eom_transverse :241-265 (new v_x)
+  const double vys = (double)((v_y > 0.0) - (v_y < 0.0));
+  const double F_R2 = v_y * v_y * p.c_r_side * 0.5 * p.rho * p.boat_area_side * vys;
+  const double sin_rud = sin(rudder);
+  const double F_RU = sin_rud * (v_x * v_x * p.c_r_front * 0.5 * p.rho * p.rudder_area);
+  const double F_C2 = v_x * p.m_plus_mx * v_r;
+  const double F_W2 = (wv * wv * wsign * p.c_r_side * 0.5 * p.rho * p.boat_area_side) * swa;
+  const double a_y = div_c(-F_R2 + F_RU + F_C2 + F_W2, p.m_plus_my, r_my);
+  v_y = first ? 0.0 : a_y * p.dt + v_y;
+
+  // eom_yawning :267-281
+  const double vrs = (double)((v_r > 0.0) - (v_r < 0.0));
+  const double vxs = (double)((v_x > 0.0) - (v_x < 0.0));
+  const double M_hull = v_r * v_r * p.c_r_side * 0.5 * p.rho * p.boat_area_side * p.boat_l * 5.0 * vrs;
+  const double M_rud = v_x * v_x * p.c_r_side * 0.5 * p.rho * p.rudder_area * sin_rud * (p.boat_b / 2) * vxs;
+  const double a_r = div_c(-M_hull + M_rud, p.i_plus_iz, r_iz);
+  v_r = first ? 0.0 : a_r * p.dt + v_r;
+
+  // get_kinematics :283-306
+  const double v = sqrt(v_x * v_x + v_y * v_y);
+  const double drift = atan2(v_x, v_y);
+  s_r = v_r * p.dt + s_r;
+  const double dir = drift - s_r;
+  double sd, cd;
+  sincos(dir, &sd, &cd);
+  s_x = (sd * v) * p.dt + s_x;
+  s_y = (cd * v) * p.dt + s_y;
+  index = index + 1;
+
+  Obs o = make_obs(p, oc, s_x, v_x, a_x, s_y, v_y, a_y, s_r, v_r, a_r, rudder, (double)fuel);
+
+  // exponential_reward (reward_functions.py:42-57), f_x = 0
+  const double ay = fabs(s_y);
+  const double f_y = div_c(ay, p.track_width, r_w) / (1.0 + exp(p.reward_k * (ay - p.reward_center)));
+  double reward = 0.0 - f_y;
+
+  // termination chain :84-105
+  uint8_t term = SACENV_TERM_NONE;
+  if (s_x >= p.goal_line) {
+    term = SACENV_TERM_REACHED_GOAL;
+    reward = reward + 1000.0;
+  } else if (fabs(s_y) > p.oob_limit || s_x < 0.0) {
+    term = SACENV_TERM_OUT_OF_BOUNDS;
+  } else if (fuel < 0) {
+    term = SACENV_TERM_OUT_OF_FUEL;
+  } else if (p.t_max <= t) {
+    term = SACENV_TERM_TIMEOUT;
+  } else if (rudder > kPi / 3 || rudder < -kPi / 3) {
+    term = SACENV_TERM_RUDDER_BROKEN;
+  }
+  // penalties :107-111
+  if (rudder > kPi / 4 || rudder < -kPi / 4) reward = reward - fabs(rudder) * 100.0;
+  if (fabs(s_r) > kPi / 2) reward = reward - 1.0;
+  ep = ep + reward;
+  if (!active) term = SACENV_TERM_NONE;  // padding lanes never end
+
+  if (term != SACENV_TERM_NONE)  // no-return atomic: nothing on the critical path waits
+    __hip_atomic_fetch_add(A.at<uint32_t>(U_CNT) + (int64_t)(term - 1) * A.np + e, 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+  if (term == SACENV_TERM_NONE && active && p.max_episode_steps > 0 && index >= p.max_episode_steps)
+    term = SACENV_TERM_TRUNCATED;
+  const bool ended = term != SACENV_TERM_NONE;
+
+  OWNER_STAMP(st_computed);
+  if (p.out_flags & SACENV_OUT_REWARD64) A.reward64()[e] = reward;
+  if (p.out_flags & SACENV_OUT_ACCEL) {
+    A.accel()[e] = a_x;
+    A.accel()[A.np + e] = a_y;
+    A.accel()[2 * A.np + e] = a_r;
+  }
+  const bool restart = ended && p.autoreset;
+  if (ended) {
+    A.final_ep()[e] = ep;
+    // terminal obs of an auto-reset env (main.py:72 reset, boat_env.py:121)
+    if (restart) store_obs(A.final_obs() + (int64_t)e * SACENV_OBS_DIM, o);
+  }
+  int cons_out = cons;
+  if (restart) {  // next episode from its pre-drawn slot: a fresh Boat (boat_env.py:152-198)
+    const double sy0 = p.experiment == 2 ? (double)sy_next : 0.0;  // :166-169
+    s_x = 0.0, s_y = sy0, s_r = 0.0, v_x = 0.0, v_y = 0.0, v_r = 0.0, rudder = 0.0;
+    t = 0.0, ep = 0.0;  // :122
+    index = 0;
+    nwv = w0v, nwa = w0a;
+    o = make_obs(p, oc, 0.0, 0.0, 0.0, sy0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, (double)p.fuel0);
+    cons_out = cons + 1;
+  }
+  // stage every output in LDS (the wave's loads of it are complete), then 16-B stores
+  l.f[0][lane] = s_x, l.f[1][lane] = s_y, l.f[2][lane] = s_r;
+  l.f[3][lane] = v_x, l.f[4][lane] = v_y, l.f[5][lane] = v_r;
+  l.f[6][lane] = rudder, l.f[7][lane] = t, l.f[8][lane] = ep;
+  l.f[9][lane] = nwv, l.f[10][lane] = nwa;
+  l.idx[lane] = index;
+  if (p.autoreset) l.cons[lane] = cons_out;
+  l.reward[lane] = (float)reward;
+  l.done[lane] = ended ? 1 : 0;
+  l.term[lane] = term;
+#pragma unroll
+  for (int k = 0; k < SACENV_OBS_DIM; ++k) l.obs[lane * SACENV_OBS_DIM + k] = o.v[k];
+  __syncthreads();
+  owner_store(A, l, ob, lane);
+  if (p.autoreset) {
+    // this launch's ended envs, for the next launch's helpers (every wave
+    // rewrites its word each launch, so the ring needs no clearing)
+    const unsigned long long m = __ballot(ended);
+    if (lane == 0) A.refill_mask(kepoch % kRing)[ob] = m;
+  }
+  if (lane == 0) A.owner_epoch()[ob] = kepoch + 1;
+#ifdef SACENV_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (lane == 0) {
+    double* d = A.accel() + (int64_t)ob * 4;
+    d[0] = (double)st_real0;
+    d[1] = (double)__builtin_amdgcn_s_memrealtime();
+    d[2] = (double)st_loaded;
+    d[3] = (double)st_computed;
+  }
+#endif
+}
+
 __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, Arena A, Tail T,
                                                 const float* __restrict__ action) {
-  __shared__ DrawLds lds;
-  __shared__ __attribute__((aligned(16))) float obs_stage[kWave * SACENV_OBS_DIM];
+  __shared__ StepLds slds;
+  DrawLds& lds = slds.draw;
   const int lane = threadIdx.x;
   const int nh = p.autoreset ? p.n_helpers : 0;
 
@@ -1045,174 +1353,7 @@ __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, Arena A, Tai
     return;
   }
 
-  // ---------------- owner: one env per lane
-  const int ob = blockIdx.x - 2 * nh;
-#ifdef SACENV_STAMPS
-  const uint64_t st_real0 = __builtin_amdgcn_s_memrealtime();
-#endif
-  const int e = ob * kWave + lane;
-  const bool active = e < p.n_envs;
-  const int kepoch = A.owner_epoch()[ob];
-  Obs o;
-  bool ended = false;
-  if (active) {
-    double s_x = A.f64(U_SX)[e], s_y = A.f64(U_SY)[e], s_r = A.f64(U_SR)[e];
-    double v_x = A.f64(U_VX)[e], v_y = A.f64(U_VY)[e], v_r = A.f64(U_VR)[e];
-    double rudder = A.f64(U_RUD)[e], t = A.f64(U_T)[e], ep = A.f64(U_EP)[e];
-    int32_t index = A.i32(U_IDX)[e];
-    const int cons = p.autoreset ? A.i32(U_CONS)[e] : 0;
-    const float act = action[e];
-    // this step's wind was evaluated one step ahead (no index-dependent load
-    // on the critical path); the next step's is fetched now, used at the end
-    const double wv = A.f64(U_WNX)[e], wa = A.f64(U_WNX)[A.np + e];
-    double nwv, nwa;
-    wind_at(p, A, T.table, cons % kSlots, e, index + 1, nwv, nwa);
-    // autoreset: the next pre-drawn episode's first wind and start y, speculatively
-    double w0v = 0.0, w0a = 0.0;
-    int32_t sy_next = 0;
-    if (p.autoreset) {
-      wind0_of_slot(p, A, T.table, (cons + 1) % kSlots, e, w0v, w0a);
-      if (p.experiment == 2) sy_next = A.i32(U_STARTY)[(int64_t)((cons + 1) % kSlots) * A.np + e];
-    }
-    const double r_mx = 1.0 / p.m_plus_mx, r_my = 1.0 / p.m_plus_my, r_iz = 1.0 / p.i_plus_iz;
-    const double r_nd = 1.0 / p.n_times_d, r_w = 1.0 / p.track_width;
-    const ObsConst oc = obs_const(p);
-
-    // BoatEnv.step :69-73
-    t = t + p.dt;
-    const int32_t fuel = p.fuel0 - (index + 1);
-    if (p.test_mode == 0) rudder = rudder + (double)act / 10;
-    const bool first = index == 0;  // integrator counter == 0 (control_blocks.py:21-22)
-    const double wsign = (double)((wv > 0.0) - (wv < 0.0));
-    double swa, cwa;
-    sincos(wa, &swa, &cwa);
-
-    // eom_longitudinal :213-239
-    const double F_R = v_x * v_x * p.c_r_front * 0.5 * p.rho * p.boat_area_front;
-    const double v_x_w = v_x * p.one_minus_wf;
-    const double J = p.n_rpm != 0.0 ? div_c(v_x_w, p.n_times_d, r_nd) : 0.0;  // :222-224
-    const double F_T = sin(J) * p.n_squared * p.rho * p.d_pow4 * p.one_minus_td;
-    const double F_C = v_y * p.m_plus_my * v_r;
-    const double F_W = (wv * wv * wsign * p.c_r_front * 0.5 * p.rho * p.boat_area_front) * cwa;
-    const double a_x = div_c(-F_R + F_T + F_C + F_W, p.m_plus_mx, r_mx);
-    v_x = first ? 3.0 : a_x * p.dt + v_x;
-
-    // eom_transverse :241-265 (new v_x)
-    const double vys = (double)((v_y > 0.0) - (v_y < 0.0));
-    const double F_R2 = v_y * v_y * p.c_r_side * 0.5 * p.rho * p.boat_area_side * vys;
-    const double sin_rud = sin(rudder);
-    const double F_RU = sin_rud * (v_x * v_x * p.c_r_front * 0.5 * p.rho * p.rudder_area);
-    const double F_C2 = v_x * p.m_plus_mx * v_r;
-    const double F_W2 = (wv * wv * wsign * p.c_r_side * 0.5 * p.rho * p.boat_area_side) * swa;
-    const double a_y = div_c(-F_R2 + F_RU + F_C2 + F_W2, p.m_plus_my, r_my);
-    v_y = first ? 0.0 : a_y * p.dt + v_y;
-
-    // eom_yawning :267-281
-    const double vrs = (double)((v_r > 0.0) - (v_r < 0.0));
-    const double vxs = (double)((v_x > 0.0) - (v_x < 0.0));
-    const double M_hull = v_r * v_r * p.c_r_side * 0.5 * p.rho * p.boat_area_side * p.boat_l * 5.0 * vrs;
-    const double M_rud = v_x * v_x * p.c_r_side * 0.5 * p.rho * p.rudder_area * sin_rud * (p.boat_b / 2) * vxs;
-    const double a_r = div_c(-M_hull + M_rud, p.i_plus_iz, r_iz);
-    v_r = first ? 0.0 : a_r * p.dt + v_r;
-
-    // get_kinematics :283-306
-    const double v = sqrt(v_x * v_x + v_y * v_y);
-    const double drift = atan2(v_x, v_y);
-    s_r = v_r * p.dt + s_r;
-    const double dir = drift - s_r;
-    double sd, cd;
-    sincos(dir, &sd, &cd);
-    s_x = (sd * v) * p.dt + s_x;
-    s_y = (cd * v) * p.dt + s_y;
-    index = index + 1;
-
-    o = make_obs(p, oc, s_x, v_x, a_x, s_y, v_y, a_y, s_r, v_r, a_r, rudder, (double)fuel);
-
-    // exponential_reward (reward_functions.py:42-57), f_x = 0
-    const double ay = fabs(s_y);
-    const double f_y = div_c(ay, p.track_width, r_w) / (1.0 + exp(p.reward_k * (ay - p.reward_center)));
-    double reward = 0.0 - f_y;
-
-    // termination chain :84-105
-    uint8_t term = SACENV_TERM_NONE;
-    if (s_x >= p.goal_line) {
-      term = SACENV_TERM_REACHED_GOAL;
-      reward = reward + 1000.0;
-    } else if (fabs(s_y) > p.oob_limit || s_x < 0.0) {
-      term = SACENV_TERM_OUT_OF_BOUNDS;
-    } else if (fuel < 0) {
-      term = SACENV_TERM_OUT_OF_FUEL;
-    } else if (p.t_max <= t) {
-      term = SACENV_TERM_TIMEOUT;
-    } else if (rudder > kPi / 3 || rudder < -kPi / 3) {
-      term = SACENV_TERM_RUDDER_BROKEN;
-    }
-    // penalties :107-111
-    if (rudder > kPi / 4 || rudder < -kPi / 4) reward = reward - fabs(rudder) * 100.0;
-    if (fabs(s_r) > kPi / 2) reward = reward - 1.0;
-    ep = ep + reward;
-
-    if (term != SACENV_TERM_NONE)  // no-return atomic: nothing on the critical path waits
-      __hip_atomic_fetch_add(A.at<uint32_t>(U_CNT) + (int64_t)(term - 1) * A.np + e, 1u,
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (term == SACENV_TERM_NONE && p.max_episode_steps > 0 && index >= p.max_episode_steps)
-      term = SACENV_TERM_TRUNCATED;
-    ended = term != SACENV_TERM_NONE;
-
-    A.reward()[e] = (float)reward;
-    A.done()[e] = ended ? 1 : 0;
-    A.term()[e] = term;
-    if (p.out_flags & SACENV_OUT_REWARD64) A.reward64()[e] = reward;
-    if (p.out_flags & SACENV_OUT_ACCEL) {
-      A.accel()[e] = a_x;
-      A.accel()[A.np + e] = a_y;
-      A.accel()[2 * A.np + e] = a_r;
-    }
-    if (ended) A.final_ep()[e] = ep;
-    if (ended && p.autoreset) {
-      // next episode from its pre-drawn slot (main.py:72 reset, boat_env.py:121)
-      store_obs(A.final_obs() + (int64_t)e * SACENV_OBS_DIM, o);
-      A.i32(U_CONS)[e] = cons + 1;
-      o = fresh_state(p, A, e, sy_next, w0v, w0a);
-    } else {
-      A.f64(U_WNX)[e] = nwv;
-      A.f64(U_WNX)[A.np + e] = nwa;
-      A.f64(U_SX)[e] = s_x;
-      A.f64(U_SY)[e] = s_y;
-      A.f64(U_SR)[e] = s_r;
-      A.f64(U_VX)[e] = v_x;
-      A.f64(U_VY)[e] = v_y;
-      A.f64(U_VR)[e] = v_r;
-      A.f64(U_RUD)[e] = rudder;
-      A.f64(U_T)[e] = t;
-      A.f64(U_EP)[e] = ep;
-      A.i32(U_IDX)[e] = index;
-    }
-  }
-  // obs rows through LDS: 64 rows x 44 B = 2816 B stored as 176 float4
-#pragma unroll
-  for (int k = 0; k < SACENV_OBS_DIM; ++k) obs_stage[lane * SACENV_OBS_DIM + k] = active ? o.v[k] : 0.0f;
-  __syncthreads();
-  {
-    const float4* src = reinterpret_cast<const float4*>(obs_stage);
-    float4* dst = reinterpret_cast<float4*>(A.obs() + (int64_t)ob * kWave * SACENV_OBS_DIM);
-    for (int i = lane; i < kWave * SACENV_OBS_DIM / 4; i += kWave) dst[i] = src[i];
-  }
-  if (p.autoreset) {
-    // this launch's ended envs, for the next launch's helpers (every wave
-    // rewrites its word each launch, so the ring needs no clearing)
-    const unsigned long long m = __ballot(ended);
-    if (lane == 0) A.refill_mask(kepoch % kRing)[ob] = m;
-  }
-  if (lane == 0) A.owner_epoch()[ob] = kepoch + 1;
-#ifdef SACENV_STAMPS
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (lane == 0) {
-    double* d = A.accel() + (int64_t)ob * 2;
-    d[0] = (double)st_real0;
-    d[1] = (double)__builtin_amdgcn_s_memrealtime();
-  }
-#endif
+  owner_wave(vreg_params(p), A, vreg_tail(T), action, slds.own, blockIdx.x - 2 * nh, lane);
 }
 
 __global__ void __launch_bounds__(256) k_wind_eval(SacenvBoatParams p, Arena A, Tail T,
@@ -1248,8 +1389,18 @@ Tail make_tail(const SacenvBoatParams& p, void* arena) {
   SacenvBoatLayout L;
   compute_layout(p.n_envs, p.n_knots, p.n_helpers, p.wind_len, p.use_wind_table, &L);
   char* b = static_cast<char*>(arena);
-  return Tail{reinterpret_cast<const double*>(b + L.spline_g),
-              reinterpret_cast<const double*>(b + L.wind_table)};
+  Tail T;
+  T.g = reinterpret_cast<const double*>(b + L.spline_g);
+  T.table = reinterpret_cast<const double*>(b + L.wind_table);
+  T.r_mx = 1.0 / p.m_plus_mx;
+  T.r_my = 1.0 / p.m_plus_my;
+  T.r_iz = 1.0 / p.i_plus_iz;
+  T.r_nd = 1.0 / p.n_times_d;
+  T.r_w = 1.0 / p.track_width;
+  T.r_goal = 1.0 / p.goal_line;
+  T.r_two_w = 1.0 / (p.track_width + p.track_width);
+  T.r_fuel = 1.0 / (double)p.fuel0;
+  return T;
 }
 
 int launch_status() {

@@ -1,0 +1,20 @@
+#!/bin/bash
+# rocprofv3 evidence for the bench kernel (run on the GPU box from the repo root):
+#   1. kernel trace + stats of the default-shaped bench run (graph replay);
+#   2. separate PMC passes (FETCH_SIZE / WRITE_SIZE / TCC hit+miss), one per
+#      run, --pmc never combined with any trace domain (pool rule).
+# Summaries land in gpurun_out/prof_*; tools/pmc_summary.py reduces them.
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+OUT=$GRAFT_REPO_ROOT/gpurun_out
+mkdir -p "$OUT"
+BENCH="python3 bench.py --steps ${PMC_STEPS:-300} --warmup 100 --no-cpu-baseline"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_trace" -o run --output-format csv \
+  -- $BENCH > "$OUT/prof_trace_bench.json" 2> "$OUT/prof_trace.log" || exit 1
+i=0
+for c in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $c -d "$OUT/prof_pmc$i" -o run --output-format csv \
+    -- $BENCH --no-graph > "$OUT/prof_pmc${i}_bench.json" 2> "$OUT/prof_pmc$i.log" || exit 1
+done
+python3 tools/pmc_summary.py "$OUT" || exit 1

@@ -35,12 +35,13 @@ def main():
     N = int(os.environ.get("STAMP_ENVS", "65536"))
     tm = int(os.environ.get("STAMP_TEST_MODE", "0"))
     env = VecBoatEnv({"base_settings": {"experiment": 6, "test_mode": tm}}, N, device="cuda",
-                     max_episode_steps=500, n_helpers=int(os.environ.get("STAMP_HELPERS", "256")))
+                     max_episode_steps=int(os.environ.get("STAMP_EPISODE", "500")),
+                     n_helpers=int(os.environ.get("STAMP_HELPERS", "256")))
     env.reset()
     acts = torch.rand(500, N, device="cuda") * 2 - 1
     nw = env.n_pad // 64
     acc_off = env.layout.accel
-    raw = env.arena[acc_off: acc_off + nw * 2 * 8].view(torch.float64).view(nw, 2)
+    raw = env.arena[acc_off: acc_off + nw * 4 * 8].view(torch.float64).view(nw, 4)
     nh = int(env.params.n_helpers)
     r64 = env.layout.reward64
     hraw = env.arena[r64: r64 + 2 * nh * 12 * 8].view(torch.float64).view(2 * nh, 12)
@@ -58,6 +59,9 @@ def main():
     print(f"N={N} owner waves={nw} helpers={nh}x2 test_mode={tm}")
     print(f"owner span (first owner start -> last owner end) us: median {np.median(owner_end):.2f} "
           f"p90 {np.percentile(owner_end, 90):.2f}")
+    for a, b, nm in ((0, 2, "state+wind loads"), (2, 3, "compute"), (3, 1, "stores/end")):
+        d = (r[..., b] - r[..., a]) / 100.0
+        print(f"    owner {nm:16s} us median {np.median(d):6.2f} p90 {np.percentile(d, 90):6.2f}")
     skew = (r[..., 0] - t0[:, None]) / 100.0
     print(f"owner start skew us: median {np.median(skew):.2f} max {skew.max():.2f}")
     for ph, name in ((0, "phase A (draw)"), (1, "phase B (fit)")):
