@@ -13,8 +13,10 @@ all-gather over RCCL that pools transitions for a shared replay buffer).
 Timing: W untimed steps, then exactly K steps bracketed by barrier +
 synchronize; value = all envs x K / max-over-ranks time. At N=1 the steps
 are replayed from hipGraphs of 100 step launches (launch-bound otherwise).
-Roofline: SURVEY.md §8(d) algorithmic 222 B per boat env-step over the
-k_step launch duration (HIP events around launches on the env's stream).
+Roofline: SURVEY.md §8(d) algorithmic 222 B per boat env-step x envs per
+launch, over k_step's average launch duration from HIP events on the
+kernel's stream (the timed region itself at N=1); `traffic` = HBM bytes per
+launch from the committed rocprofv3 PMC passes (tools/pmc.sh).
 cpu_baseline: the numpy float64 oracle (oracle/boat_oracle.py, a port of the
 reference step) on the same workload shape, one core, bounded sample.
 """
@@ -111,17 +113,20 @@ def cpu_baseline(n_envs: int, seconds: float, experiment: int) -> dict:
                     "env-steps/s for exp 6 in the survey container (BASELINE.md)"}
 
 
-def load_traffic(n_envs: int):
-    """Per-launch HBM bytes of k_step from the committed rocprofv3 PMC summary, if any."""
-    path = os.path.join(ROOT, "profiles", "pmc_k_step.json")
-    if not os.path.exists(path):
-        return None
-    try:
-        d = json.load(open(path))
-        if int(d.get("envs", -1)) == n_envs:
-            return float(d["hbm_bytes_per_launch"])
-    except Exception:  # noqa: BLE001
-        return None
+def load_traffic(n_envs: int, experiment: int):
+    """Per-launch HBM bytes of k_step from the committed rocprofv3 PMC summary
+    (tools/pmc.sh -> profiles/<round>_pmc_k_step.json, newest round first) for
+    this workload shape, or None."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_k_step.json")), reverse=True):
+        try:
+            d = json.load(open(path))
+        except Exception:  # noqa: BLE001
+            continue
+        if int(d.get("envs", -1)) == n_envs and int(d.get("experiment", 6)) == experiment \
+                and "hbm_bytes_per_launch" in d:
+            return {"hbm_bytes_per_launch": float(d["hbm_bytes_per_launch"]),
+                    "source": os.path.relpath(path, ROOT)}
     return None
 
 
@@ -183,9 +188,13 @@ def main():
     k = run(args.warmup, 0)
     torch.cuda.synchronize(dev)
     barrier(world)
+    st = torch.cuda.current_stream(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    ev0.record(st)
     k = run(args.steps, k)
+    ev1.record(st)
     torch.cuda.synchronize(dev)
     barrier(world)
     el = time.perf_counter() - t0
@@ -194,29 +203,29 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el_max = float(t.item())
 
-    # k_step launch duration: HIP events around individual launches on env's stream
-    st = torch.cuda.current_stream(dev)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.kernel_launches)]
-    torch.cuda.synchronize(dev)
-    for i, (a, b) in enumerate(evs):
-        a.record(st)
-        env.step_async(actions[(k + i) % EPISODE_STEPS])
-        b.record(st)
-    torch.cuda.synchronize(dev)
-    durs = np.array([a.elapsed_time(b) for a, b in evs]) * 1e-3  # s
-    kern_s = float(np.median(durs))
-    kern_mean = float(durs.mean())
-    # graph-paced per-step time (kernels back to back, no host in the loop)
-    graph_step_s = None
+    # k_step average launch duration from HIP events on the stream the kernel
+    # runs on. N=1: the timed region itself (K back-to-back k_step launches,
+    # graph-replayed). N>1: the timed region also holds the all-gathers, so a
+    # k_step-only graph of GRAPH_STEPS launches is replayed and timed after it.
     if use_graph:
+        kern_s = ev0.elapsed_time(ev1) * 1e-3 / args.steps
+        kern_src = f"HIP events over the timed region: {args.steps} graph-replayed k_step launches"
+    else:
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr):
+            for i in range(GRAPH_STEPS):
+                env.step_async(actions[(k + i) % EPISODE_STEPS])
+        gr.replay()
+        torch.cuda.synchronize(dev)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = max(1, args.kernel_launches // GRAPH_STEPS)
         e0.record(st)
-        for gr in graphs:
+        for _ in range(reps):
             gr.replay()
         e1.record(st)
         torch.cuda.synchronize(dev)
-        graph_step_s = e0.elapsed_time(e1) * 1e-3 / (len(graphs) * GRAPH_STEPS)
+        kern_s = e0.elapsed_time(e1) * 1e-3 / (reps * GRAPH_STEPS)
+        kern_src = f"HIP events around {reps * GRAPH_STEPS} graph-replayed k_step launches (no collective)"
 
     if rank != 0:
         if world > 1:
@@ -224,7 +233,7 @@ def main():
         return
     bytes_launch = BYTES_PER_ENV_STEP * N
     achieved = bytes_launch / kern_s
-    traffic = load_traffic(N)
+    traffic = load_traffic(N, args.experiment)
     out = {
         "metric": METRIC,
         "value": world * N * args.steps / el_max,
@@ -246,10 +255,11 @@ def main():
                    "launch": "hipGraph x100 steps" if use_graph else "eager"},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK,
-                     "traffic": traffic,
+                     "traffic": None if traffic is None else traffic["hbm_bytes_per_launch"],
                      "kernel": "k_step", "bytes_per_launch": bytes_launch,
-                     "kernel_us_median": kern_s * 1e6, "kernel_us_mean": kern_mean * 1e6,
-                     "graph_step_us": None if graph_step_s is None else graph_step_s * 1e6},
+                     "bytes_per_env_step": BYTES_PER_ENV_STEP, "kernel_avg_us": kern_s * 1e6,
+                     "timing": kern_src,
+                     "traffic_source": None if traffic is None else traffic["source"]},
         "cpu_baseline": None,
     }
     if world == 1 and not args.no_cpu_baseline:

@@ -9,8 +9,9 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=$GRAFT_REPO_ROOT/gpurun_out
 mkdir -p "$OUT"
 BENCH="python3 bench.py --steps ${PMC_STEPS:-300} --warmup 100 --no-cpu-baseline"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_trace" -o run --output-format csv \
-  -- $BENCH > "$OUT/prof_trace_bench.json" 2> "$OUT/prof_trace.log" || exit 1
+# the trace runs the default bench command itself (the judged line's command)
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_trace" -o run --output-format csv \
+  -- python3 bench.py > "$OUT/prof_trace_bench.json" 2> "$OUT/prof_trace.log" || exit 1
 i=0
 for c in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
@@ -18,3 +19,6 @@ for c in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
     -- $BENCH --no-graph > "$OUT/prof_pmc${i}_bench.json" 2> "$OUT/prof_pmc$i.log" || exit 1
 done
 python3 tools/pmc_summary.py "$OUT" || exit 1
+# and the default bench line without the profiler
+timeout -k 10 300 python3 bench.py > "$OUT/bench_default.json" 2> "$OUT/bench_default.log" || exit 1
+cat "$OUT/bench_default.json"

@@ -45,6 +45,8 @@ def main(out_dir):
     if os.path.exists(bench):
         d = json.loads(open(bench).read().strip().splitlines()[-1])
         res["envs"] = d["config"]["envs_per_gpu"]
+        res["experiment"] = d["config"]["experiment"]
+        res["bench_kernel_avg_us"] = d["roofline"]["kernel_avg_us"]
         res["algorithmic_bytes_per_launch"] = d["roofline"]["bytes_per_launch"]
     if "FETCH_SIZE_mean" in res and "WRITE_SIZE_mean" in res:
         fetch = 2.0 * res["FETCH_SIZE_mean"] * 1024.0
