@@ -36,6 +36,9 @@ sys.path.insert(0, os.path.join(ROOT, "sac-agent_amd"))
 
 METRIC = "env-steps/sec (whole node), boat_env exp-6, 65 536 envs/GPU at 1/2/4/8 MI355X"
 BYTES_PER_ENV_STEP = 222      # state r+w 152, action 4, wind 16, obs 44, reward 4, done+term 2
+TOY_BYTES_PER_ENV_STEP = 86 + 102  # parachute 86 B, car 102 B
+METRIC_MIXED = ("env-steps/sec (whole node), mixed batch boat_env exp-6 + toy_parachute + toy_car, "
+                "32 768 envs each/GPU")
 HBM_PEAK = 8.0e12             # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 EPISODE_STEPS = 500
 GRAPH_STEPS = 100
@@ -54,6 +57,9 @@ def parse():
     ap.add_argument("--kernel-launches", type=int, default=200)
     ap.add_argument("--test-mode", type=int, default=0, help="1 = rudder frozen (no terminations)")
     ap.add_argument("--helpers", type=int, default=256, help="helper waves per step launch")
+    ap.add_argument("--mixed", action="store_true",
+                    help="BASELINE configs[4]: boat exp-6 + toy_parachute + toy_car in one launch")
+    ap.add_argument("--mixed-envs", type=int, default=32768, help="envs per type per GPU (--mixed)")
     ap.add_argument("--no-autoreset", action="store_true",
                     help="diagnostic: no in-kernel auto-reset (ended envs keep stepping)")
     ap.add_argument("--episode-steps", type=int, default=EPISODE_STEPS,
@@ -81,8 +87,9 @@ def barrier(world):
         dist.barrier()
 
 
-def cpu_baseline(n_envs: int, seconds: float, experiment: int) -> dict:
-    """The oracle (numpy port of BoatEnv.step) on the bench workload, 1 thread."""
+def cpu_baseline(n_envs: int, seconds: float, experiment: int, mixed: bool = False) -> dict:
+    """The oracles (numpy ports of BoatEnv.step and of the toy scripts) on the
+    bench workload shape, 1 thread, bounded sample."""
     try:
         from threadpoolctl import threadpool_limits
     except Exception:  # noqa: BLE001
@@ -97,17 +104,25 @@ def cpu_baseline(n_envs: int, seconds: float, experiment: int) -> dict:
         # the constructor builds every env's first Boat (boat_env.py:15), untimed
         ora = OracleVecBoat(OracleConfig(experiment=experiment, test_mode=0), seeds,
                             max_episode_steps=EPISODE_STEPS)
+        toys = []
+        if mixed:
+            from toy_oracle import OracleToy
+            toys = [OracleToy(k, n_envs, max_episode_steps=EPISODE_STEPS) for k in (1, 2)]
         acts = np.random.default_rng(0).uniform(-1, 1, (64, n_envs)).astype(np.float32)
         ora.step(acts[0])  # warm
         steps, t0 = 0, time.perf_counter()
         while True:
             ora.step(acts[steps % 64])
+            for t in toys:
+                t.step()
             steps += 1
             el = time.perf_counter() - t0
             if el >= seconds and steps >= 3:
                 break
-    return {"value": n_envs * steps / el, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/boat_oracle.py numpy f64, exp {experiment}, {n_envs} envs x "
+    n_total = n_envs * (1 + len(toys))
+    what = "boat + parachute + car oracles" if mixed else "oracle/boat_oracle.py"
+    return {"value": n_total * steps / el, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"{what} numpy f64, exp {experiment}, {n_total} envs x "
                       f"{steps} steps ({el:.1f} s), auto-reset + 500-step truncation, 1 thread",
             "note": "reference BoatEnv itself (pure Python, 1 env, 1 core) measured 12 584 "
                     "env-steps/s for exp 6 in the survey container (BASELINE.md)"}
@@ -135,24 +150,31 @@ def main():
     rank, world, dev = init_dist(args.gpus)
     from sacenv import VecBoatEnv
 
-    N = args.envs
+    N = args.mixed_envs if args.mixed else args.envs
     env = VecBoatEnv({"base_settings": {"experiment": args.experiment, "test_mode": args.test_mode}},
                      N, seed=0, device=dev, autoreset=not args.no_autoreset,
                      max_episode_steps=args.episode_steps,
                      env_id_offset=rank * N, n_helpers=args.helpers)
     env.reset()
+    envs, stepper = [env], env.step_async
+    if args.mixed:
+        from sacenv.toys import CarEnv, MixedBatch, ParachuteEnv
+        toys = [ParachuteEnv(num_envs=N, device=dev, max_episode_steps=args.episode_steps),
+                CarEnv(num_envs=N, device=dev, max_episode_steps=args.episode_steps)]
+        envs += toys
+        stepper = MixedBatch(env, toys).step_async
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
     actions = (torch.rand((EPISODE_STEPS, N), generator=g, device=dev, dtype=torch.float32) * 2 - 1)
-    gathered = None
+    gathered = []
     if world > 1:
         import torch.distributed as dist
-        gathered = torch.empty(world * env.record.numel(), dtype=torch.uint8, device=dev)
+        gathered = [torch.empty(world * e.record.numel(), dtype=torch.uint8, device=dev) for e in envs]
 
     def step_eager(k: int):
-        env.step_async(actions[k % EPISODE_STEPS])
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, env.record)
+        stepper(actions[k % EPISODE_STEPS])
+        for e, buf in zip(envs if world > 1 else [], gathered):
+            dist.all_gather_into_tensor(buf, e.record)
 
     use_graph = world == 1 and not args.no_graph
     graphs = []
@@ -168,7 +190,7 @@ def main():
             gr = torch.cuda.CUDAGraph()
             with torch.cuda.graph(gr):
                 for k in range(base, base + GRAPH_STEPS):
-                    env.step_async(actions[k])
+                    stepper(actions[k])
             graphs.append(gr)
 
     def run(n_steps: int, k0: int) -> int:
@@ -214,7 +236,7 @@ def main():
         gr = torch.cuda.CUDAGraph()
         with torch.cuda.graph(gr):
             for i in range(GRAPH_STEPS):
-                env.step_async(actions[(k + i) % EPISODE_STEPS])
+                stepper(actions[(k + i) % EPISODE_STEPS])
         gr.replay()
         torch.cuda.synchronize(dev)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -231,12 +253,14 @@ def main():
         if world > 1:
             dist.destroy_process_group()
         return
-    bytes_launch = BYTES_PER_ENV_STEP * N
+    per_gpu_envs = N * len(envs)
+    bytes_env = BYTES_PER_ENV_STEP + (TOY_BYTES_PER_ENV_STEP if args.mixed else 0)
+    bytes_launch = bytes_env * N
     achieved = bytes_launch / kern_s
-    traffic = load_traffic(N, args.experiment)
+    traffic = None if args.mixed else load_traffic(N, args.experiment)
     out = {
-        "metric": METRIC,
-        "value": world * N * args.steps / el_max,
+        "metric": METRIC_MIXED if args.mixed else METRIC,
+        "value": world * per_gpu_envs * args.steps / el_max,
         "unit": "env-steps/s",
         "n_gpus": world,
         "steps": args.steps,
@@ -247,23 +271,29 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic: U(-1,1) f32 actions, per-env MT19937 wind/start draws (seeds 0..N-1)",
-        "config": {"workload": f"boat_env exp {args.experiment}, {N} envs/GPU, "
-                               f"{EPISODE_STEPS}-step episodes, in-kernel auto-reset",
-                   "experiment": args.experiment, "envs_per_gpu": N, "global_envs": world * N,
+        "config": {"workload": (f"mixed batch in one launch: boat_env exp {args.experiment} + "
+                                f"toy_parachute + toy_car, {N} envs each/GPU" if args.mixed else
+                                f"boat_env exp {args.experiment}, {N} envs/GPU") +
+                               f", {EPISODE_STEPS}-step episodes, in-kernel auto-reset",
+                   "experiment": args.experiment, "envs_per_gpu": per_gpu_envs,
+                   "global_envs": world * per_gpu_envs,
                    "episode_steps": EPISODE_STEPS, "parallelism": f"env-dp{world}",
                    "collective": "all_gather (obs,reward,done,term) 50 B/env/step" if world > 1 else None,
                    "launch": "hipGraph x100 steps" if use_graph else "eager"},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK,
                      "traffic": None if traffic is None else traffic["hbm_bytes_per_launch"],
-                     "kernel": "k_step", "bytes_per_launch": bytes_launch,
-                     "bytes_per_env_step": BYTES_PER_ENV_STEP, "kernel_avg_us": kern_s * 1e6,
+                     "kernel": "k_step<true> (mixed)" if args.mixed else "k_step",
+                     "bytes_per_launch": bytes_launch,
+                     "bytes_per_env_step": ({"boat": BYTES_PER_ENV_STEP, "parachute": 86, "car": 102}
+                                            if args.mixed else BYTES_PER_ENV_STEP),
+                     "kernel_avg_us": kern_s * 1e6,
                      "timing": kern_src,
                      "traffic_source": None if traffic is None else traffic["source"]},
         "cpu_baseline": None,
     }
     if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(N, args.cpu_seconds, args.experiment)
+        out["cpu_baseline"] = cpu_baseline(N, args.cpu_seconds, args.experiment, args.mixed)
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SACENV_ABI_VERSION 3
+#define SACENV_ABI_VERSION 4
 #define SACENV_OBS_DIM 11      /* Boat.return_state, boat_env.py:308-323 */
 #define SACENV_MT_N 624        /* MT19937 words per env (numpy legacy RNG) */
 #define SACENV_MAX_KNOTS 16    /* wind.fixed_points upper bound */
@@ -190,6 +190,65 @@ int sacenv_boat_step(const SacenvBoatParams *p, void *arena, const float *action
 int sacenv_boat_wind_eval(const SacenvBoatParams *p, const void *arena, const int32_t *env_ids,
                           const int32_t *idx, int32_t n, double *out_velocity, double *out_angle,
                           void *stream);
+
+/* ------------------------------------------------------------------------
+ * Toy integrator envs: environment/toy_parachute.py:7-41 and
+ * environment/toy_car.py:5-33 (both built on control_blocks.py:5-36
+ * Integrator). The reference runs each as a script with no Gym surface; the
+ * build exposes them as vectorised envs with the same per-iteration update:
+ * one step = one loop iteration, obs = the recorded signals (parachute [s, v],
+ * car [s_x, s_y]), reward 0, done when the script's loop would stop. */
+
+enum { SACENV_TOY_PARACHUTE = 1, SACENV_TOY_CAR = 2 };
+
+/* toy termination codes (term array; 5/6 as for the boat) */
+enum { SACENV_TOY_TERM_GROUND = 1 /* parachute s < 0: the script's break (:29-30) */ };
+
+typedef struct SacenvToyParams {
+  int32_t n_envs;
+  int32_t kind;               /* SACENV_TOY_PARACHUTE / SACENV_TOY_CAR */
+  int32_t autoreset;          /* 1: an env that ends restarts from the initial state in the step */
+  int32_t max_episode_steps;  /* > 0: truncate (term 6) after this many steps */
+  double dt;                  /* loop time step: 0.01 parachute (:21), 0.1 car (:20) */
+  double t_max;               /* loop end `while t <= t_max`: 500 (both) */
+  double integ_dt;            /* Integrator.dt (control_blocks.py:7): 0.1 */
+  /* parachute (toy_parachute.py:11-19) */
+  double h0, h1, area_closed, area_open, mass, c_w, rho, g;
+  /* car (toy_car.py:8-9, :13, :24) */
+  double car_accel, car_v_max, car_dangle;
+} SacenvToyParams;
+
+/* SoA arena of one toy env type (n_pad = n_envs rounded up to 64). */
+typedef struct SacenvToyLayout {
+  int64_t total_bytes;
+  int64_t n_pad;
+  int64_t state;      /* f64 [5][n_pad]: parachute (v_out, s_out, total_a, t, -),
+                         car (angle, v_out, s_x_out, s_y_out, t) -- the integrators'
+                         STORED (clamped) outputs and the loop variables */
+  int64_t count;      /* i32 [n_pad] iterations since reset (Integrator.counter) */
+  int64_t counters;   /* u32 [3][n_pad] cumulative: ground, timeout, truncated */
+  int64_t record;     /* u8 [14 n_pad]: obs f32 [n_pad][2] | reward f32 | done u8 | term u8 */
+  int64_t obs, reward, done, term;
+  int64_t final_obs;  /* f32 [n_pad][2] obs of the step that ended (auto-reset) */
+} SacenvToyLayout;
+
+int sacenv_toy_layout(const SacenvToyParams *p, SacenvToyLayout *out);
+/* initial state of every env (the scripts' variables before the loop) + obs */
+int sacenv_toy_init(const SacenvToyParams *p, void *arena, void *stream);
+/* restart envs ids[0..n_ids) (NULL: all) from the initial state */
+int sacenv_toy_reset(const SacenvToyParams *p, void *arena, const int32_t *ids, int32_t n_ids,
+                     void *stream);
+/* one loop iteration for every env (no action: the toys are open-loop) */
+int sacenv_toy_step(const SacenvToyParams *p, void *arena, void *stream);
+
+/* Mixed batch (BASELINE configs[4]): one launch stepping a boat arena and up
+ * to two toy arenas (toy_params[n_toys], toy_arenas[n_toys]) with
+ * heterogeneous workgroups (boat helpers, boat owners, then each toy's
+ * waves). Equivalent to sacenv_boat_step + sacenv_toy_step per toy arena;
+ * bp may be NULL for toys only. */
+int sacenv_mixed_step(const SacenvBoatParams *bp, void *boat_arena, const float *boat_action,
+                      const SacenvToyParams *toy_params, void *const *toy_arenas, int32_t n_toys,
+                      void *stream);
 
 #ifdef __cplusplus
 }

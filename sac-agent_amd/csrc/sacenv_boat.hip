@@ -1041,6 +1041,141 @@ __device__ __forceinline__ Tail vreg_tail(Tail t) {
   return t;
 }
 
+// ---------------------------------------------------------------- toy envs
+// environment/toy_parachute.py:7-41 and environment/toy_car.py:5-33, one
+// env per lane, as vectorised envs: one step = one iteration of the
+// script's loop, obs = the signals the script records. The integrators
+// (control_blocks.py:5-36) keep their STORED output (clamped to the limits,
+// :27-32) but return the unclamped value (:36); the first call returns the
+// initial value (:21-22).
+
+constexpr int UT_CNT = 40, UT_CTR = 44, UT_OBS = 56, UT_REW = 64, UT_DONE = 68, UT_TERM = 69,
+              UT_FOBS = 70, UT_TOTAL = 78;  // per-env bytes after the 5 f64 state fields
+
+__host__ __device__ inline void toy_layout(int n, SacenvToyLayout* o) {
+  const int64_t np = pad64(n);
+  o->n_pad = np;
+  o->state = 0;
+  o->count = UT_CNT * np;
+  o->counters = UT_CTR * np;
+  o->record = UT_OBS * np;
+  o->obs = UT_OBS * np;
+  o->reward = UT_REW * np;
+  o->done = UT_DONE * np;
+  o->term = UT_TERM * np;
+  o->final_obs = UT_FOBS * np;
+  o->total_bytes = align256(UT_TOTAL * np);
+}
+
+struct ToyArena {
+  char* b;
+  int64_t np;
+  __device__ __forceinline__ double* f(int k) const { return reinterpret_cast<double*>(b + 8LL * k * np); }
+  __device__ __forceinline__ int32_t* count() const { return reinterpret_cast<int32_t*>(b + UT_CNT * np); }
+  __device__ __forceinline__ uint32_t* ctr(int k) const {
+    return reinterpret_cast<uint32_t*>(b + UT_CTR * np) + (int64_t)k * np;
+  }
+  __device__ __forceinline__ float* obs() const { return reinterpret_cast<float*>(b + UT_OBS * np); }
+  __device__ __forceinline__ float* reward() const { return reinterpret_cast<float*>(b + UT_REW * np); }
+  __device__ __forceinline__ uint8_t* done() const { return reinterpret_cast<uint8_t*>(b + UT_DONE * np); }
+  __device__ __forceinline__ uint8_t* term() const { return reinterpret_cast<uint8_t*>(b + UT_TERM * np); }
+  __device__ __forceinline__ float* final_obs() const { return reinterpret_cast<float*>(b + UT_FOBS * np); }
+};
+
+// the scripts' variables before the loop, and the signals they stand for
+__device__ __forceinline__ void toy_initial(const SacenvToyParams& p, double f[5], float obs[2]) {
+  for (int k = 0; k < 5; ++k) f[k] = 0.0;
+  if (p.kind == SACENV_TOY_PARACHUTE) {
+    f[1] = p.h0;  // v_integrator = Integrator(initial_value=h_0) (:21)
+    obs[0] = (float)p.h0;
+    obs[1] = 0.0f;
+  } else {
+    obs[0] = 0.0f;
+    obs[1] = 0.0f;
+  }
+}
+
+// one loop iteration; returns the termination code (0: the loop goes on)
+__device__ __forceinline__ uint8_t toy_advance(const SacenvToyParams& p, double f[5], int& count,
+                                               float obs[2]) {
+  const bool first = count == 0;
+  uint8_t term = SACENV_TERM_NONE;
+  ++count;
+  if (p.kind == SACENV_TOY_PARACHUTE) {
+    // f = (a_integrator stored output = v, v_integrator stored output = s, total_a, t)
+    double total_a = f[2] - p.g;                               // :24
+    const double v = first ? 0.0 : total_a * p.integ_dt + f[0];  // :25
+    const double s = first ? p.h0 : v * p.integ_dt + f[1];       // :26
+    f[0] = v;
+    f[1] = s;
+    obs[0] = (float)s;
+    obs[1] = (float)v;
+    if (s < 0.0) {  // :29-30 ground reached: the script breaks
+      term = SACENV_TOY_TERM_GROUND;
+    } else {
+      const double area = s < p.h1 ? p.area_open : p.area_closed;  // :33-36
+      const double F_w = v * v * 0.5 * p.rho * p.c_w * area;
+      total_a = F_w / p.mass;  // :38
+      f[3] = f[3] + p.dt;      // :40
+      if (!(f[3] <= p.t_max)) term = SACENV_TERM_TIMEOUT;  // :23
+    }
+    f[2] = total_a;
+  } else {
+    // f = (car_angle, a_integrator stored output, v_x / v_y integrator stored outputs, t)
+    const double angle = f[0] + p.car_dangle;                          // :24
+    const double v = first ? 0.0 : p.car_accel * p.integ_dt + f[1];   // :25
+    const double vx = v * cos(angle), vy = v * sin(angle);            // :27-28
+    const double sx = first ? 0.0 : vx * p.integ_dt + f[2];           // :30
+    const double sy = first ? 0.0 : vy * p.integ_dt + f[3];           // :31
+    f[0] = angle;
+    f[1] = v >= p.car_v_max ? p.car_v_max : v;  // stored clamp (upper_limit=10, :12)
+    f[2] = sx;
+    f[3] = sy;
+    f[4] = f[4] + p.dt;  // :33
+    obs[0] = (float)sx;
+    obs[1] = (float)sy;
+    if (!(f[4] <= p.t_max)) term = SACENV_TERM_TIMEOUT;  // :22
+  }
+  return term;
+}
+
+// one toy wave: 64 envs, one per lane
+__device__ __forceinline__ void toy_wave(const SacenvToyParams& p, const ToyArena& T, int ob, int lane) {
+  const int e = ob * kWave + lane;
+  if (e >= p.n_envs) return;
+  double f[5];
+  for (int k = 0; k < 5; ++k) f[k] = T.f(k)[e];
+  int count = T.count()[e];
+  float obs[2];
+  uint8_t term = toy_advance(p, f, count, obs);
+  if (term == SACENV_TERM_NONE && p.max_episode_steps > 0 && count >= p.max_episode_steps)
+    term = SACENV_TERM_TRUNCATED;
+  if (term != SACENV_TERM_NONE) {
+    const int c = term == SACENV_TOY_TERM_GROUND ? 0 : term == SACENV_TERM_TIMEOUT ? 1 : 2;
+    T.ctr(c)[e] += 1u;
+    if (p.autoreset) {
+      T.final_obs()[2 * e] = obs[0];
+      T.final_obs()[2 * e + 1] = obs[1];
+      toy_initial(p, f, obs);
+      count = 0;
+    }
+  }
+  for (int k = 0; k < 5; ++k) T.f(k)[e] = f[k];
+  T.count()[e] = count;
+  reinterpret_cast<float2*>(T.obs())[e] = make_float2(obs[0], obs[1]);
+  T.reward()[e] = 0.0f;
+  T.done()[e] = term != SACENV_TERM_NONE ? 1 : 0;
+  T.term()[e] = term;
+}
+
+// toy arenas stepped inside a mixed launch
+struct MixedToys {
+  SacenvToyParams p[2];
+  ToyArena a[2];
+  int nb[2];
+  int n;
+};
+
 // ---------------------------------------------------------------- owner wave
 
 // Per-step SoA traffic of one owner wave goes through LDS so that every
@@ -1313,12 +1448,17 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
 #endif
 }
 
+// The step launch. Grid: 2 x n_helpers refill helpers, nb_boat owner waves,
+// then (kMixed) the waves of each toy arena: heterogeneous workgroups of one
+// launch, selected by uniform block-index ranges.
+template <bool kMixed>
 __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, Arena A, Tail T,
-                                                const float* __restrict__ action) {
+                                                const float* __restrict__ action, int nb_boat,
+                                                MixedToys M) {
   __shared__ StepLds slds;
   DrawLds& lds = slds.draw;
   const int lane = threadIdx.x;
-  const int nh = p.autoreset ? p.n_helpers : 0;
+  const int nh = nb_boat > 0 && p.autoreset ? p.n_helpers : 0;
 
   if ((int)blockIdx.x < 2 * nh) {
     // ---------------- helpers (first in the grid, so they start first)
@@ -1353,7 +1493,41 @@ __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, Arena A, Tai
     return;
   }
 
-  owner_wave(vreg_params(p), A, vreg_tail(T), action, slds.own, blockIdx.x - 2 * nh, lane);
+  int b = blockIdx.x - 2 * nh;
+  if (!kMixed || b < nb_boat) {
+    owner_wave(vreg_params(p), A, vreg_tail(T), action, slds.own, b, lane);
+    return;
+  }
+  b -= nb_boat;
+  if (b < M.nb[0]) {
+    toy_wave(M.p[0], M.a[0], b, lane);
+  } else if (M.n > 1) {
+    toy_wave(M.p[1], M.a[1], b - M.nb[0], lane);
+  }
+}
+
+
+__global__ void __launch_bounds__(kWave) k_toy_init(SacenvToyParams p, ToyArena T, const int32_t* __restrict__ ids,
+                                                    int n, int zero_counters) {
+  const int q = blockIdx.x * kWave + threadIdx.x;
+  if (q >= n) return;
+  const int e = ids != nullptr ? ids[q] : q;
+  if (e < 0 || e >= p.n_envs) return;
+  double f[5];
+  float obs[2];
+  toy_initial(p, f, obs);
+  for (int k = 0; k < 5; ++k) T.f(k)[e] = f[k];
+  T.count()[e] = 0;
+  if (zero_counters)
+    for (int k = 0; k < 3; ++k) T.ctr(k)[e] = 0u;
+  reinterpret_cast<float2*>(T.obs())[e] = make_float2(obs[0], obs[1]);
+  T.reward()[e] = 0.0f;
+  T.done()[e] = 0;
+  T.term()[e] = 0;
+}
+
+__global__ void __launch_bounds__(kWave) k_toy_step(SacenvToyParams p, ToyArena T) {
+  toy_wave(p, T, blockIdx.x, threadIdx.x);
 }
 
 __global__ void __launch_bounds__(256) k_wind_eval(SacenvBoatParams p, Arena A, Tail T,
@@ -1409,6 +1583,17 @@ int launch_status() {
 }
 
 inline int blocks_for(int n, int per) { return (n + per - 1) / per; }
+
+int check_toy(const SacenvToyParams* p) {
+  if (p == nullptr) return SACENV_E_NULL;
+  if (p->kind != SACENV_TOY_PARACHUTE && p->kind != SACENV_TOY_CAR) return SACENV_E_EXPERIMENT;
+  if (p->n_envs <= 0) return SACENV_E_SIZE;
+  return SACENV_OK;
+}
+
+ToyArena make_toy_arena(const SacenvToyParams& p, void* base) {
+  return ToyArena{static_cast<char*>(base), pad64(p.n_envs)};
+}
 
 }  // namespace
 
@@ -1496,9 +1681,84 @@ int sacenv_boat_step(const SacenvBoatParams* p, void* arena, const float* action
   int rc = check_params(p);
   if (rc) return rc;
   if (arena == nullptr || action == nullptr) return SACENV_E_NULL;
-  const int nb = (int)(pad64(p->n_envs) / kWave) + (p->autoreset ? 2 * p->n_helpers : 0);
-  hipLaunchKernelGGL(k_step, dim3(nb), dim3(kWave), 0, (hipStream_t)stream, *p, make_arena(*p, arena),
-                     make_tail(*p, arena), action);
+  const int nb_boat = (int)(pad64(p->n_envs) / kWave);
+  const int nb = nb_boat + (p->autoreset ? 2 * p->n_helpers : 0);
+  hipLaunchKernelGGL(k_step<false>, dim3(nb), dim3(kWave), 0, (hipStream_t)stream, *p, make_arena(*p, arena),
+                     make_tail(*p, arena), action, nb_boat, MixedToys{});
+  return launch_status();
+}
+
+int sacenv_toy_layout(const SacenvToyParams* p, SacenvToyLayout* out) {
+  const int rc = check_toy(p);
+  if (rc) return rc;
+  if (out == nullptr) return SACENV_E_NULL;
+  toy_layout(p->n_envs, out);
+  return SACENV_OK;
+}
+
+int sacenv_toy_init(const SacenvToyParams* p, void* arena, void* stream) {
+  const int rc = check_toy(p);
+  if (rc) return rc;
+  if (arena == nullptr) return SACENV_E_NULL;
+  hipLaunchKernelGGL(k_toy_init, dim3(blocks_for(p->n_envs, kWave)), dim3(kWave), 0, (hipStream_t)stream, *p,
+                     make_toy_arena(*p, arena), (const int32_t*)nullptr, p->n_envs, 1);
+  return launch_status();
+}
+
+int sacenv_toy_reset(const SacenvToyParams* p, void* arena, const int32_t* ids, int32_t n_ids, void* stream) {
+  const int rc = check_toy(p);
+  if (rc) return rc;
+  if (arena == nullptr) return SACENV_E_NULL;
+  const int n = ids != nullptr ? n_ids : p->n_envs;
+  if (n < 0) return SACENV_E_SIZE;
+  if (n == 0) return SACENV_OK;
+  hipLaunchKernelGGL(k_toy_init, dim3(blocks_for(n, kWave)), dim3(kWave), 0, (hipStream_t)stream, *p,
+                     make_toy_arena(*p, arena), ids, n, 0);
+  return launch_status();
+}
+
+int sacenv_toy_step(const SacenvToyParams* p, void* arena, void* stream) {
+  const int rc = check_toy(p);
+  if (rc) return rc;
+  if (arena == nullptr) return SACENV_E_NULL;
+  hipLaunchKernelGGL(k_toy_step, dim3(blocks_for(p->n_envs, kWave)), dim3(kWave), 0, (hipStream_t)stream, *p,
+                     make_toy_arena(*p, arena));
+  return launch_status();
+}
+
+int sacenv_mixed_step(const SacenvBoatParams* bp, void* boat_arena, const float* boat_action,
+                      const SacenvToyParams* toy_params, void* const* toy_arenas, int32_t n_toys,
+                      void* stream) {
+  int rc;
+  if (n_toys < 0 || n_toys > 2) return SACENV_E_SIZE;
+  if (n_toys > 0 && (toy_params == nullptr || toy_arenas == nullptr)) return SACENV_E_NULL;
+  MixedToys M{};
+  M.n = n_toys;
+  int nb = 0;
+  for (int t = 0; t < n_toys; ++t) {
+    if ((rc = check_toy(&toy_params[t]))) return rc;
+    if (toy_arenas[t] == nullptr) return SACENV_E_NULL;
+    M.p[t] = toy_params[t];
+    M.a[t] = make_toy_arena(toy_params[t], toy_arenas[t]);
+    M.nb[t] = blocks_for(toy_params[t].n_envs, kWave);
+    nb += M.nb[t];
+  }
+  SacenvBoatParams p{};
+  Arena A{};
+  Tail T{};
+  int nb_boat = 0;
+  if (bp != nullptr) {
+    if ((rc = check_params(bp))) return rc;
+    if (boat_arena == nullptr || boat_action == nullptr) return SACENV_E_NULL;
+    p = *bp;
+    A = make_arena(p, boat_arena);
+    T = make_tail(p, boat_arena);
+    nb_boat = (int)(pad64(p.n_envs) / kWave);
+    nb += nb_boat + (p.autoreset ? 2 * p.n_helpers : 0);
+  }
+  if (nb == 0) return SACENV_OK;
+  hipLaunchKernelGGL(k_step<true>, dim3(nb), dim3(kWave), 0, (hipStream_t)stream, p, A, T, boat_action, nb_boat,
+                     M);
   return launch_status();
 }
 

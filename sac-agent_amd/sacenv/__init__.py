@@ -8,7 +8,8 @@ from . import _lib
 from .config import BoatConfig
 from .spaces import Box
 
-__all__ = ["BoatConfig", "Box", "VecBoatEnv", "BoatEnv", "_lib"]
+__all__ = ["BoatConfig", "Box", "VecBoatEnv", "BoatEnv", "ParachuteEnv", "CarEnv", "VecToyEnv",
+           "MixedBatch", "_lib"]
 
 
 def __getattr__(name):  # lazy: importing torch-dependent classes only when used
@@ -18,4 +19,7 @@ def __getattr__(name):  # lazy: importing torch-dependent classes only when used
     if name == "BoatEnv":
         from .boat_env import BoatEnv
         return BoatEnv
+    if name in ("ParachuteEnv", "CarEnv", "VecToyEnv", "MixedBatch"):
+        from . import toys
+        return getattr(toys, name)
     raise AttributeError(name)

@@ -11,7 +11,7 @@ import os
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # .../sac-agent_amd
 LIB_PATH = os.environ.get("SACENV_LIB", os.path.join(PKG_ROOT, "build", "libsacenv.so"))
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 OBS_DIM = 11
 MT_N = 624
 MAX_KNOTS = 16
@@ -63,9 +63,33 @@ class BoatLayout(C.Structure):
     _fields_ = [(n, _i64) for n in LAYOUT_FIELDS]
 
 
+TOY_PARACHUTE, TOY_CAR = 1, 2
+TOY_TERM_GROUND = 1
+TOY_TERM_NAMES = ("", "ground", "", "", "", "timeout", "truncated")
+
+
+class ToyParams(C.Structure):
+    _fields_ = [
+        ("n_envs", _i32), ("kind", _i32), ("autoreset", _i32), ("max_episode_steps", _i32),
+        ("dt", _d), ("t_max", _d), ("integ_dt", _d),
+        ("h0", _d), ("h1", _d), ("area_closed", _d), ("area_open", _d), ("mass", _d),
+        ("c_w", _d), ("rho", _d), ("g", _d),
+        ("car_accel", _d), ("car_v_max", _d), ("car_dangle", _d),
+    ]
+
+
+TOY_LAYOUT_FIELDS = ("total_bytes", "n_pad", "state", "count", "counters", "record", "obs",
+                     "reward", "done", "term", "final_obs")
+
+
+class ToyLayout(C.Structure):
+    _fields_ = [(n, _i64) for n in TOY_LAYOUT_FIELDS]
+
+
 EXPORTS = ("sacenv_abi_version", "sacenv_error_string", "sacenv_boat_layout",
            "sacenv_boat_init", "sacenv_boat_reset", "sacenv_boat_reset_explicit",
-           "sacenv_boat_step", "sacenv_boat_wind_eval")
+           "sacenv_boat_step", "sacenv_boat_wind_eval", "sacenv_toy_layout", "sacenv_toy_init",
+           "sacenv_toy_reset", "sacenv_toy_step", "sacenv_mixed_step")
 
 _LIB = None
 
@@ -86,6 +110,7 @@ def load(path: str | None = None):
             "(hipcc --offload-arch=gfx950). The env has no CPU fallback.")
     lib = C.CDLL(p)
     P = C.POINTER(BoatParams)
+    TP = C.POINTER(ToyParams)
     sig = {
         "sacenv_abi_version": (C.c_int, []),
         "sacenv_error_string": (C.c_char_p, [C.c_int]),
@@ -95,6 +120,11 @@ def load(path: str | None = None):
         "sacenv_boat_reset_explicit": (C.c_int, [P, _p, _p, _i32, _p, _p, _p]),
         "sacenv_boat_step": (C.c_int, [P, _p, _p, _p]),
         "sacenv_boat_wind_eval": (C.c_int, [P, _p, _p, _p, _i32, _p, _p, _p]),
+        "sacenv_toy_layout": (C.c_int, [TP, C.POINTER(ToyLayout)]),
+        "sacenv_toy_init": (C.c_int, [TP, _p, _p]),
+        "sacenv_toy_reset": (C.c_int, [TP, _p, _p, _i32, _p]),
+        "sacenv_toy_step": (C.c_int, [TP, _p, _p]),
+        "sacenv_mixed_step": (C.c_int, [P, _p, _p, TP, C.POINTER(_p), _i32, _p]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -118,4 +148,10 @@ def check(rc: int) -> None:
 def layout(params: BoatParams) -> BoatLayout:
     out = BoatLayout()
     check(load().sacenv_boat_layout(C.byref(params), C.byref(out)))
+    return out
+
+
+def toy_layout(params: ToyParams) -> ToyLayout:
+    out = ToyLayout()
+    check(load().sacenv_toy_layout(C.byref(params), C.byref(out)))
     return out

@@ -38,7 +38,7 @@ class VecBoatEnv:
     autoreset : start the next episode inside ``step`` for envs that end
         (gym vector-env semantics: the returned obs row is the new episode's
         first obs, the terminal obs is ``info['final_obs']``). Episodes are
-        pre-drawn two ahead per env, from the env's own RNG stream in the
+        pre-drawn three ahead per env, from the env's own RNG stream in the
         reference's order, so draws match the reference exactly.
     env_id_offset : global id of this rank's first env (multi-GPU sharding).
     record_knots / record_accel / record_reward64 : extra outputs (tests, shim).

@@ -16,6 +16,10 @@ Fixture kinds
     ``Wind`` tables (``wind.py:26-99``) for many seeds, sampled at fixed
     indices, plus each table's min/max (pins the spline and the min-max
     renormalisation, ``wind.py:87-89``).
+``toy_parachute.npz`` / ``toy_car.npz``
+    The reference toy scripts (``environment/toy_parachute.py``,
+    ``environment/toy_car.py``) run as ``__main__`` with the ``Scope`` plot
+    replaced by a capture of the recorded signals.
 ``recorded_exp<k>.npz``
     The reference's own recorded runs under
     ``ressources/settings_visualized/experiment_setting_<k>/`` converted from
@@ -193,7 +197,41 @@ def convert_recorded(exp):
     print(f"{path}: rows={len(data)} term={term['termination']}")
 
 
+def run_toys():
+    """toy_parachute.py:7-41 / toy_car.py:5-33 as scripts; capture Scope signals."""
+    import runpy
+    import sys
+    H.install_standins()
+    env_dir = os.path.join(H.REF_ROOT, "environment")
+    if env_dir not in sys.path:
+        sys.path.insert(0, env_dir)
+    import control_theory.control_blocks as cb  # reference module
+    captured = {}
+
+    def capture(self, file_name="scope"):
+        captured["signals"] = [list(map(float, s)) for s in self.signals]
+        captured["labels"] = list(self.labels)
+
+    orig = cb.Scope.create_time_scope
+    cb.Scope.create_time_scope = capture
+    try:
+        for name in ("toy_parachute", "toy_car"):
+            captured.clear()
+            runpy.run_path(os.path.join(env_dir, f"{name}.py"), run_name="__main__")
+            sig = np.array(captured["signals"], dtype=np.float64)
+            path = os.path.join(HERE, f"{name}.npz")
+            np.savez_compressed(path, signals=sig, labels=np.array(captured["labels"]))
+            print(f"{path}: signals {sig.shape}")
+    finally:
+        cb.Scope.create_time_scope = orig
+
+
 def main():
+    import sys
+    if sys.argv[1:] == ["toys"]:
+        run_toys()
+        return
+    run_toys()
     for exp in range(1, 7):
         run_seeded(f"exp{exp}_uniform", {"base_settings": {"experiment": exp, "test_mode": 0}},
                    400, "uniform", action_seed=100 + exp)

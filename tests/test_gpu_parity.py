@@ -288,3 +288,80 @@ def test_bad_config_raises(gpu, built_lib):
         VecBoatEnv({"base_settings": {"experiment": 7}}, 4, device=gpu)
     with pytest.raises(ValueError):
         VecBoatEnv({"base_settings": {"experiment": 6}, "wind": {"fixed_points": 3}}, 4, device=gpu)
+
+
+# ---------------------------------------------------------------- toy envs (A17, A18)
+
+def _toy_env(kind, n, **kw):
+    from sacenv.toys import CarEnv, ParachuteEnv
+    return (ParachuteEnv if kind == 1 else CarEnv)(num_envs=n, device="cuda", **kw)
+
+
+@pytest.mark.parametrize("kind,name,tol", [(1, "toy_parachute.npz", 0.0), (2, "toy_car.npz", 1e-5)])
+def test_toy_env_reproduces_reference_script(kind, name, tol, gpu, built_lib):
+    """Every env replays the reference script's recorded signals; the loop ends where the
+    script's does (parachute: ground at iteration 2654; car: t > t_max at 5000)."""
+    sig = golden(name)["signals"]                     # [n_signals, iterations - 1]
+    n_rec = sig.shape[1]
+    env = _toy_env(kind, 100, autoreset=False)
+    rows, terms = [], []
+    for k in range(n_rec + 2):
+        env.step()
+        rows.append(env.state.clone())
+        terms.append(env.term.clone())
+    torch.cuda.synchronize()
+    st = torch.stack(rows).cpu().numpy()              # [steps, 5, N]
+    tm = torch.stack(terms).cpu().numpy()             # [steps, N]
+    cols = [1] if kind == 1 else [2, 3]
+    got = st[1:n_rec + 1][:, cols, :]                 # iterations 2 .. n_rec+1
+    want = sig.T[:, :, None]
+    np.testing.assert_allclose(got, np.broadcast_to(want, got.shape), rtol=0, atol=tol)
+    assert (tm[:n_rec] == 0).all()
+    end_term = 1 if kind == 1 else 5                  # ground / timeout
+    end_step = n_rec + 1 if kind == 1 else n_rec      # parachute breaks before recording
+    assert (tm[end_step] == end_term).all(), tm[end_step - 1: end_step + 2, :3]
+
+
+@pytest.mark.parametrize("kind", [1, 2])
+def test_toy_autoreset_vs_oracle(kind, gpu, built_lib):
+    from toy_oracle import OracleToy
+    N, T = 1000, 150
+    env = _toy_env(kind, N, autoreset=True, max_episode_steps=37)
+    ora = OracleToy(kind, N, max_episode_steps=37, autoreset=True)
+    np.testing.assert_array_equal(env.obs.cpu().numpy(), ora.reset())
+    for k in range(T):
+        env.step()
+        r = ora.step()
+        np.testing.assert_array_equal(env.term.cpu().numpy(), r["term"], err_msg=f"step {k}")
+        np.testing.assert_array_equal(env.done.cpu().numpy().astype(bool), r["done"])
+        np.testing.assert_allclose(env.obs.cpu().numpy(), r["obs"], rtol=1e-6, atol=1e-5)
+        np.testing.assert_allclose(env.state.cpu().numpy(), r["state"], rtol=0, atol=1e-5)
+        d = r["done"]
+        if d.any():
+            np.testing.assert_allclose(env.final_obs.cpu().numpy()[d], r["final_obs"][d], rtol=1e-6, atol=1e-5)
+    np.testing.assert_array_equal(env.counters.cpu().numpy()[2], np.full(N, T // 37))
+
+
+def test_mixed_launch_equals_separate_launches(gpu, built_lib):
+    """One heterogeneous launch (boat helpers + owners + parachute + car waves) produces
+    exactly what the separate per-type launches produce (ragged sizes)."""
+    from sacenv import VecBoatEnv
+    from sacenv.toys import MixedBatch
+    cfg = {"base_settings": {"experiment": 6, "test_mode": 0}}
+    b1 = VecBoatEnv(cfg, 3000, seed=5, device="cuda", max_episode_steps=13, n_helpers=16)
+    b2 = VecBoatEnv(cfg, 3000, seed=5, device="cuda", max_episode_steps=13, n_helpers=16)
+    p1, p2 = _toy_env(1, 1000, max_episode_steps=29), _toy_env(1, 1000, max_episode_steps=29)
+    c1, c2 = _toy_env(2, 777, max_episode_steps=31), _toy_env(2, 777, max_episode_steps=31)
+    mix = MixedBatch(b1, [p1, c1])
+    g = torch.Generator(device="cuda")
+    g.manual_seed(3)
+    for k in range(60):
+        a = torch.rand(3000, generator=g, device="cuda") * 2 - 1
+        mix.step_async(a)
+        b2.step_async(a)
+        p2.step_async()
+        c2.step_async()
+    torch.cuda.synchronize()
+    for x, y in ((b1, b2), (p1, p2), (c1, c2)):
+        assert torch.equal(x.record, y.record)
+        assert torch.equal(x.arena, y.arena)

@@ -34,7 +34,7 @@ def declared_functions():
 def test_library_exports_header(built_lib):
     from sacenv import _lib
     names = declared_functions()
-    assert len(names) == 8
+    assert len(names) == 13
     assert set(names) == set(_lib.EXPORTS)
     for n in names:
         assert hasattr(built_lib, n), n
@@ -62,6 +62,61 @@ def test_argument_errors_without_gpu(built_lib):
     p.n_helpers = 256
     p.autoreset = 1
     assert built_lib.sacenv_boat_reset_explicit(ctypes.byref(p), 1, 1, 1, 1, None, None) == -6
+
+
+def test_toy_argument_errors_without_gpu(built_lib):
+    from sacenv import _lib
+    from sacenv.toys import ParachuteConfig, make_toy_params
+    p = make_toy_params(_lib.TOY_PARACHUTE, ParachuteConfig(), 4)
+    assert built_lib.sacenv_toy_step(ctypes.byref(p), None, None) == -1
+    p.kind = 3
+    assert built_lib.sacenv_toy_step(ctypes.byref(p), None, None) == -2
+    p.kind = _lib.TOY_CAR
+    p.n_envs = 0
+    assert built_lib.sacenv_toy_init(ctypes.byref(p), None, None) == -4
+    p.n_envs = 4
+    assert built_lib.sacenv_mixed_step(None, None, None, ctypes.byref(p), None, 3, None) == -4
+    assert built_lib.sacenv_mixed_step(None, None, None, None, None, 1, None) == -1
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 32768])
+def test_toy_layout(built_lib, n):
+    from sacenv import _lib
+    from sacenv.toys import CarConfig, make_toy_params
+    L = _lib.toy_layout(make_toy_params(_lib.TOY_CAR, CarConfig(), n))
+    np_ = L.n_pad
+    assert np_ % 64 == 0 and n <= np_ < n + 64
+    sizes = {"state": 40, "count": 4, "counters": 12, "obs": 8, "reward": 4, "done": 1, "term": 1,
+             "final_obs": 8}
+    spans = sorted((getattr(L, f), getattr(L, f) + w * np_, f) for f, w in sizes.items())
+    for (a0, a1, f), (b0, b1, g) in zip(spans, spans[1:]):
+        assert a1 <= b0, (f, g)
+    assert L.record == L.obs and L.term + np_ == L.record + 14 * np_
+    assert spans[-1][1] <= L.total_bytes
+
+
+def test_ctypes_structs_match_c_layout(tmp_path):
+    """offsetof/sizeof of every ABI struct, from gcc on include/sacenv.h, vs the ctypes mirrors."""
+    from sacenv import _lib
+    structs = {"SacenvBoatParams": _lib.BoatParams, "SacenvBoatLayout": _lib.BoatLayout,
+               "SacenvToyParams": _lib.ToyParams, "SacenvToyLayout": _lib.ToyLayout}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "sacenv.h"', "int main(void) {"]
+    for cname, py in structs.items():
+        lines.append(f'printf("{cname} sizeof %zu\\n", sizeof({cname}));')
+        for fname, _ in py._fields_:
+            lines.append(f'printf("{cname} {fname} %zu\\n", offsetof({cname}, {fname}));')
+    lines.append("return 0; }")
+    src = tmp_path / "probe.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)],
+                   check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    got = {tuple(l.split()[:2]): int(l.split()[2]) for l in out if l.strip()}
+    for cname, py in structs.items():
+        assert got[(cname, "sizeof")] == ctypes.sizeof(py), cname
+        for fname, _ in py._fields_:
+            assert got[(cname, fname)] == getattr(py, fname).offset, (cname, fname)
 
 
 @pytest.mark.parametrize("n", [1, 63, 64, 65536, 100000])

@@ -97,3 +97,10 @@ def test_oracle_replays_recorded_episode(exp):
     assert r["term"][0] == 1  # reached_goal on the step after the last recorded row
     if exp == 6:
         assert abs(r["ep_reward"][0] - float(z["episode_reward"])) < 1e-9
+
+
+@pytest.mark.parametrize("kind,name", [(1, "toy_parachute.npz"), (2, "toy_car.npz")])
+def test_toy_oracle_matches_reference_scripts(kind, name):
+    """The toy oracle reproduces the signals the reference scripts record, bit for bit."""
+    from toy_oracle import script_signals
+    np.testing.assert_array_equal(script_signals(kind), golden(name)["signals"])
