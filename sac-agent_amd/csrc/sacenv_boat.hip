@@ -1228,7 +1228,8 @@ __device__ __forceinline__ void owner_load(const Arena& A, OwnerLds& l, int ob, 
 __device__ __forceinline__ void st16(void* dst, f4v v) { *reinterpret_cast<f4v*>(dst) = v; }
 
 // the mirror image for the outputs: 7 store instructions + 3 for the obs rows
-__device__ __forceinline__ void owner_store(const Arena& A, const OwnerLds& l, int ob, int lane) {
+__device__ __forceinline__ void owner_store(const Arena& A, const OwnerLds& l, int ob, int lane,
+                                            bool store_cons) {
   const int half = lane >> 5, c = lane & 31;
   const int64_t e0 = (int64_t)ob * kWave;
 #pragma unroll
@@ -1244,7 +1245,7 @@ __device__ __forceinline__ void owner_store(const Arena& A, const OwnerLds& l, i
                                  : reinterpret_cast<const f4v*>(l.reward + 4 * j);
     st16(dst, *src);
   }
-  if (lane < 24) {  // lanes 0-15: cons; 16-19: done; 20-23: term
+  if (lane < 24 && (store_cons || lane >= 16)) {  // lanes 0-15: cons; 16-19: done; 20-23: term
     char* dst;
     const f4v* src;
     if (lane < 16) {
@@ -1428,7 +1429,8 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
 #pragma unroll
   for (int k = 0; k < SACENV_OBS_DIM; ++k) l.obs[lane * SACENV_OBS_DIM + k] = o.v[k];
   __syncthreads();
-  owner_store(A, l, ob, lane);
+  // cons changes only for restarting envs: its row is stored only then
+  owner_store(A, l, ob, lane, __ballot(restart) != 0ull);
   if (p.autoreset) {
     // this launch's ended envs, for the next launch's helpers (every wave
     // rewrites its word each launch, so the ring needs no clearing)

@@ -11,6 +11,6 @@ B="timeout -k 10 120 python bench.py --steps 2000 --warmup 300 --no-cpu-baseline
 for v in ${VARIANTS:-base prev}; do
   if [ "$v" != "base" ]; then export SACENV_LIB=$PWD/sac-agent_amd/build/libsacenv_$v.so; else unset SACENV_LIB; fi
   $B > gpurun_out/sw_$v.json 2>/dev/null || exit 1
-  python -c "import json;d=json.load(open('gpurun_out/sw_$v.json'));print('$v', round(d['value']/1e9,3), 'G/s', round(d['ms_per_step']*1e3,2), 'us/step kernel', round(d['roofline']['kernel_us_median'],2))"
+  python -c "import json;d=json.load(open('gpurun_out/sw_$v.json'));print('$v', round(d['value']/1e9,3), 'G/s', round(d['ms_per_step']*1e3,2), 'us/step kernel', round(d['roofline']['kernel_avg_us'],2))"
 done
 echo sweep done

@@ -13,13 +13,14 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "sac-agent_amd")
-LIB = os.path.join(PKG, "build", "libsacenv_stamps.so")
+LIB = os.path.join(PKG, "build", os.environ.get("STAMP_LIB", "libsacenv_stamps.so"))
 
 
 def build():
     sys.path.insert(0, ROOT)
     import __graft_entry__ as g
-    cmd = [g._hipcc(), *g.HIPCC_FLAGS, "-DSACENV_STAMPS", "-I", os.path.join(ROOT, "include"),
+    extra = os.environ.get("STAMP_DEFINES", "").split()
+    cmd = [g._hipcc(), *g.HIPCC_FLAGS, "-DSACENV_STAMPS", *extra, "-I", os.path.join(ROOT, "include"),
            os.path.join(PKG, "csrc", "sacenv_boat.hip"), "-o", LIB]
     subprocess.run(cmd, check=True)
 
