@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SACENV_ABI_VERSION 4
+#define SACENV_ABI_VERSION 5
 #define SACENV_OBS_DIM 11      /* Boat.return_state, boat_env.py:308-323 */
 #define SACENV_MT_N 624        /* MT19937 words per env (numpy legacy RNG) */
 #define SACENV_MAX_KNOTS 16    /* wind.fixed_points upper bound */
@@ -249,6 +249,54 @@ int sacenv_toy_step(const SacenvToyParams *p, void *arena, void *stream);
 int sacenv_mixed_step(const SacenvBoatParams *bp, void *boat_arena, const float *boat_action,
                       const SacenvToyParams *toy_params, void *const *toy_arenas, int32_t n_toys,
                       void *stream);
+
+/* ------------------------------------------------------------------------
+ * Device replay buffer: agent/buffer.py:3-35 ReplayBuffer (SURVEY.md §8(f)
+ * rank 1), the consumer of the step records. Same ring semantics
+ * (index = mem_cntr % mem_size, buffer.py:14-22) and the same sampling
+ * stream: np.random.choice(min(mem_cntr, mem_size), batch) (buffer.py:27)
+ * = numpy-legacy masked-rejection randint on an MT19937 state held in the
+ * arena, so a buffer seeded like np.random.seed(s) draws the reference's
+ * batch indices bit for bit. */
+
+typedef struct SacenvReplayParams {
+  int64_t mem_size;        /* ReplayBuffer(max_size) (buffer.py:5) */
+  int32_t obs_dim;         /* prod(input_shape) */
+  int32_t act_dim;         /* n_actions */
+  int32_t reward_f32;      /* 1: store() reads f32 rewards (VecBoatEnv), 0: f64 */
+  uint32_t terminal_mask;  /* terminal = (terminal_mask >> code) & 1 for the u8 codes store()
+                              receives: 2 = "code 1" (env term: reached_goal, main.py:83-88;
+                              or a 0/1 done array) */
+} SacenvReplayParams;
+
+typedef struct SacenvReplayLayout {
+  int64_t total_bytes;
+  int64_t state;      /* f32 [mem_size][obs_dim] state_memory (buffer.py:7) */
+  int64_t new_state;  /* f32 [mem_size][obs_dim] new_state_memory (:8) */
+  int64_t action;     /* f32 [mem_size][act_dim] action_memory (:9) */
+  int64_t reward;     /* f64 [mem_size] reward_memory (:10) */
+  int64_t terminal;   /* u8 [mem_size] terminal_memory (:11) */
+  int64_t mem_cntr;   /* i64 transitions stored (:6) */
+  int64_t mt_key;     /* u32 [624] sampling stream state */
+  int64_t mt_pos;     /* i32 next word (624: twist first) */
+} SacenvReplayLayout;
+
+int sacenv_replay_layout(const SacenvReplayParams *p, SacenvReplayLayout *out);
+/* mem_cntr = 0 and the sampling stream = np.random.seed(seed) */
+int sacenv_replay_init(const SacenvReplayParams *p, void *arena, uint32_t seed, void *stream);
+/* store_transition (buffer.py:13-22) for n transitions in order: row i goes to
+ * (mem_cntr + i) % mem_size; new_state of rows whose code is nonzero is taken
+ * from final_state when it is non-NULL (auto-reset envs: the terminal obs).
+ * All pointers are device pointers; reward is f32 or f64 per params. */
+int sacenv_replay_store(const SacenvReplayParams *p, void *arena, int64_t n, const float *state,
+                        const float *action, const void *reward, const float *new_state,
+                        const float *final_state, const uint8_t *code, void *stream);
+/* sample_buffer(batch) (buffer.py:24-35): indices (i64) and the gathered rows.
+ * Any output but idx may be NULL. An empty buffer is an error (SACENV_E_SIZE:
+ * np.random.choice(0, n) raises) detected on the host from `stored`. */
+int sacenv_replay_sample(const SacenvReplayParams *p, void *arena, int32_t batch, int64_t stored,
+                         int64_t *idx, float *state, float *action, double *reward,
+                         float *new_state, uint8_t *terminal, void *stream);
 
 #ifdef __cplusplus
 }

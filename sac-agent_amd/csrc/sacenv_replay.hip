@@ -1,0 +1,278 @@
+// sacenv_replay.hip — gfx950 device replay buffer + C ABI (include/sacenv.h).
+//
+// agent/buffer.py:3-35 on the GPU. The step records of every env are appended
+// in env order with the reference's ring rule (index = mem_cntr % mem_size,
+// buffer.py:14). Sampling is np.random.choice(min(mem_cntr, mem_size), batch)
+// (buffer.py:27), which numpy's legacy RandomState computes as a
+// masked-rejection randint on 32-bit MT19937 words. One wave draws the whole
+// batch: 64 candidate words per window, a ballot keeps the accepted ones in
+// order, and the stream advances by exactly the words numpy consumes. The
+// gather of the sampled rows is a plain element-parallel copy.
+//
+// The buffer's arrays are row-major per transition (the policy reads whole
+// rows); the store is coalesced along the flattened row-major element index.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sacenv.h"
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr int kMtN = SACENV_MT_N;
+constexpr int kMtM = 397;
+constexpr uint32_t kMtUpper = 0x80000000u;
+constexpr uint32_t kMtLower = 0x7fffffffu;
+constexpr uint32_t kMtMatrixA = 0x9908b0dfu;
+
+#include "mt19937.h"
+
+__host__ __device__ inline int64_t align256(int64_t x) { return (x + 255) / 256 * 256; }
+
+__host__ __device__ inline void replay_layout(const SacenvReplayParams& p, SacenvReplayLayout* o) {
+  const int64_t M = p.mem_size;
+  int64_t off = 0;
+  o->state = off;
+  off = align256(off + 4 * M * p.obs_dim);
+  o->new_state = off;
+  off = align256(off + 4 * M * p.obs_dim);
+  o->action = off;
+  off = align256(off + 4 * M * p.act_dim);
+  o->reward = off;
+  off = align256(off + 8 * M);
+  o->terminal = off;
+  off = align256(off + M);
+  o->mem_cntr = off;
+  off += 256;
+  o->mt_key = off;
+  off = align256(off + 4 * kMtN);
+  o->mt_pos = off;
+  off += 256;
+  o->total_bytes = off;
+}
+
+struct RB {
+  char* b;
+  SacenvReplayLayout L;
+  __device__ float* state() const { return reinterpret_cast<float*>(b + L.state); }
+  __device__ float* new_state() const { return reinterpret_cast<float*>(b + L.new_state); }
+  __device__ float* action() const { return reinterpret_cast<float*>(b + L.action); }
+  __device__ double* reward() const { return reinterpret_cast<double*>(b + L.reward); }
+  __device__ uint8_t* terminal() const { return reinterpret_cast<uint8_t*>(b + L.terminal); }
+  __device__ int64_t* cntr() const { return reinterpret_cast<int64_t*>(b + L.mem_cntr); }
+  __device__ uint32_t* key() const { return reinterpret_cast<uint32_t*>(b + L.mt_key); }
+  __device__ int32_t* pos() const { return reinterpret_cast<int32_t*>(b + L.mt_pos); }
+};
+
+struct DrawLds {
+  uint32_t blk[2][kMtN];
+};
+
+__global__ void __launch_bounds__(kWave) k_rb_init(RB r, uint32_t seed) {
+  if (threadIdx.x != 0) return;
+  uint32_t x = seed;  // init_genrand (numpy RandomState._legacy_seeding)
+  for (int i = 0; i < kMtN; ++i) {
+    r.key()[i] = x;
+    x = 1812433253u * (x ^ (x >> 30)) + (uint32_t)(i + 1);
+  }
+  *r.pos() = kMtN;
+  *r.cntr() = 0;
+}
+
+// store_transition for rows [0, n): row i -> (mem_cntr + i) % M. Rows that a
+// later row of the same call overwrites (i < n - M) are skipped, so the ring
+// ends exactly as n sequential calls leave it.
+__global__ void __launch_bounds__(256) k_rb_store(SacenvReplayParams p, RB r, int64_t n,
+                                                  const float* __restrict__ state,
+                                                  const float* __restrict__ action,
+                                                  const void* __restrict__ reward,
+                                                  const float* __restrict__ new_state,
+                                                  const float* __restrict__ final_state,
+                                                  const uint8_t* __restrict__ code) {
+  const int64_t M = p.mem_size, c0 = *r.cntr();
+  const int64_t first = n > M ? n - M : 0;
+  const int D = p.obs_dim, A = p.act_dim;
+  const int64_t total = (n - first) * (D + A + 1);  // D: state + new_state, A: action, 1: scalars
+  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < total;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    // element-major over the three row arrays, then one scalar column per row
+    int64_t i, dst;
+    if (q < (n - first) * D) {
+      i = first + q / D;
+      const int k = (int)(q - (i - first) * D);
+      dst = ((c0 + i) % M) * D + k;
+      r.state()[dst] = state[i * D + k];
+      const uint8_t cd = code[i];
+      const float* src = (final_state != nullptr && cd != 0) ? final_state : new_state;
+      r.new_state()[dst] = src[i * D + k];
+    } else if (q < (n - first) * (D + A)) {
+      const int64_t qq = q - (n - first) * D;
+      i = first + qq / A;
+      const int k = (int)(qq - (i - first) * A);
+      r.action()[((c0 + i) % M) * A + k] = action[i * A + k];
+    } else {
+      i = first + (q - (n - first) * (D + A));
+      const int64_t row = (c0 + i) % M;
+      r.reward()[row] = p.reward_f32 ? (double)static_cast<const float*>(reward)[i]
+                                     : static_cast<const double*>(reward)[i];
+      const uint32_t cd = code[i];
+      r.terminal()[row] = (uint8_t)((p.terminal_mask >> (cd < 31 ? cd : 31)) & 1u);
+    }
+  }
+}
+
+__global__ void k_rb_advance(RB r, int64_t n) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) *r.cntr() += n;  // buffer.py:22
+}
+
+// np.random.choice(max_mem, batch) with replace=True, p=None: numpy legacy
+// randint(0, max_mem) -> masked rejection on 32-bit words (rng = max_mem-1;
+// rng == 0 draws nothing). One wave; words in order, accepted words fill the
+// batch in order, the stream stops after the batch-th accepted word.
+__global__ void __launch_bounds__(kWave) k_rb_draw(SacenvReplayParams p, RB r, int batch,
+                                                   int64_t* __restrict__ idx) {
+  __shared__ DrawLds l;
+  const int lane = threadIdx.x;
+  const int64_t cnt = *r.cntr();
+  const int64_t max_mem = cnt < p.mem_size ? cnt : p.mem_size;
+  const uint64_t rng = (uint64_t)(max_mem - 1);
+  if (rng == 0) {  // numpy: off + 0, no words consumed
+    for (int i = lane; i < batch; i += kWave) idx[i] = 0;
+    return;
+  }
+  uint32_t mask = (uint32_t)rng;
+  mask |= mask >> 1;
+  mask |= mask >> 2;
+  mask |= mask >> 4;
+  mask |= mask >> 8;
+  mask |= mask >> 16;
+  MtStream st;
+  st.gkey = r.key();
+  st.pos = *r.pos();
+  st.cur = 0;
+  st.loaded = false;
+  st.nxt_valid = false;
+  st.advanced = false;
+  int filled = 0;
+  while (filled < batch) {
+    const uint32_t w = mt_fetch(st, l, lane) & mask;
+    const bool acc = w <= (uint32_t)rng;
+    const unsigned long long bal = __ballot(acc);
+    const int before = __popcll(bal & ((1ull << lane) - 1ull));
+    const int take = batch - filled;
+    if (acc && before < take) idx[filled + before] = (int64_t)w;
+    const int total = __popcll(bal);
+    if (total >= take) {
+      // the take-th accepted word ends the draw: consume up to and including it
+      unsigned long long b = bal;
+      for (int t = 1; t < take; ++t) b &= b - 1ull;
+      st.pos += __ffsll((long long)b);
+      filled = batch;
+    } else {
+      st.pos += kWave;
+      filled += total;
+    }
+  }
+  mt_finish(st, l, r.pos(), lane);
+}
+
+__global__ void __launch_bounds__(256) k_rb_gather(SacenvReplayParams p, RB r, int batch,
+                                                   const int64_t* __restrict__ idx, float* __restrict__ st,
+                                                   float* __restrict__ ac, double* __restrict__ rw,
+                                                   float* __restrict__ ns, uint8_t* __restrict__ tm) {
+  const int D = p.obs_dim, A = p.act_dim;
+  const int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t nd = (int64_t)batch * D, na = (int64_t)batch * A;
+  if (q < nd) {
+    const int64_t i = q / D, k = q - i * D, row = idx[i];
+    if (st) st[q] = r.state()[row * D + k];
+    if (ns) ns[q] = r.new_state()[row * D + k];
+  } else if (q < nd + na) {
+    const int64_t qq = q - nd, i = qq / A, k = qq - i * A;
+    if (ac) ac[qq] = r.action()[idx[i] * A + k];
+  } else if (q < nd + na + batch) {
+    const int64_t i = q - nd - na, row = idx[i];
+    if (rw) rw[i] = r.reward()[row];
+    if (tm) tm[i] = r.terminal()[row];
+  }
+}
+
+int check_replay(const SacenvReplayParams* p) {
+  if (p == nullptr) return SACENV_E_NULL;
+  if (p->mem_size <= 0 || p->mem_size > 0xFFFFFFFFLL || p->obs_dim <= 0 || p->act_dim <= 0)
+    return SACENV_E_SIZE;  // randint on 32-bit words: max_mem - 1 <= 0xFFFFFFFF
+  return SACENV_OK;
+}
+
+RB make_rb(const SacenvReplayParams& p, void* arena) {
+  RB r;
+  r.b = static_cast<char*>(arena);
+  replay_layout(p, &r.L);
+  return r;
+}
+
+int status() {
+  const hipError_t err = hipGetLastError();
+  return err == hipSuccess ? SACENV_OK : (int)err;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sacenv_replay_layout(const SacenvReplayParams* p, SacenvReplayLayout* out) {
+  const int rc = check_replay(p);
+  if (rc) return rc;
+  if (out == nullptr) return SACENV_E_NULL;
+  replay_layout(*p, out);
+  return SACENV_OK;
+}
+
+int sacenv_replay_init(const SacenvReplayParams* p, void* arena, uint32_t seed, void* stream) {
+  const int rc = check_replay(p);
+  if (rc) return rc;
+  if (arena == nullptr) return SACENV_E_NULL;
+  hipLaunchKernelGGL(k_rb_init, dim3(1), dim3(kWave), 0, (hipStream_t)stream, make_rb(*p, arena), seed);
+  return status();
+}
+
+int sacenv_replay_store(const SacenvReplayParams* p, void* arena, int64_t n, const float* state,
+                        const float* action, const void* reward, const float* new_state,
+                        const float* final_state, const uint8_t* code, void* stream) {
+  int rc = check_replay(p);
+  if (rc) return rc;
+  if (n < 0) return SACENV_E_SIZE;
+  if (n == 0) return SACENV_OK;
+  if (!arena || !state || !action || !reward || !new_state || !code) return SACENV_E_NULL;
+  const int64_t rows = n > p->mem_size ? p->mem_size : n;
+  const int64_t total = rows * ((int64_t)p->obs_dim + p->act_dim + 1);
+  int64_t blocks = (total + 255) / 256;
+  if (blocks > 65535) blocks = 65535;
+  const RB r = make_rb(*p, arena);
+  hipLaunchKernelGGL(k_rb_store, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *p, r, n, state,
+                     action, reward, new_state, final_state, code);
+  if ((rc = status())) return rc;
+  hipLaunchKernelGGL(k_rb_advance, dim3(1), dim3(kWave), 0, (hipStream_t)stream, r, n);
+  return status();
+}
+
+int sacenv_replay_sample(const SacenvReplayParams* p, void* arena, int32_t batch, int64_t stored,
+                         int64_t* idx, float* state, float* action, double* reward, float* new_state,
+                         uint8_t* terminal, void* stream) {
+  int rc = check_replay(p);
+  if (rc) return rc;
+  if (batch < 0) return SACENV_E_SIZE;
+  if (stored <= 0) return SACENV_E_SIZE;  // np.random.choice(0, n) raises
+  if (arena == nullptr || idx == nullptr) return SACENV_E_NULL;
+  if (batch == 0) return SACENV_OK;
+  const RB r = make_rb(*p, arena);
+  hipLaunchKernelGGL(k_rb_draw, dim3(1), dim3(kWave), 0, (hipStream_t)stream, *p, r, batch, idx);
+  if ((rc = status())) return rc;
+  const int64_t total = (int64_t)batch * (p->obs_dim + p->act_dim + 1);
+  hipLaunchKernelGGL(k_rb_gather, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *p,
+                     r, batch, idx, state, action, reward, new_state, terminal);
+  return status();
+}
+
+}  // extern "C"

@@ -11,7 +11,7 @@ import os
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # .../sac-agent_amd
 LIB_PATH = os.environ.get("SACENV_LIB", os.path.join(PKG_ROOT, "build", "libsacenv.so"))
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 OBS_DIM = 11
 MT_N = 624
 MAX_KNOTS = 16
@@ -86,10 +86,24 @@ class ToyLayout(C.Structure):
     _fields_ = [(n, _i64) for n in TOY_LAYOUT_FIELDS]
 
 
+class ReplayParams(C.Structure):
+    _fields_ = [("mem_size", _i64), ("obs_dim", _i32), ("act_dim", _i32), ("reward_f32", _i32),
+                ("terminal_mask", C.c_uint32)]
+
+
+REPLAY_LAYOUT_FIELDS = ("total_bytes", "state", "new_state", "action", "reward", "terminal",
+                        "mem_cntr", "mt_key", "mt_pos")
+
+
+class ReplayLayout(C.Structure):
+    _fields_ = [(n, _i64) for n in REPLAY_LAYOUT_FIELDS]
+
+
 EXPORTS = ("sacenv_abi_version", "sacenv_error_string", "sacenv_boat_layout",
            "sacenv_boat_init", "sacenv_boat_reset", "sacenv_boat_reset_explicit",
            "sacenv_boat_step", "sacenv_boat_wind_eval", "sacenv_toy_layout", "sacenv_toy_init",
-           "sacenv_toy_reset", "sacenv_toy_step", "sacenv_mixed_step")
+           "sacenv_toy_reset", "sacenv_toy_step", "sacenv_mixed_step", "sacenv_replay_layout",
+           "sacenv_replay_init", "sacenv_replay_store", "sacenv_replay_sample")
 
 _LIB = None
 
@@ -111,6 +125,7 @@ def load(path: str | None = None):
     lib = C.CDLL(p)
     P = C.POINTER(BoatParams)
     TP = C.POINTER(ToyParams)
+    RP = C.POINTER(ReplayParams)
     sig = {
         "sacenv_abi_version": (C.c_int, []),
         "sacenv_error_string": (C.c_char_p, [C.c_int]),
@@ -125,6 +140,10 @@ def load(path: str | None = None):
         "sacenv_toy_reset": (C.c_int, [TP, _p, _p, _i32, _p]),
         "sacenv_toy_step": (C.c_int, [TP, _p, _p]),
         "sacenv_mixed_step": (C.c_int, [P, _p, _p, TP, C.POINTER(_p), _i32, _p]),
+        "sacenv_replay_layout": (C.c_int, [RP, C.POINTER(ReplayLayout)]),
+        "sacenv_replay_init": (C.c_int, [RP, _p, C.c_uint32, _p]),
+        "sacenv_replay_store": (C.c_int, [RP, _p, _i64, _p, _p, _p, _p, _p, _p, _p]),
+        "sacenv_replay_sample": (C.c_int, [RP, _p, _i32, _i64, _p, _p, _p, _p, _p, _p, _p]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -154,4 +173,10 @@ def layout(params: BoatParams) -> BoatLayout:
 def toy_layout(params: ToyParams) -> ToyLayout:
     out = ToyLayout()
     check(load().sacenv_toy_layout(C.byref(params), C.byref(out)))
+    return out
+
+
+def replay_layout(params: ReplayParams) -> ReplayLayout:
+    out = ReplayLayout()
+    check(load().sacenv_replay_layout(C.byref(params), C.byref(out)))
     return out

@@ -1,0 +1,152 @@
+"""Device replay buffer: agent/buffer.py:3-35 on the GPU.
+
+Two front ends over one C-ABI arena (libsacenv.so, gfx950):
+
+* ``DeviceReplayBuffer``: batched and device-resident. ``store_batch`` appends
+  the transitions of all envs of a step (one launch). ``store_env_step`` takes a
+  ``VecBoatEnv`` step directly: the new_state of an env that auto-reset is its
+  terminal obs (``info['final_obs']``), and terminal = reached_goal
+  (main.py:83-88). ``sample`` returns device tensors. Sampling follows
+  ``np.random.choice`` on the buffer's own MT19937 stream, seeded like
+  ``np.random.seed(seed)``.
+* ``ReplayBuffer``: the drop-in for ``agent.buffer.ReplayBuffer``. It has the
+  same constructor, ``store_transition`` and ``sample_buffer`` (numpy in,
+  numpy out), and samples from numpy's GLOBAL RNG stream: the state is
+  uploaded, drawn on the GPU and written back, so the batches equal the
+  reference's for the same ``np.random`` state.
+
+There is no CPU path: without libsacenv.so these classes raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _lib
+
+TERMINAL_GOAL = 1 << 1   # terminal = (code == 1): env term reached_goal, or a 0/1 done array
+
+
+class DeviceReplayBuffer:
+    def __init__(self, max_size: int, input_shape, n_actions: int, *, device=None, seed: int = 0,
+                 reward_f32: bool = True, terminal_mask: int = TERMINAL_GOAL):
+        self.lib = _lib.load()
+        self.device = torch.device(device if device is not None else "cuda")
+        if self.device.type != "cuda":
+            raise RuntimeError("DeviceReplayBuffer runs on a GPU (HIP); no CPU path")
+        shape = (int(input_shape),) if np.isscalar(input_shape) else tuple(int(d) for d in input_shape)
+        self.input_shape = shape
+        self.mem_size = int(max_size)
+        self.n_actions = int(n_actions)
+        p = _lib.ReplayParams()
+        p.mem_size, p.obs_dim, p.act_dim = self.mem_size, int(np.prod(shape)), self.n_actions
+        p.reward_f32, p.terminal_mask = int(bool(reward_f32)), int(terminal_mask)
+        self.params = p
+        self._pp = C.byref(p)
+        self.layout = L = _lib.replay_layout(p)
+        self.arena = torch.zeros(int(L.total_bytes), dtype=torch.uint8, device=self.device)
+        M, D, A = self.mem_size, p.obs_dim, self.n_actions
+
+        def view(off, dtype, *shp):
+            esz = torch.empty((), dtype=dtype).element_size()
+            return self.arena[off: off + int(np.prod(shp)) * esz].view(dtype).view(*shp)
+
+        self.state_memory = view(L.state, torch.float32, M, *shape)
+        self.new_state_memory = view(L.new_state, torch.float32, M, *shape)
+        self.action_memory = view(L.action, torch.float32, M, A)
+        self.reward_memory = view(L.reward, torch.float64, M)
+        self.terminal_memory = view(L.terminal, torch.uint8, M)
+        self._cntr = view(L.mem_cntr, torch.int64, 1)
+        self.mt_key = view(L.mt_key, torch.int32, _lib.MT_N)
+        self.mt_pos = view(L.mt_pos, torch.int32, 1)
+        self.mem_cntr = 0                        # host mirror (buffer.py:6)
+        _lib.check(self.lib.sacenv_replay_init(self._pp, self.arena.data_ptr(), int(seed) & 0xFFFFFFFF,
+                                               self.stream))
+
+    @property
+    def stream(self) -> int:
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def _dev(self, x, dtype):
+        t = torch.as_tensor(x, device=self.device)
+        return t.to(dtype).contiguous() if t.dtype != dtype else t.contiguous()
+
+    def store_batch(self, state, action, reward, new_state, code, final_state=None) -> None:
+        """Append n transitions (rows in order, buffer.py:13-22). ``code`` is u8:
+        terminal = (terminal_mask >> code) & 1; rows with code != 0 take new_state
+        from ``final_state`` if it is given."""
+        s = self._dev(state, torch.float32)
+        n = s.shape[0]
+        a = self._dev(action, torch.float32).reshape(n, -1)
+        r = self._dev(reward, torch.float32 if self.params.reward_f32 else torch.float64).reshape(n)
+        ns = self._dev(new_state, torch.float32)
+        c = self._dev(code, torch.uint8).reshape(n)
+        fs = None if final_state is None else self._dev(final_state, torch.float32)
+        if a.shape[1] != self.n_actions or s.shape != ns.shape:
+            raise ValueError("transition shapes do not match the buffer")
+        _lib.check(self.lib.sacenv_replay_store(
+            self._pp, self.arena.data_ptr(), n, s.data_ptr(), a.data_ptr(), r.data_ptr(), ns.data_ptr(),
+            None if fs is None else fs.data_ptr(), c.data_ptr(), self.stream))
+        self._keep = (s, a, r, ns, c, fs)
+        self.mem_cntr += n
+
+    def store_env_step(self, prev_obs, actions, env) -> None:
+        """The transitions of one ``VecBoatEnv.step``: (prev_obs, actions, reward,
+        obs or final_obs for envs that ended, term code)."""
+        self.store_batch(prev_obs, actions, env.reward, env.obs, env.term, final_state=env.final_obs)
+
+    def sample(self, batch_size: int):
+        """sample_buffer (buffer.py:24-35) on device: (states, actions, rewards, states_, dones, idx)."""
+        B = int(batch_size)
+        if self.mem_cntr == 0 and B > 0:
+            raise ValueError("a must be greater than 0 unless no samples are taken")
+        idx = torch.empty(B, dtype=torch.int64, device=self.device)
+        st = torch.empty((B, *self.input_shape), dtype=torch.float32, device=self.device)
+        ns = torch.empty_like(st)
+        ac = torch.empty((B, self.n_actions), dtype=torch.float32, device=self.device)
+        rw = torch.empty(B, dtype=torch.float64, device=self.device)
+        tm = torch.empty(B, dtype=torch.uint8, device=self.device)
+        _lib.check(self.lib.sacenv_replay_sample(
+            self._pp, self.arena.data_ptr(), B, self.mem_cntr, idx.data_ptr(), st.data_ptr(),
+            ac.data_ptr(), rw.data_ptr(), ns.data_ptr(), tm.data_ptr(), self.stream))
+        return st, ac, rw, ns, tm.bool(), idx
+
+
+class ReplayBuffer:
+    """Drop-in for agent.buffer.ReplayBuffer (buffer.py:3-35), GPU-backed, numpy I/O,
+    sampling from numpy's global RNG stream like ``np.random.choice`` (buffer.py:27)."""
+
+    def __init__(self, max_size, input_shape, n_actions, *, device=None):
+        self._rb = DeviceReplayBuffer(max_size, input_shape, n_actions, device=device,
+                                      reward_f32=False, terminal_mask=TERMINAL_GOAL)
+        self.mem_size = self._rb.mem_size
+
+    @property
+    def mem_cntr(self) -> int:
+        return self._rb.mem_cntr
+
+    def store_transition(self, state, action, reward, state_, done):
+        rb = self._rb
+        one = lambda x, dt: np.asarray(x, dtype=dt).reshape(1, -1)  # noqa: E731
+        rb.store_batch(torch.from_numpy(one(state, np.float32)), torch.from_numpy(one(action, np.float32)),
+                       torch.tensor([float(reward)], dtype=torch.float64),
+                       torch.from_numpy(one(state_, np.float32)),
+                       torch.tensor([1 if done else 0], dtype=torch.uint8))
+
+    def sample_buffer(self, batch_size):
+        rb = self._rb
+        st = np.random.get_state(legacy=True)
+        rb.mt_key.copy_(torch.from_numpy(np.asarray(st[1], dtype=np.uint32).view(np.int32)))
+        rb.mt_pos.fill_(int(st[2]))
+        states, actions, rewards, states_, dones, _ = rb.sample(batch_size)
+        torch.cuda.synchronize(rb.device)
+        key = rb.mt_key.cpu().numpy().view(np.uint32).copy()
+        np.random.set_state((st[0], key, int(rb.mt_pos.item()), st[3], st[4]))
+        # the reference's memory arrays are float64 (np.zeros default, buffer.py:7-10)
+        return (states.cpu().numpy().astype(np.float64), actions.cpu().numpy().astype(np.float64),
+                rewards.cpu().numpy(), states_.cpu().numpy().astype(np.float64), dones.cpu().numpy())
+
+
+__all__ = ["DeviceReplayBuffer", "ReplayBuffer", "TERMINAL_GOAL"]

@@ -20,6 +20,10 @@ Fixture kinds
     The reference toy scripts (``environment/toy_parachute.py``,
     ``environment/toy_car.py``) run as ``__main__`` with the ``Scope`` plot
     replaced by a capture of the recorded signals.
+``replay_buffer.npz``
+    The reference ``ReplayBuffer`` (``agent/buffer.py:3-35``): stored
+    transitions, then ``sample_buffer`` under a seeded global numpy stream
+    (batches and the RNG state after sampling), at several fill levels.
 ``recorded_exp<k>.npz``
     The reference's own recorded runs under
     ``ressources/settings_visualized/experiment_setting_<k>/`` converted from
@@ -226,12 +230,46 @@ def run_toys():
         cb.Scope.create_time_scope = orig
 
 
+def run_replay():
+    """agent/buffer.py ReplayBuffer: stores + np.random.choice sampling from the
+    global stream, several fill levels (partial, wrapped, one row)."""
+    H.install_standins()
+    from agent.buffer import ReplayBuffer  # reference module
+    cases = {"partial": (1000, 300, 64, 11), "wrapped": (1000, 2500, 1024, 12),
+             "one_row": (50, 1, 16, 13), "small": (7, 5, 300, 14)}
+    out = {}
+    for name, (M, n_store, batch, seed) in cases.items():
+        rng = np.random.default_rng(seed)
+        rb = ReplayBuffer(M, (11,), 1)
+        S = rng.standard_normal((n_store, 11)).astype(np.float32)
+        S2 = rng.standard_normal((n_store, 11)).astype(np.float32)
+        A = rng.uniform(-1, 1, (n_store, 1)).astype(np.float32)
+        R = rng.standard_normal(n_store)
+        Dn = rng.random(n_store) < 0.1
+        for i in range(n_store):
+            rb.store_transition(S[i], A[i], R[i], S2[i], bool(Dn[i]))
+        np.random.seed(seed * 7 + 1)
+        b = rb.sample_buffer(batch)
+        after = np.random.get_state()
+        out.update({f"{name}_{k}": v for k, v in dict(
+            M=M, S=S, S2=S2, A=A, R=R, D=Dn, seed=seed * 7 + 1, batch=batch,
+            states=b[0], actions=b[1], rewards=b[2], states_=b[3], dones=b[4],
+            key_after=np.asarray(after[1], np.uint32), pos_after=after[2]).items()})
+    path = os.path.join(HERE, "replay_buffer.npz")
+    np.savez_compressed(path, cases=np.array(list(cases)), **out)
+    print(f"{path}: {list(cases)}")
+
+
 def main():
     import sys
     if sys.argv[1:] == ["toys"]:
         run_toys()
         return
+    if sys.argv[1:] == ["replay"]:
+        run_replay()
+        return
     run_toys()
+    run_replay()
     for exp in range(1, 7):
         run_seeded(f"exp{exp}_uniform", {"base_settings": {"experiment": exp, "test_mode": 0}},
                    400, "uniform", action_seed=100 + exp)

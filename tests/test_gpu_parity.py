@@ -365,3 +365,64 @@ def test_mixed_launch_equals_separate_launches(gpu, built_lib):
     for x, y in ((b1, b2), (p1, p2), (c1, c2)):
         assert torch.equal(x.record, y.record)
         assert torch.equal(x.arena, y.arena)
+
+
+# ---------------------------------------------------------------- replay buffer (§8(f))
+
+@pytest.mark.parametrize("case", ["partial", "wrapped", "one_row", "small"])
+def test_replay_dropin_matches_reference_buffer(case, gpu, built_lib):
+    """sacenv.replay.ReplayBuffer == agent.buffer.ReplayBuffer: same stored rows, same
+    np.random.choice batches from numpy's global stream, same stream state after."""
+    from sacenv.replay import ReplayBuffer
+    z = golden("replay_buffer.npz")
+    g = lambda k: z[f"{case}_{k}"]  # noqa: E731
+    S, S2, A, R, D = g("S"), g("S2"), g("A"), g("R"), g("D")
+    rb = ReplayBuffer(int(g("M")), (11,), 1, device="cuda")
+    if len(R) <= 300:
+        for i in range(len(R)):
+            rb.store_transition(S[i], A[i], R[i], S2[i], bool(D[i]))
+    else:  # batched store of the same sequence (ring wraps inside the call)
+        rb._rb.store_batch(torch.from_numpy(S), torch.from_numpy(A), torch.from_numpy(R),
+                           torch.from_numpy(S2), torch.from_numpy(D.astype(np.uint8)))
+    assert rb.mem_cntr == len(R)
+    np.random.seed(int(g("seed")))
+    got = rb.sample_buffer(int(g("batch")))
+    for x, k in zip(got, ("states", "actions", "rewards", "states_", "dones")):
+        np.testing.assert_array_equal(x, g(k), err_msg=k)
+    st = np.random.get_state()
+    assert st[2] == int(g("pos_after"))
+    np.testing.assert_array_equal(np.asarray(st[1], np.uint32), g("key_after"))
+
+
+def test_replay_store_env_step_uses_final_obs(gpu, built_lib):
+    """Batched path: transitions of a VecBoatEnv step; envs that auto-reset store their
+    terminal obs as new_state and terminal = reached_goal only (main.py:83-88)."""
+    from sacenv import VecBoatEnv
+    from sacenv.replay import DeviceReplayBuffer
+    cfg = {"base_settings": {"experiment": 6, "test_mode": 1}, "boat_env": {"goal_line": 40}}
+    env = VecBoatEnv(cfg, 512, seed=3, device="cuda", max_episode_steps=60, n_helpers=8)
+    rb = DeviceReplayBuffer(50_000, (11,), 1, device="cuda", seed=5)
+    obs = env.reset().clone()
+    steps = 80
+    a = torch.zeros(512, device="cuda")
+    done_any = goal_any = False
+    for k in range(steps):
+        env.step(a)
+        rb.store_env_step(obs, a.view(-1, 1), env)
+        d = env.done.bool()
+        row0 = k * 512
+        torch.cuda.synchronize()
+        ns = rb.new_state_memory[row0: row0 + 512]
+        assert torch.equal(ns[d], env.final_obs[d]) and torch.equal(ns[~d], env.obs[~d])
+        assert torch.equal(rb.state_memory[row0: row0 + 512], obs)
+        assert torch.equal(rb.terminal_memory[row0: row0 + 512].bool(), env.term == 1)
+        assert torch.equal(rb.reward_memory[row0: row0 + 512], env.reward.double())
+        done_any |= bool(d.any())
+        goal_any |= bool((env.term == 1).any())
+        obs = env.obs.clone()
+    assert done_any and goal_any
+    # sampling: indices follow np.random.choice on the buffer's own stream (seed 5)
+    st, ac, rw, ns, tm, idx = rb.sample(1024)
+    want = np.random.RandomState(5).choice(min(rb.mem_cntr, rb.mem_size), 1024)
+    np.testing.assert_array_equal(idx.cpu().numpy(), want)
+    assert torch.equal(st, rb.state_memory[idx]) and torch.equal(ns, rb.new_state_memory[idx])

@@ -34,7 +34,7 @@ def declared_functions():
 def test_library_exports_header(built_lib):
     from sacenv import _lib
     names = declared_functions()
-    assert len(names) == 13
+    assert len(names) == 17
     assert set(names) == set(_lib.EXPORTS)
     for n in names:
         assert hasattr(built_lib, n), n
@@ -99,7 +99,8 @@ def test_ctypes_structs_match_c_layout(tmp_path):
     """offsetof/sizeof of every ABI struct, from gcc on include/sacenv.h, vs the ctypes mirrors."""
     from sacenv import _lib
     structs = {"SacenvBoatParams": _lib.BoatParams, "SacenvBoatLayout": _lib.BoatLayout,
-               "SacenvToyParams": _lib.ToyParams, "SacenvToyLayout": _lib.ToyLayout}
+               "SacenvToyParams": _lib.ToyParams, "SacenvToyLayout": _lib.ToyLayout,
+               "SacenvReplayParams": _lib.ReplayParams, "SacenvReplayLayout": _lib.ReplayLayout}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "sacenv.h"', "int main(void) {"]
     for cname, py in structs.items():
         lines.append(f'printf("{cname} sizeof %zu\\n", sizeof({cname}));')
@@ -337,3 +338,35 @@ def test_package_imports_without_gpu():
     import sacenv
     assert sacenv.BoatConfig is not None
     assert "oracle" not in sys.modules.get("sacenv").__dict__
+
+
+# ---------------------------------------------------------------- replay buffer sampling
+
+def _ring_model(M, S, S2, A, R, D):
+    """agent/buffer.py:13-22 store_transition, restated."""
+    n = len(R)
+    st, st2 = np.zeros((M, S.shape[1])), np.zeros((M, S.shape[1]))
+    ac, rw, dn = np.zeros((M, A.shape[1])), np.zeros(M), np.zeros(M, bool)
+    for i in range(n):
+        j = i % M
+        st[j], st2[j], ac[j], rw[j], dn[j] = S[i], S2[i], A[i], R[i], D[i]
+    return st, ac, rw, st2, dn
+
+
+def test_replay_sampling_algorithm_matches_reference():
+    """The draw the sampling kernel implements (masked-rejection randint on MT19937
+    words, nothing drawn when max_mem == 1) reproduces the reference ReplayBuffer's
+    np.random.choice batches and leaves the global stream where numpy does."""
+    z = np.load(os.path.join(ROOT, "tests", "golden", "replay_buffer.npz"), allow_pickle=False)
+    for c in z["cases"]:
+        g = lambda k: z[f"{c}_{k}"]  # noqa: E731
+        M, batch, seed = int(g("M")), int(g("batch")), int(g("seed"))
+        max_mem = min(len(g("R")), M)
+        mt = PyMT(seed)
+        idx = np.array([0 if max_mem == 1 else mt.randint(0, max_mem) for _ in range(batch)])
+        mem = _ring_model(M, g("S"), g("S2"), g("A"), g("R"), g("D"))
+        for got, want in zip((m[idx] for m in mem), ("states", "actions", "rewards", "states_", "dones")):
+            np.testing.assert_array_equal(got, g(want), err_msg=f"{c}:{want}")
+        # stream state after the draw: the same words consumed as numpy (both twist lazily)
+        assert mt.pos == int(g("pos_after")), c
+        assert mt.key == [int(x) for x in g("key_after")], c
