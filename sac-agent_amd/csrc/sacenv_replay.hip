@@ -82,7 +82,11 @@ __global__ void __launch_bounds__(kWave) k_rb_init(RB r, uint32_t seed) {
 
 // store_transition for rows [0, n): row i -> (mem_cntr + i) % M. Rows that a
 // later row of the same call overwrites (i < n - M) are skipped, so the ring
-// ends exactly as n sequential calls leave it.
+// ends exactly as n sequential calls leave it. Element-parallel over the
+// (n - first) x (D + A + 1) stored columns with 32-bit index math. mem_cntr
+// advances in a second launch (k_rb_advance), after every workgroup has read
+// it: stream order instead of a grid-wide atomic (one word takes ~90
+// returning atomics/µs) or an agent-scope acq_rel fence per workgroup.
 __global__ void __launch_bounds__(256) k_rb_store(SacenvReplayParams p, RB r, int64_t n,
                                                   const float* __restrict__ state,
                                                   const float* __restrict__ action,
@@ -92,28 +96,29 @@ __global__ void __launch_bounds__(256) k_rb_store(SacenvReplayParams p, RB r, in
                                                   const uint8_t* __restrict__ code) {
   const int64_t M = p.mem_size, c0 = *r.cntr();
   const int64_t first = n > M ? n - M : 0;
-  const int D = p.obs_dim, A = p.act_dim;
-  const int64_t total = (n - first) * (D + A + 1);  // D: state + new_state, A: action, 1: scalars
-  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < total;
-       q += (int64_t)gridDim.x * blockDim.x) {
-    // element-major over the three row arrays, then one scalar column per row
-    int64_t i, dst;
-    if (q < (n - first) * D) {
-      i = first + q / D;
-      const int k = (int)(q - (i - first) * D);
-      dst = ((c0 + i) % M) * D + k;
-      r.state()[dst] = state[i * D + k];
-      const uint8_t cd = code[i];
-      const float* src = (final_state != nullptr && cd != 0) ? final_state : new_state;
-      r.new_state()[dst] = src[i * D + k];
-    } else if (q < (n - first) * (D + A)) {
-      const int64_t qq = q - (n - first) * D;
-      i = first + qq / A;
-      const int k = (int)(qq - (i - first) * A);
-      r.action()[((c0 + i) % M) * A + k] = action[i * A + k];
+  const uint32_t rows = (uint32_t)(n - first);
+  const uint32_t base = (uint32_t)((c0 + first) % M);  // ring row of stored row 0
+  const uint32_t D = (uint32_t)p.obs_dim, A = (uint32_t)p.act_dim, Mu = (uint32_t)M;
+  const uint32_t nD = rows * D, nA = rows * A, total = nD + nA + rows;
+  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < total; q += gridDim.x * blockDim.x) {
+    if (q < nD) {
+      const uint32_t j = q / D, k = q - j * D;
+      uint32_t row = base + j;
+      row = row >= Mu ? row - Mu : row;
+      const int64_t src = (first + j) * (int64_t)D + k;
+      r.state()[(int64_t)row * D + k] = state[src];
+      const float* ns = (final_state != nullptr && code[first + j] != 0) ? final_state : new_state;
+      r.new_state()[(int64_t)row * D + k] = ns[src];
+    } else if (q < nD + nA) {
+      const uint32_t qq = q - nD, j = qq / A, k = qq - j * A;
+      uint32_t row = base + j;
+      row = row >= Mu ? row - Mu : row;
+      r.action()[(int64_t)row * A + k] = action[(first + j) * (int64_t)A + k];
     } else {
-      i = first + (q - (n - first) * (D + A));
-      const int64_t row = (c0 + i) % M;
+      const uint32_t j = q - nD - nA;
+      uint32_t row = base + j;
+      row = row >= Mu ? row - Mu : row;
+      const int64_t i = first + j;
       r.reward()[row] = p.reward_f32 ? (double)static_cast<const float*>(reward)[i]
                                      : static_cast<const double*>(reward)[i];
       const uint32_t cd = code[i];
@@ -200,8 +205,8 @@ __global__ void __launch_bounds__(256) k_rb_gather(SacenvReplayParams p, RB r, i
 
 int check_replay(const SacenvReplayParams* p) {
   if (p == nullptr) return SACENV_E_NULL;
-  if (p->mem_size <= 0 || p->mem_size > 0xFFFFFFFFLL || p->obs_dim <= 0 || p->act_dim <= 0)
-    return SACENV_E_SIZE;  // randint on 32-bit words: max_mem - 1 <= 0xFFFFFFFF
+  if (p->mem_size <= 0 || p->mem_size > 0x7FFFFFFFLL || p->obs_dim <= 0 || p->act_dim <= 0)
+    return SACENV_E_SIZE;  // 32-bit ring rows; randint on 32-bit words
   return SACENV_OK;
 }
 
@@ -247,8 +252,9 @@ int sacenv_replay_store(const SacenvReplayParams* p, void* arena, int64_t n, con
   if (!arena || !state || !action || !reward || !new_state || !code) return SACENV_E_NULL;
   const int64_t rows = n > p->mem_size ? p->mem_size : n;
   const int64_t total = rows * ((int64_t)p->obs_dim + p->act_dim + 1);
+  if (total >= (1LL << 32)) return SACENV_E_SIZE;  // 32-bit element index per call
   int64_t blocks = (total + 255) / 256;
-  if (blocks > 65535) blocks = 65535;
+  if (blocks > 8192) blocks = 8192;
   const RB r = make_rb(*p, arena);
   hipLaunchKernelGGL(k_rb_store, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *p, r, n, state,
                      action, reward, new_state, final_state, code);
