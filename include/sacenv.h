@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SACENV_ABI_VERSION 5
+#define SACENV_ABI_VERSION 6
 #define SACENV_OBS_DIM 11      /* Boat.return_state, boat_env.py:308-323 */
 #define SACENV_MT_N 624        /* MT19937 words per env (numpy legacy RNG) */
 #define SACENV_MAX_KNOTS 16    /* wind.fixed_points upper bound */
@@ -164,6 +164,17 @@ int sacenv_boat_init(const SacenvBoatParams *p, void *arena, const uint32_t *see
  * written to layout.obs. Draw order per env is the reference's. */
 int sacenv_boat_reset(const SacenvBoatParams *p, void *arena, const int32_t *ids, int32_t n_ids,
                       void *stream);
+
+/* Done-mask compaction: ids (device i32[n]) of the nonzero
+ * bytes of done[0..n) in ascending order, and their number in *count (device
+ * i32). Stream-ordered; nothing is read back to the host. */
+int sacenv_compact_done(const uint8_t *done, int32_t n, int32_t *ids, int32_t *count, void *stream);
+
+/* sacenv_boat_reset for the device-resident list ids[0 .. *count) (count is a
+ * DEVICE pointer, e.g. from sacenv_compact_done): BoatEnv.reset for exactly
+ * the envs that ended, with no host synchronisation (graph-capturable). */
+int sacenv_boat_reset_list(const SacenvBoatParams *p, void *arena, const int32_t *ids,
+                           const int32_t *count, void *stream);
 
 /* Non-autoreset mode only: reset with caller-supplied draws (no RNG):
  * start_y[n_ids] (device i32), knots[n_ids][2][n_knots] (device f64,

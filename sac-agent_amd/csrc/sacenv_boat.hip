@@ -874,45 +874,102 @@ __global__ void __launch_bounds__(kWave) k_seed(SacenvBoatParams p, Arena A, con
 // mode 1: reset listed envs. non-autoreset: slot 0 <- a new draw;
 //         autoreset: start the next pre-drawn slot, then refill the freed one.
 // mode 2: explicit draws (non-autoreset), slot 0.
+// One Boat per listed env. ids == NULL: env = block index. dev_count != NULL:
+// the list length is read on the device (ids[0 .. *dev_count), grid-stride),
+// so a reset of the envs sacenv_compact_done found needs no host round trip.
 __global__ void __launch_bounds__(kWave) k_draw(SacenvBoatParams p, Arena A, Tail T, int mode,
                                                 const int32_t* __restrict__ ids,
                                                 const int32_t* __restrict__ ex_start_y,
-                                                const double* __restrict__ ex_knots) {
+                                                const double* __restrict__ ex_knots,
+                                                const int32_t* __restrict__ dev_count) {
   __shared__ DrawLds lds;
-  const int b = blockIdx.x;
   const int lane = threadIdx.x;
-  const int e = ids != nullptr ? ids[b] : b;
-  if (e < 0 || e >= p.n_envs) return;  // uniform per block
+  const int nq = dev_count != nullptr ? *dev_count : (int)gridDim.x;
+  if ((int)blockIdx.x >= nq) return;
   load_g(p, T.g, lds, lane);
-  int32_t start_y;
-  int slot = 0;
-  if (mode == 2) {
-    start_y = draw_episode_wave(p, A, lds, e, 0, lane, ex_start_y + b,
-                                ex_knots != nullptr ? ex_knots + (int64_t)b * 2 * p.n_knots : nullptr);
-  } else if (!p.autoreset) {
-    start_y = draw_episode_wave(p, A, lds, e, 0, lane, nullptr, nullptr);
-  } else if (mode == 0) {
-    start_y = draw_episode_wave(p, A, lds, e, 0, lane, nullptr, nullptr);
-    for (int s = 1; s < kSlots; ++s) draw_episode_wave(p, A, lds, e, s, lane, nullptr, nullptr);
-    if (lane == 0) {
-      A.i32(U_CONS)[e] = 0;
-      A.i32(U_FILL)[e] = kSlots;
+  for (int q = blockIdx.x; q < nq; q += gridDim.x) {
+    const int e = ids != nullptr ? ids[q] : q;
+    if (e < 0 || e >= p.n_envs) continue;  // uniform per block
+    int32_t start_y;
+    int slot = 0;
+    if (mode == 2) {
+      start_y = draw_episode_wave(p, A, lds, e, 0, lane, ex_start_y + q,
+                                  ex_knots != nullptr ? ex_knots + (int64_t)q * 2 * p.n_knots : nullptr);
+    } else if (!p.autoreset) {
+      start_y = draw_episode_wave(p, A, lds, e, 0, lane, nullptr, nullptr);
+    } else if (mode == 0) {
+      start_y = draw_episode_wave(p, A, lds, e, 0, lane, nullptr, nullptr);
+      for (int s = 1; s < kSlots; ++s) draw_episode_wave(p, A, lds, e, s, lane, nullptr, nullptr);
+      if (lane == 0) {
+        A.i32(U_CONS)[e] = 0;
+        A.i32(U_FILL)[e] = kSlots;
+      }
+    } else {
+      const int c = A.i32(U_CONS)[e] + 1;
+      slot = c % kSlots;
+      start_y = A.i32(U_STARTY)[(int64_t)slot * A.np + e];
+      if (lane == 0) A.i32(U_CONS)[e] = c;
+      const int f = A.i32(U_FILL)[e];
+      draw_episode_wave(p, A, lds, e, f % kSlots, lane, nullptr, nullptr);
+      if (lane == 0) A.i32(U_FILL)[e] = f + 1;
     }
-  } else {
-    const int c = A.i32(U_CONS)[e] + 1;
-    slot = c % kSlots;
-    start_y = A.i32(U_STARTY)[(int64_t)slot * A.np + e];
-    if (lane == 0) A.i32(U_CONS)[e] = c;
-    const int f = A.i32(U_FILL)[e];
-    draw_episode_wave(p, A, lds, e, f % kSlots, lane, nullptr, nullptr);
-    if (lane == 0) A.i32(U_FILL)[e] = f + 1;
+    if (lane == 0) {
+      double wv0, wa0;
+      wind0_of_slot(p, A, T.table, slot, e, wv0, wa0);
+      const Obs o = fresh_state(p, A, T, e, start_y, wv0, wa0);
+      store_obs(A.obs() + (int64_t)e * SACENV_OBS_DIM, o);
+    }
+    __syncthreads();
   }
-  if (lane == 0) {
-    double wv0, wa0;
-    wind0_of_slot(p, A, T.table, slot, e, wv0, wa0);
-    const Obs o = fresh_state(p, A, T, e, start_y, wv0, wa0);
-    store_obs(A.obs() + (int64_t)e * SACENV_OBS_DIM, o);
+}
+
+// Done-mask compaction (the reset list of BoatEnv.reset for the envs that
+// ended): ids of the nonzero bytes of done[0..n), ascending,
+// and their count. One workgroup of 1024 lanes, 64 bytes per lane per pass:
+// per-lane counts -> DPP wave scan -> LDS scan of the 16 wave totals.
+__global__ void __launch_bounds__(1024) k_compact(const uint8_t* __restrict__ done, int n, int aligned,
+                                                  int32_t* __restrict__ ids, int32_t* __restrict__ count) {
+  __shared__ int wsum[16];
+  __shared__ int base_s;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (t == 0) base_s = 0;
+  __syncthreads();
+  for (int64_t c0 = 0; c0 < n; c0 += 1024 * 64) {
+    const int64_t e0 = c0 + (int64_t)t * 64;
+    uint64_t bits = 0;  // bit j: done[e0 + j] != 0
+    if (aligned && e0 + 64 <= n) {
+      const uint4* v = reinterpret_cast<const uint4*>(done + e0);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint4 x = v[k];
+        const uint32_t wds[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+#pragma unroll
+          for (int by = 0; by < 4; ++by)
+            if ((wds[d] >> (8 * by)) & 0xffu) bits |= 1ull << (16 * k + 4 * d + by);
+      }
+    } else {
+      for (int j = 0; j < 64 && e0 + j < n; ++j)
+        if (done[e0 + j]) bits |= 1ull << j;
+    }
+    const int cnt = __popcll(bits);
+    const int incl = wave_incl_scan(cnt);
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    int wbase = 0;
+    for (int k = 0; k < w; ++k) wbase += wsum[k];
+    int pos = base_s + wbase + incl - cnt;
+    while (bits) {
+      const int j = __ffsll((long long)bits) - 1;
+      bits &= bits - 1ull;
+      ids[pos++] = (int32_t)(e0 + j);
+    }
+    __syncthreads();
+    if (t == 1023) base_s += wbase + incl;
+    __syncthreads();
   }
+  if (t == 0) *count = base_s;
 }
 
 // Refill work pending after the last step launch (k-1), done before a
@@ -1559,7 +1616,7 @@ int sacenv_boat_init(const SacenvBoatParams* p, void* arena, const uint32_t* see
   hipLaunchKernelGGL(k_seed, dim3(blocks_for(p->n_envs, kWave)), dim3(kWave), 0, s, *p, A, seeds);
   if ((rc = launch_status())) return rc;
   hipLaunchKernelGGL(k_draw, dim3(p->n_envs), dim3(kWave), 0, s, *p, A, T, 0, (const int32_t*)nullptr,
-                     (const int32_t*)nullptr, (const double*)nullptr);
+                     (const int32_t*)nullptr, (const double*)nullptr, (const int32_t*)nullptr);
   return launch_status();
 }
 
@@ -1582,7 +1639,36 @@ int sacenv_boat_reset(const SacenvBoatParams* p, void* arena, const int32_t* ids
     if ((rc = launch_status())) return rc;
   }
   hipLaunchKernelGGL(k_draw, dim3(nb), dim3(kWave), 0, s, *p, A, T, 1, ids, (const int32_t*)nullptr,
-                     (const double*)nullptr);
+                     (const double*)nullptr, (const int32_t*)nullptr);
+  return launch_status();
+}
+
+int sacenv_compact_done(const uint8_t* done, int32_t n, int32_t* ids, int32_t* count, void* stream) {
+  if (n < 0) return SACENV_E_SIZE;
+  if (count == nullptr || (n > 0 && (done == nullptr || ids == nullptr))) return SACENV_E_NULL;
+  const int aligned = (reinterpret_cast<uintptr_t>(done) & 15u) == 0;
+  hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, (hipStream_t)stream, done, n, aligned, ids, count);
+  return launch_status();
+}
+
+int sacenv_boat_reset_list(const SacenvBoatParams* p, void* arena, const int32_t* ids, const int32_t* count,
+                           void* stream) {
+  int rc = check_params(p);
+  if (rc) return rc;
+  if (arena == nullptr || ids == nullptr || count == nullptr) return SACENV_E_NULL;
+  const hipStream_t s = (hipStream_t)stream;
+  const Arena A = make_arena(*p, arena);
+  const Tail T = make_tail(*p, arena);
+  if (p->autoreset) {
+    hipLaunchKernelGGL(k_drain, dim3(p->n_helpers), dim3(kWave), 0, s, *p, A, T);
+    if ((rc = launch_status())) return rc;
+    hipLaunchKernelGGL(k_drain_done, dim3(blocks_for((int)(A.np / kWave), 256)), dim3(256), 0, s, A);
+    if ((rc = launch_status())) return rc;
+  }
+  // at most one workgroup per CU-slot; each loops over its share of the device-side list
+  const int grid = p->n_envs < 1024 ? p->n_envs : 1024;
+  hipLaunchKernelGGL(k_draw, dim3(grid), dim3(kWave), 0, s, *p, A, T, 1, ids, (const int32_t*)nullptr,
+                     (const double*)nullptr, count);
   return launch_status();
 }
 
@@ -1596,7 +1682,7 @@ int sacenv_boat_reset_explicit(const SacenvBoatParams* p, void* arena, const int
   if (n_ids < 0) return SACENV_E_SIZE;
   if (n_ids == 0) return SACENV_OK;
   hipLaunchKernelGGL(k_draw, dim3(n_ids), dim3(kWave), 0, (hipStream_t)stream, *p, make_arena(*p, arena),
-                     make_tail(*p, arena), 2, ids, start_y, knots);
+                     make_tail(*p, arena), 2, ids, start_y, knots, (const int32_t*)nullptr);
   return launch_status();
 }
 

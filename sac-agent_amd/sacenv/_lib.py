@@ -11,7 +11,7 @@ import os
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # .../sac-agent_amd
 LIB_PATH = os.environ.get("SACENV_LIB", os.path.join(PKG_ROOT, "build", "libsacenv.so"))
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 OBS_DIM = 11
 MT_N = 624
 MAX_KNOTS = 16
@@ -103,7 +103,8 @@ EXPORTS = ("sacenv_abi_version", "sacenv_error_string", "sacenv_boat_layout",
            "sacenv_boat_init", "sacenv_boat_reset", "sacenv_boat_reset_explicit",
            "sacenv_boat_step", "sacenv_boat_wind_eval", "sacenv_toy_layout", "sacenv_toy_init",
            "sacenv_toy_reset", "sacenv_toy_step", "sacenv_mixed_step", "sacenv_replay_layout",
-           "sacenv_replay_init", "sacenv_replay_store", "sacenv_replay_sample")
+           "sacenv_replay_init", "sacenv_replay_store", "sacenv_replay_sample",
+           "sacenv_compact_done", "sacenv_boat_reset_list")
 
 _LIB = None
 
@@ -140,6 +141,8 @@ def load(path: str | None = None):
         "sacenv_toy_reset": (C.c_int, [TP, _p, _p, _i32, _p]),
         "sacenv_toy_step": (C.c_int, [TP, _p, _p]),
         "sacenv_mixed_step": (C.c_int, [P, _p, _p, TP, C.POINTER(_p), _i32, _p]),
+        "sacenv_compact_done": (C.c_int, [_p, _i32, _p, _p, _p]),
+        "sacenv_boat_reset_list": (C.c_int, [P, _p, _p, _p, _p]),
         "sacenv_replay_layout": (C.c_int, [RP, C.POINTER(ReplayLayout)]),
         "sacenv_replay_init": (C.c_int, [RP, _p, C.c_uint32, _p]),
         "sacenv_replay_store": (C.c_int, [RP, _p, _i64, _p, _p, _p, _p, _p, _p, _p]),

@@ -161,6 +161,27 @@ class VecBoatEnv:
                 self._keep = ids
         return self.obs
 
+    def compact_done(self, done=None):
+        """(ids, count) device tensors: the envs whose ``done`` byte is set, ascending
+        (done-mask compaction on the GPU; no host round trip)."""
+        d = self.done if done is None else torch.as_tensor(done, dtype=torch.uint8, device=self.device)
+        d = d.contiguous()
+        ids = torch.empty(d.numel(), dtype=torch.int32, device=self.device)
+        count = torch.empty(1, dtype=torch.int32, device=self.device)
+        _lib.check(self.lib.sacenv_compact_done(d.data_ptr(), d.numel(), ids.data_ptr(),
+                                                count.data_ptr(), self.stream))
+        self._keep_c = d
+        return ids, count
+
+    def reset_done(self, done=None) -> torch.Tensor:
+        """BoatEnv.reset for every env whose ``done`` byte is set (default: the last
+        step's done mask), entirely on the device: compaction + reset of the list."""
+        ids, count = self.compact_done(done)
+        _lib.check(self.lib.sacenv_boat_reset_list(self._pp, self._ptr, ids.data_ptr(),
+                                                   count.data_ptr(), self.stream))
+        self._keep = (ids, count)
+        return self.obs
+
     def reset_explicit(self, env_ids, start_y, knots=None) -> torch.Tensor:
         """Reset with caller-supplied draws (replaying recorded episodes; autoreset=False)."""
         ids = torch.as_tensor(env_ids, dtype=torch.int32, device=self.device).contiguous()

@@ -426,3 +426,44 @@ def test_replay_store_env_step_uses_final_obs(gpu, built_lib):
     want = np.random.RandomState(5).choice(min(rb.mem_cntr, rb.mem_size), 1024)
     np.testing.assert_array_equal(idx.cpu().numpy(), want)
     assert torch.equal(st, rb.state_memory[idx]) and torch.equal(ns, rb.new_state_memory[idx])
+
+
+# ---------------------------------------------------------------- done compaction + device-list reset
+
+@pytest.mark.parametrize("n,offset", [(0, 0), (1, 0), (63, 0), (4096, 0), (65537, 0), (70000, 3)])
+def test_compact_done_matches_nonzero(n, offset, gpu, built_lib):
+    from sacenv import _lib
+    lib = _lib.load()
+    g = torch.Generator(device="cuda")
+    g.manual_seed(n + offset)
+    buf = (torch.rand(n + offset + 1, generator=g, device="cuda") < 0.1).to(torch.uint8)
+    buf[offset: offset + n: 97] = 7                       # nonzero values other than 1
+    d = buf[offset: offset + n]                            # offset 3: unaligned start
+    ids = torch.full((max(n, 1),), -1, dtype=torch.int32, device="cuda")
+    cnt = torch.empty(1, dtype=torch.int32, device="cuda")
+    _lib.check(lib.sacenv_compact_done(d.data_ptr(), n, ids.data_ptr(), cnt.data_ptr(),
+                                       torch.cuda.current_stream().cuda_stream))
+    want = torch.nonzero(d).flatten().to(torch.int32)
+    assert int(cnt.item()) == want.numel()
+    assert torch.equal(ids[: want.numel()], want)
+
+
+@pytest.mark.parametrize("autoreset", [False, True])
+def test_reset_done_equals_reset_of_ids(autoreset, gpu, built_lib):
+    """reset_done (device compaction + device-count reset) == reset(ids) from the host."""
+    from sacenv import VecBoatEnv
+    cfg = {"base_settings": {"experiment": 6, "test_mode": 0}}
+    kw = dict(seed=9, device="cuda", autoreset=autoreset, max_episode_steps=0, n_helpers=8)
+    e1, e2 = VecBoatEnv(cfg, 3001, **kw), VecBoatEnv(cfg, 3001, **kw)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(1)
+    for k in range(40):
+        a = torch.rand(3001, generator=g, device="cuda") * 2 - 1
+        e1.step(a)
+        e2.step(a)
+        if k % 7 == 6:
+            mask = (torch.rand(3001, generator=g, device="cuda") < 0.2).to(torch.uint8)
+            e1.reset_done(mask)
+            e2.reset(torch.nonzero(mask).flatten())
+    torch.cuda.synchronize()
+    assert torch.equal(e1.arena, e2.arena)
