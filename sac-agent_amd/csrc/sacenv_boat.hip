@@ -1156,11 +1156,11 @@ struct MixedToys {
 
 // ---------------------------------------------------------------- owner wave
 
-// Per-step SoA traffic of one owner wave goes through LDS so that every
-// global access is 16 B per lane: lanes 0-31 move 512 contiguous bytes of one
-// field, lanes 32-63 of the next. Per-lane 8-byte accesses are issue-bound on
-// gfx950 (twice the instructions for the same bytes), and the step is
-// dominated by its memory instructions, not its arithmetic.
+// The owner wave's SoA state is loaded 16 B per lane and redistributed through
+// LDS: lanes 0-31 read 512 contiguous bytes of one field, lanes 32-63 of the
+// next (6 load instructions instead of 13). Outputs are stored per lane as
+// soon as they are final (EARLY_STORE); the obs rows go out through LDS as
+// float4 (64 rows x 44 B = 176 float4).
 constexpr int kF64 = 11;  // s_x s_y s_r v_x v_y v_r rudder t ep_reward wind_next[2]
 struct OwnerLds {
   double f[kF64][kWave];
@@ -1202,49 +1202,10 @@ __device__ __forceinline__ void owner_load(const Arena& A, OwnerLds& l, int ob, 
   __syncthreads();
 }
 
-// 16-B store (plain: write-through sc1 and nt measured no faster here)
-__device__ __forceinline__ void st16(void* dst, f4v v) { *reinterpret_cast<f4v*>(dst) = v; }
-
-// the mirror image for the outputs: 7 store instructions + 3 for the obs rows
-__device__ __forceinline__ void owner_store(const Arena& A, const OwnerLds& l, int ob, int lane,
-                                            bool store_cons) {
-  const int half = lane >> 5, c = lane & 31;
-  const int64_t e0 = (int64_t)ob * kWave;
-#pragma unroll
-  for (int q = 0; q < 5; ++q)
-    st16(f64_field(A, 2 * q + half, e0 + 2 * c), *reinterpret_cast<const f4v*>(&l.f[2 * q + half][2 * c]));
-  {  // lanes 0-31: wind_next angle; 32-47: index; 48-63: reward
-    const int j = lane & 15;
-    char* dst = lane < 32   ? f64_field(A, 10, e0 + 2 * c)
-                : lane < 48 ? reinterpret_cast<char*>(A.i32(U_IDX) + e0 + 4 * j)
-                            : reinterpret_cast<char*>(A.reward() + e0 + 4 * j);
-    const f4v* src = lane < 32   ? reinterpret_cast<const f4v*>(&l.f[10][2 * c])
-                     : lane < 48 ? reinterpret_cast<const f4v*>(l.idx + 4 * j)
-                                 : reinterpret_cast<const f4v*>(l.reward + 4 * j);
-    st16(dst, *src);
-  }
-  if (lane < 24 && (store_cons || lane >= 16)) {  // lanes 0-15: cons; 16-19: done; 20-23: term
-    char* dst;
-    const f4v* src;
-    if (lane < 16) {
-      dst = reinterpret_cast<char*>(A.i32(U_CONS) + e0 + 4 * lane);
-      src = reinterpret_cast<const f4v*>(l.cons + 4 * lane);
-    } else if (lane < 20) {
-      dst = reinterpret_cast<char*>(A.done() + e0 + 16 * (lane - 16));
-      src = reinterpret_cast<const f4v*>(l.done + 16 * (lane - 16));
-    } else {
-      dst = reinterpret_cast<char*>(A.term() + e0 + 16 * (lane - 20));
-      src = reinterpret_cast<const f4v*>(l.term + 16 * (lane - 20));
-    }
-    st16(dst, *src);
-  }
-  // obs rows: 64 rows x 44 B = 2816 B = 176 float4
-  const f4v* src = reinterpret_cast<const f4v*>(l.obs);
-  f4v* dst = reinterpret_cast<f4v*>(A.obs() + e0 * SACENV_OBS_DIM);
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-    if (lane + kWave * i < kWave * SACENV_OBS_DIM / 4) st16(dst + lane + kWave * i, src[lane + kWave * i]);
-}
+// Each dynamics field is stored as soon as it is final, so the write traffic
+// drains while the wave still computes (measured: -0.15 us/step against
+// staging every output for 16-B stores at the end).
+#define EARLY_STORE(u, v) (A.f64(u)[e] = (v))
 
 // One owner wave: BoatEnv.step for 64 consecutive envs, one per lane.
 __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Arena& A, const Tail& T,
@@ -1293,6 +1254,8 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   t = t + p.dt;
   const int32_t fuel = p.fuel0 - (index + 1);
   if (p.test_mode == 0) rudder = rudder + div_c((double)act, 10.0, 0.1);  // action / 10
+  EARLY_STORE(U_T, t);
+  EARLY_STORE(U_RUD, rudder);
   const bool first = index == 0;  // integrator counter == 0 (control_blocks.py:21-22)
   const double wsign = (double)((wv > 0.0) - (wv < 0.0));
   double swa, cwa;
@@ -1307,6 +1270,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   const double F_W = (wv * wv * wsign * p.c_r_front * 0.5 * p.rho * p.boat_area_front) * cwa;
   const double a_x = div_c(-F_R + F_T + F_C + F_W, p.m_plus_mx, r_mx);
   v_x = first ? 3.0 : a_x * p.dt + v_x;
+  EARLY_STORE(U_VX, v_x);
 
   // eom_transverse :241-265 (new v_x)
   const double vys = (double)((v_y > 0.0) - (v_y < 0.0));
@@ -1317,6 +1281,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   const double F_W2 = (wv * wv * wsign * p.c_r_side * 0.5 * p.rho * p.boat_area_side) * swa;
   const double a_y = div_c(-F_R2 + F_RU + F_C2 + F_W2, p.m_plus_my, r_my);
   v_y = first ? 0.0 : a_y * p.dt + v_y;
+  EARLY_STORE(U_VY, v_y);
 
   // eom_yawning :267-281
   const double vrs = (double)((v_r > 0.0) - (v_r < 0.0));
@@ -1325,6 +1290,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   const double M_rud = v_x * v_x * p.c_r_side * 0.5 * p.rho * p.rudder_area * sin_rud * (p.boat_b / 2) * vxs;
   const double a_r = div_c(-M_hull + M_rud, p.i_plus_iz, r_iz);
   v_r = first ? 0.0 : a_r * p.dt + v_r;
+  EARLY_STORE(U_VR, v_r);
 
   // get_kinematics :283-306
   const double v = sqrt(v_x * v_x + v_y * v_y);
@@ -1336,6 +1302,10 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   s_x = (sd * v) * p.dt + s_x;
   s_y = (cd * v) * p.dt + s_y;
   index = index + 1;
+  EARLY_STORE(U_SR, s_r);
+  EARLY_STORE(U_SX, s_x);
+  EARLY_STORE(U_SY, s_y);
+  A.i32(U_IDX)[e] = index;
 
   Obs o = make_obs(p, oc, s_x, v_x, a_x, s_y, v_y, a_y, s_r, v_r, a_r, rudder, (double)fuel);
 
@@ -1394,21 +1364,33 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
     o = make_obs(p, oc, 0.0, 0.0, 0.0, sy0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, (double)p.fuel0);
     cons_out = cons + 1;
   }
-  // stage every output in LDS (the wave's loads of it are complete), then 16-B stores
-  l.f[0][lane] = s_x, l.f[1][lane] = s_y, l.f[2][lane] = s_r;
-  l.f[3][lane] = v_x, l.f[4][lane] = v_y, l.f[5][lane] = v_r;
-  l.f[6][lane] = rudder, l.f[7][lane] = t, l.f[8][lane] = ep;
-  l.f[9][lane] = nwv, l.f[10][lane] = nwa;
-  l.idx[lane] = index;
-  if (p.autoreset) l.cons[lane] = cons_out;
-  l.reward[lane] = (float)reward;
-  l.done[lane] = ended ? 1 : 0;
-  l.term[lane] = term;
+  // the dynamics' fields went out as they were computed; what is left: the
+  // fresh state of restarting envs (same lane, same address: the later store
+  // wins), ep_reward, the next wind, and the record
+  if (restart) {
+    A.f64(U_SX)[e] = s_x, A.f64(U_SY)[e] = s_y, A.f64(U_SR)[e] = s_r;
+    A.f64(U_VX)[e] = v_x, A.f64(U_VY)[e] = v_y, A.f64(U_VR)[e] = v_r;
+    A.f64(U_RUD)[e] = rudder, A.f64(U_T)[e] = t;
+    A.i32(U_IDX)[e] = index;
+    A.i32(U_CONS)[e] = cons_out;
+  }
+  A.f64(U_EP)[e] = ep;
+  A.f64(U_WNX)[e] = nwv;
+  A.f64(U_WNX)[A.np + e] = nwa;
+  A.reward()[e] = (float)reward;
+  A.done()[e] = ended ? 1 : 0;
+  A.term()[e] = term;
 #pragma unroll
   for (int k = 0; k < SACENV_OBS_DIM; ++k) l.obs[lane * SACENV_OBS_DIM + k] = o.v[k];
   __syncthreads();
-  // cons changes only for restarting envs: its row is stored only then
-  owner_store(A, l, ob, lane, __ballot(restart) != 0ull);
+  {
+    const f4v* src = reinterpret_cast<const f4v*>(l.obs);
+    f4v* dst = reinterpret_cast<f4v*>(A.obs() + (int64_t)ob * kWave * SACENV_OBS_DIM);
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      if (lane + kWave * i < kWave * SACENV_OBS_DIM / 4) dst[lane + kWave * i] = src[lane + kWave * i];
+  }
+
   if (p.autoreset) {
     // this launch's ended envs, for the next launch's helpers (every wave
     // rewrites its word each launch, so the ring needs no clearing)
