@@ -28,6 +28,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
 
 #include "sacenv.h"
 
@@ -1180,13 +1181,18 @@ __device__ __forceinline__ char* f64_field(const Arena& A, int k, int64_t e) {
 }
 
 // wave-wide 16-B gathers of the owner's SoA inputs into LDS: 6 load instructions
-__device__ __forceinline__ void owner_load(const Arena& A, OwnerLds& l, int ob, int lane) {
+__device__ __forceinline__ void owner_load(const Arena& A, OwnerLds& l, int ob, int lane, bool t_idx) {
   const int half = lane >> 5, c = lane & 31;
   const int64_t e0 = (int64_t)ob * kWave;
   f4v v[6];
 #pragma unroll
-  for (int q = 0; q < 5; ++q)
+  for (int q = 0; q < 5; ++q) {
+    if (q == 3 && half == 1 && t_idx) {  // field 7 = t, derived from the index
+      v[q] = f4v{0.f, 0.f, 0.f, 0.f};
+      continue;
+    }
     v[q] = *reinterpret_cast<const f4v*>(f64_field(A, 2 * q + half, e0 + 2 * c));
+  }
   {  // lanes 0-31: wind_next angle; 32-47: index; 48-63: cons (4 envs per lane)
     const char* src = lane < 32 ? f64_field(A, 10, e0 + 2 * c)
                                 : reinterpret_cast<const char*>(A.i32(lane < 48 ? U_IDX : U_CONS) + e0 +
@@ -1200,6 +1206,16 @@ __device__ __forceinline__ void owner_load(const Arena& A, OwnerLds& l, int ob, 
   else
     *reinterpret_cast<f4v*>((lane < 48 ? l.idx : l.cons) + 4 * (lane & 15)) = v[5];
   __syncthreads();
+}
+
+// t += dt (boat_env.py:69) accumulates exactly when dt = m * 2^e with m < 2^22:
+// every partial sum k*dt (k <= 2^31) is then a double, so t == index * dt
+// bit for bit and t need not be carried in HBM (8 B read + 8 B write per
+// env-step for the default dt = 0.25).
+__host__ __device__ inline bool t_from_index(double dt) {
+  uint64_t bits;
+  memcpy(&bits, &dt, sizeof bits);
+  return (bits & ((1ull << 30) - 1ull)) == 0ull;
 }
 
 // Each dynamics field is stored as soon as it is final, so the write traffic
@@ -1228,7 +1244,8 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   const bool active = e < p.n_envs;
   const int kepoch = A.owner_epoch()[ob];
   const float act = action[active ? e : 0];
-  owner_load(A, l, ob, lane);
+  const bool t_idx = t_from_index(p.dt);
+  owner_load(A, l, ob, lane, t_idx);
   double s_x = l.f[0][lane], s_y = l.f[1][lane], s_r = l.f[2][lane];
   double v_x = l.f[3][lane], v_y = l.f[4][lane], v_r = l.f[5][lane];
   double rudder = l.f[6][lane], t = l.f[7][lane], ep = l.f[8][lane];
@@ -1251,10 +1268,10 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   const ObsConst oc = obs_const(T);
 
   // BoatEnv.step :69-73
-  t = t + p.dt;
+  t = t_idx ? (double)(index + 1) * p.dt : t + p.dt;  // boat_env.py:69
   const int32_t fuel = p.fuel0 - (index + 1);
   if (p.test_mode == 0) rudder = rudder + div_c((double)act, 10.0, 0.1);  // action / 10
-  EARLY_STORE(U_T, t);
+  if (!t_idx) EARLY_STORE(U_T, t);
   EARLY_STORE(U_RUD, rudder);
   const bool first = index == 0;  // integrator counter == 0 (control_blocks.py:21-22)
   const double wsign = (double)((wv > 0.0) - (wv < 0.0));
@@ -1370,7 +1387,8 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   if (restart) {
     A.f64(U_SX)[e] = s_x, A.f64(U_SY)[e] = s_y, A.f64(U_SR)[e] = s_r;
     A.f64(U_VX)[e] = v_x, A.f64(U_VY)[e] = v_y, A.f64(U_VR)[e] = v_r;
-    A.f64(U_RUD)[e] = rudder, A.f64(U_T)[e] = t;
+    A.f64(U_RUD)[e] = rudder;
+    if (!t_idx) A.f64(U_T)[e] = t;
     A.i32(U_IDX)[e] = index;
     A.i32(U_CONS)[e] = cons_out;
   }

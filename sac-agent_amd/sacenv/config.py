@@ -108,6 +108,13 @@ def _get(obj, key):
     return getattr(obj, key, None)
 
 
+def t_from_index(dt: float) -> bool:
+    """Mirror of the kernel's rule: ``t += dt`` is exact (t == index * dt) when
+    dt's significand has at most 22 bits; the kernel then keeps no t in HBM."""
+    bits = np.array([dt], dtype=np.float64).view(np.uint64)[0]
+    return int(bits) & ((1 << 30) - 1) == 0
+
+
 def spline_g(n: int) -> np.ndarray:
     """G with (second derivative / 6) = G @ knot_values for the not-a-knot cubic.
 
@@ -179,5 +186,5 @@ def observation_bounds():
     return low, high
 
 
-__all__ = ["BoatConfig", "make_params", "spline_g", "observation_bounds"]
+__all__ = ["BoatConfig", "make_params", "spline_g", "observation_bounds", "t_from_index"]
 _ = fields  # keep dataclasses import explicit for readers

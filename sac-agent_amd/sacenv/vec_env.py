@@ -19,7 +19,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .config import BoatConfig, make_params, observation_bounds
+from .config import BoatConfig, make_params, observation_bounds, t_from_index
 from .spaces import Box
 
 RECORD_BYTES = _lib.RECORD_BYTES  # packed per-env record: obs f32x11 | reward f32 | done u8 | term u8
@@ -78,8 +78,10 @@ class VecBoatEnv:
 
         f64, i32 = torch.float64, torch.int32
         # carried state (SoA views, first N entries of each n_pad array)
-        for name in ("s_x", "s_y", "s_r", "v_x", "v_y", "v_r", "rudder", "t", "ep_reward"):
+        for name in ("s_x", "s_y", "s_r", "v_x", "v_y", "v_r", "rudder", "ep_reward"):
             setattr(self, name, view(getattr(L, name), f64, NP)[:N])
+        self._t_view = view(L.t, f64, NP)[:N]
+        self._t_from_index = t_from_index(float(self.cfg.dt))
         self.index = view(L.index, i32, NP)[:N]
         self.cons = view(L.cons, i32, NP)[:N]
         self.mt_pos = view(L.mt_pos, i32, NP)[:N]
@@ -133,6 +135,14 @@ class VecBoatEnv:
     @property
     def stream(self) -> int:
         return torch.cuda.current_stream(self.device).cuda_stream
+
+    @property
+    def t(self) -> torch.Tensor:
+        """Boat.t of each env: index * dt when dt makes ``t += dt`` exact (the kernel
+        then carries no t), else the carried f64 field."""
+        if self._t_from_index:
+            return self.index.to(torch.float64) * float(self.cfg.dt)
+        return self._t_view
 
     @property
     def start_y(self) -> torch.Tensor:

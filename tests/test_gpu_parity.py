@@ -467,3 +467,28 @@ def test_reset_done_equals_reset_of_ids(autoreset, gpu, built_lib):
             e2.reset(torch.nonzero(mask).flatten())
     torch.cuda.synchronize()
     assert torch.equal(e1.arena, e2.arena)
+
+
+@pytest.mark.parametrize("dt,t_max", [(0.1, 30.0), (0.25, 12.0)])
+def test_time_accumulation_carried_and_derived(dt, t_max, gpu, built_lib):
+    """dt = 0.1 keeps t in HBM (t += dt rounds); dt = 0.25 derives t = index * dt (exact).
+    Both must time out on the same step as the oracle's accumulated t (boat_env.py:69, :99)."""
+    from sacenv import VecBoatEnv
+    from sacenv.config import t_from_index
+    assert t_from_index(0.25) and not t_from_index(0.1)
+    N = 200
+    seeds = np.arange(N, dtype=np.uint64) + 77
+    cfg = {"base_settings": {"experiment": 6, "test_mode": 1, "dt": dt, "t_max": t_max}}
+    env = VecBoatEnv(cfg, N, seeds=seeds, device=gpu, autoreset=True, n_helpers=8)
+    ora = OracleVecBoat(OracleConfig(experiment=6, test_mode=1, dt=dt, t_max=t_max), seeds)
+    env.reset()
+    ora.reset()
+    steps = int(round(t_max / dt)) + 5
+    zero = np.zeros(N, np.float32)
+    for k in range(steps):
+        _, _, _, info = env.step(torch.zeros(N, device=gpu))
+        r = ora.step(zero)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(info["term"].cpu().numpy(), r["term"], err_msg=f"step {k}")
+        np.testing.assert_array_equal(env.t.cpu().numpy(), ora.t, err_msg=f"step {k}")
+    assert (env.counters.cpu().numpy()[4] >= 1).all()   # every env timed out at least once
