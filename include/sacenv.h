@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SACENV_ABI_VERSION 6
+#define SACENV_ABI_VERSION 7
 #define SACENV_OBS_DIM 11      /* Boat.return_state, boat_env.py:308-323 */
 #define SACENV_MT_N 624        /* MT19937 words per env (numpy legacy RNG) */
 #define SACENV_MAX_KNOTS 16    /* wind.fixed_points upper bound */
@@ -126,6 +126,8 @@ typedef struct SacenvBoatLayout {
   int64_t wind_y;             /* f64 [4][2][n_knots][n_pad] folded knot values per slot, curve */
   int64_t wind_m;             /* f64 [4][2][n_knots][n_pad] folded 2nd derivatives / 6 */
   int64_t knots_raw;          /* f64 [4][2][n_knots][n_pad] drawn knots (SACENV_OUT_KNOTS) */
+  int64_t refill_y;           /* f64 [3][n_pad][2][n_knots] knots drawn by phase A in launch k
+                                 (ring k % 3, rank order), fitted by phase B in launch k+1 */
   int64_t mt_key;             /* u32 [n_pad][624] per-env MT19937 state */
   int64_t record;             /* u8 [50 n_pad]: obs f32 [n_pad][11] | reward f32 [n_pad]
                                  | done u8 [n_pad] | term u8 [n_pad]  (the all-gather payload) */

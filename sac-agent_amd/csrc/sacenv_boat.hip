@@ -86,8 +86,9 @@ __host__ __device__ inline void compute_layout(int n, int nk, int nh, int L, int
   o->wind_y = uw * np;
   o->wind_m = (uw + wk) * np;
   o->knots_raw = (uw + 2 * wk) * np;
-  o->mt_key = (uw + 3 * wk) * np;
-  const int64_t ur = uw + 3 * wk + U_MT_BYTES;
+  o->refill_y = (uw + 3 * wk) * np;
+  o->mt_key = (uw + 3 * wk + kRing * 16LL * nk) * np;
+  const int64_t ur = uw + 3 * wk + kRing * 16LL * nk + U_MT_BYTES;
   o->record = ur * np;
   o->obs = ur * np;
   o->reward = (ur + 44) * np;
@@ -128,8 +129,13 @@ struct Arena {
   __device__ __forceinline__ double* wind_y() const { return at<double>(U_WIND); }
   __device__ __forceinline__ double* wind_m() const { return at<double>(U_WIND + wk()); }
   __device__ __forceinline__ double* knots_raw() const { return at<double>(U_WIND + 2 * wk()); }
-  __device__ __forceinline__ uint32_t* mt_key() const { return at<uint32_t>(U_WIND + 3 * wk()); }
-  __device__ __forceinline__ int64_t ur() const { return U_WIND + 3 * wk() + U_MT_BYTES; }
+  // raw knot values drawn by phase A, [ring][rank][curve][knot]: phase B reads its
+  // first row at a fixed address (no list -> slot dependency)
+  __device__ __forceinline__ double* refill_y(int r) const {
+    return at<double>(U_WIND + 3 * wk()) + (int64_t)r * np * 2 * nk;
+  }
+  __device__ __forceinline__ uint32_t* mt_key() const { return at<uint32_t>(U_WIND + 3 * wk() + kRing * 16LL * nk); }
+  __device__ __forceinline__ int64_t ur() const { return U_WIND + 3 * wk() + kRing * 16LL * nk + U_MT_BYTES; }
   __device__ __forceinline__ float* obs() const { return at<float>(ur()); }
   __device__ __forceinline__ float* reward() const { return at<float>(ur() + 44); }
   __device__ __forceinline__ uint8_t* done() const { return at<uint8_t>(ur() + 48); }
@@ -191,8 +197,10 @@ struct DrawLds {
 #endif
 };
 
-// diagnostic phase clocks (tools/stamps.py; -DSACENV_STAMPS builds only)
-#ifdef SACENV_STAMPS
+// diagnostic phase clocks (tools/stamps.py; -DSACENV_STAMPS builds only).
+// SACENV_STAMPS_LIGHT keeps only each wave's start and end clock (no waits
+// inserted: the end clock is when the wave's last instruction issued).
+#if defined(SACENV_STAMPS) && !defined(SACENV_STAMPS_LIGHT)
 #define DRAW_STAMP(l, i)                                                   \
   do {                                                                     \
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");            \
@@ -647,17 +655,18 @@ __device__ void fit_store_wave(const SacenvBoatParams& p, const Arena& A, DrawLd
 }
 
 // knot values -> per-curve rows of l.y (lanes 16c + j), used before a fit
+// raw_row != NULL (phase A): the unfolded knots also go to the refill row
+// phase B fits from
 __device__ __forceinline__ void store_draw(const SacenvBoatParams& p, const Arena& A, const DrawLds& l,
-                                           int e, int slot, int32_t start_y, bool raw_to_wind,
+                                           int e, int slot, int32_t start_y, double* raw_row,
                                            int lane) {
   const int nk = p.n_knots;
   const int ncurves = p.use_wind_table ? 0 : n_curves(p.experiment);
   if (lane == 0) A.i32(U_STARTY)[(int64_t)slot * A.np + e] = start_y;
   const int c = lane >> 4, j = lane & 15;
   if (c < ncurves && j < nk) {
-    const int64_t o = A.wix(slot, c, j, e);
-    if (p.out_flags & SACENV_OUT_KNOTS) A.knots_raw()[o] = l.y[c][j];
-    if (raw_to_wind) A.wind_y()[o] = l.y[c][j];  // phase A: unfolded, fitted by phase B
+    if (p.out_flags & SACENV_OUT_KNOTS) A.knots_raw()[A.wix(slot, c, j, e)] = l.y[c][j];
+    if (raw_row != nullptr) raw_row[c * nk + j] = l.y[c][j];
   }
 }
 
@@ -667,7 +676,7 @@ __device__ int32_t draw_episode_wave(const SacenvBoatParams& p, const Arena& A, 
                                      const double* ex_knots) {
   const int32_t start_y = draw_knots_wave(p, A, l, e, lane, ex_start_y, ex_knots);
   __syncthreads();
-  store_draw(p, A, l, e, slot, start_y, false, lane);
+  store_draw(p, A, l, e, slot, start_y, nullptr, lane);
   fit_store_wave(p, A, l, e, slot, lane);
   return start_y;
 }
@@ -763,7 +772,8 @@ __device__ int phase_a(const SacenvBoatParams& p, const Arena& A, const Tail& T,
     const int32_t start_y = draw_knots_wave(p, A, l, e, lane, nullptr, nullptr);
     __syncthreads();
     DRAW_STAMP(l, 3);
-    store_draw(p, A, l, e, slot, start_y, !fit, lane);
+    store_draw(p, A, l, e, slot, start_y,
+               fit ? nullptr : A.refill_y(r) + (int64_t)rr * 2 * p.n_knots, lane);
     if (fit) fit_store_wave(p, A, l, e, slot, lane);
     if (lane == 0) {
       A.i32(U_FILL)[e] = f + 1;
@@ -775,7 +785,26 @@ __device__ int phase_a(const SacenvBoatParams& p, const Arena& A, const Tail& T,
   return done;
 }
 
-// Phase B for list ring r: fit the raw knots phase A stored.
+// Phase B for list ring r: fit the raw knots phase A stored in its rank's
+// refill row (no list -> slot dependency before the knots load). Prefetching
+// the first item for all three rings ahead of the launch counter measured
+// slower (more in-flight traffic at the owners' load burst).
+struct FirstItem {
+  int cnt;   // refill_count[r]
+  int v;     // refill_list[r][h]: env * kSlots + slot
+  double y;  // refill_y[r][h][lane] (lanes < 2 n_knots)
+};
+
+__device__ FirstItem load_first_item(const SacenvBoatParams& p, const Arena& A, int r, int h, int lane) {
+  FirstItem f;
+  const int hh = h < A.np ? h : (int)A.np - 1;  // speculative: used only if h < count <= n_envs
+  f.cnt = A.refill_count()[r];
+  f.v = A.refill_list(r)[hh];
+  const int nk2 = 2 * p.n_knots;
+  f.y = A.refill_y(r)[(int64_t)hh * nk2 + (lane < nk2 ? lane : 0)];
+  return f;
+}
+
 __device__ int phase_b(const SacenvBoatParams& p, const Arena& A, const Tail& T, DrawLds& l, int r,
                        int h, int H, int lane) {
   const GRegs g = fetch_g(p, T.g, lane);
@@ -787,10 +816,9 @@ __device__ int phase_b(const SacenvBoatParams& p, const Arena& A, const Tail& T,
   const int ncurves = n_curves(p.experiment);
   int done = 0;
   for (int rr = h; rr < cnt; rr += H) {
-    const int v = A.refill_list(r)[rr];
-    const int e = v / kSlots, slot = v % kSlots;
-    const int c = lane >> 4, j = lane & 15;
-    if (c < ncurves && j < nk) l.y[c][j] = A.wind_y()[A.wix(slot, c, j, e)];
+    const FirstItem it = load_first_item(p, A, r, rr, lane);
+    const int e = it.v / kSlots, slot = it.v % kSlots;
+    if (lane < ncurves * nk) l.y[lane / nk][lane % nk] = it.y;
     DRAW_STAMP(l, 2);
     fit_store_wave(p, A, l, e, slot, lane);
     ++done;
@@ -1223,6 +1251,15 @@ __host__ __device__ inline bool t_from_index(double dt) {
 // staging every output for 16-B stores at the end).
 #define EARLY_STORE(u, v) (A.f64(u)[e] = (v))
 
+// 64 obs rows (2816 B) from LDS to a 16-B aligned row block: 3 float4 stores
+__device__ __forceinline__ void store_obs_block(const float* lds_rows, float* dst_rows, int lane) {
+  const f4v* src = reinterpret_cast<const f4v*>(lds_rows);
+  f4v* dst = reinterpret_cast<f4v*>(dst_rows);
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    if (lane + kWave * i < kWave * SACENV_OBS_DIM / 4) dst[lane + kWave * i] = src[lane + kWave * i];
+}
+
 // One owner wave: BoatEnv.step for 64 consecutive envs, one per lane.
 __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Arena& A, const Tail& T,
                                            const float* __restrict__ action, OwnerLds& l, int ob,
@@ -1230,11 +1267,17 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
 #ifdef SACENV_STAMPS
   const uint64_t st_real0 = __builtin_amdgcn_s_memrealtime();
   uint64_t st_loaded = 0, st_computed = 0;
+#ifndef SACENV_STAMPS_LIGHT
 #define OWNER_STAMP(v)                                          \
   do {                                                          \
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); \
     v = __builtin_amdgcn_s_memrealtime();                       \
   } while (0)
+#else
+#define OWNER_STAMP(v) \
+  do {                 \
+  } while (0)
+#endif
 #else
 #define OWNER_STAMP(v) \
   do {                 \
@@ -1366,19 +1409,19 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
     A.accel()[2 * A.np + e] = a_r;
   }
   const bool restart = ended && p.autoreset;
-  if (ended) {
-    A.final_ep()[e] = ep;
-    // terminal obs of an auto-reset env (main.py:72 reset, boat_env.py:121)
-    if (restart) store_obs(A.final_obs() + (int64_t)e * SACENV_OBS_DIM, o);
-  }
+  if (ended) A.final_ep()[e] = ep;
+#ifdef SACENV_FINAL_NARROW  // A/B switch: per-lane terminal-obs stores
+  if (restart) store_obs(A.final_obs() + (int64_t)e * SACENV_OBS_DIM, o);
+#endif
   int cons_out = cons;
+  Obs fo;  // first obs of the next episode (restarting lanes)
   if (restart) {  // next episode from its pre-drawn slot: a fresh Boat (boat_env.py:152-198)
     const double sy0 = p.experiment == 2 ? (double)sy_next : 0.0;  // :166-169
     s_x = 0.0, s_y = sy0, s_r = 0.0, v_x = 0.0, v_y = 0.0, v_r = 0.0, rudder = 0.0;
     t = 0.0, ep = 0.0;  // :122
     index = 0;
     nwv = w0v, nwa = w0a;
-    o = make_obs(p, oc, 0.0, 0.0, 0.0, sy0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, (double)p.fuel0);
+    fo = make_obs(p, oc, 0.0, 0.0, 0.0, sy0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, (double)p.fuel0);
     cons_out = cons + 1;
   }
   // the dynamics' fields went out as they were computed; what is left: the
@@ -1398,16 +1441,34 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   A.reward()[e] = (float)reward;
   A.done()[e] = ended ? 1 : 0;
   A.term()[e] = term;
+  // obs rows through LDS, stored as float4 (64 rows x 44 B = 176 float4)
 #pragma unroll
   for (int k = 0; k < SACENV_OBS_DIM; ++k) l.obs[lane * SACENV_OBS_DIM + k] = o.v[k];
   __syncthreads();
-  {
-    const f4v* src = reinterpret_cast<const f4v*>(l.obs);
-    f4v* dst = reinterpret_cast<f4v*>(A.obs() + (int64_t)ob * kWave * SACENV_OBS_DIM);
+  const int64_t row0 = (int64_t)ob * kWave * SACENV_OBS_DIM;
+#ifdef SACENV_FINAL_NARROW
+  if (__ballot(restart) != 0ull) {
+    __syncthreads();
+    if (restart)
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
-      if (lane + kWave * i < kWave * SACENV_OBS_DIM / 4) dst[lane + kWave * i] = src[lane + kWave * i];
+      for (int k = 0; k < SACENV_OBS_DIM; ++k) l.obs[lane * SACENV_OBS_DIM + k] = fo.v[k];
+    __syncthreads();
   }
+  if (false) {
+#else
+  if (__ballot(restart) != 0ull) {  // uniform
+#endif
+    // final_obs block of the wave = this step's obs rows: the terminal obs of
+    // every env that ended (main.py:72 reset, boat_env.py:121); other rows of
+    // the block carry this step's obs (final_obs is valid where done)
+    store_obs_block(l.obs, A.final_obs() + row0, lane);
+    __syncthreads();
+    if (restart)
+#pragma unroll
+      for (int k = 0; k < SACENV_OBS_DIM; ++k) l.obs[lane * SACENV_OBS_DIM + k] = fo.v[k];
+    __syncthreads();
+  }
+  store_obs_block(l.obs, A.obs() + row0, lane);
 
   if (p.autoreset) {
     // this launch's ended envs, for the next launch's helpers (every wave
@@ -1417,7 +1478,9 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   }
   if (lane == 0) A.owner_epoch()[ob] = kepoch + 1;
 #ifdef SACENV_STAMPS
+#ifndef SACENV_STAMPS_LIGHT
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
   if (lane == 0) {
     double* d = A.accel() + (int64_t)ob * 4;
     d[0] = (double)st_real0;
@@ -1447,18 +1510,26 @@ __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, Arena A, Tai
 #endif
     const int hb = blockIdx.x;
     const int k = A.helper_epoch()[hb];
+
 #ifdef SACENV_STAMPS
     for (int i = 0; i < 8; ++i) lds.stamp[i] = 0;
     DRAW_STAMP(lds, 0);
 #endif
-    int nd;
-    if (hb < nh)  // phase A on launch k-1's masks (ring (k-1) % 3)
+    int nd = 0;
+    if (hb < nh) {  // phase A on launch k-1's masks (ring (k-1) % 3)
+#ifndef SACENV_DIAG_NO_PHASE_A  // timing diagnostics only (slots are then not refilled)
       nd = phase_a(p, A, T, lds, (k + 2) % kRing, hb, nh, false, lane);
-    else          // phase B on the list phase A built in launch k-1 (ring (k-2) % 3)
+#endif
+    } else {        // phase B on the list phase A built in launch k-1 (ring (k-2) % 3)
+#ifndef SACENV_DIAG_NO_PHASE_B
       nd = phase_b(p, A, T, lds, (k + 1) % kRing, hb - nh, nh, lane);
+#endif
+    }
     if (lane == 0) A.helper_epoch()[hb] = k + 1;
 #ifdef SACENV_STAMPS
+#ifndef SACENV_STAMPS_LIGHT
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
     if (lane == 0) {
       double* d = A.reward64() + (int64_t)hb * 12;
       d[0] = (double)hs_real0;

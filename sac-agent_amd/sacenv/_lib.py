@@ -11,7 +11,7 @@ import os
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # .../sac-agent_amd
 LIB_PATH = os.environ.get("SACENV_LIB", os.path.join(PKG_ROOT, "build", "libsacenv.so"))
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 OBS_DIM = 11
 MT_N = 624
 MAX_KNOTS = 16
@@ -54,7 +54,7 @@ LAYOUT_FIELDS = (
     "total_bytes", "n_pad", "s_x", "s_y", "s_r", "v_x", "v_y", "v_r", "rudder", "t",
     "ep_reward", "wind_next", "index", "cons", "fill", "mt_pos", "start_y", "counters",
     "refill_list",
-    "wind_y", "wind_m", "knots_raw", "mt_key", "record", "obs", "reward", "done", "term",
+    "wind_y", "wind_m", "knots_raw", "refill_y", "mt_key", "record", "obs", "reward", "done", "term",
     "final_obs", "final_ep_reward", "accel", "reward64", "refill_mask", "refill_count", "owner_epoch",
     "helper_epoch", "spline_g", "wind_table")
 

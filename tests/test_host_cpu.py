@@ -133,7 +133,7 @@ def test_arena_layout(built_lib, n):
     sizes = {"s_x": 8, "s_y": 8, "s_r": 8, "v_x": 8, "v_y": 8, "v_r": 8, "rudder": 8, "t": 8,
              "ep_reward": 8, "wind_next": 16, "index": 4, "cons": 4, "fill": 4, "mt_pos": 4, "start_y": 16,
              "counters": 20, "refill_list": 12, "wind_y": 64 * nk, "wind_m": 64 * nk,
-             "knots_raw": 64 * nk, "mt_key": 2496, "obs": 44, "reward": 4, "done": 1, "term": 1,
+             "knots_raw": 64 * nk, "refill_y": 48 * nk, "mt_key": 2496, "obs": 44, "reward": 4, "done": 1, "term": 1,
              "final_obs": 44, "final_ep_reward": 8, "accel": 24, "reward64": 8}
     spans = sorted((getattr(L, f), getattr(L, f) + w * np_, f) for f, w in sizes.items())
     for (a0, a1, f), (b0, b1, g) in zip(spans, spans[1:]):

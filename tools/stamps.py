@@ -21,7 +21,7 @@ def build():
     import __graft_entry__ as g
     extra = os.environ.get("STAMP_DEFINES", "").split()
     cmd = [g._hipcc(), *g.HIPCC_FLAGS, "-DSACENV_STAMPS", *extra, "-I", os.path.join(ROOT, "include"),
-           os.path.join(PKG, "csrc", "sacenv_boat.hip"), "-o", LIB]
+           *[os.path.join(PKG, "csrc", f) for f in g.SOURCES], "-o", LIB]
     subprocess.run(cmd, check=True)
 
 
@@ -60,7 +60,8 @@ def main():
     print(f"N={N} owner waves={nw} helpers={nh}x2 test_mode={tm}")
     print(f"owner span (first owner start -> last owner end) us: median {np.median(owner_end):.2f} "
           f"p90 {np.percentile(owner_end, 90):.2f}")
-    for a, b, nm in ((0, 2, "state+wind loads"), (2, 3, "compute"), (3, 1, "stores/end")):
+    light = "LIGHT" in os.environ.get("STAMP_DEFINES", "")
+    for a, b, nm in (() if light else ((0, 2, "state+wind loads"), (2, 3, "compute"), (3, 1, "stores/end"))):
         d = (r[..., b] - r[..., a]) / 100.0
         print(f"    owner {nm:16s} us median {np.median(d):6.2f} p90 {np.percentile(d, 90):6.2f}")
     skew = (r[..., 0] - t0[:, None]) / 100.0
@@ -76,8 +77,10 @@ def main():
               f"{hs[..., 2].max():.0f}; start median {np.median(start):.2f} us; "
               f"last busy end median {np.median(last):.2f} p90 {np.percentile(last, 90):.2f} us; "
               f"busy wave duration median {np.median(np.where(busy, end - start, np.nan)[busy]):.2f} us")
-        names = (("epoch", "masks+scan", "rank walk -> e", "pos/key -> knots", "stores/end") if ph == 0
-                 else ("epoch", "count", "list+raw y", "fit+stores/end"))
+        names = (() if light else ("epoch", "masks+scan", "rank walk -> e", "pos/key -> knots", "stores/end")
+                 if ph == 0 else ("epoch", "count", "list+raw y", "fit+stores/end"))
+        if not names:
+            continue
         b = hs[busy]                                   # [items, 12]
         marks = [b[:, 0]] + [b[:, 4 + i] for i in range(len(names) - 1)] + [b[:, 1]]
         for i, nm in enumerate(names):
