@@ -73,11 +73,17 @@ def init_dist(n_gpus: int):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != n_gpus:
         raise SystemExit(f"--gpus {n_gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    if os.environ.get("SACENV_BENCH_ONE_DEVICE"):  # rehearsal of the N>1 path on a 1-GPU box
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("SACENV_BENCH_BACKEND", "nccl")  # gloo: rehearsal on one GPU
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     return rank, world, torch.device("cuda", local)
 
 
@@ -166,15 +172,33 @@ def main():
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
     actions = (torch.rand((EPISODE_STEPS, N), generator=g, device=dev, dtype=torch.float32) * 2 - 1)
-    gathered = []
     if world > 1:
         import torch.distributed as dist
-        gathered = [torch.empty(world * e.record.numel(), dtype=torch.uint8, device=dev) for e in envs]
+        # Step k's packed records are copied to a staging buffer and all-gathered on a
+        # side stream while step k+1 runs (the env step needs only the local obs; the
+        # pooled records feed the shared replay buffer). Double-buffered: step k+2
+        # reuses step k's staging buffer after that gather has completed.
+        gather_stream = torch.cuda.Stream(device=dev)
+        stage = [[torch.empty_like(e.record) for e in envs] for _ in range(2)]
+        gathered = [[torch.empty(world * e.record.numel(), dtype=torch.uint8, device=dev)
+                     for e in envs] for _ in range(2)]
+        gather_done = [torch.cuda.Event(), torch.cuda.Event()]
+        for ev in gather_done:
+            ev.record(torch.cuda.current_stream(dev))
 
     def step_eager(k: int):
         stepper(actions[k % EPISODE_STEPS])
-        for e, buf in zip(envs if world > 1 else [], gathered):
-            dist.all_gather_into_tensor(buf, e.record)
+        if world > 1:
+            b = k % 2
+            cur = torch.cuda.current_stream(dev)
+            cur.wait_event(gather_done[b])
+            for e, st in zip(envs, stage[b]):
+                st.copy_(e.record)
+            gather_stream.wait_stream(cur)
+            with torch.cuda.stream(gather_stream):
+                for st, out in zip(stage[b], gathered[b]):
+                    dist.all_gather_into_tensor(out, st)
+                gather_done[b].record(gather_stream)
 
     use_graph = world == 1 and not args.no_graph
     graphs = []
@@ -278,7 +302,8 @@ def main():
                    "experiment": args.experiment, "envs_per_gpu": per_gpu_envs,
                    "global_envs": world * per_gpu_envs,
                    "episode_steps": EPISODE_STEPS, "parallelism": f"env-dp{world}",
-                   "collective": "all_gather (obs,reward,done,term) 50 B/env/step" if world > 1 else None,
+                   "collective": ("all_gather (obs,reward,done,term) 50 B/env/step, RCCL on a side "
+                                  "stream overlapped with the next step") if world > 1 else None,
                    "launch": "hipGraph x100 steps" if use_graph else "eager"},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK,

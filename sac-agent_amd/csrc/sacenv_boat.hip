@@ -1421,7 +1421,16 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
     t = 0.0, ep = 0.0;  // :122
     index = 0;
     nwv = w0v, nwa = w0a;
-    fo = make_obs(p, oc, 0.0, 0.0, 0.0, sy0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, (double)p.fuel0);
+    if (p.experiment == 2 || p.fuel0 == 0) {
+      fo = make_obs(p, oc, 0.0, 0.0, 0.0, sy0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, (double)p.fuel0);
+    } else {  // make_obs of the zero state, folded: (0+W)/(2W) = 0.5 and fuel0/fuel0 = 1 exactly
+      constexpr float kRud0 = (float)((0.0 + kPi / 3) * (1.0 / (kPi / 3 - (-kPi / 3))));
+#pragma unroll
+      for (int k = 0; k < SACENV_OBS_DIM; ++k) fo.v[k] = 0.0f;
+      fo.v[3] = 0.5f;
+      fo.v[9] = kRud0;
+      fo.v[10] = 1.0f;
+    }
     cons_out = cons + 1;
   }
   // the dynamics' fields went out as they were computed; what is left: the
