@@ -1500,7 +1500,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
 #endif
 }
 
-// The step launch. Grid: 2 x n_helpers refill helpers, nb_boat owner waves,
+// The step launch. Grid: nb_boat owner waves, 2 x n_helpers refill helpers,
 // then (kMixed) the waves of each toy arena: heterogeneous workgroups of one
 // launch, selected by uniform block-index ranges.
 template <bool kMixed>
@@ -1512,12 +1512,16 @@ __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, Arena A, Tai
   const int lane = threadIdx.x;
   const int nh = nb_boat > 0 && p.autoreset ? p.n_helpers : 0;
 
-  if ((int)blockIdx.x < 2 * nh) {
-    // ---------------- helpers (first in the grid, so they start first)
+  // grid order: owners, helpers, toys (owners dispatched first: -0.1 us/step
+  // against helpers first; the helpers' work has slack)
+  const int hb_raw = (int)blockIdx.x - nb_boat;
+  const bool is_helper = hb_raw >= 0 && hb_raw < 2 * nh;
+  if (is_helper) {
+    // ---------------- helpers
 #ifdef SACENV_STAMPS
     const uint64_t hs_real0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    const int hb = blockIdx.x;
+    const int hb = hb_raw;
     const int k = A.helper_epoch()[hb];
 
 #ifdef SACENV_STAMPS
@@ -1553,7 +1557,7 @@ __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, Arena A, Tai
     return;
   }
 
-  int b = blockIdx.x - 2 * nh;
+  int b = (int)blockIdx.x < nb_boat ? (int)blockIdx.x : (int)blockIdx.x - 2 * nh;
   if (!kMixed || b < nb_boat) {
     owner_wave(vreg_params(p), A, vreg_tail(T), action, slds.own, b, lane);
     return;
