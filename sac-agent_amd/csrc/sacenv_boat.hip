@@ -166,6 +166,25 @@ struct Arena {
   __device__ __forceinline__ int64_t wix(int slot, int c, int k, int e) const {
     return ((int64_t)(slot * 2 + c) * nk + k) * np + e;
   }
+  // Per-lane accesses as uniform base + 32-bit byte offset: the compiler then
+  // uses the SGPR-base addressing mode (no 64-bit address arithmetic in VALU).
+  // Offsets stay below 2^32 for n_envs <= 2^22 (check_params).
+  template <class T>
+  __device__ __forceinline__ T& at_e(int64_t unit, uint32_t off) const {
+    return *reinterpret_cast<T*>(b + unit * np + off);
+  }
+  __device__ __forceinline__ double& f64e(int u, uint32_t eo) const { return at_e<double>(u, eo); }
+  __device__ __forceinline__ int32_t& i32e(int u, uint32_t eo4) const { return at_e<int32_t>(u, eo4); }
+  // byte offset of wind coefficient (slot, curve, knot) of env e inside a wind array
+  __device__ __forceinline__ uint32_t wofs(int slot, int c, int k, int e) const {
+    return ((uint32_t)((slot * 2 + c) * nk + k) * (uint32_t)np + (uint32_t)e) * 8u;
+  }
+  __device__ __forceinline__ double wy_at(uint32_t off) const {
+    return *reinterpret_cast<const double*>(reinterpret_cast<const char*>(wind_y()) + off);
+  }
+  __device__ __forceinline__ double wm_at(uint32_t off) const {
+    return *reinterpret_cast<const double*>(reinterpret_cast<const char*>(wind_m()) + off);
+  }
 };
 
 __host__ inline Arena make_arena(const SacenvBoatParams& p, void* base) {
@@ -243,10 +262,8 @@ __device__ __forceinline__ double curve_lds(const SacenvBoatParams& p, const Dra
 __device__ __forceinline__ double curve_env(const SacenvBoatParams& p, const Arena& A, int slot, int c,
                                             int e, int i) {
   const Knot k = knot_coord(p, i);
-  const int64_t o = A.wix(slot, c, k.j, e);
-  const double* wy = A.wind_y();
-  const double* wm = A.wind_m();
-  return spline_piece(wy[o], wy[o + A.np], wm[o], wm[o + A.np], k.t);
+  const uint32_t o = A.wofs(slot, c, k.j, e), o1 = o + (uint32_t)A.np * 8u;
+  return spline_piece(A.wy_at(o), A.wy_at(o1), A.wm_at(o), A.wm_at(o1), k.t);
 }
 
 __host__ __device__ __forceinline__ int n_curves(int experiment) {
@@ -305,18 +322,18 @@ __device__ __forceinline__ void wind0_of_slot(const SacenvBoatParams& p, const A
       wa = p.wind_dir_rad;
       return;
     case 4:
-      wv = A.wind_y()[A.wix(slot, 0, 0, e)];
+      wv = A.wy_at(A.wofs(slot, 0, 0, e));
       wa = p.wind_dir_rad;
       return;
     case 5: {
       wv = p.max_velocity;
-      const double r = A.wind_y()[A.wix(slot, 0, 0, e)] <= 0.5 / 2 ? 0.0 : 1.0;
+      const double r = A.wy_at(A.wofs(slot, 0, 0, e)) <= 0.5 / 2 ? 0.0 : 1.0;
       wa = (r * kPi) + kPi / 2;
       return;
     }
     case 6:
-      wv = A.wind_y()[A.wix(slot, 0, 0, e)];
-      wa = A.wind_y()[A.wix(slot, 1, 0, e)];
+      wv = A.wy_at(A.wofs(slot, 0, 0, e));
+      wa = A.wy_at(A.wofs(slot, 1, 0, e));
       return;
     default:
       wv = 0.0;
@@ -1203,15 +1220,14 @@ union StepLds {
   OwnerLds own;
 };
 
-// byte address of (f64 field k, env e); fields 0..8 are U_SX..U_EP, 9/10 are wind_next
-__device__ __forceinline__ char* f64_field(const Arena& A, int k, int64_t e) {
-  return A.b + (int64_t)(8 * k) * A.np + 8 * e;
-}
 
 // wave-wide 16-B gathers of the owner's SoA inputs into LDS: 6 load instructions
 __device__ __forceinline__ void owner_load(const Arena& A, OwnerLds& l, int ob, int lane, bool t_idx) {
   const int half = lane >> 5, c = lane & 31;
   const int64_t e0 = (int64_t)ob * kWave;
+  // uniform row base + 32-bit per-lane offset (field 2q+half, envs e0+2c, e0+2c+1)
+  const char* row = A.b + e0 * 8;
+  const uint32_t lo = (uint32_t)half * 8u * (uint32_t)A.np + (uint32_t)c * 16u;
   f4v v[6];
 #pragma unroll
   for (int q = 0; q < 5; ++q) {
@@ -1219,13 +1235,13 @@ __device__ __forceinline__ void owner_load(const Arena& A, OwnerLds& l, int ob, 
       v[q] = f4v{0.f, 0.f, 0.f, 0.f};
       continue;
     }
-    v[q] = *reinterpret_cast<const f4v*>(f64_field(A, 2 * q + half, e0 + 2 * c));
+    v[q] = *reinterpret_cast<const f4v*>(row + (int64_t)(16 * q) * A.np + lo);
   }
   {  // lanes 0-31: wind_next angle; 32-47: index; 48-63: cons (4 envs per lane)
-    const char* src = lane < 32 ? f64_field(A, 10, e0 + 2 * c)
-                                : reinterpret_cast<const char*>(A.i32(lane < 48 ? U_IDX : U_CONS) + e0 +
-                                                                4 * (lane & 15));
-    v[5] = *reinterpret_cast<const f4v*>(src);
+    const uint32_t np = (uint32_t)A.np, j = (uint32_t)(lane & 15);
+    const uint32_t off = lane < 32 ? 80u * np + (uint32_t)e0 * 8u + (uint32_t)c * 16u
+                                   : (lane < 48 ? (uint32_t)U_IDX : (uint32_t)U_CONS) * np + (uint32_t)e0 * 4u + j * 16u;
+    v[5] = *reinterpret_cast<const f4v*>(A.b + off);
   }
 #pragma unroll
   for (int q = 0; q < 5; ++q) *reinterpret_cast<f4v*>(&l.f[2 * q + half][2 * c]) = v[q];
@@ -1249,15 +1265,17 @@ __host__ __device__ inline bool t_from_index(double dt) {
 // Each dynamics field is stored as soon as it is final, so the write traffic
 // drains while the wave still computes (measured: -0.15 us/step against
 // staging every output for 16-B stores at the end).
-#define EARLY_STORE(u, v) (A.f64(u)[e] = (v))
+#define EARLY_STORE(u, v) (A.f64e(u, eo) = (v))
 
 // 64 obs rows (2816 B) from LDS to a 16-B aligned row block: 3 float4 stores
 __device__ __forceinline__ void store_obs_block(const float* lds_rows, float* dst_rows, int lane) {
   const f4v* src = reinterpret_cast<const f4v*>(lds_rows);
-  f4v* dst = reinterpret_cast<f4v*>(dst_rows);
 #pragma unroll
-  for (int i = 0; i < 3; ++i)
-    if (lane + kWave * i < kWave * SACENV_OBS_DIM / 4) dst[lane + kWave * i] = src[lane + kWave * i];
+  for (int i = 0; i < 3; ++i) {
+    const uint32_t q = (uint32_t)lane + kWave * i;
+    if (q < kWave * SACENV_OBS_DIM / 4)
+      *reinterpret_cast<f4v*>(reinterpret_cast<char*>(dst_rows) + q * 16u) = src[q];
+  }
 }
 
 // One owner wave: BoatEnv.step for 64 consecutive envs, one per lane.
@@ -1284,9 +1302,10 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   } while (0)
 #endif
   const int e = ob * kWave + lane;
+  const uint32_t eo = (uint32_t)e * 8u, eo4 = (uint32_t)e * 4u;  // per-lane byte offsets
   const bool active = e < p.n_envs;
   const int kepoch = A.owner_epoch()[ob];
-  const float act = action[active ? e : 0];
+  const float act = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(action) + (active ? eo4 : 0u));
   const bool t_idx = t_from_index(p.dt);
   owner_load(A, l, ob, lane, t_idx);
   double s_x = l.f[0][lane], s_y = l.f[1][lane], s_r = l.f[2][lane];
@@ -1304,7 +1323,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   int32_t sy_next = 0;
   if (p.autoreset) {
     wind0_of_slot(p, A, T.table, (cons + 1) % kSlots, e, w0v, w0a);
-    if (p.experiment == 2) sy_next = A.i32(U_STARTY)[(int64_t)((cons + 1) % kSlots) * A.np + e];
+    if (p.experiment == 2) sy_next = A.i32e(U_STARTY + 4 * ((cons + 1) % kSlots), eo4);
   }
   OWNER_STAMP(st_loaded);
   const double r_mx = T.r_mx, r_my = T.r_my, r_iz = T.r_iz, r_nd = T.r_nd, r_w = T.r_w;
@@ -1365,7 +1384,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   EARLY_STORE(U_SR, s_r);
   EARLY_STORE(U_SX, s_x);
   EARLY_STORE(U_SY, s_y);
-  A.i32(U_IDX)[e] = index;
+  A.i32e(U_IDX, eo4) = index;
 
   Obs o = make_obs(p, oc, s_x, v_x, a_x, s_y, v_y, a_y, s_r, v_r, a_r, rudder, (double)fuel);
 
@@ -1395,21 +1414,21 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   if (!active) term = SACENV_TERM_NONE;  // padding lanes never end
 
   if (term != SACENV_TERM_NONE)  // no-return atomic: nothing on the critical path waits
-    __hip_atomic_fetch_add(A.at<uint32_t>(U_CNT) + (int64_t)(term - 1) * A.np + e, 1u, __ATOMIC_RELAXED,
+    __hip_atomic_fetch_add(&A.at_e<uint32_t>(U_CNT + 4 * (term - 1), eo4), 1u, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
   if (term == SACENV_TERM_NONE && active && p.max_episode_steps > 0 && index >= p.max_episode_steps)
     term = SACENV_TERM_TRUNCATED;
   const bool ended = term != SACENV_TERM_NONE;
 
   OWNER_STAMP(st_computed);
-  if (p.out_flags & SACENV_OUT_REWARD64) A.reward64()[e] = reward;
+  if (p.out_flags & SACENV_OUT_REWARD64) A.at_e<double>(A.ur() + 126, eo) = reward;
   if (p.out_flags & SACENV_OUT_ACCEL) {
-    A.accel()[e] = a_x;
-    A.accel()[A.np + e] = a_y;
-    A.accel()[2 * A.np + e] = a_r;
+    A.at_e<double>(A.ur() + 102, eo) = a_x;
+    A.at_e<double>(A.ur() + 110, eo) = a_y;
+    A.at_e<double>(A.ur() + 118, eo) = a_r;
   }
   const bool restart = ended && p.autoreset;
-  if (ended) A.final_ep()[e] = ep;
+  if (ended) A.at_e<double>(A.ur() + 94, eo) = ep;
 #ifdef SACENV_FINAL_NARROW  // A/B switch: per-lane terminal-obs stores
   if (restart) store_obs(A.final_obs() + (int64_t)e * SACENV_OBS_DIM, o);
 #endif
@@ -1437,19 +1456,19 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   // fresh state of restarting envs (same lane, same address: the later store
   // wins), ep_reward, the next wind, and the record
   if (restart) {
-    A.f64(U_SX)[e] = s_x, A.f64(U_SY)[e] = s_y, A.f64(U_SR)[e] = s_r;
-    A.f64(U_VX)[e] = v_x, A.f64(U_VY)[e] = v_y, A.f64(U_VR)[e] = v_r;
-    A.f64(U_RUD)[e] = rudder;
-    if (!t_idx) A.f64(U_T)[e] = t;
-    A.i32(U_IDX)[e] = index;
-    A.i32(U_CONS)[e] = cons_out;
+    A.f64e(U_SX, eo) = s_x, A.f64e(U_SY, eo) = s_y, A.f64e(U_SR, eo) = s_r;
+    A.f64e(U_VX, eo) = v_x, A.f64e(U_VY, eo) = v_y, A.f64e(U_VR, eo) = v_r;
+    A.f64e(U_RUD, eo) = rudder;
+    if (!t_idx) A.f64e(U_T, eo) = t;
+    A.i32e(U_IDX, eo4) = index;
+    A.i32e(U_CONS, eo4) = cons_out;
   }
-  A.f64(U_EP)[e] = ep;
-  A.f64(U_WNX)[e] = nwv;
-  A.f64(U_WNX)[A.np + e] = nwa;
-  A.reward()[e] = (float)reward;
-  A.done()[e] = ended ? 1 : 0;
-  A.term()[e] = term;
+  A.f64e(U_EP, eo) = ep;
+  A.f64e(U_WNX, eo) = nwv;
+  A.f64e(U_WNX + 8, eo) = nwa;
+  A.at_e<float>(A.ur() + 44, eo4) = (float)reward;
+  A.at_e<uint8_t>(A.ur() + 48, (uint32_t)e) = ended ? 1 : 0;
+  A.at_e<uint8_t>(A.ur() + 49, (uint32_t)e) = term;
   // obs rows through LDS, stored as float4 (64 rows x 44 B = 176 float4)
 #pragma unroll
   for (int k = 0; k < SACENV_OBS_DIM; ++k) l.obs[lane * SACENV_OBS_DIM + k] = o.v[k];
@@ -1614,7 +1633,7 @@ __global__ void __launch_bounds__(256) k_wind_eval(SacenvBoatParams p, Arena A, 
 int check_params(const SacenvBoatParams* p) {
   if (p == nullptr) return SACENV_E_NULL;
   if (p->experiment < 1 || p->experiment > 6) return SACENV_E_EXPERIMENT;
-  if (p->n_envs <= 0 || p->wind_len <= 0) return SACENV_E_SIZE;
+  if (p->n_envs <= 0 || p->n_envs > (1 << 22) || p->wind_len <= 0) return SACENV_E_SIZE;  // 32-bit offsets
   if (n_curves(p->experiment) > 0 && (p->n_knots < 4 || p->n_knots > kMaxK)) return SACENV_E_KNOTS;
   if (p->n_knots < 2 || p->n_knots > kMaxK) return SACENV_E_KNOTS;
   if (n_curves(p->experiment) > 0 && !p->use_wind_table && p->wind_len < 2) return SACENV_E_SIZE;
