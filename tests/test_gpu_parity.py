@@ -492,3 +492,41 @@ def test_time_accumulation_carried_and_derived(dt, t_max, gpu, built_lib):
         np.testing.assert_array_equal(info["term"].cpu().numpy(), r["term"], err_msg=f"step {k}")
         np.testing.assert_array_equal(env.t.cpu().numpy(), ora.t, err_msg=f"step {k}")
     assert (env.counters.cpu().numpy()[4] >= 1).all()   # every env timed out at least once
+
+
+@pytest.mark.parametrize("exp", [1, 2, 3, 4, 5, 6])
+def test_autoreset_all_experiments_ragged_vs_oracle(exp, gpu, built_lib):
+    """Every experiment, a ragged env count (1000 = 15 full waves + 40), auto-reset with
+    truncation and natural terminations (narrow track), all envs against the oracle:
+    term codes bit-exact, obs / final_obs / final episode reward / state within tolerance."""
+    from sacenv import VecBoatEnv
+    N, S, TR = 1000, 160, 37
+    seeds = (np.arange(N, dtype=np.uint64) * 7919 + 13) % (2 ** 32)
+    cfg = {"base_settings": {"experiment": exp, "test_mode": 0}, "boat_env": {"track_width": 30}}
+    env = VecBoatEnv(cfg, N, seeds=seeds, device=gpu, autoreset=True, max_episode_steps=TR,
+                     n_helpers=9)
+    ora = OracleVecBoat(OracleConfig(experiment=exp, test_mode=0, track_width=30), seeds,
+                        max_episode_steps=TR)
+    np.testing.assert_allclose(env.reset().cpu().numpy(), ora.reset(), rtol=OBS_TOL, atol=OBS_TOL)
+    rng = np.random.default_rng(exp)
+    n_nat = 0
+    for k in range(S):
+        a = rng.uniform(-1, 1, N).astype(np.float32)
+        o, r, d, info = env.step(torch.from_numpy(a).to(gpu))
+        ro = ora.step(a)
+        torch.cuda.synchronize()
+        term = info["term"].cpu().numpy()
+        np.testing.assert_array_equal(term, ro["term"], err_msg=f"step {k}")
+        done = term != 0
+        n_nat += int(((term > 0) & (term < 6)).sum())
+        np.testing.assert_allclose(o.cpu().numpy(), ro["reset_obs"], rtol=OBS_TOL, atol=OBS_TOL)
+        np.testing.assert_allclose(r.cpu().numpy(), ro["reward"], rtol=1e-6, atol=1e-5)
+        if done.any():
+            np.testing.assert_allclose(info["final_obs"].cpu().numpy()[done], ro["obs"][done],
+                                       rtol=OBS_TOL, atol=OBS_TOL)
+            np.testing.assert_allclose(info["final_ep_reward"].cpu().numpy()[done],
+                                       ro["ep_reward"][done], rtol=0, atol=1e-5)
+        assert np.abs(env.s_x.cpu().numpy() - ora.s_x).max() <= STATE_TOL
+        assert np.abs(env.s_y.cpu().numpy() - ora.s_y).max() <= STATE_TOL
+    assert n_nat > 0
+    np.testing.assert_array_equal(env.counters.cpu().numpy().T, ora.counters)
