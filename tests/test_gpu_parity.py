@@ -530,3 +530,50 @@ def test_autoreset_all_experiments_ragged_vs_oracle(exp, gpu, built_lib):
         assert np.abs(env.s_y.cpu().numpy() - ora.s_y).max() <= STATE_TOL
     assert n_nat > 0
     np.testing.assert_array_equal(env.counters.cpu().numpy().T, ora.counters)
+
+
+# ---------------------------------------------------------------- recorder (§8(f) rank 3)
+
+def test_vec_recorder_reproduces_reference_episode_csv(tmp_path, gpu, built_lib):
+    """VecRecorder on the reference's recorded exp-6 episode (wind table + start y replayed):
+    the episode CSV matches the reference's own episode_0_data.csv row for row (state within
+    1e-5, action and n exact), info.csv holds the reached_goal row and the episode reward."""
+    import csv
+    from sacenv import VecBoatEnv
+    from sacenv.recorder import COLUMNS, VecRecorder
+    z = golden("recorded_exp6.npz")
+    tr, cols = z["trace"], [str(c) for c in z["columns"]]
+    assert tuple(cols) == COLUMNS
+    table = np.stack([z["wind_velocity"], z["wind_angle"]])
+    env = VecBoatEnv({"base_settings": {"experiment": 6, "test_mode": 1}}, 3, device=gpu,
+                     autoreset=False, wind_table=table, record_reward64=True)
+    y0 = int(tr[0, cols.index("boat_position_y")])
+    env.reset_explicit([0, 1, 2], [y0, y0, y0])
+    rec = VecRecorder(env, [1], str(tmp_path), flush_steps=700)
+    n = len(tr)
+    acts = np.zeros(n, np.float32)
+    acts[: n - 1] = tr[1:, cols.index("action_rudder")]       # row k+1 holds step k's action
+    for k in range(n):
+        rec.record()
+        a = torch.full((3,), float(acts[k]), dtype=torch.float32, device=gpu)
+        env.step(a)
+        rec.after_step(a)
+    rec.close()
+    d = tmp_path / "episodes" / "env_1"
+    with open(d / "episode_0_data.csv") as f:
+        rows = list(csv.reader(f, delimiter=";"))
+    assert tuple(rows[0]) == COLUMNS and len(rows) == n + 1
+    got = np.array([[float(x) for x in r] for r in rows[1:]])
+    state_cols = [cols.index(c) for c in COLUMNS[:5]] + [cols.index("rudder_angle")]
+    np.testing.assert_allclose(got[:, state_cols], tr[:, state_cols], rtol=0, atol=1e-5)
+    np.testing.assert_array_equal(got[:, cols.index("action_rudder")].astype(np.float32),
+                                  tr[:, cols.index("action_rudder")].astype(np.float32))
+    np.testing.assert_allclose(got[:, cols.index("reward")], tr[:, cols.index("reward")], rtol=1e-9, atol=1e-12)
+    assert (got[:, cols.index("n")] == 20).all()
+    with open(d / "info.csv") as f:
+        info = list(csv.reader(f, delimiter=";"))
+    assert info[0][0] == "termination" and info[1][0] == "reached_goal" and info[1][1] == "1"
+    assert abs(float(info[1][-1]) - float(z["episode_reward"])) < 1e-6
+    with open(d / "wind.csv") as f:
+        w = np.array([[float(x) for x in r] for r in list(csv.reader(f, delimiter=";"))[1:]])
+    np.testing.assert_array_equal(w, table.T)
