@@ -1,4 +1,4 @@
-"""World-size-2 gloo test of the env-parallel record gather (CPU, no GPU).
+"""World-size 1/2/4 gloo tests of the env-parallel record gather (CPU, no GPU).
 
 Each rank runs its shard of envs (global-id seeds) on the CPU oracle, packs
 the step outputs in the kernel's record layout and all-gathers them; rank 0
@@ -55,11 +55,12 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_gather_pools_all_shards_world2():
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_gather_pools_all_shards(world):
+    """gloo at world sizes 1-4."""
     import sys
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from boat_oracle import OracleConfig, OracleVecBoat
-    world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

@@ -1,0 +1,99 @@
+"""the CPU restatement at N=1 (exp 1), one core and all cores.
+
+C1 is the reference's own CPU-runnable case: one env per process.
+* 1 core: oracle/boat_oracle.py with one env, pinned to one CPU
+  (``os.sched_setaffinity``, the ``taskset -c 0`` of §8(d)).
+* all cores: one such process per CPU of this process's affinity set (capped by
+  ``--max-procs``: the GPU box gives a job 16 CPUs while ``nproc`` shows the host's).
+Actions U(-1,1) float64 from ``np.random.default_rng(rank)``; auto-reset on done or
+every 500 steps, as in §8(d). Each process runs for a fixed wall time.
+
+Test / measurement infrastructure: this imports the oracle and is never part of the
+product path. Prints one JSON line.
+
+    python tools/cpu_c1.py [--seconds 10] [--max-procs 16]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import multiprocessing as mp
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(rank: int, cpu: int, seconds: float, q) -> None:
+    os.environ["OMP_NUM_THREADS"] = "1"
+    try:
+        os.sched_setaffinity(0, {cpu})
+    except OSError:
+        pass
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from boat_oracle import OracleConfig, OracleVecBoat
+    ora = OracleVecBoat(OracleConfig(experiment=1, test_mode=0), [rank], max_episode_steps=500)
+    ora.reset()
+    rng = np.random.default_rng(rank)
+    acts = rng.uniform(-1.0, 1.0, (4096, 1))
+    ora.step(acts[0])
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        for k in range(256):
+            ora.step(acts[(steps + k) % 4096])
+        steps += 256
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    q.put((rank, steps, el))
+
+
+def _leg(cpus, seconds):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_run, args=(r, c, seconds, q)) for r, c in enumerate(cpus)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=seconds * 10 + 120) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+    # whole-leg rate: every process's steps over the longest process's time
+    return sum(s for _, s, _ in res) / max(e for _, _, e in res)
+
+
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor()
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seconds", type=float, default=10.0)
+    ap.add_argument("--max-procs", type=int, default=16)
+    a = ap.parse_args(argv)
+    cpus = sorted(os.sched_getaffinity(0))
+    allc = cpus[:max(1, a.max_procs)]
+    one = _leg(cpus[:1], a.seconds)
+    many = _leg(allc, a.seconds)
+    print(json.dumps({
+        "config": "C1: exp 1, 1 env per process, oracle/boat_oracle.py (numpy f64)",
+        "one_core": {"env_steps_per_s": one, "procs": 1},
+        "all_cores": {"env_steps_per_s": many, "procs": len(allc)},
+        "os_cpu_count": os.cpu_count(), "affinity_cpus": len(cpus), "cpu_model": _cpu_model(),
+        "numpy": np.__version__, "python": platform.python_version(),
+        "note": "the reference BoatEnv itself: 13 385 env-steps/s on 1 core, 101 354 on 8 "
+                "(SURVEY.md §8(d), survey container)"}))
+
+
+if __name__ == "__main__":
+    main()
