@@ -11,12 +11,15 @@ all-gather over RCCL that pools transitions for a shared replay buffer).
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
 Timing: W untimed steps, then exactly K steps bracketed by barrier +
-synchronize; value = all envs x K / max-over-ranks time. At N=1 the steps
-are replayed from hipGraphs of 100 step launches (launch-bound otherwise).
-Roofline: SURVEY.md §8(d) algorithmic 222 B per boat env-step x envs per
-launch, over k_step's average launch duration from HIP events on the
-kernel's stream (the timed region itself at N=1); `traffic` = HBM bytes per
-launch from the committed rocprofv3 PMC passes (tools/pmc.sh).
+synchronize; value = all envs x K / max-over-ranks time. Every 32 steps the
+slot refill (k_refill: the RNG draws and spline fits of the episodes that
+replace the ended ones) runs as its own launch INSIDE the timed region. At
+N=1 the 32-step segments are replayed from hipGraphs (launch-bound
+otherwise). Roofline: SURVEY.md §8(d) algorithmic 222 B per boat env-step x
+envs per launch, over k_step's average launch duration from HIP events on
+the kernel's stream around the 32-launch segments of the timed region (the
+refills in between excluded; they are in ms_per_step); `traffic` = HBM bytes
+per launch from the committed rocprofv3 PMC passes (tools/pmc.sh).
 cpu_baseline: the numpy float64 oracle (oracle/boat_oracle.py, a port of the
 reference step) on the same workload shape, one core, bounded sample.
 """
@@ -41,7 +44,8 @@ METRIC_MIXED = ("env-steps/sec (whole node), mixed batch boat_env exp-6 + toy_pa
                 "32 768 envs each/GPU")
 HBM_PEAK = 8.0e12             # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 EPISODE_STEPS = 500
-GRAPH_STEPS = 100
+SEG = 32               # step launches per refill (sacenv _lib.REFILL_PERIOD); one graph per segment
+ACTION_STEPS = 512     # the pre-generated action table cycles every 512 steps (16 segments)
 
 
 def parse():
@@ -56,7 +60,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--kernel-launches", type=int, default=200)
     ap.add_argument("--test-mode", type=int, default=0, help="1 = rudder frozen (no terminations)")
-    ap.add_argument("--helpers", type=int, default=256, help="helper waves per step launch")
+    ap.add_argument("--helpers", type=int, default=2048, help="workgroups of a refill launch")
     ap.add_argument("--mixed", action="store_true",
                     help="BASELINE configs[4]: boat exp-6 + toy_parachute + toy_car in one launch")
     ap.add_argument("--mixed-envs", type=int, default=32768, help="envs per type per GPU (--mixed)")
@@ -160,8 +164,12 @@ def main():
     env = VecBoatEnv({"base_settings": {"experiment": args.experiment, "test_mode": args.test_mode}},
                      N, seed=0, device=dev, autoreset=not args.no_autoreset,
                      max_episode_steps=args.episode_steps,
-                     env_id_offset=rank * N, n_helpers=args.helpers)
+                     env_id_offset=rank * N, n_helpers=args.helpers, auto_refill=False)
     env.reset()
+    from sacenv import _lib
+    assert SEG == _lib.REFILL_PERIOD
+    autoreset = not args.no_autoreset
+    refill = env.refill if autoreset else (lambda: None)
     envs, stepper = [env], env.step_async
     if args.mixed:
         from sacenv.toys import CarEnv, MixedBatch, ParachuteEnv
@@ -171,7 +179,7 @@ def main():
         stepper = MixedBatch(env, toys).step_async
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
-    actions = (torch.rand((EPISODE_STEPS, N), generator=g, device=dev, dtype=torch.float32) * 2 - 1)
+    actions = (torch.rand((ACTION_STEPS, N), generator=g, device=dev, dtype=torch.float32) * 2 - 1)
     if world > 1:
         import torch.distributed as dist
         # Step k's packed records are copied to a staging buffer and all-gathered on a
@@ -187,7 +195,9 @@ def main():
             ev.record(torch.cuda.current_stream(dev))
 
     def step_eager(k: int):
-        stepper(actions[k % EPISODE_STEPS])
+        stepper(actions[k % ACTION_STEPS])
+        if (k + 1) % SEG == 0:
+            refill()
         if world > 1:
             b = k % 2
             cur = torch.cuda.current_stream(dev)
@@ -202,6 +212,14 @@ def main():
 
     use_graph = world == 1 and not args.no_graph
     graphs = []
+
+    def capture(k0: int) -> torch.cuda.CUDAGraph:
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr):
+            for k in range(k0, k0 + SEG):
+                stepper(actions[k % ACTION_STEPS])
+        return gr
+
     if use_graph:
         s = torch.cuda.Stream(device=dev)
         s.wait_stream(torch.cuda.current_stream(dev))
@@ -209,22 +227,28 @@ def main():
             for k in range(3):
                 step_eager(k)
         torch.cuda.current_stream(dev).wait_stream(s)
+        refill()
         torch.cuda.synchronize(dev)
-        for base in range(0, EPISODE_STEPS, GRAPH_STEPS):
-            gr = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gr):
-                for k in range(base, base + GRAPH_STEPS):
-                    stepper(actions[k])
-            graphs.append(gr)
+        graphs = [capture(base) for base in range(0, ACTION_STEPS, SEG)]
 
-    def run(n_steps: int, k0: int) -> int:
+    st = torch.cuda.current_stream(dev)
+    seg_events = []
+
+    def run(n_steps: int, k0: int, timed: bool = False) -> int:
         k = k0
         done = 0
         while done < n_steps:
-            if use_graph and k % GRAPH_STEPS == 0 and n_steps - done >= GRAPH_STEPS:
-                graphs[(k % EPISODE_STEPS) // GRAPH_STEPS].replay()
-                k += GRAPH_STEPS
-                done += GRAPH_STEPS
+            if use_graph and k % SEG == 0 and n_steps - done >= SEG:
+                if timed:
+                    ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    ea.record(st)
+                graphs[(k % ACTION_STEPS) // SEG].replay()
+                if timed:
+                    eb.record(st)
+                    seg_events.append((ea, eb))
+                refill()
+                k += SEG
+                done += SEG
             else:
                 step_eager(k)
                 k += 1
@@ -234,12 +258,11 @@ def main():
     k = run(args.warmup, 0)
     torch.cuda.synchronize(dev)
     barrier(world)
-    st = torch.cuda.current_stream(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     ev0.record(st)
-    k = run(args.steps, k)
+    k = run(args.steps, k, timed=True)
     ev1.record(st)
     torch.cuda.synchronize(dev)
     barrier(world)
@@ -250,28 +273,27 @@ def main():
     el_max = float(t.item())
 
     # k_step average launch duration from HIP events on the stream the kernel
-    # runs on. N=1: the timed region itself (K back-to-back k_step launches,
-    # graph-replayed). N>1: the timed region also holds the all-gathers, so a
-    # k_step-only graph of GRAPH_STEPS launches is replayed and timed after it.
-    if use_graph:
-        kern_s = ev0.elapsed_time(ev1) * 1e-3 / args.steps
-        kern_src = f"HIP events over the timed region: {args.steps} graph-replayed k_step launches"
+    # runs on, around 32-launch graph segments (refills excluded). N=1: the
+    # segments of the timed region itself. N>1: the timed region also holds
+    # the all-gathers, so k_step-only segments are replayed and timed after it.
+    if not use_graph:
+        k0 = (k + SEG - 1) // SEG * SEG
+        while k < k0:  # align to a segment boundary (refill after the last eager step)
+            step_eager(k)
+            k += 1
+        graphs = [capture(base) for base in range(0, ACTION_STEPS, SEG)]
+        use_graph = True
+        run(SEG, k)
+        torch.cuda.synchronize(dev)
+        run(max(SEG, args.kernel_launches // SEG * SEG), k, timed=True)
+        torch.cuda.synchronize(dev)
+        kern_src = (f"HIP events around {len(seg_events)} graph-replayed 32-launch k_step segments "
+                    "after the timed region (no collective; refills between segments excluded)")
     else:
-        gr = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(gr):
-            for i in range(GRAPH_STEPS):
-                stepper(actions[(k + i) % EPISODE_STEPS])
-        gr.replay()
-        torch.cuda.synchronize(dev)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        reps = max(1, args.kernel_launches // GRAPH_STEPS)
-        e0.record(st)
-        for _ in range(reps):
-            gr.replay()
-        e1.record(st)
-        torch.cuda.synchronize(dev)
-        kern_s = e0.elapsed_time(e1) * 1e-3 / (reps * GRAPH_STEPS)
-        kern_src = f"HIP events around {reps * GRAPH_STEPS} graph-replayed k_step launches (no collective)"
+        kern_src = (f"HIP events around the {len(seg_events)} graph-replayed 32-launch k_step "
+                    "segments of the timed region (refills between segments excluded)")
+    kern_s = sum(a.elapsed_time(b) for a, b in seg_events) * 1e-3 / (SEG * len(seg_events))
+    step_s = ev0.elapsed_time(ev1) * 1e-3 / args.steps
 
     if rank != 0:
         if world > 1:
@@ -304,7 +326,9 @@ def main():
                    "episode_steps": EPISODE_STEPS, "parallelism": f"env-dp{world}",
                    "collective": ("all_gather (obs,reward,done,term) 50 B/env/step, RCCL on a side "
                                   "stream overlapped with the next step") if world > 1 else None,
-                   "launch": "hipGraph x100 steps" if use_graph else "eager"},
+                   "launch": ("hipGraph segments of 32 k_step launches + 1 k_refill launch"
+                              if world == 1 and not args.no_graph else "eager"),
+                   "refill": "k_refill every 32 steps, inside the timed region" if autoreset else None},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK,
                      "traffic": None if traffic is None else traffic["hbm_bytes_per_launch"],
@@ -313,6 +337,7 @@ def main():
                      "bytes_per_env_step": ({"boat": BYTES_PER_ENV_STEP, "parachute": 86, "car": 102}
                                             if args.mixed else BYTES_PER_ENV_STEP),
                      "kernel_avg_us": kern_s * 1e6,
+                     "step_us_incl_refill": step_s * 1e6,
                      "timing": kern_src,
                      "traffic_source": None if traffic is None else traffic["source"]},
         "cpu_baseline": None,

@@ -35,12 +35,13 @@
 extern "C" {
 #endif
 
-#define SACENV_ABI_VERSION 7
+#define SACENV_ABI_VERSION 8
 #define SACENV_OBS_DIM 11      /* Boat.return_state, boat_env.py:308-323 */
 #define SACENV_MT_N 624        /* MT19937 words per env (numpy legacy RNG) */
 #define SACENV_MAX_KNOTS 16    /* wind.fixed_points upper bound */
 #define SACENV_N_COUNTERS 5    /* info-dict termination counters, boat_env.py:24-32 */
-#define SACENV_SLOTS 4         /* episode slots per env in autoreset mode (active + 3 ahead) */
+#define SACENV_SLOTS 33        /* episode slots per env in autoreset mode (active + 32 ahead) */
+#define SACENV_REFILL_PERIOD 32 /* autoreset: at most this many step launches between refills */
 #define SACENV_RECORD_BYTES 50 /* packed per-env step record (see layout.record) */
 
 /* termination codes; 1..5 follow the info-dict key order boat_env.py:24-32,
@@ -86,7 +87,7 @@ typedef struct SacenvBoatParams {
   int32_t start_y_half;       /* int(0.8*track_width) (boat_env.py:147-150) */
   int32_t max_episode_steps;  /* > 0: truncate (term 6) after this many steps; 0: off */
   int32_t autoreset;          /* 1: envs that end start their next episode inside step */
-  int32_t n_helpers;          /* autoreset: helper waves per step launch (1..4096) */
+  int32_t n_helpers;          /* autoreset: workgroups of a sacenv_boat_refill launch (1..4096) */
   int32_t out_flags;          /* SACENV_OUT_* bitmask */
   int32_t use_wind_table;     /* 1: wind from layout.wind_table [2][L] for every env */
   double dt, t_max, goal_line, oob_limit, track_width;  /* oob = width + offset (:200-201) */
@@ -115,19 +116,22 @@ typedef struct SacenvBoatLayout {
   int64_t n_pad;
   int64_t s_x, s_y, s_r, v_x, v_y, v_r, rudder, t, ep_reward; /* f64 [n_pad] */
   int64_t wind_next;          /* f64 [2][n_pad] Wind.get_wind(index) for the NEXT step (v, angle) */
+  int64_t wind_coef;          /* f64 [2 curves][y0 y1 m0 m1][n_pad]: the active episode's spline piece
+                                 of the interval of the next wind sample (a copy of its slot's
+                                 wind_y/wind_m, refreshed in an episode's first step and when the
+                                 sample crosses a knot) */
+  int64_t wind0_next;         /* f64 [2][n_pad] autoreset: Wind.get_wind(0) of the NEXT episode (copy,
+                                 refreshed in each episode's first step) */
+  int64_t start_y_next;       /* i32 [n_pad] autoreset: Boat.s_y_start of the next episode (same) */
   int64_t index;              /* i32 [n_pad] steps since reset; fuel = fuel0 - index */
-  int64_t cons;               /* i32 [n_pad] episodes started (active slot = cons % 4) */
-  int64_t fill;               /* i32 [n_pad] episodes drawn (autoreset) */
+  int64_t cons;               /* i32 [n_pad] episodes started (active slot = cons % SLOTS) */
+  int64_t fill;               /* i32 [n_pad] episodes drawn (autoreset; cons < fill <= cons + SLOTS) */
   int64_t mt_pos;             /* i32 [n_pad] next MT word index, 624 => twist first */
-  int64_t start_y;            /* i32 [4][n_pad] Boat.s_y_start per slot */
+  int64_t start_y;            /* i32 [SLOTS][n_pad] Boat.s_y_start per slot */
   int64_t counters;           /* u32 [5][n_pad] cumulative termination counters */
-  int64_t refill_list;        /* i32 [3][n_pad] ranked (env*4 + slot) drawn by phase A of launch k
-                                 (ring k % 3), spline-fitted by phase B of launch k+1 */
-  int64_t wind_y;             /* f64 [4][2][n_knots][n_pad] folded knot values per slot, curve */
-  int64_t wind_m;             /* f64 [4][2][n_knots][n_pad] folded 2nd derivatives / 6 */
-  int64_t knots_raw;          /* f64 [4][2][n_knots][n_pad] drawn knots (SACENV_OUT_KNOTS) */
-  int64_t refill_y;           /* f64 [3][n_pad][2][n_knots] knots drawn by phase A in launch k
-                                 (ring k % 3, rank order), fitted by phase B in launch k+1 */
+  int64_t wind_y;             /* f64 [SLOTS][2][n_knots][n_pad] folded knot values per slot, curve */
+  int64_t wind_m;             /* f64 [SLOTS][2][n_knots][n_pad] folded 2nd derivatives / 6 */
+  int64_t knots_raw;          /* f64 [SLOTS][2][n_knots][n_pad] drawn knots (SACENV_OUT_KNOTS) */
   int64_t mt_key;             /* u32 [n_pad][624] per-env MT19937 state */
   int64_t record;             /* u8 [50 n_pad]: obs f32 [n_pad][11] | reward f32 [n_pad]
                                  | done u8 [n_pad] | term u8 [n_pad]  (the all-gather payload) */
@@ -136,14 +140,20 @@ typedef struct SacenvBoatLayout {
   int64_t final_ep_reward;    /* f64 [n_pad] episode reward of envs that ended */
   int64_t accel;              /* f64 [3][n_pad] a_x, a_y, a_r */
   int64_t reward64;           /* f64 [n_pad] */
-  int64_t refill_mask;        /* u64 [3][n_pad/64] per owner wave: envs that ended in launch k
-                                 (ring index k % 3), i.e. whose freed slot awaits a refill */
-  int64_t refill_count;       /* i32 [3] (256 B): entries of refill_list per ring index */
+  int64_t refill_mask;        /* u64 [n_pad/64] per owner wave: envs that ended since the last
+                                 sacenv_boat_refill (tagged with mask_gen) */
+  int64_t mask_gen;           /* i32 [n_pad/64] refill generation each refill_mask word belongs to */
+  int64_t status;             /* i32 [64] (256 B): [0] refill generation, [1] SACENV_STATUS_* bits */
   int64_t owner_epoch;        /* i32 [n_pad/64] per owner-block launch counter */
-  int64_t helper_epoch;       /* i32 [2 n_helpers] per helper-block launch counter (phase A, B) */
   int64_t spline_g;           /* f64 [n_knots][n_knots]: (m/6) = G @ knots (written by init) */
   int64_t wind_table;         /* f64 [2][wind_len] (velocity, angle), if use_wind_table */
 } SacenvBoatLayout;
+
+/* status bits (layout.status[1]); sticky until the arena is re-initialised */
+enum {
+  SACENV_STATUS_SLOT_UNDERFLOW = 1 /* an env restarted past its pre-drawn episodes: more than
+                                      SACENV_REFILL_PERIOD step launches without a refill */
+};
 
 int sacenv_abi_version(void);
 const char *sacenv_error_string(int code);
@@ -156,8 +166,8 @@ int sacenv_boat_layout(const SacenvBoatParams *p, SacenvBoatLayout *out);
  * constants, and build every env's first Boat — BoatEnv.__init__ constructs
  * one (boat_env.py:15; Boat.__init__ :144-201, Wind wind.py:26-99) — drawing
  * in the reference's order (randint :147, then 8 knot values per random
- * curve wind.py:78). In autoreset mode the next three episodes are pre-drawn
- * too (same per-env stream, same order). `seeds` is a DEVICE u32 [n_envs];
+ * curve wind.py:78). In autoreset mode the next SLOTS-1 episodes are
+ * pre-drawn too (same per-env stream, same order). `seeds` is a DEVICE u32 [n_envs];
  * `obs` (nullable) receives the first observations [n_envs][11] f32. */
 int sacenv_boat_init(const SacenvBoatParams *p, void *arena, const uint32_t *seeds, void *stream);
 
@@ -190,12 +200,18 @@ int sacenv_boat_reset_explicit(const SacenvBoatParams *p, void *arena, const int
  * [n_envs]. Outputs go to the arena's record (+ optional outputs). With
  * autoreset, an env that ends starts its next (pre-drawn) episode in the same
  * launch: its obs row is the new episode's, the terminal obs is in
- * final_obs. Helper waves of the same launch refill freed slots in two
- * phases: phase A draws (RNG) the replacement episodes of the envs that ended
- * in launch k-1, phase B fits the wind splines of the episodes phase A drew
- * in launch k-1. A freed slot is thus ready two launches after it is freed,
- * and four slots keep an env that ends every step supplied. */
+ * final_obs. The launch only CONSUMES pre-drawn episodes (no RNG or spline
+ * work on the step's path); sacenv_boat_refill replaces them. */
 int sacenv_boat_step(const SacenvBoatParams *p, void *arena, const float *action, void *stream);
+
+/* Autoreset mode: draw (RNG, Boat.__init__ boat_env.py:144-201 / Wind
+ * wind.py:26-99) and spline-fit the replacement episodes of every env that
+ * ended since the previous refill, topping its slot ring up to SLOTS
+ * episodes, in the env's own draw order. Call it at least once every
+ * SACENV_REFILL_PERIOD step launches (sacenv_boat_step / sacenv_mixed_step),
+ * counted from init; more often is harmless. Envs that restart more often
+ * than that without a refill set SACENV_STATUS_SLOT_UNDERFLOW. */
+int sacenv_boat_refill(const SacenvBoatParams *p, void *arena, void *stream);
 
 /* Wind.get_wind(index) (wind.py:20-24) of each env's CURRENT episode for n
  * (env, index) pairs (device i32 arrays) -> device f64 out arrays. Exposes
@@ -256,8 +272,7 @@ int sacenv_toy_step(const SacenvToyParams *p, void *arena, void *stream);
 
 /* Mixed batch (BASELINE configs[4]): one launch stepping a boat arena and up
  * to two toy arenas (toy_params[n_toys], toy_arenas[n_toys]) with
- * heterogeneous workgroups (boat helpers, boat owners, then each toy's
- * waves). Equivalent to sacenv_boat_step + sacenv_toy_step per toy arena;
+ * heterogeneous workgroups (boat owners, then each toy's waves). Equivalent to sacenv_boat_step + sacenv_toy_step per toy arena;
  * bp may be NULL for toys only. */
 int sacenv_mixed_step(const SacenvBoatParams *bp, void *boat_arena, const float *boat_action,
                       const SacenvToyParams *toy_params, void *const *toy_arenas, int32_t n_toys,

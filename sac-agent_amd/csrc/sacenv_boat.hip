@@ -1,26 +1,21 @@
 // sacenv_boat.hip — gfx950 kernels + C ABI for the vectorised boat env.
 //
-// One step launch (autoreset mode) runs three kinds of wave64 workgroups:
-//   * owner waves (one lane per env, 64 consecutive envs): BoatEnv.step
-//     (boat_env.py:67-115) on float64 SoA state. An env that ends (terminated
-//     or truncated) starts its next episode at once from a PRE-DRAWN slot
-//     (4 slots/env: the active episode + 3 ahead), so no RNG or spline work
-//     ever sits on the step's critical path. Each owner wave publishes a
-//     64-bit mask of its ended envs (one plain store, no atomics).
-//   * phase-A helpers: for the envs that ended in the PREVIOUS launch, draw
-//     the replacement episode from the env's own numpy-legacy MT19937 stream
-//     (Boat.__init__ boat_env.py:144-201: randint, then the wind knots,
-//     wind.py:69-90) into the freed slot, one wave per env.
-//   * phase-B helpers: for the envs drawn by the previous launch's phase A,
-//     fit the not-a-knot spline, find its exact grid-sample min/max from the
-//     critical points (instead of the reference's 10 000-sample scan,
-//     wind.py:80-89), renormalise and scale the curve (wind.py:86-99).
-// Helpers rank the flagged envs from the masks (DPP scans, no atomics), so
-// the work is balanced exactly. Nothing is handed between workgroups inside a
-// launch: a slot freed in launch k is drawn in k+1, fitted in k+2 and used no
-// earlier than k+3, which four slots guarantee even for an env that ends in
-// every launch. Masks/lists are ring-buffered by per-block launch counters,
-// so graph replay needs no per-launch arguments.
+// The step launch (k_step) runs owner waves only: one lane per env, 64
+// consecutive envs per wave, BoatEnv.step (boat_env.py:67-115) on float64
+// SoA state. In autoreset mode an env that ends (terminated or truncated)
+// starts its next episode at once from a PRE-DRAWN slot (SLOTS = 33 per env:
+// the active episode + 32 ahead), so no RNG or spline work ever sits on the
+// step's path; each owner wave ORs a 64-bit mask of its ended envs into its
+// own word (plain load/store, no atomics).
+// The refill launch (k_refill, at least every 32 steps) ranks the flagged
+// envs from those masks (DPP scans, no atomics) and, one wave per env, draws
+// the replacement episodes from the env's own numpy-legacy MT19937 stream
+// (Boat.__init__ boat_env.py:144-201: randint, then the wind knots,
+// wind.py:69-90), fits the not-a-knot spline, finds its exact grid-sample
+// min/max from the critical points (instead of the reference's 10 000-sample
+// scan, wind.py:80-89) and stores the renormalised, scaled curve
+// (wind.py:86-99). Kept out of the step launch, this work no longer shares
+// SIMDs with the owners (measured: in-step helper waves cost 1.6 us/step).
 //
 // Floating-point order follows the reference expression by expression
 // (left-to-right products, no FMA contraction: -ffp-contract=off); the only
@@ -44,25 +39,29 @@ constexpr uint32_t kMtLower = 0x7fffffffu;
 constexpr uint32_t kMtMatrixA = 0x9908b0dfu;
 constexpr int kMaxK = SACENV_MAX_KNOTS;
 constexpr int kSlots = SACENV_SLOTS;
-constexpr int kRing = 3;          // ring depth of masks / lists (written k, read k+1, k+2)
-constexpr int kMaskLds = 1024;    // refill masks staged in LDS (owner waves <= 1024)
 constexpr double kPi = 3.141592653589793;  // np.pi
 
 // ---------------------------------------------------------------- arena
 // Per-env byte widths; a field's offset is (sum of widths before it) * n_pad.
 // n_pad is a multiple of 64, so every array is 64-byte aligned.
+// U_COEF / U_W0N / U_SYN are lane-coalesced copies of slot data the step
+// reads every launch (see owner_wave): the active episode's spline piece
+// (y0, y1, m0, m1 per curve) of the interval of the next wind sample, and
+// the next episode's first wind and start y. Slots differ from env to env,
+// so reading them from the slot ring itself would scatter every wave's loads
+// over up to 33 rows.
 constexpr int U_SX = 0, U_SY = 8, U_SR = 16, U_VX = 24, U_VY = 32, U_VR = 40, U_RUD = 48,
-              U_T = 56, U_EP = 64, U_WNX = 72, U_IDX = 88, U_CONS = 92, U_FILL = 96,
-              U_MTPOS = 100, U_STARTY = 104, U_CNT = 104 + 4 * kSlots,
-              U_LIST = U_CNT + 4 * SACENV_N_COUNTERS, U_WIND = U_LIST + 4 * kRing;
+              U_T = 56, U_EP = 64, U_WNX = 72, U_COEF = 88, U_W0N = 152, U_IDX = 168,
+              U_CONS = 172, U_FILL = 176, U_MTPOS = 180, U_SYN = 184, U_STARTY = 188,
+              U_CNT = U_STARTY + 4 * kSlots,
+              U_WIND = U_CNT + 4 * SACENV_N_COUNTERS;
 constexpr int U_MT_BYTES = 4 * kMtN;
 constexpr int64_t kWindUnits = 16LL * kSlots;  // f64 x 2 curves x slots, per knot
 
 __host__ __device__ inline int64_t pad64(int64_t n) { return (n + 63) / 64 * 64; }
 __host__ __device__ inline int64_t align256(int64_t x) { return (x + 255) / 256 * 256; }
 
-__host__ __device__ inline void compute_layout(int n, int nk, int nh, int L, int use_table,
-                                               SacenvBoatLayout* o) {
+__host__ __device__ inline void compute_layout(int n, int nk, int L, int use_table, SacenvBoatLayout* o) {
   const int64_t np = pad64(n), nw = np / 64;
   o->n_pad = np;
   o->s_x = U_SX * np;
@@ -75,20 +74,21 @@ __host__ __device__ inline void compute_layout(int n, int nk, int nh, int L, int
   o->t = U_T * np;
   o->ep_reward = U_EP * np;
   o->wind_next = U_WNX * np;
+  o->wind_coef = U_COEF * np;
+  o->wind0_next = U_W0N * np;
+  o->start_y_next = U_SYN * np;
   o->index = U_IDX * np;
   o->cons = U_CONS * np;
   o->fill = U_FILL * np;
   o->mt_pos = U_MTPOS * np;
   o->start_y = U_STARTY * np;
   o->counters = U_CNT * np;
-  o->refill_list = U_LIST * np;
   const int64_t uw = U_WIND, wk = kWindUnits * nk;
   o->wind_y = uw * np;
   o->wind_m = (uw + wk) * np;
   o->knots_raw = (uw + 2 * wk) * np;
-  o->refill_y = (uw + 3 * wk) * np;
-  o->mt_key = (uw + 3 * wk + kRing * 16LL * nk) * np;
-  const int64_t ur = uw + 3 * wk + kRing * 16LL * nk + U_MT_BYTES;
+  o->mt_key = (uw + 3 * wk) * np;
+  const int64_t ur = uw + 3 * wk + U_MT_BYTES;
   o->record = ur * np;
   o->obs = ur * np;
   o->reward = (ur + 44) * np;
@@ -100,13 +100,13 @@ __host__ __device__ inline void compute_layout(int n, int nk, int nh, int L, int
   o->reward64 = (ur + 126) * np;
   int64_t off = align256((ur + 134) * np);
   o->refill_mask = off;
-  off += align256(8 * kRing * nw);
-  o->refill_count = off;
+  off += align256(8 * nw);
+  o->mask_gen = off;
+  off += align256(4 * nw);
+  o->status = off;
   off += 256;
   o->owner_epoch = off;
   off += align256(4 * nw);
-  o->helper_epoch = off;
-  off += align256(4LL * 2 * (nh > 0 ? nh : 1));
   o->spline_g = off;
   off += align256(8LL * kMaxK * kMaxK);
   o->wind_table = off;
@@ -129,13 +129,8 @@ struct Arena {
   __device__ __forceinline__ double* wind_y() const { return at<double>(U_WIND); }
   __device__ __forceinline__ double* wind_m() const { return at<double>(U_WIND + wk()); }
   __device__ __forceinline__ double* knots_raw() const { return at<double>(U_WIND + 2 * wk()); }
-  // raw knot values drawn by phase A, [ring][rank][curve][knot]: phase B reads its
-  // first row at a fixed address (no list -> slot dependency)
-  __device__ __forceinline__ double* refill_y(int r) const {
-    return at<double>(U_WIND + 3 * wk()) + (int64_t)r * np * 2 * nk;
-  }
-  __device__ __forceinline__ uint32_t* mt_key() const { return at<uint32_t>(U_WIND + 3 * wk() + kRing * 16LL * nk); }
-  __device__ __forceinline__ int64_t ur() const { return U_WIND + 3 * wk() + kRing * 16LL * nk + U_MT_BYTES; }
+  __device__ __forceinline__ uint32_t* mt_key() const { return at<uint32_t>(U_WIND + 3 * wk()); }
+  __device__ __forceinline__ int64_t ur() const { return U_WIND + 3 * wk() + U_MT_BYTES; }
   __device__ __forceinline__ float* obs() const { return at<float>(ur()); }
   __device__ __forceinline__ float* reward() const { return at<float>(ur() + 44); }
   __device__ __forceinline__ uint8_t* done() const { return at<uint8_t>(ur() + 48); }
@@ -145,23 +140,18 @@ struct Arena {
   __device__ __forceinline__ double* accel() const { return at<double>(ur() + 102); }
   __device__ __forceinline__ double* reward64() const { return at<double>(ur() + 126); }
   __device__ __forceinline__ char* tail() const { return b + align256((ur() + 134) * np); }
-  // ended-env mask of owner wave w, ring slot r (written by launch k, r = k % 3)
-  __device__ __forceinline__ unsigned long long* refill_mask(int r) const {
-    return reinterpret_cast<unsigned long long*>(tail()) + (int64_t)r * nwaves();
+  // envs of owner wave w that ended since the refill of generation mask_gen[w]
+  __device__ __forceinline__ unsigned long long* refill_mask() const {
+    return reinterpret_cast<unsigned long long*>(tail());
   }
-  __device__ __forceinline__ int32_t* refill_count() const {
-    return reinterpret_cast<int32_t*>(tail() + align256(8 * kRing * nwaves()));
+  __device__ __forceinline__ int32_t* mask_gen() const {
+    return reinterpret_cast<int32_t*>(tail() + align256(8 * nwaves()));
   }
-  __device__ __forceinline__ int32_t* refill_list(int r) const {
-    return i32(U_LIST) + (int64_t)r * np;
+  // [0] refill generation, [1] SACENV_STATUS_* bits
+  __device__ __forceinline__ int32_t* status() const {
+    return reinterpret_cast<int32_t*>(tail() + align256(8 * nwaves()) + align256(4 * nwaves()));
   }
-  __device__ __forceinline__ int32_t* owner_epoch() const {
-    return reinterpret_cast<int32_t*>(tail() + align256(8 * kRing * nwaves()) + 256);
-  }
-  __device__ __forceinline__ int32_t* helper_epoch() const {
-    return reinterpret_cast<int32_t*>(tail() + align256(8 * kRing * nwaves()) + 256 +
-                                      align256(4 * nwaves()));
-  }
+  __device__ __forceinline__ int32_t* owner_epoch() const { return status() + 64; }
   // slot-major wind coefficient of (slot, curve, knot) for env e
   __device__ __forceinline__ int64_t wix(int slot, int c, int k, int e) const {
     return ((int64_t)(slot * 2 + c) * nk + k) * np + e;
@@ -205,7 +195,6 @@ struct Tail {
 // ---------------------------------------------------------------- LDS of a drawing wave
 
 struct DrawLds {
-  unsigned long long masks[kMaskLds];
   uint32_t win[kWave];    // MT window (tempered words pos .. pos+63)
   uint32_t blk[2][kMtN];  // current MT block, next (twisted) block
   double y[2][kMaxK];     // knot values per curve (unfolded)
@@ -671,20 +660,15 @@ __device__ void fit_store_wave(const SacenvBoatParams& p, const Arena& A, DrawLd
   __syncthreads();
 }
 
-// knot values -> per-curve rows of l.y (lanes 16c + j), used before a fit
-// raw_row != NULL (phase A): the unfolded knots also go to the refill row
-// phase B fits from
+// start y and (SACENV_OUT_KNOTS) the raw knot values of a drawn episode
 __device__ __forceinline__ void store_draw(const SacenvBoatParams& p, const Arena& A, const DrawLds& l,
-                                           int e, int slot, int32_t start_y, double* raw_row,
-                                           int lane) {
+                                           int e, int slot, int32_t start_y, int lane) {
   const int nk = p.n_knots;
   const int ncurves = p.use_wind_table ? 0 : n_curves(p.experiment);
   if (lane == 0) A.i32(U_STARTY)[(int64_t)slot * A.np + e] = start_y;
   const int c = lane >> 4, j = lane & 15;
-  if (c < ncurves && j < nk) {
-    if (p.out_flags & SACENV_OUT_KNOTS) A.knots_raw()[A.wix(slot, c, j, e)] = l.y[c][j];
-    if (raw_row != nullptr) raw_row[c * nk + j] = l.y[c][j];
-  }
+  if (c < ncurves && j < nk && (p.out_flags & SACENV_OUT_KNOTS))
+    A.knots_raw()[A.wix(slot, c, j, e)] = l.y[c][j];
 }
 
 // Boat(config) in one go (init / host-driven resets): draw + fit into slot.
@@ -693,43 +677,41 @@ __device__ int32_t draw_episode_wave(const SacenvBoatParams& p, const Arena& A, 
                                      const double* ex_knots) {
   const int32_t start_y = draw_knots_wave(p, A, l, e, lane, ex_start_y, ex_knots);
   __syncthreads();
-  store_draw(p, A, l, e, slot, start_y, nullptr, lane);
+  store_draw(p, A, l, e, slot, start_y, lane);
   fit_store_wave(p, A, l, e, slot, lane);
   return start_y;
 }
 
 // ---------------------------------------------------------------- refill ranking
 
-// Owner wave w flagged its ended envs in one 64-bit mask. Every helper ranks
-// the flagged envs the same way (lane l owns the masks of waves l, l+64, ...;
-// envs ordered by lane, then mask, then bit) with DPP scans, so rank rr maps
-// to one env without atomics or cross-lane shuffles.
+// Owner wave w flagged its ended envs in one 64-bit mask. Every refill wave
+// ranks the flagged envs the same way (lane l owns the masks of waves l,
+// l+64, ...; envs ordered by lane, then mask, then bit) with DPP scans, so
+// rank rr maps to one env without atomics or cross-lane shuffles. The 8 KB
+// of masks stay in L2 (no LDS copy: more refill waves fit per CU).
 struct Ranking {
   int incl, cnt, total, R;
 };
 
-__device__ Ranking rank_masks(const Arena& A, DrawLds& l, int r, int lane) {
+constexpr int kMaskRegs = 16;  // masks per lane held in registers (owner waves <= 1024)
+
+__device__ Ranking rank_masks(const Arena& A, int lane) {
   const int nw = A.nwaves();
-  const unsigned long long* masks = A.refill_mask(r);
+  const unsigned long long* masks = A.refill_mask();
   Ranking k;
   k.R = (nw + kWave - 1) / kWave;  // masks per lane
   int cnt = 0;
-  // fixed trip count and clamped (branch-free) addresses, so all 16 loads
-  // are in flight at once before the first wait; then staged in LDS
-  unsigned long long mv[kMaskLds / kWave];
+  // fixed trip count and clamped (branch-free) addresses, so all loads are in
+  // flight at once before the first wait
+  unsigned long long mv[kMaskRegs];
 #pragma unroll
-  for (int i = 0; i < kMaskLds / kWave; ++i) {
+  for (int i = 0; i < kMaskRegs; ++i) {
     const int w = lane + kWave * i;
     mv[i] = masks[w < nw ? w : nw - 1];
   }
 #pragma unroll
-  for (int i = 0; i < kMaskLds / kWave; ++i) {
-    const int w = lane + kWave * i;
-    const unsigned long long m = w < nw ? mv[i] : 0ull;
-    l.masks[w] = m;
-    cnt += __popcll(m);
-  }
-  for (int i = kMaskLds / kWave; i < k.R; ++i) {
+  for (int i = 0; i < kMaskRegs; ++i) cnt += lane + kWave * i < nw ? __popcll(mv[i]) : 0;
+  for (int i = kMaskRegs; i < k.R; ++i) {
     const int w = lane + kWave * i;
     cnt += w < nw ? __popcll(masks[w]) : 0;
   }
@@ -739,17 +721,16 @@ __device__ Ranking rank_masks(const Arena& A, DrawLds& l, int r, int lane) {
   return k;
 }
 
-// env of rank rr (l.masks published by a barrier after rank_masks)
-__device__ int ranked_env(const Arena& A, const DrawLds& l, const Ranking& k, int r, int rr, int lane) {
+// env of rank rr
+__device__ int ranked_env(const Arena& A, const Ranking& k, int rr, int lane) {
   const int nw = A.nwaves();
-  const unsigned long long* masks = A.refill_mask(r);
+  const unsigned long long* masks = A.refill_mask();
   const int L = __ffsll((long long)__ballot(k.incl > rr)) - 1;  // owning lane
   int rem = rr - __builtin_amdgcn_readlane(k.incl - k.cnt, L);
   int e = -1;
   for (int i0 = 0; i0 < k.R && e < 0; i0 += kWave) {  // lane q takes L's mask i0 + q
     const int w = L + kWave * (i0 + lane);
-    const unsigned long long v =
-        (i0 + lane < k.R && w < nw) ? (k.R <= kMaskLds / kWave ? l.masks[w] : masks[w]) : 0ull;
+    const unsigned long long v = (i0 + lane < k.R && w < nw) ? masks[w] : 0ull;
     const int pc = __popcll(v);
     const int ip = wave_incl_scan(pc);
     const int chunk = __builtin_amdgcn_readlane(ip, kWave - 1);
@@ -766,81 +747,6 @@ __device__ int ranked_env(const Arena& A, const DrawLds& l, const Ranking& k, in
     rem -= chunk;
   }
   return e;
-}
-
-// Phase A for the envs flagged in mask ring r: draw each replacement episode
-// into the env's next free slot (raw knots), and record (env, slot) at its
-// rank for phase B. `fit` also fits at once (host-driven drains).
-__device__ int phase_a(const SacenvBoatParams& p, const Arena& A, const Tail& T, DrawLds& l, int r,
-                       int h, int H, bool fit, int lane) {
-  const GRegs g = fetch_g(p, T.g, lane);  // in flight together with the masks
-  const Ranking k = rank_masks(A, l, r, lane);
-  DRAW_STAMP(l, 1);
-  const bool curves = !p.use_wind_table && n_curves(p.experiment) > 0;
-  if (h == 0 && lane == 0) A.refill_count()[r] = (curves && !fit) ? k.total : 0;
-  if (h >= k.total) return 0;
-  publish_g(g, l, lane);  // its barrier also publishes l.masks
-  int done = 0;
-  for (int rr = h; rr < k.total; rr += H) {
-    const int e = ranked_env(A, l, k, r, rr, lane);
-    DRAW_STAMP(l, 2);
-    const int f = A.i32(U_FILL)[e];
-    const int slot = f % kSlots;
-    const int32_t start_y = draw_knots_wave(p, A, l, e, lane, nullptr, nullptr);
-    __syncthreads();
-    DRAW_STAMP(l, 3);
-    store_draw(p, A, l, e, slot, start_y,
-               fit ? nullptr : A.refill_y(r) + (int64_t)rr * 2 * p.n_knots, lane);
-    if (fit) fit_store_wave(p, A, l, e, slot, lane);
-    if (lane == 0) {
-      A.i32(U_FILL)[e] = f + 1;
-      if (curves && !fit) A.refill_list(r)[rr] = e * kSlots + slot;
-    }
-    __syncthreads();
-    ++done;
-  }
-  return done;
-}
-
-// Phase B for list ring r: fit the raw knots phase A stored in its rank's
-// refill row (no list -> slot dependency before the knots load). Prefetching
-// the first item for all three rings ahead of the launch counter measured
-// slower (more in-flight traffic at the owners' load burst).
-struct FirstItem {
-  int cnt;   // refill_count[r]
-  int v;     // refill_list[r][h]: env * kSlots + slot
-  double y;  // refill_y[r][h][lane] (lanes < 2 n_knots)
-};
-
-__device__ FirstItem load_first_item(const SacenvBoatParams& p, const Arena& A, int r, int h, int lane) {
-  FirstItem f;
-  const int hh = h < A.np ? h : (int)A.np - 1;  // speculative: used only if h < count <= n_envs
-  f.cnt = A.refill_count()[r];
-  f.v = A.refill_list(r)[hh];
-  const int nk2 = 2 * p.n_knots;
-  f.y = A.refill_y(r)[(int64_t)hh * nk2 + (lane < nk2 ? lane : 0)];
-  return f;
-}
-
-__device__ int phase_b(const SacenvBoatParams& p, const Arena& A, const Tail& T, DrawLds& l, int r,
-                       int h, int H, int lane) {
-  const GRegs g = fetch_g(p, T.g, lane);
-  const int cnt = A.refill_count()[r];
-  DRAW_STAMP(l, 1);
-  if (h >= cnt) return 0;
-  publish_g(g, l, lane);
-  const int nk = p.n_knots;
-  const int ncurves = n_curves(p.experiment);
-  int done = 0;
-  for (int rr = h; rr < cnt; rr += H) {
-    const FirstItem it = load_first_item(p, A, r, rr, lane);
-    const int e = it.v / kSlots, slot = it.v % kSlots;
-    if (lane < ncurves * nk) l.y[lane / nk][lane % nk] = it.y;
-    DRAW_STAMP(l, 2);
-    fit_store_wave(p, A, l, e, slot, lane);
-    ++done;
-  }
-  return done;
 }
 
 // scalar state of a fresh Boat (boat_env.py:152-198) and its observation;
@@ -916,7 +822,7 @@ __global__ void __launch_bounds__(kWave) k_seed(SacenvBoatParams p, Arena A, con
   A.i32(U_FILL)[e] = 0;
 }
 
-// mode 0: first Boat (init). autoreset: slots 0..3 <- episodes 1..4.
+// mode 0: first Boat (init). autoreset: slots 0..SLOTS-1 <- episodes 0..SLOTS-1.
 // mode 1: reset listed envs. non-autoreset: slot 0 <- a new draw;
 //         autoreset: start the next pre-drawn slot, then refill the freed one.
 // mode 2: explicit draws (non-autoreset), slot 0.
@@ -951,11 +857,14 @@ __global__ void __launch_bounds__(kWave) k_draw(SacenvBoatParams p, Arena A, Tai
         A.i32(U_FILL)[e] = kSlots;
       }
     } else {
+      // start the next pre-drawn episode and draw one more behind the last
+      // (per-env draw order: the refill continues from fill)
       const int c = A.i32(U_CONS)[e] + 1;
+      const int f = A.i32(U_FILL)[e];
+      if (c >= f && lane == 0) atomicOr(&A.status()[1], SACENV_STATUS_SLOT_UNDERFLOW);
       slot = c % kSlots;
       start_y = A.i32(U_STARTY)[(int64_t)slot * A.np + e];
       if (lane == 0) A.i32(U_CONS)[e] = c;
-      const int f = A.i32(U_FILL)[e];
       draw_episode_wave(p, A, lds, e, f % kSlots, lane, nullptr, nullptr);
       if (lane == 0) A.i32(U_FILL)[e] = f + 1;
     }
@@ -1018,23 +927,29 @@ __global__ void __launch_bounds__(1024) k_compact(const uint8_t* __restrict__ do
   if (t == 0) *count = base_s;
 }
 
-// Refill work pending after the last step launch (k-1), done before a
-// host-driven reset consumes more slots (per-env draw order): phase B of
-// the list phase A built in launch k-1, and phase A+B of launch k-1's masks.
-__global__ void __launch_bounds__(kWave) k_drain(SacenvBoatParams p, Arena A, Tail T) {
+// sacenv_boat_refill: every env flagged in the refill masks gets its slot
+// ring topped up to SLOTS episodes (fill = cons + SLOTS), drawn and fitted
+// in the env's order, one wave per env (rank h, h + grid, ...). Block 0 then
+// bumps the refill generation, so the next step launch's owners start their
+// masks afresh; a mask word that still carries an older generation is
+// re-ranked harmlessly (its envs are full: nothing to draw).
+__global__ void __launch_bounds__(kWave) k_refill(SacenvBoatParams p, Arena A, Tail T) {
   __shared__ DrawLds lds;
   const int lane = threadIdx.x;
-  const int k = A.helper_epoch()[0];
-  phase_b(p, A, T, lds, (k + 1) % kRing, blockIdx.x, gridDim.x, lane);
-  __syncthreads();
-  phase_a(p, A, T, lds, (k + 2) % kRing, blockIdx.x, gridDim.x, true, lane);
-}
-
-__global__ void k_drain_done(Arena A) {
-  const int k = A.helper_epoch()[0];
-  const int w = blockIdx.x * blockDim.x + threadIdx.x;
-  if (w == 0) A.refill_count()[(k + 1) % kRing] = 0;
-  if (w < A.nwaves()) A.refill_mask((k + 2) % kRing)[w] = 0ull;
+  const GRegs g = fetch_g(p, T.g, lane);  // in flight together with the masks
+  const Ranking k = rank_masks(A, lane);
+  if (blockIdx.x == 0 && lane == 0) A.status()[0] += 1;
+  if ((int)blockIdx.x >= k.total) return;
+  publish_g(g, lds, lane);
+  for (int rr = blockIdx.x; rr < k.total; rr += gridDim.x) {
+    const int e = ranked_env(A, k, rr, lane);
+    const int c = A.i32(U_CONS)[e];
+    int f = A.i32(U_FILL)[e];
+    if (c >= f && lane == 0) atomicOr(&A.status()[1], SACENV_STATUS_SLOT_UNDERFLOW);
+    for (; f < c + kSlots; ++f) draw_episode_wave(p, A, lds, e, f % kSlots, lane, nullptr, nullptr);
+    if (lane == 0) A.i32(U_FILL)[e] = f;
+    __syncthreads();
+  }
 }
 
 // Uniform fp64 constants as VGPR copies: the step reads ~40 config doubles,
@@ -1208,16 +1123,13 @@ struct MixedToys {
 // soon as they are final (EARLY_STORE); the obs rows go out through LDS as
 // float4 (64 rows x 44 B = 176 float4).
 constexpr int kF64 = 11;  // s_x s_y s_r v_x v_y v_r rudder t ep_reward wind_next[2]
+constexpr int kCoef = 8;  // wind_coef fields: 2 curves x (y0, y1, m0, m1)
 struct OwnerLds {
   double f[kF64][kWave];
   int32_t idx[kWave], cons[kWave];
   float reward[kWave];
   uint8_t done[kWave], term[kWave];
   float obs[kWave * SACENV_OBS_DIM];
-};
-union StepLds {
-  DrawLds draw;
-  OwnerLds own;
 };
 
 
@@ -1305,8 +1217,21 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   const uint32_t eo = (uint32_t)e * 8u, eo4 = (uint32_t)e * 4u;  // per-lane byte offsets
   const bool active = e < p.n_envs;
   const int kepoch = A.owner_epoch()[ob];
+  // this wave's refill-mask word and the current refill generation (uniform)
+  unsigned long long mask_acc = 0ull;
+  int mgen = 0, rgen = 0;
+#ifndef SACENV_DIAG_NO_MASK  // timing diagnostics only
+  if (p.autoreset) {
+#else
+  if (false) {
+#endif
+    mask_acc = A.refill_mask()[ob];
+    mgen = A.mask_gen()[ob];
+    rgen = A.status()[0];
+  }
   const float act = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(action) + (active ? eo4 : 0u));
   const bool t_idx = t_from_index(p.dt);
+  const int nc = p.use_wind_table ? 0 : n_curves(p.experiment);  // spline curves of the wind
   owner_load(A, l, ob, lane, t_idx);
   double s_x = l.f[0][lane], s_y = l.f[1][lane], s_r = l.f[2][lane];
   double v_x = l.f[3][lane], v_y = l.f[4][lane], v_r = l.f[5][lane];
@@ -1316,14 +1241,59 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   const double wv = l.f[9][lane], wa = l.f[10][lane];
   int32_t index = l.idx[lane];
   const int cons = p.autoreset ? l.cons[lane] : 0;
-  double nwv, nwa;
-  wind_at(p, A, T.table, cons % kSlots, e, index + 1, nwv, nwa);
-  // autoreset: the next pre-drawn episode's first wind and start y, speculatively
+  // Wind.get_wind(index + 1) for the next step, evaluated at the end. Curves:
+  // from the lane's copy of its spline piece (wind_coef, coalesced loads
+  // issued here, consumed at the end), refreshed from the active slot only
+  // in an episode's first step or when the sample enters the next knot
+  // interval: a handful of lanes per launch take the scattered slot loads.
+  double nwv = 0.0, nwa = 0.0;
+  double cf[kCoef];
+#pragma unroll
+  for (int k = 0; k < kCoef; ++k) cf[k] = k < 4 * nc ? A.f64e(U_COEF + 8 * k, eo) : 0.0;
+#ifdef SACENV_DIAG_NO_CF  // timing diagnostics only (wrong winds)
+#pragma unroll
+  for (int k = 0; k < kCoef; ++k) cf[k] = (double)k;
+#endif
+  const int wi = index + 1 > p.wind_len - 1 ? p.wind_len - 1 : index + 1;  // wind.py IndexError guard
+  const Knot kn = knot_coord(p, wi);
+  bool refresh = false;
+  if (nc == 0) {
+    wind_at(p, A, T.table, 0, e, index + 1, nwv, nwa);  // constants or the shared table
+  } else {
+    const int jp = knot_coord(p, index > p.wind_len - 1 ? p.wind_len - 1 : index).j;
+    refresh = index == 0 || kn.j != jp;
+    if (refresh) {
+      const int slot = cons % kSlots;
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+        if (c < nc) {
+          const uint32_t o = A.wofs(slot, c, kn.j, e), o1 = o + (uint32_t)A.np * 8u;
+          cf[4 * c] = A.wy_at(o), cf[4 * c + 1] = A.wy_at(o1);
+          cf[4 * c + 2] = A.wm_at(o), cf[4 * c + 3] = A.wm_at(o1);
+        }
+    }
+  }
+  // autoreset: the next pre-drawn episode's first wind and start y, read
+  // speculatively from their lane-coalesced copies, which a lane refreshes
+  // from the slot ring during the first step of each episode (index 0)
   double w0v = 0.0, w0a = 0.0;
   int32_t sy_next = 0;
+  const bool hdr_refresh = p.autoreset && index == 0;
   if (p.autoreset) {
-    wind0_of_slot(p, A, T.table, (cons + 1) % kSlots, e, w0v, w0a);
-    if (p.experiment == 2) sy_next = A.i32e(U_STARTY + 4 * ((cons + 1) % kSlots), eo4);
+    if (nc > 0) {
+#ifndef SACENV_DIAG_NO_W0  // timing diagnostics only
+      w0v = A.f64e(U_W0N, eo);
+      w0a = A.f64e(U_W0N + 8, eo);
+#endif
+    } else {
+      wind0_of_slot(p, A, T.table, 0, e, w0v, w0a);  // constants or the shared table
+    }
+    if (p.experiment == 2) sy_next = A.i32e(U_SYN, eo4);
+    if (hdr_refresh) {
+      const int ns = (cons + 1) % kSlots;
+      if (nc > 0) wind0_of_slot(p, A, T.table, ns, e, w0v, w0a);
+      if (p.experiment == 2) sy_next = A.i32e(U_STARTY + 4 * ns, eo4);
+    }
   }
   OWNER_STAMP(st_loaded);
   const double r_mx = T.r_mx, r_my = T.r_my, r_iz = T.r_iz, r_nd = T.r_nd, r_w = T.r_w;
@@ -1464,6 +1434,28 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
     A.i32e(U_CONS, eo4) = cons_out;
   }
   A.f64e(U_EP, eo) = ep;
+  if (nc > 0 && !restart) {  // the next step's wind from the piece (wind.py:20-24, :86-99)
+    const double c0 = spline_piece(cf[0], cf[1], cf[2], cf[3], kn.t);
+    if (p.experiment == 6) {
+      nwv = c0;
+      nwa = spline_piece(cf[4], cf[5], cf[6], cf[7], kn.t);
+    } else if (p.experiment == 4) {
+      nwv = c0;
+      nwa = p.wind_dir_rad;
+    } else {  // 5: rectified angle (wind.py:92-99)
+      nwv = p.max_velocity;
+      nwa = ((c0 <= 0.5 / 2 ? 0.0 : 1.0) * kPi) + kPi / 2;
+    }
+  }
+  if (refresh) {
+#pragma unroll
+    for (int k = 0; k < kCoef; ++k)
+      if (k < 4 * nc) A.f64e(U_COEF + 8 * k, eo) = cf[k];
+  }
+  if (hdr_refresh) {
+    if (nc > 0) A.f64e(U_W0N, eo) = w0v, A.f64e(U_W0N + 8, eo) = w0a;
+    if (p.experiment == 2) A.i32e(U_SYN, eo4) = sy_next;
+  }
   A.f64e(U_WNX, eo) = nwv;
   A.f64e(U_WNX + 8, eo) = nwa;
   A.at_e<float>(A.ur() + 44, eo4) = (float)reward;
@@ -1499,10 +1491,13 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   store_obs_block(l.obs, A.obs() + row0, lane);
 
   if (p.autoreset) {
-    // this launch's ended envs, for the next launch's helpers (every wave
-    // rewrites its word each launch, so the ring needs no clearing)
-    const unsigned long long m = __ballot(ended);
-    if (lane == 0) A.refill_mask(kepoch % kRing)[ob] = m;
+    // envs that ended since the last refill (a word of an older generation
+    // starts afresh): what the next sacenv_boat_refill draws for
+    const unsigned long long m = __ballot(ended) | (mgen == rgen ? mask_acc : 0ull);
+    if (lane == 0 && (m != mask_acc || mgen != rgen)) {
+      A.refill_mask()[ob] = m;
+      A.mask_gen()[ob] = rgen;
+    }
   }
   if (lane == 0) A.owner_epoch()[ob] = kepoch + 1;
 #ifdef SACENV_STAMPS
@@ -1519,66 +1514,18 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
 #endif
 }
 
-// The step launch. Grid: nb_boat owner waves, 2 x n_helpers refill helpers,
-// then (kMixed) the waves of each toy arena: heterogeneous workgroups of one
-// launch, selected by uniform block-index ranges.
+// The step launch. Grid: nb_boat owner waves, then (kMixed) the waves of
+// each toy arena: heterogeneous workgroups of one launch, selected by
+// uniform block-index ranges.
 template <bool kMixed>
 __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, Arena A, Tail T,
                                                 const float* __restrict__ action, int nb_boat,
                                                 MixedToys M) {
-  __shared__ StepLds slds;
-  DrawLds& lds = slds.draw;
+  __shared__ OwnerLds slds;
   const int lane = threadIdx.x;
-  const int nh = nb_boat > 0 && p.autoreset ? p.n_helpers : 0;
-
-  // grid order: owners, helpers, toys (owners dispatched first: -0.1 us/step
-  // against helpers first; the helpers' work has slack)
-  const int hb_raw = (int)blockIdx.x - nb_boat;
-  const bool is_helper = hb_raw >= 0 && hb_raw < 2 * nh;
-  if (is_helper) {
-    // ---------------- helpers
-#ifdef SACENV_STAMPS
-    const uint64_t hs_real0 = __builtin_amdgcn_s_memrealtime();
-#endif
-    const int hb = hb_raw;
-    const int k = A.helper_epoch()[hb];
-
-#ifdef SACENV_STAMPS
-    for (int i = 0; i < 8; ++i) lds.stamp[i] = 0;
-    DRAW_STAMP(lds, 0);
-#endif
-    int nd = 0;
-    if (hb < nh) {  // phase A on launch k-1's masks (ring (k-1) % 3)
-#ifndef SACENV_DIAG_NO_PHASE_A  // timing diagnostics only (slots are then not refilled)
-      nd = phase_a(p, A, T, lds, (k + 2) % kRing, hb, nh, false, lane);
-#endif
-    } else {        // phase B on the list phase A built in launch k-1 (ring (k-2) % 3)
-#ifndef SACENV_DIAG_NO_PHASE_B
-      nd = phase_b(p, A, T, lds, (k + 1) % kRing, hb - nh, nh, lane);
-#endif
-    }
-    if (lane == 0) A.helper_epoch()[hb] = k + 1;
-#ifdef SACENV_STAMPS
-#ifndef SACENV_STAMPS_LIGHT
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-    if (lane == 0) {
-      double* d = A.reward64() + (int64_t)hb * 12;
-      d[0] = (double)hs_real0;
-      d[1] = (double)__builtin_amdgcn_s_memrealtime();
-      d[2] = (double)nd;
-      d[3] = hb < nh ? 0.0 : 1.0;
-      for (int i = 0; i < 8; ++i) d[4 + i] = (double)lds.stamp[i];
-    }
-#else
-    (void)nd;
-#endif
-    return;
-  }
-
-  int b = (int)blockIdx.x < nb_boat ? (int)blockIdx.x : (int)blockIdx.x - 2 * nh;
+  int b = (int)blockIdx.x;
   if (!kMixed || b < nb_boat) {
-    owner_wave(vreg_params(p), A, vreg_tail(T), action, slds.own, b, lane);
+    owner_wave(vreg_params(p), A, vreg_tail(T), action, slds, b, lane);
     return;
   }
   b -= nb_boat;
@@ -1634,6 +1581,9 @@ int check_params(const SacenvBoatParams* p) {
   if (p == nullptr) return SACENV_E_NULL;
   if (p->experiment < 1 || p->experiment > 6) return SACENV_E_EXPERIMENT;
   if (p->n_envs <= 0 || p->n_envs > (1 << 22) || p->wind_len <= 0) return SACENV_E_SIZE;  // 32-bit offsets
+  // per-lane wind offsets (Arena::wofs) are 32-bit: SLOTS x 2 curves x knots rows of n_pad f64
+  if ((int64_t)kWindUnits * (p->n_knots < 2 ? 2 : p->n_knots) * pad64(p->n_envs) >= (1LL << 32))
+    return SACENV_E_SIZE;
   if (n_curves(p->experiment) > 0 && (p->n_knots < 4 || p->n_knots > kMaxK)) return SACENV_E_KNOTS;
   if (p->n_knots < 2 || p->n_knots > kMaxK) return SACENV_E_KNOTS;
   if (n_curves(p->experiment) > 0 && !p->use_wind_table && p->wind_len < 2) return SACENV_E_SIZE;
@@ -1644,7 +1594,7 @@ int check_params(const SacenvBoatParams* p) {
 
 Tail make_tail(const SacenvBoatParams& p, void* arena) {
   SacenvBoatLayout L;
-  compute_layout(p.n_envs, p.n_knots, p.n_helpers, p.wind_len, p.use_wind_table, &L);
+  compute_layout(p.n_envs, p.n_knots, p.wind_len, p.use_wind_table, &L);
   char* b = static_cast<char*>(arena);
   Tail T;
   T.g = reinterpret_cast<const double*>(b + L.spline_g);
@@ -1703,7 +1653,7 @@ int sacenv_boat_layout(const SacenvBoatParams* p, SacenvBoatLayout* out) {
   const int rc = check_params(p);
   if (rc) return rc;
   if (out == nullptr) return SACENV_E_NULL;
-  compute_layout(p->n_envs, p->n_knots, p->n_helpers, p->wind_len, p->use_wind_table, out);
+  compute_layout(p->n_envs, p->n_knots, p->wind_len, p->use_wind_table, out);
   return SACENV_OK;
 }
 
@@ -1734,13 +1684,6 @@ int sacenv_boat_reset(const SacenvBoatParams* p, void* arena, const int32_t* ids
   const hipStream_t s = (hipStream_t)stream;
   const Arena A = make_arena(*p, arena);
   const Tail T = make_tail(*p, arena);
-  if (p->autoreset) {
-    // slots freed by the last step launches are refilled first: per-env draw order
-    hipLaunchKernelGGL(k_drain, dim3(p->n_helpers), dim3(kWave), 0, s, *p, A, T);
-    if ((rc = launch_status())) return rc;
-    hipLaunchKernelGGL(k_drain_done, dim3(blocks_for((int)(A.np / kWave), 256)), dim3(256), 0, s, A);
-    if ((rc = launch_status())) return rc;
-  }
   hipLaunchKernelGGL(k_draw, dim3(nb), dim3(kWave), 0, s, *p, A, T, 1, ids, (const int32_t*)nullptr,
                      (const double*)nullptr, (const int32_t*)nullptr);
   return launch_status();
@@ -1762,12 +1705,6 @@ int sacenv_boat_reset_list(const SacenvBoatParams* p, void* arena, const int32_t
   const hipStream_t s = (hipStream_t)stream;
   const Arena A = make_arena(*p, arena);
   const Tail T = make_tail(*p, arena);
-  if (p->autoreset) {
-    hipLaunchKernelGGL(k_drain, dim3(p->n_helpers), dim3(kWave), 0, s, *p, A, T);
-    if ((rc = launch_status())) return rc;
-    hipLaunchKernelGGL(k_drain_done, dim3(blocks_for((int)(A.np / kWave), 256)), dim3(256), 0, s, A);
-    if ((rc = launch_status())) return rc;
-  }
   // at most one workgroup per CU-slot; each loops over its share of the device-side list
   const int grid = p->n_envs < 1024 ? p->n_envs : 1024;
   hipLaunchKernelGGL(k_draw, dim3(grid), dim3(kWave), 0, s, *p, A, T, 1, ids, (const int32_t*)nullptr,
@@ -1794,9 +1731,18 @@ int sacenv_boat_step(const SacenvBoatParams* p, void* arena, const float* action
   if (rc) return rc;
   if (arena == nullptr || action == nullptr) return SACENV_E_NULL;
   const int nb_boat = (int)(pad64(p->n_envs) / kWave);
-  const int nb = nb_boat + (p->autoreset ? 2 * p->n_helpers : 0);
-  hipLaunchKernelGGL(k_step<false>, dim3(nb), dim3(kWave), 0, (hipStream_t)stream, *p, make_arena(*p, arena),
-                     make_tail(*p, arena), action, nb_boat, MixedToys{});
+  hipLaunchKernelGGL(k_step<false>, dim3(nb_boat), dim3(kWave), 0, (hipStream_t)stream, *p,
+                     make_arena(*p, arena), make_tail(*p, arena), action, nb_boat, MixedToys{});
+  return launch_status();
+}
+
+int sacenv_boat_refill(const SacenvBoatParams* p, void* arena, void* stream) {
+  int rc = check_params(p);
+  if (rc) return rc;
+  if (arena == nullptr) return SACENV_E_NULL;
+  if (!p->autoreset) return SACENV_E_MODE;
+  hipLaunchKernelGGL(k_refill, dim3(p->n_helpers), dim3(kWave), 0, (hipStream_t)stream, *p,
+                     make_arena(*p, arena), make_tail(*p, arena));
   return launch_status();
 }
 
@@ -1866,7 +1812,7 @@ int sacenv_mixed_step(const SacenvBoatParams* bp, void* boat_arena, const float*
     A = make_arena(p, boat_arena);
     T = make_tail(p, boat_arena);
     nb_boat = (int)(pad64(p.n_envs) / kWave);
-    nb += nb_boat + (p.autoreset ? 2 * p.n_helpers : 0);
+    nb += nb_boat;
   }
   if (nb == 0) return SACENV_OK;
   hipLaunchKernelGGL(k_step<true>, dim3(nb), dim3(kWave), 0, (hipStream_t)stream, p, A, T, boat_action, nb_boat,

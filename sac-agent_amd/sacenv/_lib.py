@@ -11,12 +11,14 @@ import os
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # .../sac-agent_amd
 LIB_PATH = os.environ.get("SACENV_LIB", os.path.join(PKG_ROOT, "build", "libsacenv.so"))
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 OBS_DIM = 11
 MT_N = 624
 MAX_KNOTS = 16
 N_COUNTERS = 5
-SLOTS = 4
+SLOTS = 33
+REFILL_PERIOD = 32  # autoreset: step launches allowed between sacenv_boat_refill calls
+STATUS_SLOT_UNDERFLOW = 1
 RECORD_BYTES = 50
 
 TERM_NONE, TERM_REACHED_GOAL, TERM_OUT_OF_BOUNDS, TERM_OUT_OF_FUEL, \
@@ -52,11 +54,10 @@ class BoatParams(C.Structure):
 
 LAYOUT_FIELDS = (
     "total_bytes", "n_pad", "s_x", "s_y", "s_r", "v_x", "v_y", "v_r", "rudder", "t",
-    "ep_reward", "wind_next", "index", "cons", "fill", "mt_pos", "start_y", "counters",
-    "refill_list",
-    "wind_y", "wind_m", "knots_raw", "refill_y", "mt_key", "record", "obs", "reward", "done", "term",
-    "final_obs", "final_ep_reward", "accel", "reward64", "refill_mask", "refill_count", "owner_epoch",
-    "helper_epoch", "spline_g", "wind_table")
+    "ep_reward", "wind_next", "wind_coef", "wind0_next", "start_y_next", "index", "cons", "fill", "mt_pos", "start_y", "counters",
+    "wind_y", "wind_m", "knots_raw", "mt_key", "record", "obs", "reward", "done", "term",
+    "final_obs", "final_ep_reward", "accel", "reward64", "refill_mask", "mask_gen", "status",
+    "owner_epoch", "spline_g", "wind_table")
 
 
 class BoatLayout(C.Structure):
@@ -101,7 +102,7 @@ class ReplayLayout(C.Structure):
 
 EXPORTS = ("sacenv_abi_version", "sacenv_error_string", "sacenv_boat_layout",
            "sacenv_boat_init", "sacenv_boat_reset", "sacenv_boat_reset_explicit",
-           "sacenv_boat_step", "sacenv_boat_wind_eval", "sacenv_toy_layout", "sacenv_toy_init",
+           "sacenv_boat_step", "sacenv_boat_refill", "sacenv_boat_wind_eval", "sacenv_toy_layout", "sacenv_toy_init",
            "sacenv_toy_reset", "sacenv_toy_step", "sacenv_mixed_step", "sacenv_replay_layout",
            "sacenv_replay_init", "sacenv_replay_store", "sacenv_replay_sample",
            "sacenv_compact_done", "sacenv_boat_reset_list")
@@ -135,6 +136,7 @@ def load(path: str | None = None):
         "sacenv_boat_reset": (C.c_int, [P, _p, _p, _i32, _p]),
         "sacenv_boat_reset_explicit": (C.c_int, [P, _p, _p, _i32, _p, _p, _p]),
         "sacenv_boat_step": (C.c_int, [P, _p, _p, _p]),
+        "sacenv_boat_refill": (C.c_int, [P, _p, _p]),
         "sacenv_boat_wind_eval": (C.c_int, [P, _p, _p, _p, _i32, _p, _p, _p]),
         "sacenv_toy_layout": (C.c_int, [TP, C.POINTER(ToyLayout)]),
         "sacenv_toy_init": (C.c_int, [TP, _p, _p]),

@@ -186,6 +186,8 @@ class MixedBatch:
         _lib.check(self.lib.sacenv_mixed_step(
             b._pp if b is not None else None, b.arena.data_ptr() if b is not None else None,
             a.data_ptr() if b is not None else None, self._tp, self._ta, len(self.toys), stream))
+        if b is not None:
+            b._after_step()
 
 
 __all__ = ["ParachuteConfig", "CarConfig", "VecToyEnv", "ParachuteEnv", "CarEnv", "MixedBatch",

@@ -38,18 +38,23 @@ class VecBoatEnv:
     autoreset : start the next episode inside ``step`` for envs that end
         (gym vector-env semantics: the returned obs row is the new episode's
         first obs, the terminal obs is ``info['final_obs']``). Episodes are
-        pre-drawn three ahead per env, from the env's own RNG stream in the
-        reference's order, so draws match the reference exactly.
+        pre-drawn up to 32 ahead per env (``_lib.SLOTS``), from the env's own
+        RNG stream in the reference's order, so draws match the reference
+        exactly; a refill launch tops the slots up (see ``refill``).
     env_id_offset : global id of this rank's first env (multi-GPU sharding).
     record_knots / record_accel / record_reward64 : extra outputs (tests, shim).
     wind_table : [2, int(t_max/dt)] recorded wind (velocity, angle) for all envs.
-    n_helpers : autoreset helper waves per step launch (slot refills).
+    n_helpers : autoreset: workgroups of a refill launch (one env's draws each).
+    auto_refill : autoreset: launch ``refill()`` after every ``_lib.REFILL_PERIOD``-th
+        step issued through this object. Pass False when capturing steps into a
+        graph and place ``refill()`` yourself (at most REFILL_PERIOD steps apart).
     """
 
     def __init__(self, config=None, num_envs: int = 1, *, seed: int = 0, seeds=None,
                  device=None, max_episode_steps: int = 0, autoreset: bool = True,
                  env_id_offset: int = 0, record_knots: bool = False, record_accel: bool = False,
-                 record_reward64: bool = False, wind_table=None, n_helpers: int = 256):
+                 record_reward64: bool = False, wind_table=None, n_helpers: int = 2048,
+                 auto_refill: bool = True):
         self.lib = _lib.load()
         self.cfg = BoatConfig.from_any(config)
         self.num_envs = N = int(num_envs)
@@ -60,6 +65,8 @@ class VecBoatEnv:
             raise RuntimeError("VecBoatEnv runs on a GPU (HIP); no CPU path")
         self.env_id_offset = int(env_id_offset)
         self.autoreset = bool(autoreset)
+        self.auto_refill = bool(auto_refill)
+        self._since_refill = 0
         flags = ((_lib.OUT_KNOTS if record_knots else 0) | (_lib.OUT_ACCEL if record_accel else 0)
                  | (_lib.OUT_REWARD64 if record_reward64 else 0))
         self.params = make_params(self.cfg, N, max_episode_steps=max_episode_steps,
@@ -83,6 +90,8 @@ class VecBoatEnv:
         self._t_view = view(L.t, f64, NP)[:N]
         self._t_from_index = t_from_index(float(self.cfg.dt))
         self.index = view(L.index, i32, NP)[:N]
+        # Wind.get_wind(index) of the NEXT step, pre-evaluated by the step launch
+        self.wind_next = view(L.wind_next, f64, 2, NP)[:, :N]
         self.cons = view(L.cons, i32, NP)[:N]
         self.mt_pos = view(L.mt_pos, i32, NP)[:N]
         self.start_y_slots = view(L.start_y, i32, _lib.SLOTS, NP)[:, :N]
@@ -102,6 +111,7 @@ class VecBoatEnv:
         self.final_ep_reward = view(L.final_ep_reward, f64, NP)[:N]
         self.accel = view(L.accel, f64, 3, NP)[:, :N]
         self.reward64 = view(L.reward64, f64, NP)[:N]
+        self.status = view(L.status, i32, 64)        # [0] refill generation, [1] status bits
         if wind_table is not None:
             wt = torch.as_tensor(np.asarray(wind_table, np.float64).reshape(2, -1))
             if wt.shape[1] != self.cfg.wind_len:
@@ -208,6 +218,27 @@ class VecBoatEnv:
     def step_async(self, actions: torch.Tensor) -> None:
         """Enqueue one step; ``actions`` is a contiguous f32 device tensor of N values."""
         _lib.check(self.lib.sacenv_boat_step(self._pp, self._ptr, actions.data_ptr(), self.stream))
+        self._after_step()
+
+    def _after_step(self) -> None:
+        if self.autoreset:
+            self._since_refill += 1
+            if self.auto_refill and self._since_refill >= _lib.REFILL_PERIOD:
+                self.refill()
+
+    def refill(self) -> None:
+        """Enqueue the slot refill (autoreset): draw and fit the replacement episodes of
+        every env that ended since the last refill. Needed at least every
+        ``_lib.REFILL_PERIOD`` steps; ``auto_refill`` does it for eager stepping."""
+        _lib.check(self.lib.sacenv_boat_refill(self._pp, self._ptr, self.stream))
+        self._since_refill = 0
+
+    def check_status(self) -> None:
+        """Raise if the device flagged an error (synchronises): an env that restarted
+        past its pre-drawn episodes (refills further apart than REFILL_PERIOD steps)."""
+        bits = int(self.status[1].item())
+        if bits & _lib.STATUS_SLOT_UNDERFLOW:
+            raise _lib.SacenvError("slot underflow: more than REFILL_PERIOD steps without refill()")
 
     def step(self, actions):
         """BoatEnv.step for all envs (boat_env.py:67-115).

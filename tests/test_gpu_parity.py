@@ -128,7 +128,7 @@ def test_wind_tables_vs_reference(name, gpu, built_lib):
 def test_rng_draws_bit_exact_across_many_resets(autoreset, gpu, built_lib):
     """Knots/start-y of 150 consecutive Boats per env == numpy RandomState (crosses
     many 624-word MT blocks, incl. windows straddling a block end). In autoreset
-    mode the draws happen two episodes ahead; the sequence is the same."""
+    mode the draws happen 32 episodes ahead; the sequence is the same."""
     from sacenv import VecBoatEnv
     seeds = np.array([0, 5, 99, 2**32 - 1], np.uint64)
     env = VecBoatEnv({"base_settings": {"experiment": 6}}, len(seeds), seeds=seeds, device=gpu,
@@ -167,9 +167,10 @@ def test_spline_g_on_device(gpu, built_lib):
 
 def test_autoreset_every_step_one_step_episodes(gpu, built_lib):
     """|action| > 10.5 breaks the rudder on the first step: every env ends in every
-    launch, the worst case for the 3-slot pipeline. Draws must stay exact."""
+    launch, the worst case for the slot ring (32 episodes consumed between two
+    refills, then 32 drawn per env by one refill wave). Draws must stay exact."""
     from sacenv import VecBoatEnv
-    E, S = 70, 12
+    E, S = 70, 100
     seeds = np.arange(E, dtype=np.uint64) * 7 + 3
     env = VecBoatEnv({"base_settings": {"experiment": 6, "test_mode": 0}}, E, seeds=seeds,
                      device=gpu, autoreset=True, n_helpers=5, record_knots=True)
@@ -186,6 +187,43 @@ def test_autoreset_every_step_one_step_episodes(gpu, built_lib):
                                    atol=OBS_TOL)
         np.testing.assert_array_equal(env.start_y.cpu().numpy(), ora.start_y)
         np.testing.assert_array_equal(env.knots_raw.cpu().numpy().transpose(2, 0, 1), ora.knots)
+    env.check_status()
+
+
+@pytest.mark.parametrize("period", [1, 7, 32])
+def test_refill_schedule_any_period_up_to_32(period, gpu, built_lib):
+    """Refills placed by hand (auto_refill off) every `period` steps, once doubled,
+    give the same episodes as the oracle; a ring that runs dry sets the status bit."""
+    from sacenv import VecBoatEnv, _lib
+    E = 130
+    seeds = np.arange(E, dtype=np.uint64) * 3 + 11
+    cfg = {"base_settings": {"experiment": 6, "test_mode": 0}}
+    env = VecBoatEnv(cfg, E, seeds=seeds, device=gpu, autoreset=True, n_helpers=16,
+                     record_knots=True, auto_refill=False, max_episode_steps=3)
+    ora = OracleVecBoat(OracleConfig(experiment=6), seeds, max_episode_steps=3)
+    rng = np.random.default_rng(period)
+    for k in range(96):
+        a = rng.uniform(-1, 1, E).astype(np.float32)
+        if k % 5 == 0:
+            a[: E // 2] = 20.0      # half the envs end at once
+        o, r, d, info = env.step(torch.from_numpy(a).to(gpu))
+        ro = ora.step(a)
+        if (k + 1) % period == 0:
+            env.refill()
+            if k == 40:
+                env.refill()        # back to back: harmless
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(info["term"].cpu().numpy(), ro["term"], err_msg=f"{k}")
+        np.testing.assert_allclose(o.cpu().numpy(), ro["reset_obs"], rtol=OBS_TOL, atol=OBS_TOL)
+        np.testing.assert_array_equal(env.knots_raw.cpu().numpy().transpose(2, 0, 1), ora.knots)
+    env.check_status()
+    # no refill for more than REFILL_PERIOD launches of one-step episodes: flagged
+    dry = VecBoatEnv(cfg, 64, seed=1, device=gpu, autoreset=True, auto_refill=False, n_helpers=4)
+    for _ in range(_lib.REFILL_PERIOD + 1):
+        dry.step(torch.full((64,), 20.0, device=gpu))
+    dry.refill()
+    with pytest.raises(_lib.SacenvError):
+        dry.check_status()
 
 
 @pytest.mark.parametrize("exp", [1, 2, 3, 4, 5, 6])
@@ -530,6 +568,42 @@ def test_autoreset_all_experiments_ragged_vs_oracle(exp, gpu, built_lib):
         assert np.abs(env.s_y.cpu().numpy() - ora.s_y).max() <= STATE_TOL
     assert n_nat > 0
     np.testing.assert_array_equal(env.counters.cpu().numpy().T, ora.counters)
+
+
+@pytest.mark.parametrize("exp", [4, 5, 6])
+@pytest.mark.parametrize("autoreset", [False, True])
+def test_wind_piece_cache_across_intervals_and_episodes(exp, autoreset, gpu, built_lib):
+    """The step reads the next wind from a per-env cached spline piece (layout.wind_coef),
+    refreshed from the episode's slot only on a new episode or an interval crossing.
+    Short wind tables (L = 120, 17 steps per knot interval) and frozen rudders (episodes
+    run to the timeout, so every interval and the end-of-table clamp are crossed), for
+    2.6 episodes: the wind each step uses equals the oracle's (wind.py:20-24, :69-99)."""
+    from sacenv import VecBoatEnv
+    N, t_max = 333, 30.0
+    L = int(t_max / 0.25)
+    seeds = np.arange(N, dtype=np.uint64) * 31 + 5
+    cfg = {"base_settings": {"experiment": exp, "test_mode": 1, "t_max": t_max}}
+    env = VecBoatEnv(cfg, N, seeds=seeds, device=gpu, autoreset=autoreset, n_helpers=8)
+    ora = OracleVecBoat(OracleConfig(experiment=exp, test_mode=1, t_max=t_max), seeds)
+    env.reset()
+    ora.reset()
+    zero = np.zeros(N, np.float32)
+    crossed = 0
+    for k in range(int(2.6 * L)):
+        wnext = env.wind_next.cpu().numpy().T.copy()       # the wind this step will use
+        _, _, _, info = env.step(torch.zeros(N, device=gpu))
+        r = ora.step(zero)
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(wnext, r["wind"], rtol=0, atol=1e-12, err_msg=f"step {k}")
+        term = info["term"].cpu().numpy()
+        np.testing.assert_array_equal(term, r["term"], err_msg=f"step {k}")
+        ended = np.flatnonzero(term)
+        if ended.size and not autoreset:
+            env.reset(ended)
+        assert np.abs(env.s_y.cpu().numpy() - ora.s_y).max() <= STATE_TOL
+        crossed += int((r["state"]["index"] % 17 == 0).sum())
+    assert (env.counters.cpu().numpy()[4] >= 1).all()       # every env timed out
+    assert crossed > 0
 
 
 # ---------------------------------------------------------------- recorder (§8(f) rank 3)

@@ -34,7 +34,7 @@ def declared_functions():
 def test_library_exports_header(built_lib):
     from sacenv import _lib
     names = declared_functions()
-    assert len(names) == 19
+    assert len(names) == 20
     assert set(names) == set(_lib.EXPORTS)
     for n in names:
         assert hasattr(built_lib, n), n
@@ -62,6 +62,15 @@ def test_argument_errors_without_gpu(built_lib):
     p.n_helpers = 256
     p.autoreset = 1
     assert built_lib.sacenv_boat_reset_explicit(ctypes.byref(p), 1, 1, 1, 1, None, None) == -6
+    assert built_lib.sacenv_boat_refill(ctypes.byref(p), None, None) == -1
+    p.autoreset = 0
+    assert built_lib.sacenv_boat_refill(ctypes.byref(p), 1, None) == -6
+    # per-lane wind offsets are 32-bit: SLOTS x 2 curves x knots x n_pad f64 < 2**32 bytes
+    p.n_knots = 16
+    p.n_envs = 1 << 20
+    assert built_lib.sacenv_boat_step(ctypes.byref(p), 1, 1, None) == -4
+    p.n_envs = 1 << 18
+    assert built_lib.sacenv_boat_step(ctypes.byref(p), None, None, None) == -1
 
 
 def test_toy_argument_errors_without_gpu(built_lib):
@@ -125,15 +134,17 @@ def test_arena_layout(built_lib, n):
     """Fields are aligned, disjoint and inside total_bytes; record is contiguous."""
     from sacenv import _lib
     from sacenv.config import BoatConfig, make_params
-    p = make_params(BoatConfig(experiment=6), n, n_helpers=256, use_wind_table=True)
+    p = make_params(BoatConfig(experiment=6), n, use_wind_table=True)
     L = _lib.layout(p)
     np_ = L.n_pad
     assert np_ % 64 == 0 and n <= np_ < n + 64
     nk = 8
+    S = _lib.SLOTS
     sizes = {"s_x": 8, "s_y": 8, "s_r": 8, "v_x": 8, "v_y": 8, "v_r": 8, "rudder": 8, "t": 8,
-             "ep_reward": 8, "wind_next": 16, "index": 4, "cons": 4, "fill": 4, "mt_pos": 4, "start_y": 16,
-             "counters": 20, "refill_list": 12, "wind_y": 64 * nk, "wind_m": 64 * nk,
-             "knots_raw": 64 * nk, "refill_y": 48 * nk, "mt_key": 2496, "obs": 44, "reward": 4, "done": 1, "term": 1,
+             "ep_reward": 8, "wind_next": 16, "wind_coef": 64, "wind0_next": 16, "start_y_next": 4,
+             "index": 4, "cons": 4, "fill": 4, "mt_pos": 4,
+             "start_y": 4 * S, "counters": 20, "wind_y": 16 * S * nk, "wind_m": 16 * S * nk,
+             "knots_raw": 16 * S * nk, "mt_key": 2496, "obs": 44, "reward": 4, "done": 1, "term": 1,
              "final_obs": 44, "final_ep_reward": 8, "accel": 24, "reward64": 8}
     spans = sorted((getattr(L, f), getattr(L, f) + w * np_, f) for f, w in sizes.items())
     for (a0, a1, f), (b0, b1, g) in zip(spans, spans[1:]):
@@ -141,9 +152,8 @@ def test_arena_layout(built_lib, n):
     for a0, a1, f in spans:
         assert a0 % 64 == 0, f
     assert L.record == L.obs and L.term + np_ == L.record + 50 * np_
-    tail = [("refill_mask", 24 * np_ // 64), ("refill_count", 12), ("owner_epoch", 4 * np_ // 64),
-            ("helper_epoch", 4 * 2 * 256),
-            ("spline_g", 8 * 256), ("wind_table", 16 * 10000)]
+    tail = [("refill_mask", 8 * np_ // 64), ("mask_gen", 4 * np_ // 64), ("status", 256),
+            ("owner_epoch", 4 * np_ // 64), ("spline_g", 8 * 256), ("wind_table", 16 * 10000)]
     end = spans[-1][1]
     for f, w in tail:
         off = getattr(L, f)
