@@ -60,7 +60,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--kernel-launches", type=int, default=200)
     ap.add_argument("--test-mode", type=int, default=0, help="1 = rudder frozen (no terminations)")
-    ap.add_argument("--helpers", type=int, default=2048, help="workgroups of a refill launch")
+    ap.add_argument("--helpers", type=int, default=4096, help="workgroups of a refill draw launch")
     ap.add_argument("--mixed", action="store_true",
                     help="BASELINE configs[4]: boat exp-6 + toy_parachute + toy_car in one launch")
     ap.add_argument("--mixed-envs", type=int, default=32768, help="envs per type per GPU (--mixed)")

@@ -87,7 +87,7 @@ typedef struct SacenvBoatParams {
   int32_t start_y_half;       /* int(0.8*track_width) (boat_env.py:147-150) */
   int32_t max_episode_steps;  /* > 0: truncate (term 6) after this many steps; 0: off */
   int32_t autoreset;          /* 1: envs that end start their next episode inside step */
-  int32_t n_helpers;          /* autoreset: workgroups of a sacenv_boat_refill launch (1..4096) */
+  int32_t n_helpers;          /* autoreset: workgroups of sacenv_boat_refill's draw launch (1..65536) */
   int32_t out_flags;          /* SACENV_OUT_* bitmask */
   int32_t use_wind_table;     /* 1: wind from layout.wind_table [2][L] for every env */
   double dt, t_max, goal_line, oob_limit, track_width;  /* oob = width + offset (:200-201) */
@@ -129,6 +129,8 @@ typedef struct SacenvBoatLayout {
   int64_t mt_pos;             /* i32 [n_pad] next MT word index, 624 => twist first */
   int64_t start_y;            /* i32 [SLOTS][n_pad] Boat.s_y_start per slot */
   int64_t counters;           /* u32 [5][n_pad] cumulative termination counters */
+  int64_t refill_list;        /* i32 [3][n_pad] by refill rank: env, first and end episode number drawn
+                                 (sacenv_boat_refill's draw launch -> its fit launch) */
   int64_t wind_y;             /* f64 [SLOTS][2][n_knots][n_pad] folded knot values per slot, curve */
   int64_t wind_m;             /* f64 [SLOTS][2][n_knots][n_pad] folded 2nd derivatives / 6 */
   int64_t knots_raw;          /* f64 [SLOTS][2][n_knots][n_pad] drawn knots (SACENV_OUT_KNOTS) */
@@ -141,9 +143,9 @@ typedef struct SacenvBoatLayout {
   int64_t accel;              /* f64 [3][n_pad] a_x, a_y, a_r */
   int64_t reward64;           /* f64 [n_pad] */
   int64_t refill_mask;        /* u64 [n_pad/64] per owner wave: envs that ended since the last
-                                 sacenv_boat_refill (tagged with mask_gen) */
-  int64_t mask_gen;           /* i32 [n_pad/64] refill generation each refill_mask word belongs to */
-  int64_t status;             /* i32 [64] (256 B): [0] refill generation, [1] SACENV_STATUS_* bits */
+                                 sacenv_boat_refill */
+  int64_t status;             /* i32 [64] (256 B): [0] refills done, [1] SACENV_STATUS_* bits,
+                                 [2] envs ranked by the last refill */
   int64_t owner_epoch;        /* i32 [n_pad/64] per owner-block launch counter */
   int64_t spline_g;           /* f64 [n_knots][n_knots]: (m/6) = G @ knots (written by init) */
   int64_t wind_table;         /* f64 [2][wind_len] (velocity, angle), if use_wind_table */

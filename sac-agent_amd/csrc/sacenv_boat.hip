@@ -54,7 +54,7 @@ constexpr int U_SX = 0, U_SY = 8, U_SR = 16, U_VX = 24, U_VY = 32, U_VR = 40, U_
               U_T = 56, U_EP = 64, U_WNX = 72, U_COEF = 88, U_W0N = 152, U_IDX = 168,
               U_CONS = 172, U_FILL = 176, U_MTPOS = 180, U_SYN = 184, U_STARTY = 188,
               U_CNT = U_STARTY + 4 * kSlots,
-              U_WIND = U_CNT + 4 * SACENV_N_COUNTERS;
+              U_LIST = U_CNT + 4 * SACENV_N_COUNTERS, U_WIND = U_LIST + 12;
 constexpr int U_MT_BYTES = 4 * kMtN;
 constexpr int64_t kWindUnits = 16LL * kSlots;  // f64 x 2 curves x slots, per knot
 
@@ -83,6 +83,7 @@ __host__ __device__ inline void compute_layout(int n, int nk, int L, int use_tab
   o->mt_pos = U_MTPOS * np;
   o->start_y = U_STARTY * np;
   o->counters = U_CNT * np;
+  o->refill_list = U_LIST * np;
   const int64_t uw = U_WIND, wk = kWindUnits * nk;
   o->wind_y = uw * np;
   o->wind_m = (uw + wk) * np;
@@ -101,8 +102,6 @@ __host__ __device__ inline void compute_layout(int n, int nk, int L, int use_tab
   int64_t off = align256((ur + 134) * np);
   o->refill_mask = off;
   off += align256(8 * nw);
-  o->mask_gen = off;
-  off += align256(4 * nw);
   o->status = off;
   off += 256;
   o->owner_epoch = off;
@@ -140,18 +139,17 @@ struct Arena {
   __device__ __forceinline__ double* accel() const { return at<double>(ur() + 102); }
   __device__ __forceinline__ double* reward64() const { return at<double>(ur() + 126); }
   __device__ __forceinline__ char* tail() const { return b + align256((ur() + 134) * np); }
-  // envs of owner wave w that ended since the refill of generation mask_gen[w]
+  // envs of owner wave w that ended since the last refill
   __device__ __forceinline__ unsigned long long* refill_mask() const {
     return reinterpret_cast<unsigned long long*>(tail());
   }
-  __device__ __forceinline__ int32_t* mask_gen() const {
+  // [0] refills done, [1] SACENV_STATUS_* bits, [2] envs ranked by the last refill
+  __device__ __forceinline__ int32_t* status() const {
     return reinterpret_cast<int32_t*>(tail() + align256(8 * nwaves()));
   }
-  // [0] refill generation, [1] SACENV_STATUS_* bits
-  __device__ __forceinline__ int32_t* status() const {
-    return reinterpret_cast<int32_t*>(tail() + align256(8 * nwaves()) + align256(4 * nwaves()));
-  }
   __device__ __forceinline__ int32_t* owner_epoch() const { return status() + 64; }
+  // refill rank -> [0] env, [1] first and [2] end episode number drawn
+  __device__ __forceinline__ int32_t* refill_list(int k) const { return i32(U_LIST + 4 * k); }
   // slot-major wind coefficient of (slot, curve, knot) for env e
   __device__ __forceinline__ int64_t wix(int slot, int c, int k, int e) const {
     return ((int64_t)(slot * 2 + c) * nk + k) * np + e;
@@ -194,10 +192,12 @@ struct Tail {
 
 // ---------------------------------------------------------------- LDS of a drawing wave
 
-struct DrawLds {
+struct RngLds {           // an episode draw (k_refill: 5.3 KB, more waves per CU)
   uint32_t win[kWave];    // MT window (tempered words pos .. pos+63)
   uint32_t blk[2][kMtN];  // current MT block, next (twisted) block
   double y[2][kMaxK];     // knot values per curve (unfolded)
+};
+struct DrawLds : RngLds {  // draw + wave fit (init / host resets)
   double m[2][kMaxK];     // second derivatives / 6 per curve (unfolded)
   double g[kMaxK * kMaxK];
 #ifdef SACENV_STAMPS
@@ -241,11 +241,6 @@ __device__ __forceinline__ Knot knot_coord(const SacenvBoatParams& p, int i) {
 __device__ __forceinline__ double spline_piece(double y0, double y1, double m0, double m1, double t) {
   const double u = 1.0 - t;
   return u * y0 + t * y1 + (u * u * u - u) * m0 + (t * t * t - t) * m1;
-}
-
-__device__ __forceinline__ double curve_lds(const SacenvBoatParams& p, const DrawLds& l, int c, int i) {
-  const Knot k = knot_coord(p, i);
-  return spline_piece(l.y[c][k.j], l.y[c][k.j + 1], l.m[c][k.j], l.m[c][k.j + 1], k.t);
 }
 
 __device__ __forceinline__ double curve_env(const SacenvBoatParams& p, const Arena& A, int slot, int c,
@@ -426,9 +421,12 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
 // (tests/test_host_cpu.py::test_grid_extrema_rule_is_exact). The ten
 // candidates are split over S lanes (lane s evaluates candidates s, s+S, ...);
 // critical points need only grid-point accuracy, so approximate rcp/rsq do.
+// Interval j's piece is (y0, y1, a, b) = (y[j], y[j+1], m[j], m[j+1]): every
+// candidate lies in [lo, hi], whose grid samples all fall in interval j.
 template <int S>
-__device__ void interval_extrema(const SacenvBoatParams& p, const DrawLds& l, int c, int j, int s,
-                                 double& mn, double& mx) {
+__device__ __forceinline__ void interval_extrema(const SacenvBoatParams& p, int j, int s, double y0,
+                                                 double y1, double a, double b, double& mn,
+                                                 double& mx) {
   mn = INFINITY;
   mx = -INFINITY;
   const int L = p.wind_len;
@@ -440,8 +438,6 @@ __device__ void interval_extrema(const SacenvBoatParams& p, const DrawLds& l, in
   if (hi > L - 1) hi = L - 1;
   while (hi >= 0 && knot_coord(p, hi).j > j) --hi;
   if (lo > hi) return;
-  const double a = l.m[c][j], b = l.m[c][j + 1];
-  const double y0 = l.y[c][j], y1 = l.y[c][j + 1];
   const double qa = 3.0 * (b - a), qb = 6.0 * a, qc = y1 - y0 - 2.0 * a - b;
   double r0 = -1.0, r1 = -1.0;  // roots of the derivative in [0,1]; -1 = none
   const double scale = fabs(qa) + fabs(qb) + fabs(qc);
@@ -476,7 +472,7 @@ __device__ void interval_extrema(const SacenvBoatParams& p, const DrawLds& l, in
       i = ok ? i : lo;
     }
     if (q < 10) {
-      const double v = curve_lds(p, l, c, i);
+      const double v = spline_piece(y0, y1, a, b, knot_coord(p, i).t);
       mn = fmin(mn, v);
       mx = fmax(mx, v);
     }
@@ -490,34 +486,13 @@ __device__ __forceinline__ void load_g(const SacenvBoatParams& p, const double* 
   __syncthreads();
 }
 
-// G split in two so its global load overlaps other loads: fetch to registers
-// first, publish to LDS once the wave knows it has work.
-struct GRegs {
-  double v[kMaxK * kMaxK / kWave];
-};
-__device__ __forceinline__ GRegs fetch_g(const SacenvBoatParams& p, const double* g, int lane) {
-  GRegs r;
-  const int nn = p.n_knots * p.n_knots;
-#pragma unroll
-  for (int k = 0; k < kMaxK * kMaxK / kWave; ++k) {  // clamped: no branch per load
-    const int i = lane + kWave * k;
-    r.v[k] = g[i < nn ? i : nn - 1];
-  }
-  return r;
-}
-__device__ __forceinline__ void publish_g(const GRegs& r, DrawLds& l, int lane) {
-#pragma unroll
-  for (int k = 0; k < kMaxK * kMaxK / kWave; ++k) l.g[lane + kWave * k] = r.v[k];
-  __syncthreads();
-}
-
 // ---------------------------------------------------------------- episode draw
 
 // The RNG half of Boat(config) for env `e`, by all 64 lanes (e uniform):
 // np.random.randint(-hw, hw) (boat_env.py:147-150), then n knot values per
 // random curve (wind.py:78; velocity first in exp 6) into l.y. Explicit
 // draws (replays) bypass the RNG. Returns start_y in all lanes.
-__device__ int32_t draw_knots_wave(const SacenvBoatParams& p, const Arena& A, DrawLds& l, int e,
+__device__ int32_t draw_knots_wave(const SacenvBoatParams& p, const Arena& A, RngLds& l, int e,
                                    int lane, const int32_t* ex_start_y, const double* ex_knots) {
   const int nk = p.n_knots;
   // draws follow the reference even when a recorded wind table overrides the
@@ -598,6 +573,26 @@ __device__ int32_t draw_knots_wave(const SacenvBoatParams& p, const Arena& A, Dr
   return -p.start_y_half + (int32_t)val;
 }
 
+// wind.py:87-89 min-max renormalisation of one knot's (value, 2nd derivative)
+// when the grid samples leave [0, 1], then the table scaling of wind.py:86-89
+// (velocity * max_v, angle * pi * 2; exp 5 keeps the unit curve for the
+// rectifier, wind.py:92-99)
+__device__ __forceinline__ void fold_knot(const SacenvBoatParams& p, int c, double mn, double mx, double& yv,
+                                          double& mv) {
+  if (mn < 0.0 || mx > 1.0) {
+    const double span = mx - mn;
+    yv = (yv - mn) / span;
+    mv = mv / span;
+  }
+  if (p.experiment == 4 || (p.experiment == 6 && c == 0)) {
+    yv = yv * p.max_velocity;
+    mv = mv * p.max_velocity;
+  } else if (p.experiment == 6 && c == 1) {
+    yv = yv * kPi * 2;
+    mv = mv * kPi * 2;
+  }
+}
+
 // The spline half: from the knot values in l.y (lanes 16c + j hold knot j of
 // curve c), second derivatives m = G @ y, exact grid min/max, the min-max
 // renormalisation (wind.py:87-89) and the table scaling (wind.py:86-99);
@@ -624,9 +619,12 @@ __device__ void fit_store_wave(const SacenvBoatParams& p, const Arena& A, DrawLd
   {
     const int cc = lane >> 5, u = lane & 31;
     if (nk - 1 <= 8) {
-      if (cc < ncurves && (u >> 2) < nk - 1) interval_extrema<4>(p, l, cc, u >> 2, u & 3, mn, mx);
+      const int jj = u >> 2;
+      if (cc < ncurves && jj < nk - 1)
+        interval_extrema<4>(p, jj, u & 3, l.y[cc][jj], l.y[cc][jj + 1], l.m[cc][jj], l.m[cc][jj + 1], mn, mx);
     } else {
-      if (cc < ncurves && u < nk - 1) interval_extrema<1>(p, l, cc, u, 0, mn, mx);
+      if (cc < ncurves && u < nk - 1)
+        interval_extrema<1>(p, u, 0, l.y[cc][u], l.y[cc][u + 1], l.m[cc][u], l.m[cc][u + 1], mn, mx);
     }
   }
   mn = row16_min(mn);
@@ -639,20 +637,7 @@ __device__ void fit_store_wave(const SacenvBoatParams& p, const Arena& A, DrawLd
   mn = c == 0 ? cmn0 : cmn1;
   mx = c == 0 ? cmx0 : cmx1;
   if (knot_lane) {
-    if (mn < 0.0 || mx > 1.0) {  // wind.py:87-89 min-max renormalisation
-      const double span = mx - mn;
-      yv = (yv - mn) / span;
-      mv = mv / span;
-    }
-    // table scaling of wind.py:86-89: velocity * max_v, angle * pi * 2;
-    // exp 5 keeps the unit curve for the rectifier (wind.py:92-99).
-    if (p.experiment == 4 || (p.experiment == 6 && c == 0)) {
-      yv = yv * p.max_velocity;
-      mv = mv * p.max_velocity;
-    } else if (p.experiment == 6 && c == 1) {
-      yv = yv * kPi * 2;
-      mv = mv * kPi * 2;
-    }
+    fold_knot(p, c, mn, mx, yv, mv);
     const int64_t o = A.wix(slot, c, j, e);
     A.wind_y()[o] = yv;
     A.wind_m()[o] = mv;
@@ -660,14 +645,14 @@ __device__ void fit_store_wave(const SacenvBoatParams& p, const Arena& A, DrawLd
   __syncthreads();
 }
 
-// start y and (SACENV_OUT_KNOTS) the raw knot values of a drawn episode
-__device__ __forceinline__ void store_draw(const SacenvBoatParams& p, const Arena& A, const DrawLds& l,
-                                           int e, int slot, int32_t start_y, int lane) {
+// start y and (raw, or SACENV_OUT_KNOTS) the raw knot values of a drawn episode
+__device__ __forceinline__ void store_draw(const SacenvBoatParams& p, const Arena& A, const RngLds& l,
+                                           int e, int slot, int32_t start_y, int lane, bool raw = false) {
   const int nk = p.n_knots;
   const int ncurves = p.use_wind_table ? 0 : n_curves(p.experiment);
   if (lane == 0) A.i32(U_STARTY)[(int64_t)slot * A.np + e] = start_y;
   const int c = lane >> 4, j = lane & 15;
-  if (c < ncurves && j < nk && (p.out_flags & SACENV_OUT_KNOTS))
+  if (c < ncurves && j < nk && (raw || (p.out_flags & SACENV_OUT_KNOTS)))
     A.knots_raw()[A.wix(slot, c, j, e)] = l.y[c][j];
 }
 
@@ -927,28 +912,102 @@ __global__ void __launch_bounds__(1024) k_compact(const uint8_t* __restrict__ do
   if (t == 0) *count = base_s;
 }
 
-// sacenv_boat_refill: every env flagged in the refill masks gets its slot
-// ring topped up to SLOTS episodes (fill = cons + SLOTS), drawn and fitted
-// in the env's order, one wave per env (rank h, h + grid, ...). Block 0 then
-// bumps the refill generation, so the next step launch's owners start their
-// masks afresh; a mask word that still carries an older generation is
-// re-ranked harmlessly (its envs are full: nothing to draw).
-__global__ void __launch_bounds__(kWave) k_refill(SacenvBoatParams p, Arena A, Tail T) {
-  __shared__ DrawLds lds;
+// sacenv_boat_refill, launch 1: every env flagged in the refill masks gets
+// its slot ring topped up to SLOTS episodes (fill = cons + SLOTS), drawn in
+// the env's order (start y and raw knots), one wave per env (rank h,
+// h + grid, ...). Block 0 counts the refill and publishes the rank count for
+// launch 2, which also clears the masks.
+__global__ void __launch_bounds__(kWave) k_refill(SacenvBoatParams p, Arena A) {
+  __shared__ RngLds lds;
   const int lane = threadIdx.x;
-  const GRegs g = fetch_g(p, T.g, lane);  // in flight together with the masks
   const Ranking k = rank_masks(A, lane);
-  if (blockIdx.x == 0 && lane == 0) A.status()[0] += 1;
-  if ((int)blockIdx.x >= k.total) return;
-  publish_g(g, lds, lane);
+  if (blockIdx.x == 0 && lane == 0) {
+    A.status()[0] += 1;
+    A.status()[2] = k.total;
+  }
   for (int rr = blockIdx.x; rr < k.total; rr += gridDim.x) {
     const int e = ranked_env(A, k, rr, lane);
     const int c = A.i32(U_CONS)[e];
-    int f = A.i32(U_FILL)[e];
-    if (c >= f && lane == 0) atomicOr(&A.status()[1], SACENV_STATUS_SLOT_UNDERFLOW);
-    for (; f < c + kSlots; ++f) draw_episode_wave(p, A, lds, e, f % kSlots, lane, nullptr, nullptr);
-    if (lane == 0) A.i32(U_FILL)[e] = f;
-    __syncthreads();
+    const int f0 = A.i32(U_FILL)[e];
+    if (c >= f0 && lane == 0) atomicOr(&A.status()[1], SACENV_STATUS_SLOT_UNDERFLOW);
+    int f = f0;
+    for (; f < c + kSlots; ++f) {
+      const int32_t start_y = draw_knots_wave(p, A, lds, e, lane, nullptr, nullptr);
+      __syncthreads();
+      store_draw(p, A, lds, e, f % kSlots, start_y, lane, true);
+      __syncthreads();
+    }
+    if (lane == 0) {
+      A.i32(U_FILL)[e] = f;
+      A.refill_list(0)[rr] = e;
+      A.refill_list(1)[rr] = f0;
+      A.refill_list(2)[rr] = f;
+    }
+  }
+}
+
+// sacenv_boat_refill, launch 2: the spline fits of the episodes launch 1
+// drew. A group of GS lanes (8, or 16 for more than 8 knots) fits one
+// (env, curve): lane j forms m[j] = (G @ y)[j] and the grid extrema of
+// interval j, the group reduces min/max by shuffles, and lane j folds and
+// stores knot j (the operations of fit_store_wave in the same order:
+// bit-identical coefficients). Grid-stride over the groups; the refill masks
+// launch 1 ranked are cleared here (stream order: launch 1 has read them).
+template <int GS>
+__device__ void fit_group(const SacenvBoatParams& p, const Arena& A, const double* g, int item, int j,
+                          int nc) {
+  const int nk = p.n_knots;
+  const int rr = item / nc, c = item - rr * nc;
+  const int e = A.refill_list(0)[rr], f0 = A.refill_list(1)[rr], f1 = A.refill_list(2)[rr];
+  for (int f = f0; f < f1; ++f) {  // uniform across the group
+    const int slot = f % kSlots;
+    const double* raw = A.knots_raw();
+    double yk[GS];
+#pragma unroll
+    for (int k = 0; k < GS; ++k) yk[k] = k < nk ? raw[A.wix(slot, c, k, e)] : 0.0;
+    const int jj = j < nk ? j : nk - 1, j1 = jj + 1 < nk ? jj + 1 : jj;
+    double yv = raw[A.wix(slot, c, jj, e)];
+    const double y1 = raw[A.wix(slot, c, j1, e)];
+    double mv = 0.0;
+#pragma unroll
+    for (int k = 0; k < GS; ++k)
+      if (k < nk) mv += g[jj * nk + k] * yk[k];
+    const double m1 = __shfl_down(mv, 1, GS);
+    double mn = INFINITY, mx = -INFINITY;
+    if (j < nk - 1) interval_extrema<1>(p, j, 0, yv, y1, mv, m1, mn, mx);
+#pragma unroll
+    for (int o = GS / 2; o > 0; o >>= 1) {
+      mn = fmin(mn, __shfl_xor(mn, o, GS));
+      mx = fmax(mx, __shfl_xor(mx, o, GS));
+    }
+    if (j < nk) {
+      fold_knot(p, c, mn, mx, yv, mv);
+      const int64_t o = A.wix(slot, c, j, e);
+      A.wind_y()[o] = yv;
+      A.wind_m()[o] = mv;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kWave) k_refill_fit(SacenvBoatParams p, Arena A, Tail T) {
+  __shared__ double g[kMaxK * kMaxK];
+  const int lane = threadIdx.x;
+  for (int w = blockIdx.x * kWave + lane; w < A.nwaves(); w += gridDim.x * kWave) A.refill_mask()[w] = 0ull;
+  const int nc = p.use_wind_table ? 0 : n_curves(p.experiment);
+  const int nk = p.n_knots;
+  const int GS = nk > 8 ? 16 : 8;
+  const int items = A.status()[2] * nc;  // (env, curve) groups
+  if (items == 0 || (int)blockIdx.x * (kWave / GS) >= items) return;  // uniform
+  for (int i = lane; i < nk * nk; i += kWave) g[i] = T.g[i];
+  __syncthreads();
+  const int per = kWave / GS;
+  for (int base = blockIdx.x * per; base < items; base += gridDim.x * per) {
+    const int item = base + lane / GS;
+    if (item >= items) break;
+    if (GS == 8)
+      fit_group<8>(p, A, g, item, lane & 7, nc);
+    else
+      fit_group<16>(p, A, g, item, lane & 15, nc);
   }
 }
 
@@ -1217,18 +1276,6 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   const uint32_t eo = (uint32_t)e * 8u, eo4 = (uint32_t)e * 4u;  // per-lane byte offsets
   const bool active = e < p.n_envs;
   const int kepoch = A.owner_epoch()[ob];
-  // this wave's refill-mask word and the current refill generation (uniform)
-  unsigned long long mask_acc = 0ull;
-  int mgen = 0, rgen = 0;
-#ifndef SACENV_DIAG_NO_MASK  // timing diagnostics only
-  if (p.autoreset) {
-#else
-  if (false) {
-#endif
-    mask_acc = A.refill_mask()[ob];
-    mgen = A.mask_gen()[ob];
-    rgen = A.status()[0];
-  }
   const float act = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(action) + (active ? eo4 : 0u));
   const bool t_idx = t_from_index(p.dt);
   const int nc = p.use_wind_table ? 0 : n_curves(p.experiment);  // spline curves of the wind
@@ -1491,13 +1538,12 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   store_obs_block(l.obs, A.obs() + row0, lane);
 
   if (p.autoreset) {
-    // envs that ended since the last refill (a word of an older generation
-    // starts afresh): what the next sacenv_boat_refill draws for
-    const unsigned long long m = __ballot(ended) | (mgen == rgen ? mask_acc : 0ull);
-    if (lane == 0 && (m != mask_acc || mgen != rgen)) {
-      A.refill_mask()[ob] = m;
-      A.mask_gen()[ob] = rgen;
-    }
+    // envs that ended since the last refill, what the next sacenv_boat_refill
+    // draws for: a no-return atomic OR into this wave's word (nothing waits on
+    // it; the refill's fit launch clears the words after its draw launch read them)
+    const unsigned long long m = __ballot(ended);
+    if (lane == 0 && m != 0ull)
+      __hip_atomic_fetch_or(&A.refill_mask()[ob], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (lane == 0) A.owner_epoch()[ob] = kepoch + 1;
 #ifdef SACENV_STAMPS
@@ -1588,7 +1634,7 @@ int check_params(const SacenvBoatParams* p) {
   if (p->n_knots < 2 || p->n_knots > kMaxK) return SACENV_E_KNOTS;
   if (n_curves(p->experiment) > 0 && !p->use_wind_table && p->wind_len < 2) return SACENV_E_SIZE;
   if (p->start_y_half < 1) return SACENV_E_RANGE;
-  if (p->autoreset && (p->n_helpers < 1 || p->n_helpers > 4096)) return SACENV_E_SIZE;
+  if (p->autoreset && (p->n_helpers < 1 || p->n_helpers > 65536)) return SACENV_E_SIZE;
   return SACENV_OK;
 }
 
@@ -1741,8 +1787,12 @@ int sacenv_boat_refill(const SacenvBoatParams* p, void* arena, void* stream) {
   if (rc) return rc;
   if (arena == nullptr) return SACENV_E_NULL;
   if (!p->autoreset) return SACENV_E_MODE;
-  hipLaunchKernelGGL(k_refill, dim3(p->n_helpers), dim3(kWave), 0, (hipStream_t)stream, *p,
-                     make_arena(*p, arena), make_tail(*p, arena));
+  const Arena A = make_arena(*p, arena);
+  hipLaunchKernelGGL(k_refill, dim3(p->n_helpers), dim3(kWave), 0, (hipStream_t)stream, *p, A);
+  if ((rc = launch_status())) return rc;
+  const int nw = (int)(A.np / kWave);
+  hipLaunchKernelGGL(k_refill_fit, dim3(nw < 4096 ? nw : 4096), dim3(kWave), 0, (hipStream_t)stream, *p, A,
+                     make_tail(*p, arena));
   return launch_status();
 }
 

@@ -53,7 +53,7 @@ class VecBoatEnv:
     def __init__(self, config=None, num_envs: int = 1, *, seed: int = 0, seeds=None,
                  device=None, max_episode_steps: int = 0, autoreset: bool = True,
                  env_id_offset: int = 0, record_knots: bool = False, record_accel: bool = False,
-                 record_reward64: bool = False, wind_table=None, n_helpers: int = 2048,
+                 record_reward64: bool = False, wind_table=None, n_helpers: int = 4096,
                  auto_refill: bool = True):
         self.lib = _lib.load()
         self.cfg = BoatConfig.from_any(config)
@@ -111,7 +111,7 @@ class VecBoatEnv:
         self.final_ep_reward = view(L.final_ep_reward, f64, NP)[:N]
         self.accel = view(L.accel, f64, 3, NP)[:, :N]
         self.reward64 = view(L.reward64, f64, NP)[:N]
-        self.status = view(L.status, i32, 64)        # [0] refill generation, [1] status bits
+        self.status = view(L.status, i32, 64)        # [0] refills done, [1] status bits
         if wind_table is not None:
             wt = torch.as_tensor(np.asarray(wind_table, np.float64).reshape(2, -1))
             if wt.shape[1] != self.cfg.wind_len:

@@ -143,7 +143,7 @@ def test_arena_layout(built_lib, n):
     sizes = {"s_x": 8, "s_y": 8, "s_r": 8, "v_x": 8, "v_y": 8, "v_r": 8, "rudder": 8, "t": 8,
              "ep_reward": 8, "wind_next": 16, "wind_coef": 64, "wind0_next": 16, "start_y_next": 4,
              "index": 4, "cons": 4, "fill": 4, "mt_pos": 4,
-             "start_y": 4 * S, "counters": 20, "wind_y": 16 * S * nk, "wind_m": 16 * S * nk,
+             "start_y": 4 * S, "counters": 20, "refill_list": 12, "wind_y": 16 * S * nk, "wind_m": 16 * S * nk,
              "knots_raw": 16 * S * nk, "mt_key": 2496, "obs": 44, "reward": 4, "done": 1, "term": 1,
              "final_obs": 44, "final_ep_reward": 8, "accel": 24, "reward64": 8}
     spans = sorted((getattr(L, f), getattr(L, f) + w * np_, f) for f, w in sizes.items())
@@ -152,7 +152,7 @@ def test_arena_layout(built_lib, n):
     for a0, a1, f in spans:
         assert a0 % 64 == 0, f
     assert L.record == L.obs and L.term + np_ == L.record + 50 * np_
-    tail = [("refill_mask", 8 * np_ // 64), ("mask_gen", 4 * np_ // 64), ("status", 256),
+    tail = [("refill_mask", 8 * np_ // 64), ("status", 256),
             ("owner_epoch", 4 * np_ // 64), ("spline_g", 8 * 256), ("wind_table", 16 * 10000)]
     end = spans[-1][1]
     for f, w in tail:
