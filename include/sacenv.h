@@ -115,13 +115,11 @@ typedef struct SacenvBoatLayout {
   int64_t total_bytes;
   int64_t n_pad;
   int64_t s_x, s_y, s_r, v_x, v_y, v_r, rudder, t, ep_reward; /* f64 [n_pad] */
-  int64_t wind_next;          /* f64 [2][n_pad] Wind.get_wind(index) for the NEXT step (v, angle) */
-  int64_t wind_coef;          /* f64 [2 curves][y0 y1 m0 m1][n_pad]: the active episode's spline piece
-                                 of the interval of the next wind sample (a copy of its slot's
-                                 wind_y/wind_m, refreshed in an episode's first step and when the
-                                 sample crosses a knot) */
-  int64_t wind0_next;         /* f64 [2][n_pad] autoreset: Wind.get_wind(0) of the NEXT episode (copy,
-                                 refreshed in each episode's first step) */
+  int64_t wind_coef;          /* f64 [2 curves][y0 y1 m0 m1][n_pad]: the active episode's spline piece of
+                                 the interval of the next step's wind sample (a copy of its slot's
+                                 wind_y/wind_m; a new episode starts from (y(0), 0, 0, 0)) */
+  int64_t wind0_next;         /* f64 [2][n_pad] autoreset: the next episode's curve values at grid
+                                 index 0 (copy, refreshed in each episode's first step) */
   int64_t start_y_next;       /* i32 [n_pad] autoreset: Boat.s_y_start of the next episode (same) */
   int64_t index;              /* i32 [n_pad] steps since reset; fuel = fuel0 - index */
   int64_t cons;               /* i32 [n_pad] episodes started (active slot = cons % SLOTS) */

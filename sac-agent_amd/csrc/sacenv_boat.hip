@@ -46,13 +46,14 @@ constexpr double kPi = 3.141592653589793;  // np.pi
 // n_pad is a multiple of 64, so every array is 64-byte aligned.
 // U_COEF / U_W0N / U_SYN are lane-coalesced copies of slot data the step
 // reads every launch (see owner_wave): the active episode's spline piece
-// (y0, y1, m0, m1 per curve) of the interval of the next wind sample, and
-// the next episode's first wind and start y. Slots differ from env to env,
-// so reading them from the slot ring itself would scatter every wave's loads
-// over up to 33 rows.
+// (y0, y1, m0, m1 per curve) of the interval of this step's wind sample, and
+// the next episode's curve values at grid index 0 and start y. Slots differ
+// from env to env, so reading them from the slot ring itself would scatter
+// every wave's loads over up to 33 rows. U_COEF follows the carried state
+// directly: fields 0..16 are loaded as one run (owner_load).
 constexpr int U_SX = 0, U_SY = 8, U_SR = 16, U_VX = 24, U_VY = 32, U_VR = 40, U_RUD = 48,
-              U_T = 56, U_EP = 64, U_WNX = 72, U_COEF = 88, U_W0N = 152, U_IDX = 168,
-              U_CONS = 172, U_FILL = 176, U_MTPOS = 180, U_SYN = 184, U_STARTY = 188,
+              U_T = 56, U_EP = 64, U_COEF = 72, U_W0N = 136, U_IDX = 152,
+              U_CONS = 156, U_FILL = 160, U_MTPOS = 164, U_SYN = 168, U_STARTY = 172,
               U_CNT = U_STARTY + 4 * kSlots,
               U_LIST = U_CNT + 4 * SACENV_N_COUNTERS, U_WIND = U_LIST + 12;
 constexpr int U_MT_BYTES = 4 * kMtN;
@@ -73,7 +74,6 @@ __host__ __device__ inline void compute_layout(int n, int nk, int L, int use_tab
   o->rudder = U_RUD * np;
   o->t = U_T * np;
   o->ep_reward = U_EP * np;
-  o->wind_next = U_WNX * np;
   o->wind_coef = U_COEF * np;
   o->wind0_next = U_W0N * np;
   o->start_y_next = U_SYN * np;
@@ -284,42 +284,6 @@ __device__ __forceinline__ void wind_at(const SacenvBoatParams& p, const Arena& 
       wa = curve_env(p, A, slot, 1, e, idx);
       return;
     default:  // 1, 2: no wind
-      wv = 0.0;
-      wa = 0.0;
-      return;
-  }
-}
-
-// Wind.get_wind(0) of a slot's episode: at grid index 0 the spline is exactly
-// its first (folded) knot value, so no curve evaluation is needed.
-__device__ __forceinline__ void wind0_of_slot(const SacenvBoatParams& p, const Arena& A,
-                                              const double* table, int slot, int e, double& wv,
-                                              double& wa) {
-  if (p.use_wind_table) {
-    wv = table[0];
-    wa = table[p.wind_len];
-    return;
-  }
-  switch (p.experiment) {
-    case 3:
-      wv = p.max_velocity;
-      wa = p.wind_dir_rad;
-      return;
-    case 4:
-      wv = A.wy_at(A.wofs(slot, 0, 0, e));
-      wa = p.wind_dir_rad;
-      return;
-    case 5: {
-      wv = p.max_velocity;
-      const double r = A.wy_at(A.wofs(slot, 0, 0, e)) <= 0.5 / 2 ? 0.0 : 1.0;
-      wa = (r * kPi) + kPi / 2;
-      return;
-    }
-    case 6:
-      wv = A.wy_at(A.wofs(slot, 0, 0, e));
-      wa = A.wy_at(A.wofs(slot, 1, 0, e));
-      return;
-    default:
       wv = 0.0;
       wa = 0.0;
       return;
@@ -735,12 +699,18 @@ __device__ int ranked_env(const Arena& A, const Ranking& k, int rr, int lane) {
 }
 
 // scalar state of a fresh Boat (boat_env.py:152-198) and its observation;
-// (wv0, wa0) = Wind.get_wind(0) of the new episode, the first step's wind
+// the wind piece copy of the episode in `slot` starts at its first interval
 __device__ __forceinline__ Obs fresh_state(const SacenvBoatParams& p, const Arena& A, const Tail& T, int e,
-                                           int32_t start_y, double wv0, double wa0) {
+                                           int32_t start_y, int slot) {
   const double s_y = p.experiment == 2 ? (double)start_y : 0.0;  // :166-169
-  A.f64(U_WNX)[e] = wv0;
-  A.f64(U_WNX)[A.np + e] = wa0;
+  const int nc = p.use_wind_table ? 0 : n_curves(p.experiment);
+  for (int c = 0; c < nc; ++c) {
+    const uint32_t o = A.wofs(slot, c, 0, e), o1 = o + (uint32_t)A.np * 8u;
+    A.f64(U_COEF + 32 * c)[e] = A.wy_at(o);
+    A.f64(U_COEF + 32 * c + 8)[e] = A.wy_at(o1);
+    A.f64(U_COEF + 32 * c + 16)[e] = A.wm_at(o);
+    A.f64(U_COEF + 32 * c + 24)[e] = A.wm_at(o1);
+  }
   A.f64(U_SX)[e] = 0.0;
   A.f64(U_SY)[e] = s_y;
   A.f64(U_SR)[e] = 0.0;
@@ -854,9 +824,7 @@ __global__ void __launch_bounds__(kWave) k_draw(SacenvBoatParams p, Arena A, Tai
       if (lane == 0) A.i32(U_FILL)[e] = f + 1;
     }
     if (lane == 0) {
-      double wv0, wa0;
-      wind0_of_slot(p, A, T.table, slot, e, wv0, wa0);
-      const Obs o = fresh_state(p, A, T, e, start_y, wv0, wa0);
+      const Obs o = fresh_state(p, A, T, e, start_y, slot);
       store_obs(A.obs() + (int64_t)e * SACENV_OBS_DIM, o);
     }
     __syncthreads();
@@ -1181,7 +1149,7 @@ struct MixedToys {
 // next (6 load instructions instead of 13). Outputs are stored per lane as
 // soon as they are final (EARLY_STORE); the obs rows go out through LDS as
 // float4 (64 rows x 44 B = 176 float4).
-constexpr int kF64 = 11;  // s_x s_y s_r v_x v_y v_r rudder t ep_reward wind_next[2]
+constexpr int kF64 = 17;  // s_x s_y s_r v_x v_y v_r rudder t ep_reward | wind_coef[8]
 constexpr int kCoef = 8;  // wind_coef fields: 2 curves x (y0, y1, m0, m1)
 struct OwnerLds {
   double f[kF64][kWave];
@@ -1192,34 +1160,37 @@ struct OwnerLds {
 };
 
 
-// wave-wide 16-B gathers of the owner's SoA inputs into LDS: 6 load instructions
-__device__ __forceinline__ void owner_load(const Arena& A, OwnerLds& l, int ob, int lane, bool t_idx) {
+// wave-wide 16-B gathers of the owner's SoA inputs into LDS: fields 0..nf-1
+// (the state, then the wind piece of nc curves) two fields per instruction,
+// field 16 with index and cons: at most 9 load instructions
+__device__ __forceinline__ void owner_load(const Arena& A, OwnerLds& l, int ob, int lane, bool t_idx, int nf) {
   const int half = lane >> 5, c = lane & 31;
   const int64_t e0 = (int64_t)ob * kWave;
   // uniform row base + 32-bit per-lane offset (field 2q+half, envs e0+2c, e0+2c+1)
   const char* row = A.b + e0 * 8;
   const uint32_t lo = (uint32_t)half * 8u * (uint32_t)A.np + (uint32_t)c * 16u;
-  f4v v[6];
+  f4v v[9];
 #pragma unroll
-  for (int q = 0; q < 5; ++q) {
-    if (q == 3 && half == 1 && t_idx) {  // field 7 = t, derived from the index
-      v[q] = f4v{0.f, 0.f, 0.f, 0.f};
-      continue;
-    }
-    v[q] = *reinterpret_cast<const f4v*>(row + (int64_t)(16 * q) * A.np + lo);
+  for (int q = 0; q < 8; ++q) {
+    const int fi = 2 * q + half;
+    v[q] = f4v{0.f, 0.f, 0.f, 0.f};
+    if (fi < nf && !(fi == 7 && t_idx))  // field 7 = t is derived from the index when exact
+      v[q] = *reinterpret_cast<const f4v*>(row + (int64_t)(16 * q) * A.np + lo);
   }
-  {  // lanes 0-31: wind_next angle; 32-47: index; 48-63: cons (4 envs per lane)
+  {  // lanes 0-31: field 16; 32-47: index; 48-63: cons (4 envs per lane)
     const uint32_t np = (uint32_t)A.np, j = (uint32_t)(lane & 15);
-    const uint32_t off = lane < 32 ? 80u * np + (uint32_t)e0 * 8u + (uint32_t)c * 16u
+    const uint32_t off = lane < 32 ? 128u * np + (uint32_t)e0 * 8u + (uint32_t)c * 16u
                                    : (lane < 48 ? (uint32_t)U_IDX : (uint32_t)U_CONS) * np + (uint32_t)e0 * 4u + j * 16u;
-    v[5] = *reinterpret_cast<const f4v*>(A.b + off);
+    v[8] = f4v{0.f, 0.f, 0.f, 0.f};
+    if (lane >= 32 || nf > 16) v[8] = *reinterpret_cast<const f4v*>(A.b + off);
   }
 #pragma unroll
-  for (int q = 0; q < 5; ++q) *reinterpret_cast<f4v*>(&l.f[2 * q + half][2 * c]) = v[q];
+  for (int q = 0; q < 8; ++q)
+    if (2 * q < nf) *reinterpret_cast<f4v*>(&l.f[2 * q + half][2 * c]) = v[q];
   if (lane < 32)
-    *reinterpret_cast<f4v*>(&l.f[10][2 * c]) = v[5];
+    *reinterpret_cast<f4v*>(&l.f[16][2 * c]) = v[8];
   else
-    *reinterpret_cast<f4v*>((lane < 48 ? l.idx : l.cons) + 4 * (lane & 15)) = v[5];
+    *reinterpret_cast<f4v*>((lane < 48 ? l.idx : l.cons) + 4 * (lane & 15)) = v[8];
   __syncthreads();
 }
 
@@ -1279,66 +1250,71 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   const float act = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(action) + (active ? eo4 : 0u));
   const bool t_idx = t_from_index(p.dt);
   const int nc = p.use_wind_table ? 0 : n_curves(p.experiment);  // spline curves of the wind
-  owner_load(A, l, ob, lane, t_idx);
+  owner_load(A, l, ob, lane, t_idx, 9 + 4 * nc);
   double s_x = l.f[0][lane], s_y = l.f[1][lane], s_r = l.f[2][lane];
   double v_x = l.f[3][lane], v_y = l.f[4][lane], v_r = l.f[5][lane];
   double rudder = l.f[6][lane], t = l.f[7][lane], ep = l.f[8][lane];
-  // this step's wind was evaluated one step ahead (no index-dependent load
-  // on the critical path); the next step's is fetched now, used at the end
-  const double wv = l.f[9][lane], wa = l.f[10][lane];
   int32_t index = l.idx[lane];
   const int cons = p.autoreset ? l.cons[lane] : 0;
-  // Wind.get_wind(index + 1) for the next step, evaluated at the end. Curves:
-  // from the lane's copy of its spline piece (wind_coef, coalesced loads
-  // issued here, consumed at the end), refreshed from the active slot only
-  // in an episode's first step or when the sample enters the next knot
-  // interval: a handful of lanes per launch take the scattered slot loads.
-  double nwv = 0.0, nwa = 0.0;
+  // Wind.get_wind(index) (wind.py:20-24, IndexError guard) of this step. Curves:
+  // from the lane's copy of its spline piece (wind_coef, loaded with the
+  // state). The copy is refreshed from the active slot at the end of a step
+  // whose successor enters the next knot interval, and in an episode's first
+  // step (a new episode starts with the degenerate piece (y(0), 0, 0, 0),
+  // exact at t = 0): the few lanes that refresh issue their scattered slot
+  // loads here and store the piece at the end.
   double cf[kCoef];
 #pragma unroll
-  for (int k = 0; k < kCoef; ++k) cf[k] = k < 4 * nc ? A.f64e(U_COEF + 8 * k, eo) : 0.0;
-#ifdef SACENV_DIAG_NO_CF  // timing diagnostics only (wrong winds)
-#pragma unroll
-  for (int k = 0; k < kCoef; ++k) cf[k] = (double)k;
-#endif
-  const int wi = index + 1 > p.wind_len - 1 ? p.wind_len - 1 : index + 1;  // wind.py IndexError guard
-  const Knot kn = knot_coord(p, wi);
+  for (int k = 0; k < kCoef; ++k) cf[k] = k < 4 * nc ? l.f[9 + k][lane] : 0.0;
+  const int wi = index > p.wind_len - 1 ? p.wind_len - 1 : index;
+  double wv = 0.0, wa = 0.0;
   bool refresh = false;
+  int jn = 0;
   if (nc == 0) {
-    wind_at(p, A, T.table, 0, e, index + 1, nwv, nwa);  // constants or the shared table
+    wind_at(p, A, T.table, 0, e, wi, wv, wa);  // constants or the shared table
   } else {
-    const int jp = knot_coord(p, index > p.wind_len - 1 ? p.wind_len - 1 : index).j;
-    refresh = index == 0 || kn.j != jp;
-    if (refresh) {
+    const double tt = knot_coord(p, wi).t;
+    const double c0 = spline_piece(cf[0], cf[1], cf[2], cf[3], tt);
+    if (p.experiment == 6) {
+      wv = c0;
+      wa = spline_piece(cf[4], cf[5], cf[6], cf[7], tt);
+    } else if (p.experiment == 4) {
+      wv = c0;
+      wa = p.wind_dir_rad;
+    } else {  // 5: rectified angle (wind.py:92-99)
+      wv = p.max_velocity;
+      wa = ((c0 <= 0.5 / 2 ? 0.0 : 1.0) * kPi) + kPi / 2;
+    }
+    const int wn = index + 1 > p.wind_len - 1 ? p.wind_len - 1 : index + 1;
+    jn = knot_coord(p, wn).j;
+    refresh = index == 0 || jn != knot_coord(p, wi).j;
+    if (refresh) {  // the piece of the next step's interval
       const int slot = cons % kSlots;
 #pragma unroll
       for (int c = 0; c < 2; ++c)
         if (c < nc) {
-          const uint32_t o = A.wofs(slot, c, kn.j, e), o1 = o + (uint32_t)A.np * 8u;
+          const uint32_t o = A.wofs(slot, c, jn, e), o1 = o + (uint32_t)A.np * 8u;
           cf[4 * c] = A.wy_at(o), cf[4 * c + 1] = A.wy_at(o1);
           cf[4 * c + 2] = A.wm_at(o), cf[4 * c + 3] = A.wm_at(o1);
         }
     }
   }
-  // autoreset: the next pre-drawn episode's first wind and start y, read
-  // speculatively from their lane-coalesced copies, which a lane refreshes
-  // from the slot ring during the first step of each episode (index 0)
-  double w0v = 0.0, w0a = 0.0;
+  // autoreset: the next pre-drawn episode's curve values at grid index 0 and
+  // start y, read speculatively from their lane-coalesced copies, which a
+  // lane refreshes from the slot ring in the first step of each episode
+  double y0n[2] = {0.0, 0.0};
   int32_t sy_next = 0;
   const bool hdr_refresh = p.autoreset && index == 0;
   if (p.autoreset) {
-    if (nc > 0) {
-#ifndef SACENV_DIAG_NO_W0  // timing diagnostics only
-      w0v = A.f64e(U_W0N, eo);
-      w0a = A.f64e(U_W0N + 8, eo);
-#endif
-    } else {
-      wind0_of_slot(p, A, T.table, 0, e, w0v, w0a);  // constants or the shared table
-    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+      if (c < nc) y0n[c] = A.f64e(U_W0N + 8 * c, eo);
     if (p.experiment == 2) sy_next = A.i32e(U_SYN, eo4);
     if (hdr_refresh) {
       const int ns = (cons + 1) % kSlots;
-      if (nc > 0) wind0_of_slot(p, A, T.table, ns, e, w0v, w0a);
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+        if (c < nc) y0n[c] = A.wy_at(A.wofs(ns, c, 0, e));
       if (p.experiment == 2) sy_next = A.i32e(U_STARTY + 4 * ns, eo4);
     }
   }
@@ -1456,7 +1432,6 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
     s_x = 0.0, s_y = sy0, s_r = 0.0, v_x = 0.0, v_y = 0.0, v_r = 0.0, rudder = 0.0;
     t = 0.0, ep = 0.0;  // :122
     index = 0;
-    nwv = w0v, nwa = w0a;
     if (p.experiment == 2 || p.fuel0 == 0) {
       fo = make_obs(p, oc, 0.0, 0.0, 0.0, sy0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, (double)p.fuel0);
     } else {  // make_obs of the zero state, folded: (0+W)/(2W) = 0.5 and fuel0/fuel0 = 1 exactly
@@ -1481,30 +1456,26 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
     A.i32e(U_CONS, eo4) = cons_out;
   }
   A.f64e(U_EP, eo) = ep;
-  if (nc > 0 && !restart) {  // the next step's wind from the piece (wind.py:20-24, :86-99)
-    const double c0 = spline_piece(cf[0], cf[1], cf[2], cf[3], kn.t);
-    if (p.experiment == 6) {
-      nwv = c0;
-      nwa = spline_piece(cf[4], cf[5], cf[6], cf[7], kn.t);
-    } else if (p.experiment == 4) {
-      nwv = c0;
-      nwa = p.wind_dir_rad;
-    } else {  // 5: rectified angle (wind.py:92-99)
-      nwv = p.max_velocity;
-      nwa = ((c0 <= 0.5 / 2 ? 0.0 : 1.0) * kPi) + kPi / 2;
-    }
-  }
-  if (refresh) {
+  if (restart && nc > 0) {  // the new episode's degenerate piece: y(0) at t = 0
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+      if (c < nc) {
+        A.f64e(U_COEF + 32 * c, eo) = y0n[c];
+        A.f64e(U_COEF + 32 * c + 8, eo) = 0.0;
+        A.f64e(U_COEF + 32 * c + 16, eo) = 0.0;
+        A.f64e(U_COEF + 32 * c + 24, eo) = 0.0;
+      }
+  } else if (refresh) {
 #pragma unroll
     for (int k = 0; k < kCoef; ++k)
       if (k < 4 * nc) A.f64e(U_COEF + 8 * k, eo) = cf[k];
   }
   if (hdr_refresh) {
-    if (nc > 0) A.f64e(U_W0N, eo) = w0v, A.f64e(U_W0N + 8, eo) = w0a;
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+      if (c < nc) A.f64e(U_W0N + 8 * c, eo) = y0n[c];
     if (p.experiment == 2) A.i32e(U_SYN, eo4) = sy_next;
   }
-  A.f64e(U_WNX, eo) = nwv;
-  A.f64e(U_WNX + 8, eo) = nwa;
   A.at_e<float>(A.ur() + 44, eo4) = (float)reward;
   A.at_e<uint8_t>(A.ur() + 48, (uint32_t)e) = ended ? 1 : 0;
   A.at_e<uint8_t>(A.ur() + 49, (uint32_t)e) = term;

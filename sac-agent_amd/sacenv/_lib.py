@@ -54,7 +54,7 @@ class BoatParams(C.Structure):
 
 LAYOUT_FIELDS = (
     "total_bytes", "n_pad", "s_x", "s_y", "s_r", "v_x", "v_y", "v_r", "rudder", "t",
-    "ep_reward", "wind_next", "wind_coef", "wind0_next", "start_y_next", "index", "cons", "fill", "mt_pos", "start_y", "counters",
+    "ep_reward", "wind_coef", "wind0_next", "start_y_next", "index", "cons", "fill", "mt_pos", "start_y", "counters",
     "refill_list",
     "wind_y", "wind_m", "knots_raw", "mt_key", "record", "obs", "reward", "done", "term",
     "final_obs", "final_ep_reward", "accel", "reward64", "refill_mask", "status",

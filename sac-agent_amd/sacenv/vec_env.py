@@ -90,8 +90,6 @@ class VecBoatEnv:
         self._t_view = view(L.t, f64, NP)[:N]
         self._t_from_index = t_from_index(float(self.cfg.dt))
         self.index = view(L.index, i32, NP)[:N]
-        # Wind.get_wind(index) of the NEXT step, pre-evaluated by the step launch
-        self.wind_next = view(L.wind_next, f64, 2, NP)[:, :N]
         self.cons = view(L.cons, i32, NP)[:N]
         self.mt_pos = view(L.mt_pos, i32, NP)[:N]
         self.start_y_slots = view(L.start_y, i32, _lib.SLOTS, NP)[:, :N]

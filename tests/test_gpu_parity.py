@@ -573,7 +573,7 @@ def test_autoreset_all_experiments_ragged_vs_oracle(exp, gpu, built_lib):
 @pytest.mark.parametrize("exp", [4, 5, 6])
 @pytest.mark.parametrize("autoreset", [False, True])
 def test_wind_piece_cache_across_intervals_and_episodes(exp, autoreset, gpu, built_lib):
-    """The step reads the next wind from a per-env cached spline piece (layout.wind_coef),
+    """The step evaluates its wind from a per-env copy of its spline piece (layout.wind_coef),
     refreshed from the episode's slot only on a new episode or an interval crossing.
     Short wind tables (L = 120, 17 steps per knot interval) and frozen rudders (episodes
     run to the timeout, so every interval and the end-of-table clamp are crossed), for
@@ -590,7 +590,9 @@ def test_wind_piece_cache_across_intervals_and_episodes(exp, autoreset, gpu, bui
     zero = np.zeros(N, np.float32)
     crossed = 0
     for k in range(int(2.6 * L)):
-        wnext = env.wind_next.cpu().numpy().T.copy()       # the wind this step will use
+        idx = torch.clamp(env.index, max=L - 1)
+        wv, wa = env.wind_eval(torch.arange(N, device=gpu), idx)   # the wind this step will use
+        wnext = torch.stack([wv, wa], 1).cpu().numpy()
         _, _, _, info = env.step(torch.zeros(N, device=gpu))
         r = ora.step(zero)
         torch.cuda.synchronize()

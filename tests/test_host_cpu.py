@@ -141,7 +141,7 @@ def test_arena_layout(built_lib, n):
     nk = 8
     S = _lib.SLOTS
     sizes = {"s_x": 8, "s_y": 8, "s_r": 8, "v_x": 8, "v_y": 8, "v_r": 8, "rudder": 8, "t": 8,
-             "ep_reward": 8, "wind_next": 16, "wind_coef": 64, "wind0_next": 16, "start_y_next": 4,
+             "ep_reward": 8, "wind_coef": 64, "wind0_next": 16, "start_y_next": 4,
              "index": 4, "cons": 4, "fill": 4, "mt_pos": 4,
              "start_y": 4 * S, "counters": 20, "refill_list": 12, "wind_y": 16 * S * nk, "wind_m": 16 * S * nk,
              "knots_raw": 16 * S * nk, "mt_key": 2496, "obs": 44, "reward": 4, "done": 1, "term": 1,
