@@ -11,13 +11,13 @@ all-gather over RCCL that pools transitions for a shared replay buffer).
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
 Timing: W untimed steps, then exactly K steps bracketed by barrier +
-synchronize; value = all envs x K / max-over-ranks time. Every 32 steps the
+synchronize; value = all envs x K / max-over-ranks time. Every 64 steps the
 slot refill (k_refill: the RNG draws and spline fits of the episodes that
 replace the ended ones) runs as its own launch INSIDE the timed region. At
-N=1 the 32-step segments are replayed from hipGraphs (launch-bound
+N=1 the 64-step segments are replayed from hipGraphs (launch-bound
 otherwise). Roofline: SURVEY.md §8(d) algorithmic 222 B per boat env-step x
 envs per launch, over k_step's average launch duration from HIP events on
-the kernel's stream around the 32-launch segments of the timed region (the
+the kernel's stream around the 64-launch segments of the timed region (the
 refills in between excluded; they are in ms_per_step); `traffic` = HBM bytes
 per launch from the committed rocprofv3 PMC passes (tools/pmc.sh).
 cpu_baseline: the numpy float64 oracle (oracle/boat_oracle.py, a port of the
@@ -44,8 +44,8 @@ METRIC_MIXED = ("env-steps/sec (whole node), mixed batch boat_env exp-6 + toy_pa
                 "32 768 envs each/GPU")
 HBM_PEAK = 8.0e12             # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 EPISODE_STEPS = 500
-SEG = 32               # step launches per refill (sacenv _lib.REFILL_PERIOD); one graph per segment
-ACTION_STEPS = 512     # the pre-generated action table cycles every 512 steps (16 segments)
+SEG = 64               # step launches per refill (sacenv _lib.REFILL_PERIOD); one graph per segment
+ACTION_STEPS = 512     # the pre-generated action table cycles every 512 steps (8 segments)
 
 
 def parse():
@@ -60,7 +60,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--kernel-launches", type=int, default=200)
     ap.add_argument("--test-mode", type=int, default=0, help="1 = rudder frozen (no terminations)")
-    ap.add_argument("--helpers", type=int, default=4096, help="workgroups of a refill draw launch")
+    ap.add_argument("--helpers", type=int, default=8192, help="workgroups of a refill draw launch")
     ap.add_argument("--mixed", action="store_true",
                     help="BASELINE configs[4]: boat exp-6 + toy_parachute + toy_car in one launch")
     ap.add_argument("--mixed-envs", type=int, default=32768, help="envs per type per GPU (--mixed)")
@@ -273,7 +273,7 @@ def main():
     el_max = float(t.item())
 
     # k_step average launch duration from HIP events on the stream the kernel
-    # runs on, around 32-launch graph segments (refills excluded). N=1: the
+    # runs on, around 64-launch graph segments (refills excluded). N=1: the
     # segments of the timed region itself. N>1: the timed region also holds
     # the all-gathers, so k_step-only segments are replayed and timed after it.
     if not use_graph:
@@ -287,10 +287,10 @@ def main():
         torch.cuda.synchronize(dev)
         run(max(SEG, args.kernel_launches // SEG * SEG), k, timed=True)
         torch.cuda.synchronize(dev)
-        kern_src = (f"HIP events around {len(seg_events)} graph-replayed 32-launch k_step segments "
+        kern_src = (f"HIP events around {len(seg_events)} graph-replayed {SEG}-launch k_step segments "
                     "after the timed region (no collective; refills between segments excluded)")
     else:
-        kern_src = (f"HIP events around the {len(seg_events)} graph-replayed 32-launch k_step "
+        kern_src = (f"HIP events around the {len(seg_events)} graph-replayed {SEG}-launch k_step "
                     "segments of the timed region (refills between segments excluded)")
     kern_s = sum(a.elapsed_time(b) for a, b in seg_events) * 1e-3 / (SEG * len(seg_events))
     step_s = ev0.elapsed_time(ev1) * 1e-3 / args.steps
@@ -326,9 +326,9 @@ def main():
                    "episode_steps": EPISODE_STEPS, "parallelism": f"env-dp{world}",
                    "collective": ("all_gather (obs,reward,done,term) 50 B/env/step, RCCL on a side "
                                   "stream overlapped with the next step") if world > 1 else None,
-                   "launch": ("hipGraph segments of 32 k_step launches + 1 k_refill launch"
+                   "launch": (f"hipGraph segments of {SEG} k_step launches + the 2 refill launches"
                               if world == 1 and not args.no_graph else "eager"),
-                   "refill": "k_refill every 32 steps, inside the timed region" if autoreset else None},
+                   "refill": f"k_refill + k_refill_fit every {SEG} steps, inside the timed region" if autoreset else None},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK,
                      "traffic": None if traffic is None else traffic["hbm_bytes_per_launch"],

@@ -3,11 +3,11 @@
 // The step launch (k_step) runs owner waves only: one lane per env, 64
 // consecutive envs per wave, BoatEnv.step (boat_env.py:67-115) on float64
 // SoA state. In autoreset mode an env that ends (terminated or truncated)
-// starts its next episode at once from a PRE-DRAWN slot (SLOTS = 33 per env:
-// the active episode + 32 ahead), so no RNG or spline work ever sits on the
+// starts its next episode at once from a PRE-DRAWN slot (SLOTS = 65 per env:
+// the active episode + 64 ahead), so no RNG or spline work ever sits on the
 // step's path; each owner wave ORs a 64-bit mask of its ended envs into its
 // own word (plain load/store, no atomics).
-// The refill launch (k_refill, at least every 32 steps) ranks the flagged
+// The refill launches (k_refill + k_refill_fit, at least every 64 steps) ranks the flagged
 // envs from those masks (DPP scans, no atomics) and, one wave per env, draws
 // the replacement episodes from the env's own numpy-legacy MT19937 stream
 // (Boat.__init__ boat_env.py:144-201: randint, then the wind knots,
@@ -457,7 +457,8 @@ __device__ __forceinline__ void load_g(const SacenvBoatParams& p, const double* 
 // random curve (wind.py:78; velocity first in exp 6) into l.y. Explicit
 // draws (replays) bypass the RNG. Returns start_y in all lanes.
 __device__ int32_t draw_knots_wave(const SacenvBoatParams& p, const Arena& A, RngLds& l, int e,
-                                   int lane, const int32_t* ex_start_y, const double* ex_knots) {
+                                   int lane, const int32_t* ex_start_y, const double* ex_knots,
+                                   int pos0 = -1) {
   const int nk = p.n_knots;
   // draws follow the reference even when a recorded wind table overrides the
   // curves; only the spline fit is skipped then
@@ -470,7 +471,7 @@ __device__ int32_t draw_knots_wave(const SacenvBoatParams& p, const Arena& A, Rn
   }
   MtStream st;
   st.gkey = A.mt_key() + (int64_t)e * kMtN;
-  st.pos = A.i32(U_MTPOS)[e];
+  st.pos = pos0 >= 0 ? pos0 : A.i32(U_MTPOS)[e];  // pos0: prefetched by the caller
   st.cur = 0;
   st.loaded = false;
   st.nxt_valid = false;
@@ -638,11 +639,12 @@ __device__ int32_t draw_episode_wave(const SacenvBoatParams& p, const Arena& A, 
 // l+64, ...; envs ordered by lane, then mask, then bit) with DPP scans, so
 // rank rr maps to one env without atomics or cross-lane shuffles. The 8 KB
 // of masks stay in L2 (no LDS copy: more refill waves fit per CU).
+constexpr int kMaskRegs = 16;  // masks per lane held in registers (owner waves <= 1024)
+
 struct Ranking {
   int incl, cnt, total, R;
+  unsigned long long mv[kMaskRegs];  // this lane's masks (waves lane, lane + 64, ...)
 };
-
-constexpr int kMaskRegs = 16;  // masks per lane held in registers (owner waves <= 1024)
 
 __device__ Ranking rank_masks(const Arena& A, int lane) {
   const int nw = A.nwaves();
@@ -652,14 +654,16 @@ __device__ Ranking rank_masks(const Arena& A, int lane) {
   int cnt = 0;
   // fixed trip count and clamped (branch-free) addresses, so all loads are in
   // flight at once before the first wait
-  unsigned long long mv[kMaskRegs];
 #pragma unroll
   for (int i = 0; i < kMaskRegs; ++i) {
     const int w = lane + kWave * i;
-    mv[i] = masks[w < nw ? w : nw - 1];
+    k.mv[i] = masks[w < nw ? w : nw - 1];
   }
 #pragma unroll
-  for (int i = 0; i < kMaskRegs; ++i) cnt += lane + kWave * i < nw ? __popcll(mv[i]) : 0;
+  for (int i = 0; i < kMaskRegs; ++i) {
+    if (lane + kWave * i >= nw) k.mv[i] = 0ull;
+    cnt += __popcll(k.mv[i]);
+  }
   for (int i = kMaskRegs; i < k.R; ++i) {
     const int w = lane + kWave * i;
     cnt += w < nw ? __popcll(masks[w]) : 0;
@@ -679,7 +683,18 @@ __device__ int ranked_env(const Arena& A, const Ranking& k, int rr, int lane) {
   int e = -1;
   for (int i0 = 0; i0 < k.R && e < 0; i0 += kWave) {  // lane q takes L's mask i0 + q
     const int w = L + kWave * (i0 + lane);
-    const unsigned long long v = (i0 + lane < k.R && w < nw) ? masks[w] : 0ull;
+    unsigned long long v = 0ull;
+    if (k.R <= kMaskRegs) {  // lane q <- mask q of lane L, from registers (no reload)
+#pragma unroll
+      for (int i = 0; i < kMaskRegs; ++i) {
+        const unsigned long long mi =
+            ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(k.mv[i] >> 32), L) << 32) |
+            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)k.mv[i], L);
+        if (lane == i) v = mi;
+      }
+    } else if (i0 + lane < k.R && w < nw) {
+      v = masks[w];
+    }
     const int pc = __popcll(v);
     const int ip = wave_incl_scan(pc);
     const int chunk = __builtin_amdgcn_readlane(ip, kWave - 1);
@@ -897,10 +912,12 @@ __global__ void __launch_bounds__(kWave) k_refill(SacenvBoatParams p, Arena A) {
     const int e = ranked_env(A, k, rr, lane);
     const int c = A.i32(U_CONS)[e];
     const int f0 = A.i32(U_FILL)[e];
+    int pos = A.i32(U_MTPOS)[e];  // in flight with cons / fill
     if (c >= f0 && lane == 0) atomicOr(&A.status()[1], SACENV_STATUS_SLOT_UNDERFLOW);
     int f = f0;
     for (; f < c + kSlots; ++f) {
-      const int32_t start_y = draw_knots_wave(p, A, lds, e, lane, nullptr, nullptr);
+      const int32_t start_y = draw_knots_wave(p, A, lds, e, lane, nullptr, nullptr, pos);
+      pos = -1;
       __syncthreads();
       store_draw(p, A, lds, e, f % kSlots, start_y, lane, true);
       __syncthreads();

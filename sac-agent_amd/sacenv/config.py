@@ -135,7 +135,7 @@ def spline_g(n: int) -> np.ndarray:
 
 
 def make_params(cfg: BoatConfig, n_envs: int, *, max_episode_steps: int = 0,
-                autoreset: bool = True, n_helpers: int = 4096, out_flags: int = 0,
+                autoreset: bool = True, n_helpers: int = 8192, out_flags: int = 0,
                 use_wind_table: bool = False) -> _lib.BoatParams:
     cfg.validate()
     p = _lib.BoatParams()

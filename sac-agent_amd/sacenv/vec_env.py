@@ -38,7 +38,7 @@ class VecBoatEnv:
     autoreset : start the next episode inside ``step`` for envs that end
         (gym vector-env semantics: the returned obs row is the new episode's
         first obs, the terminal obs is ``info['final_obs']``). Episodes are
-        pre-drawn up to 32 ahead per env (``_lib.SLOTS``), from the env's own
+        pre-drawn up to 64 ahead per env (``_lib.SLOTS``), from the env's own
         RNG stream in the reference's order, so draws match the reference
         exactly; a refill launch tops the slots up (see ``refill``).
     env_id_offset : global id of this rank's first env (multi-GPU sharding).
@@ -53,7 +53,7 @@ class VecBoatEnv:
     def __init__(self, config=None, num_envs: int = 1, *, seed: int = 0, seeds=None,
                  device=None, max_episode_steps: int = 0, autoreset: bool = True,
                  env_id_offset: int = 0, record_knots: bool = False, record_accel: bool = False,
-                 record_reward64: bool = False, wind_table=None, n_helpers: int = 4096,
+                 record_reward64: bool = False, wind_table=None, n_helpers: int = 8192,
                  auto_refill: bool = True):
         self.lib = _lib.load()
         self.cfg = BoatConfig.from_any(config)
