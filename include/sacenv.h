@@ -115,9 +115,9 @@ typedef struct SacenvBoatLayout {
   int64_t total_bytes;
   int64_t n_pad;
   int64_t s_x, s_y, s_r, v_x, v_y, v_r, rudder, t, ep_reward; /* f64 [n_pad] */
-  int64_t wind_coef;          /* f64 [2 curves][y0 y1 m0 m1][n_pad]: the active episode's spline piece of
+  int64_t wind_coef;          /* f64 [2 curves][y0 m0 y1 m1][n_pad]: the active episode's spline piece of
                                  the interval of the next step's wind sample (a copy of its slot's
-                                 wind_y/wind_m; a new episode starts from (y(0), 0, 0, 0)) */
+                                 wind_knots; a new episode starts from (y(0), 0, 0, 0)) */
   int64_t wind0_next;         /* f64 [2][n_pad] autoreset: the next episode's curve values at grid
                                  index 0 (copy, refreshed in each episode's first step) */
   int64_t start_y_next;       /* i32 [n_pad] autoreset: Boat.s_y_start of the next episode (same) */
@@ -129,9 +129,11 @@ typedef struct SacenvBoatLayout {
   int64_t counters;           /* u32 [5][n_pad] cumulative termination counters */
   int64_t refill_list;        /* i32 [3][n_pad] by refill rank: env, first and end episode number drawn
                                  (sacenv_boat_refill's draw launch -> its fit launch) */
-  int64_t wind_y;             /* f64 [SLOTS][2][n_knots][n_pad] folded knot values per slot, curve */
-  int64_t wind_m;             /* f64 [SLOTS][2][n_knots][n_pad] folded 2nd derivatives / 6 */
-  int64_t knots_raw;          /* f64 [SLOTS][2][n_knots][n_pad] drawn knots (SACENV_OUT_KNOTS) */
+  int64_t wind_knots;         /* f64 [n_pad][SLOTS][2][n_knots][2]: per episode slot and curve, each
+                                 knot's folded value and 2nd derivative / 6 (episode-contiguous:
+                                 the refill writes whole lines) */
+  int64_t knots_raw;          /* f64 [n_pad][SLOTS][2][n_knots] drawn knot values (autoreset refills
+                                 always; init / host resets with SACENV_OUT_KNOTS) */
   int64_t mt_key;             /* u32 [n_pad][624] per-env MT19937 state */
   int64_t record;             /* u8 [50 n_pad]: obs f32 [n_pad][11] | reward f32 [n_pad]
                                  | done u8 [n_pad] | term u8 [n_pad]  (the all-gather payload) */

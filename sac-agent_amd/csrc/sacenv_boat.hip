@@ -85,8 +85,7 @@ __host__ __device__ inline void compute_layout(int n, int nk, int L, int use_tab
   o->counters = U_CNT * np;
   o->refill_list = U_LIST * np;
   const int64_t uw = U_WIND, wk = kWindUnits * nk;
-  o->wind_y = uw * np;
-  o->wind_m = (uw + wk) * np;
+  o->wind_knots = uw * np;
   o->knots_raw = (uw + 2 * wk) * np;
   o->mt_key = (uw + 3 * wk) * np;
   const int64_t ur = uw + 3 * wk + U_MT_BYTES;
@@ -125,8 +124,8 @@ struct Arena {
   __device__ __forceinline__ int32_t* i32(int u) const { return at<int32_t>(u); }
   __device__ __forceinline__ int nwaves() const { return (int)(np / 64); }
   __device__ __forceinline__ int64_t wk() const { return kWindUnits * nk; }
-  __device__ __forceinline__ double* wind_y() const { return at<double>(U_WIND); }
-  __device__ __forceinline__ double* wind_m() const { return at<double>(U_WIND + wk()); }
+  // episode-contiguous slot storage: [env][slot][curve][knot] (+ [y, m] pairs)
+  __device__ __forceinline__ double* wind_knots() const { return at<double>(U_WIND); }
   __device__ __forceinline__ double* knots_raw() const { return at<double>(U_WIND + 2 * wk()); }
   __device__ __forceinline__ uint32_t* mt_key() const { return at<uint32_t>(U_WIND + 3 * wk()); }
   __device__ __forceinline__ int64_t ur() const { return U_WIND + 3 * wk() + U_MT_BYTES; }
@@ -150,9 +149,36 @@ struct Arena {
   __device__ __forceinline__ int32_t* owner_epoch() const { return status() + 64; }
   // refill rank -> [0] env, [1] first and [2] end episode number drawn
   __device__ __forceinline__ int32_t* refill_list(int k) const { return i32(U_LIST + 4 * k); }
-  // slot-major wind coefficient of (slot, curve, knot) for env e
+  // element index of (env, slot, curve, knot) in knots_raw; x2 (+1) in wind_knots
   __device__ __forceinline__ int64_t wix(int slot, int c, int k, int e) const {
+#ifdef SACENV_SLOT_MAJOR  // A/B layout switch (same field sizes): [slot][curve][knot][env]
     return ((int64_t)(slot * 2 + c) * nk + k) * np + e;
+#else
+    return (((int64_t)e * kSlots + slot) * 2 + c) * nk + k;
+#endif
+  }
+  // byte offset of knot k's (y, m) pair: 32-bit (check_params bounds the
+  // region below 4 GiB), so the step's gathers use SGPR base + VGPR offset
+  __device__ __forceinline__ uint32_t wko(int slot, int c, int k, int e) const {
+#ifdef SACENV_SLOT_MAJOR
+    return (((uint32_t)(slot * 2 + c) * (uint32_t)nk + (uint32_t)k) * (uint32_t)np + (uint32_t)e) * 16u;
+#else
+    return ((((uint32_t)e * (uint32_t)kSlots + (uint32_t)slot) * 2u + (uint32_t)c) * (uint32_t)nk + (uint32_t)k) * 16u;
+#endif
+  }
+  // (y, m) of knot k and k+1: 32 contiguous bytes
+  __device__ __forceinline__ void piece(int slot, int c, int k, int e, double (&q)[4]) const {
+    const char* base = reinterpret_cast<const char*>(wind_knots()) + wko(slot, c, k, e);
+#ifdef SACENV_SLOT_MAJOR
+    const uint32_t next = (uint32_t)np * 16u;
+#else
+    const uint32_t next = 16u;
+#endif
+    const double2 a = *reinterpret_cast<const double2*>(base), b = *reinterpret_cast<const double2*>(base + next);
+    q[0] = a.x, q[1] = a.y, q[2] = b.x, q[3] = b.y;  // memory order: y0, m0, y1, m1
+  }
+  __device__ __forceinline__ double wy0(int slot, int c, int e) const {
+    return *reinterpret_cast<const double*>(reinterpret_cast<const char*>(wind_knots()) + wko(slot, c, 0, e));
   }
   // Per-lane accesses as uniform base + 32-bit byte offset: the compiler then
   // uses the SGPR-base addressing mode (no 64-bit address arithmetic in VALU).
@@ -163,16 +189,6 @@ struct Arena {
   }
   __device__ __forceinline__ double& f64e(int u, uint32_t eo) const { return at_e<double>(u, eo); }
   __device__ __forceinline__ int32_t& i32e(int u, uint32_t eo4) const { return at_e<int32_t>(u, eo4); }
-  // byte offset of wind coefficient (slot, curve, knot) of env e inside a wind array
-  __device__ __forceinline__ uint32_t wofs(int slot, int c, int k, int e) const {
-    return ((uint32_t)((slot * 2 + c) * nk + k) * (uint32_t)np + (uint32_t)e) * 8u;
-  }
-  __device__ __forceinline__ double wy_at(uint32_t off) const {
-    return *reinterpret_cast<const double*>(reinterpret_cast<const char*>(wind_y()) + off);
-  }
-  __device__ __forceinline__ double wm_at(uint32_t off) const {
-    return *reinterpret_cast<const double*>(reinterpret_cast<const char*>(wind_m()) + off);
-  }
 };
 
 __host__ inline Arena make_arena(const SacenvBoatParams& p, void* base) {
@@ -246,8 +262,9 @@ __device__ __forceinline__ double spline_piece(double y0, double y1, double m0, 
 __device__ __forceinline__ double curve_env(const SacenvBoatParams& p, const Arena& A, int slot, int c,
                                             int e, int i) {
   const Knot k = knot_coord(p, i);
-  const uint32_t o = A.wofs(slot, c, k.j, e), o1 = o + (uint32_t)A.np * 8u;
-  return spline_piece(A.wy_at(o), A.wy_at(o1), A.wm_at(o), A.wm_at(o1), k.t);
+  double q[4];
+  A.piece(slot, c, k.j, e, q);
+  return spline_piece(q[0], q[2], q[1], q[3], k.t);
 }
 
 __host__ __device__ __forceinline__ int n_curves(int experiment) {
@@ -603,9 +620,7 @@ __device__ void fit_store_wave(const SacenvBoatParams& p, const Arena& A, DrawLd
   mx = c == 0 ? cmx0 : cmx1;
   if (knot_lane) {
     fold_knot(p, c, mn, mx, yv, mv);
-    const int64_t o = A.wix(slot, c, j, e);
-    A.wind_y()[o] = yv;
-    A.wind_m()[o] = mv;
+    *reinterpret_cast<double2*>(A.wind_knots() + 2 * A.wix(slot, c, j, e)) = double2{yv, mv};
   }
   __syncthreads();
 }
@@ -720,11 +735,9 @@ __device__ __forceinline__ Obs fresh_state(const SacenvBoatParams& p, const Aren
   const double s_y = p.experiment == 2 ? (double)start_y : 0.0;  // :166-169
   const int nc = p.use_wind_table ? 0 : n_curves(p.experiment);
   for (int c = 0; c < nc; ++c) {
-    const uint32_t o = A.wofs(slot, c, 0, e), o1 = o + (uint32_t)A.np * 8u;
-    A.f64(U_COEF + 32 * c)[e] = A.wy_at(o);
-    A.f64(U_COEF + 32 * c + 8)[e] = A.wy_at(o1);
-    A.f64(U_COEF + 32 * c + 16)[e] = A.wm_at(o);
-    A.f64(U_COEF + 32 * c + 24)[e] = A.wm_at(o1);
+    double q[4];
+    A.piece(slot, c, 0, e, q);
+    for (int k = 0; k < 4; ++k) A.f64(U_COEF + 32 * c + 8 * k)[e] = q[k];
   }
   A.f64(U_SX)[e] = 0.0;
   A.f64(U_SY)[e] = s_y;
@@ -967,9 +980,7 @@ __device__ void fit_group(const SacenvBoatParams& p, const Arena& A, const doubl
     }
     if (j < nk) {
       fold_knot(p, c, mn, mx, yv, mv);
-      const int64_t o = A.wix(slot, c, j, e);
-      A.wind_y()[o] = yv;
-      A.wind_m()[o] = mv;
+      *reinterpret_cast<double2*>(A.wind_knots() + 2 * A.wix(slot, c, j, e)) = double2{yv, mv};
     }
   }
 }
@@ -1287,14 +1298,15 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   double wv = 0.0, wa = 0.0;
   bool refresh = false;
   int jn = 0;
+  double rq[kCoef];  // refreshed piece (refresh lanes), stored at the end
   if (nc == 0) {
     wind_at(p, A, T.table, 0, e, wi, wv, wa);  // constants or the shared table
   } else {
     const double tt = knot_coord(p, wi).t;
-    const double c0 = spline_piece(cf[0], cf[1], cf[2], cf[3], tt);
+    const double c0 = spline_piece(cf[0], cf[2], cf[1], cf[3], tt);  // cf: y0 m0 y1 m1
     if (p.experiment == 6) {
       wv = c0;
-      wa = spline_piece(cf[4], cf[5], cf[6], cf[7], tt);
+      wa = spline_piece(cf[4], cf[6], cf[5], cf[7], tt);
     } else if (p.experiment == 4) {
       wv = c0;
       wa = p.wind_dir_rad;
@@ -1305,34 +1317,35 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
     const int wn = index + 1 > p.wind_len - 1 ? p.wind_len - 1 : index + 1;
     jn = knot_coord(p, wn).j;
     refresh = index == 0 || jn != knot_coord(p, wi).j;
-    if (refresh) {  // the piece of the next step's interval
+    if (refresh) {  // the piece of the next step's interval, stored at the end
+      // (own registers, read only there: no merge copy that would wait here)
       const int slot = cons % kSlots;
 #pragma unroll
       for (int c = 0; c < 2; ++c)
         if (c < nc) {
-          const uint32_t o = A.wofs(slot, c, jn, e), o1 = o + (uint32_t)A.np * 8u;
-          cf[4 * c] = A.wy_at(o), cf[4 * c + 1] = A.wy_at(o1);
-          cf[4 * c + 2] = A.wm_at(o), cf[4 * c + 3] = A.wm_at(o1);
+          double q[4];
+          A.piece(slot, c, jn, e, q);
+          rq[4 * c] = q[0], rq[4 * c + 1] = q[1], rq[4 * c + 2] = q[2], rq[4 * c + 3] = q[3];
         }
     }
   }
   // autoreset: the next pre-drawn episode's curve values at grid index 0 and
   // start y, read speculatively from their lane-coalesced copies, which a
   // lane refreshes from the slot ring in the first step of each episode
-  double y0n[2] = {0.0, 0.0};
-  int32_t sy_next = 0;
+  double y0c[2] = {0.0, 0.0}, y0g[2];  // copy / gathered (hdr lanes): selected at the end
+  int32_t syc = 0, syg = 0;
   const bool hdr_refresh = p.autoreset && index == 0;
   if (p.autoreset) {
 #pragma unroll
     for (int c = 0; c < 2; ++c)
-      if (c < nc) y0n[c] = A.f64e(U_W0N + 8 * c, eo);
-    if (p.experiment == 2) sy_next = A.i32e(U_SYN, eo4);
+      if (c < nc) y0c[c] = A.f64e(U_W0N + 8 * c, eo);
+    if (p.experiment == 2) syc = A.i32e(U_SYN, eo4);
     if (hdr_refresh) {
       const int ns = (cons + 1) % kSlots;
 #pragma unroll
       for (int c = 0; c < 2; ++c)
-        if (c < nc) y0n[c] = A.wy_at(A.wofs(ns, c, 0, e));
-      if (p.experiment == 2) sy_next = A.i32e(U_STARTY + 4 * ns, eo4);
+        if (c < nc) y0g[c] = A.wy0(ns, c, e);
+      if (p.experiment == 2) syg = A.i32e(U_STARTY + 4 * ns, eo4);
     }
   }
   OWNER_STAMP(st_loaded);
@@ -1445,7 +1458,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   int cons_out = cons;
   Obs fo;  // first obs of the next episode (restarting lanes)
   if (restart) {  // next episode from its pre-drawn slot: a fresh Boat (boat_env.py:152-198)
-    const double sy0 = p.experiment == 2 ? (double)sy_next : 0.0;  // :166-169
+    const double sy0 = p.experiment == 2 ? (double)(hdr_refresh ? syg : syc) : 0.0;  // :166-169
     s_x = 0.0, s_y = sy0, s_r = 0.0, v_x = 0.0, v_y = 0.0, v_r = 0.0, rudder = 0.0;
     t = 0.0, ep = 0.0;  // :122
     index = 0;
@@ -1477,7 +1490,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
 #pragma unroll
     for (int c = 0; c < 2; ++c)
       if (c < nc) {
-        A.f64e(U_COEF + 32 * c, eo) = y0n[c];
+        A.f64e(U_COEF + 32 * c, eo) = hdr_refresh ? y0g[c] : y0c[c];  // (y0, m0, y1, m1) = (y(0), 0, 0, 0)
         A.f64e(U_COEF + 32 * c + 8, eo) = 0.0;
         A.f64e(U_COEF + 32 * c + 16, eo) = 0.0;
         A.f64e(U_COEF + 32 * c + 24, eo) = 0.0;
@@ -1485,13 +1498,13 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   } else if (refresh) {
 #pragma unroll
     for (int k = 0; k < kCoef; ++k)
-      if (k < 4 * nc) A.f64e(U_COEF + 8 * k, eo) = cf[k];
+      if (k < 4 * nc) A.f64e(U_COEF + 8 * k, eo) = rq[k];
   }
   if (hdr_refresh) {
 #pragma unroll
     for (int c = 0; c < 2; ++c)
-      if (c < nc) A.f64e(U_W0N + 8 * c, eo) = y0n[c];
-    if (p.experiment == 2) A.i32e(U_SYN, eo4) = sy_next;
+      if (c < nc) A.f64e(U_W0N + 8 * c, eo) = y0g[c];
+    if (p.experiment == 2) A.i32e(U_SYN, eo4) = syg;
   }
   A.at_e<float>(A.ur() + 44, eo4) = (float)reward;
   A.at_e<uint8_t>(A.ur() + 48, (uint32_t)e) = ended ? 1 : 0;
@@ -1615,10 +1628,9 @@ int check_params(const SacenvBoatParams* p) {
   if (p == nullptr) return SACENV_E_NULL;
   if (p->experiment < 1 || p->experiment > 6) return SACENV_E_EXPERIMENT;
   if (p->n_envs <= 0 || p->n_envs > (1 << 22) || p->wind_len <= 0) return SACENV_E_SIZE;  // 32-bit offsets
-  // per-lane wind offsets (Arena::wofs) are 32-bit: SLOTS x 2 curves x knots rows of n_pad f64
-  if ((int64_t)kWindUnits * (p->n_knots < 2 ? 2 : p->n_knots) * pad64(p->n_envs) >= (1LL << 32))
-    return SACENV_E_SIZE;
   if (n_curves(p->experiment) > 0 && (p->n_knots < 4 || p->n_knots > kMaxK)) return SACENV_E_KNOTS;
+  // 32-bit byte offsets into wind_knots (Arena::wko): n_pad x SLOTS x 2 curves x knots x 16 B
+  if (pad64(p->n_envs) * kSlots * 2 * 16 * (p->n_knots > 1 ? p->n_knots : 1) >= (1LL << 32)) return SACENV_E_SIZE;
   if (p->n_knots < 2 || p->n_knots > kMaxK) return SACENV_E_KNOTS;
   if (n_curves(p->experiment) > 0 && !p->use_wind_table && p->wind_len < 2) return SACENV_E_SIZE;
   if (p->start_y_half < 1) return SACENV_E_RANGE;

@@ -56,7 +56,7 @@ LAYOUT_FIELDS = (
     "total_bytes", "n_pad", "s_x", "s_y", "s_r", "v_x", "v_y", "v_r", "rudder", "t",
     "ep_reward", "wind_coef", "wind0_next", "start_y_next", "index", "cons", "fill", "mt_pos", "start_y", "counters",
     "refill_list",
-    "wind_y", "wind_m", "knots_raw", "mt_key", "record", "obs", "reward", "done", "term",
+    "wind_knots", "knots_raw", "mt_key", "record", "obs", "reward", "done", "term",
     "final_obs", "final_ep_reward", "accel", "reward64", "refill_mask", "status",
     "owner_epoch", "spline_g", "wind_table")
 

@@ -94,9 +94,8 @@ class VecBoatEnv:
         self.mt_pos = view(L.mt_pos, i32, NP)[:N]
         self.start_y_slots = view(L.start_y, i32, _lib.SLOTS, NP)[:, :N]
         self.counters = view(L.counters, i32, _lib.N_COUNTERS, NP)[:, :N]
-        self.wind_y = view(L.wind_y, f64, _lib.SLOTS, 2, nk, NP)
-        self.wind_m = view(L.wind_m, f64, _lib.SLOTS, 2, nk, NP)
-        self.knots_raw_slots = view(L.knots_raw, f64, _lib.SLOTS, 2, nk, NP)
+        self.wind_knots = view(L.wind_knots, f64, NP, _lib.SLOTS, 2, nk, 2)
+        self.knots_raw_slots = view(L.knots_raw, f64, NP, _lib.SLOTS, 2, nk)
         self.mt_key = view(L.mt_key, i32, NP, _lib.MT_N)[:N]
         self.spline_g = view(L.spline_g, f64, nk, nk)
         # outputs: the packed record (the all-gather payload) and extras
@@ -162,9 +161,8 @@ class VecBoatEnv:
     def knots_raw(self) -> torch.Tensor:
         """Knot values [2, n_knots, N] of each env's current episode (record_knots)."""
         slot = (self.cons % _lib.SLOTS).long() if self.autoreset else torch.zeros_like(self.cons).long()
-        k = self.knots_raw_slots[:, :, :, : self.num_envs]            # [3, 2, nk, N]
-        idx = slot.view(1, 1, 1, -1).expand(1, k.shape[1], k.shape[2], -1)
-        return k.gather(0, idx)[0]
+        k = self.knots_raw_slots[: self.num_envs]                     # [N, SLOTS, 2, nk]
+        return k[torch.arange(self.num_envs, device=k.device), slot].permute(1, 2, 0)
 
     # ------------------------------------------------------------------ gym API
     def reset(self, env_ids=None) -> torch.Tensor:

@@ -65,11 +65,11 @@ def test_argument_errors_without_gpu(built_lib):
     assert built_lib.sacenv_boat_refill(ctypes.byref(p), None, None) == -1
     p.autoreset = 0
     assert built_lib.sacenv_boat_refill(ctypes.byref(p), 1, None) == -6
-    # per-lane wind offsets are 32-bit: SLOTS x 2 curves x knots x n_pad f64 < 2**32 bytes
+    # 32-bit byte offsets into wind_knots: n_pad x SLOTS x 2 x knots x 16 B < 2**32
     p.n_knots = 16
-    p.n_envs = 1 << 20
-    assert built_lib.sacenv_boat_step(ctypes.byref(p), 1, 1, None) == -4
     p.n_envs = 1 << 17
+    assert built_lib.sacenv_boat_step(ctypes.byref(p), 1, 1, None) == -4
+    p.n_envs = 1 << 16
     assert built_lib.sacenv_boat_step(ctypes.byref(p), None, None, None) == -1
 
 
@@ -143,7 +143,7 @@ def test_arena_layout(built_lib, n):
     sizes = {"s_x": 8, "s_y": 8, "s_r": 8, "v_x": 8, "v_y": 8, "v_r": 8, "rudder": 8, "t": 8,
              "ep_reward": 8, "wind_coef": 64, "wind0_next": 16, "start_y_next": 4,
              "index": 4, "cons": 4, "fill": 4, "mt_pos": 4,
-             "start_y": 4 * S, "counters": 20, "refill_list": 12, "wind_y": 16 * S * nk, "wind_m": 16 * S * nk,
+             "start_y": 4 * S, "counters": 20, "refill_list": 12, "wind_knots": 32 * S * nk,
              "knots_raw": 16 * S * nk, "mt_key": 2496, "obs": 44, "reward": 4, "done": 1, "term": 1,
              "final_obs": 44, "final_ep_reward": 8, "accel": 24, "reward64": 8}
     spans = sorted((getattr(L, f), getattr(L, f) + w * np_, f) for f, w in sizes.items())
