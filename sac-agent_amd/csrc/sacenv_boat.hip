@@ -5,15 +5,16 @@
 // SoA state. In autoreset mode an env that ends (terminated or truncated)
 // starts its next episode at once from a PRE-DRAWN slot (SLOTS = 65 per env:
 // the active episode + 64 ahead), so no RNG or spline work ever sits on the
-// step's path; each owner wave ORs a 64-bit mask of its ended envs into its
-// own word (plain load/store, no atomics).
-// The refill launches (k_refill + k_refill_fit, at least every 64 steps) ranks the flagged
-// envs from those masks (DPP scans, no atomics) and, one wave per env, draws
+// step's path, and the step keeps no refill bookkeeping beyond the episode
+// counter `cons`.
+// The refill launches (at least every 64 steps): k_need_masks marks the envs
+// whose ring is short (fill < cons + SLOTS); k_refill ranks them from those
+// masks (DPP scans, no atomics) and, one wave per env, draws
 // the replacement episodes from the env's own numpy-legacy MT19937 stream
 // (Boat.__init__ boat_env.py:144-201: randint, then the wind knots,
 // wind.py:69-90), fits the not-a-knot spline, finds its exact grid-sample
 // min/max from the critical points (instead of the reference's 10 000-sample
-// scan, wind.py:80-89) and stores the renormalised, scaled curve
+// scan, wind.py:80-89) and k_refill_fit stores the renormalised, scaled curve
 // (wind.py:86-99). Kept out of the step launch, this work no longer shares
 // SIMDs with the owners (measured: in-step helper waves cost 1.6 us/step).
 //
@@ -103,8 +104,6 @@ __host__ __device__ inline void compute_layout(int n, int nk, int L, int use_tab
   off += align256(8 * nw);
   o->status = off;
   off += 256;
-  o->owner_epoch = off;
-  off += align256(4 * nw);
   o->spline_g = off;
   off += align256(8LL * kMaxK * kMaxK);
   o->wind_table = off;
@@ -142,11 +141,11 @@ struct Arena {
   __device__ __forceinline__ unsigned long long* refill_mask() const {
     return reinterpret_cast<unsigned long long*>(tail());
   }
+
   // [0] refills done, [1] SACENV_STATUS_* bits, [2] envs ranked by the last refill
   __device__ __forceinline__ int32_t* status() const {
     return reinterpret_cast<int32_t*>(tail() + align256(8 * nwaves()));
   }
-  __device__ __forceinline__ int32_t* owner_epoch() const { return status() + 64; }
   // refill rank -> [0] env, [1] first and [2] end episode number drawn
   __device__ __forceinline__ int32_t* refill_list(int k) const { return i32(U_LIST + 4 * k); }
   // element index of (env, slot, curve, knot) in knots_raw; x2 (+1) in wind_knots
@@ -649,7 +648,7 @@ __device__ int32_t draw_episode_wave(const SacenvBoatParams& p, const Arena& A, 
 
 // ---------------------------------------------------------------- refill ranking
 
-// Owner wave w flagged its ended envs in one 64-bit mask. Every refill wave
+// Mask w flags the envs of owner wave w to refill. Every refill wave
 // ranks the flagged envs the same way (lane l owns the masks of waves l,
 // l+64, ...; envs ordered by lane, then mask, then bit) with DPP scans, so
 // rank rr maps to one env without atomics or cross-lane shuffles. The 8 KB
@@ -912,10 +911,13 @@ __global__ void __launch_bounds__(1024) k_compact(const uint8_t* __restrict__ do
 // its slot ring topped up to SLOTS episodes (fill = cons + SLOTS), drawn in
 // the env's order (start y and raw knots), one wave per env (rank h,
 // h + grid, ...). Block 0 counts the refill and publishes the rank count for
-// launch 2, which also clears the masks.
+// launch 2.
 __global__ void __launch_bounds__(kWave) k_refill(SacenvBoatParams p, Arena A) {
   __shared__ RngLds lds;
   const int lane = threadIdx.x;
+#ifdef SACENV_DIAG_NO_REFILL  // timing diagnostics only
+  if (lane >= 0) return;
+#endif
   const Ranking k = rank_masks(A, lane);
   if (blockIdx.x == 0 && lane == 0) {
     A.status()[0] += 1;
@@ -949,8 +951,7 @@ __global__ void __launch_bounds__(kWave) k_refill(SacenvBoatParams p, Arena A) {
 // (env, curve): lane j forms m[j] = (G @ y)[j] and the grid extrema of
 // interval j, the group reduces min/max by shuffles, and lane j folds and
 // stores knot j (the operations of fit_store_wave in the same order:
-// bit-identical coefficients). Grid-stride over the groups; the refill masks
-// launch 1 ranked are cleared here (stream order: launch 1 has read them).
+// bit-identical coefficients). Grid-stride over the groups.
 template <int GS>
 __device__ void fit_group(const SacenvBoatParams& p, const Arena& A, const double* g, int item, int j,
                           int nc) {
@@ -988,7 +989,6 @@ __device__ void fit_group(const SacenvBoatParams& p, const Arena& A, const doubl
 __global__ void __launch_bounds__(kWave) k_refill_fit(SacenvBoatParams p, Arena A, Tail T) {
   __shared__ double g[kMaxK * kMaxK];
   const int lane = threadIdx.x;
-  for (int w = blockIdx.x * kWave + lane; w < A.nwaves(); w += gridDim.x * kWave) A.refill_mask()[w] = 0ull;
   const int nc = p.use_wind_table ? 0 : n_curves(p.experiment);
   const int nk = p.n_knots;
   const int GS = nk > 8 ? 16 : 8;
@@ -1005,6 +1005,17 @@ __global__ void __launch_bounds__(kWave) k_refill_fit(SacenvBoatParams p, Arena 
     else
       fit_group<16>(p, A, g, item, lane & 15, nc);
   }
+}
+
+// sacenv_boat_refill, launch 0: which envs consumed pre-drawn episodes since
+// their ring was last topped up (fill < cons + SLOTS), one 64-bit mask per
+// owner wave. Derived from the episode counters, so the step launch keeps no
+// flags of its own (measured: owner-side flag words cost 0.25-0.4 us/step).
+__global__ void __launch_bounds__(kWave) k_need_masks(SacenvBoatParams p, Arena A) {
+  const int w = blockIdx.x, e = w * kWave + threadIdx.x;
+  const bool need = e < p.n_envs && A.i32(U_FILL)[e] < A.i32(U_CONS)[e] + kSlots;
+  const unsigned long long m = __ballot(need);
+  if (threadIdx.x == 0) A.refill_mask()[w] = m;
 }
 
 // Uniform fp64 constants as VGPR copies: the step reads ~40 config doubles,
@@ -1274,7 +1285,6 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   const int e = ob * kWave + lane;
   const uint32_t eo = (uint32_t)e * 8u, eo4 = (uint32_t)e * 4u;  // per-lane byte offsets
   const bool active = e < p.n_envs;
-  const int kepoch = A.owner_epoch()[ob];
   const float act = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(action) + (active ? eo4 : 0u));
   const bool t_idx = t_from_index(p.dt);
   const int nc = p.use_wind_table ? 0 : n_curves(p.experiment);  // spline curves of the wind
@@ -1317,6 +1327,9 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
     const int wn = index + 1 > p.wind_len - 1 ? p.wind_len - 1 : index + 1;
     jn = knot_coord(p, wn).j;
     refresh = index == 0 || jn != knot_coord(p, wi).j;
+#ifdef SACENV_DIAG_NO_REFRESH  // timing diagnostics only
+    refresh = false;
+#endif
     if (refresh) {  // the piece of the next step's interval, stored at the end
       // (own registers, read only there: no merge copy that would wait here)
       const int slot = cons % kSlots;
@@ -1334,7 +1347,11 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   // lane refreshes from the slot ring in the first step of each episode
   double y0c[2] = {0.0, 0.0}, y0g[2];  // copy / gathered (hdr lanes): selected at the end
   int32_t syc = 0, syg = 0;
+#ifndef SACENV_DIAG_NO_REFRESH
   const bool hdr_refresh = p.autoreset && index == 0;
+#else
+  const bool hdr_refresh = false;
+#endif
   if (p.autoreset) {
 #pragma unroll
     for (int c = 0; c < 2; ++c)
@@ -1477,7 +1494,11 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   // the dynamics' fields went out as they were computed; what is left: the
   // fresh state of restarting envs (same lane, same address: the later store
   // wins), ep_reward, the next wind, and the record
+#ifdef SACENV_DIAG_NO_RESTORE
+  if (false) {
+#else
   if (restart) {
+#endif
     A.f64e(U_SX, eo) = s_x, A.f64e(U_SY, eo) = s_y, A.f64e(U_SR, eo) = s_r;
     A.f64e(U_VX, eo) = v_x, A.f64e(U_VY, eo) = v_y, A.f64e(U_VR, eo) = v_r;
     A.f64e(U_RUD, eo) = rudder;
@@ -1524,7 +1545,11 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   }
   if (false) {
 #else
+#ifdef SACENV_DIAG_NO_FINAL
+  if (false) {
+#else
   if (__ballot(restart) != 0ull) {  // uniform
+#endif
 #endif
     // final_obs block of the wave = this step's obs rows: the terminal obs of
     // every env that ended (main.py:72 reset, boat_env.py:121); other rows of
@@ -1538,15 +1563,6 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   }
   store_obs_block(l.obs, A.obs() + row0, lane);
 
-  if (p.autoreset) {
-    // envs that ended since the last refill, what the next sacenv_boat_refill
-    // draws for: a no-return atomic OR into this wave's word (nothing waits on
-    // it; the refill's fit launch clears the words after its draw launch read them)
-    const unsigned long long m = __ballot(ended);
-    if (lane == 0 && m != 0ull)
-      __hip_atomic_fetch_or(&A.refill_mask()[ob], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  if (lane == 0) A.owner_epoch()[ob] = kepoch + 1;
 #ifdef SACENV_STAMPS
 #ifndef SACENV_STAMPS_LIGHT
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1788,6 +1804,8 @@ int sacenv_boat_refill(const SacenvBoatParams* p, void* arena, void* stream) {
   if (arena == nullptr) return SACENV_E_NULL;
   if (!p->autoreset) return SACENV_E_MODE;
   const Arena A = make_arena(*p, arena);
+  hipLaunchKernelGGL(k_need_masks, dim3((unsigned)(A.np / kWave)), dim3(kWave), 0, (hipStream_t)stream, *p, A);
+  if ((rc = launch_status())) return rc;
   hipLaunchKernelGGL(k_refill, dim3(p->n_helpers), dim3(kWave), 0, (hipStream_t)stream, *p, A);
   if ((rc = launch_status())) return rc;
   const int nw = (int)(A.np / kWave);

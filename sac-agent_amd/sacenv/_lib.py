@@ -58,7 +58,7 @@ LAYOUT_FIELDS = (
     "refill_list",
     "wind_knots", "knots_raw", "mt_key", "record", "obs", "reward", "done", "term",
     "final_obs", "final_ep_reward", "accel", "reward64", "refill_mask", "status",
-    "owner_epoch", "spline_g", "wind_table")
+    "spline_g", "wind_table")
 
 
 class BoatLayout(C.Structure):

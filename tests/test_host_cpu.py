@@ -153,7 +153,7 @@ def test_arena_layout(built_lib, n):
         assert a0 % 64 == 0, f
     assert L.record == L.obs and L.term + np_ == L.record + 50 * np_
     tail = [("refill_mask", 8 * np_ // 64), ("status", 256),
-            ("owner_epoch", 4 * np_ // 64), ("spline_g", 8 * 256), ("wind_table", 16 * 10000)]
+            ("spline_g", 8 * 256), ("wind_table", 16 * 10000)]
     end = spans[-1][1]
     for f, w in tail:
         off = getattr(L, f)

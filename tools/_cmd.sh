@@ -2,7 +2,6 @@ set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?
-echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log
+echo "pytest rc=$rc"; tail -2 gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ]; then exit $rc; fi
-VARIANTS="base prev" bash tools/ab.sh || exit 1
-for v in base prev; do python -c "import json;d=json.load(open('gpurun_out/ab_$v.json'));r=d['roofline'];print('$v step', round(r['step_us_incl_refill'],3), 'kstep', round(r['kernel_avg_us'],3))"; done
+VARIANTS="base norefill" bash tools/ab.sh || exit 1
