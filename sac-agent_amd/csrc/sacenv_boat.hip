@@ -1469,9 +1469,10 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   }
   const bool restart = ended && p.autoreset;
   if (ended) A.at_e<double>(A.ur() + 94, eo) = ep;
-#ifdef SACENV_FINAL_NARROW  // A/B switch: per-lane terminal-obs stores
+  // terminal obs of the envs that auto-reset (main.py:72 reset, boat_env.py:121):
+  // per-lane stores (measured 0.13 us/step cheaper than a 2.8-KB block store per
+  // restarting wave with two extra barriers)
   if (restart) store_obs(A.final_obs() + (int64_t)e * SACENV_OBS_DIM, o);
-#endif
   int cons_out = cons;
   Obs fo;  // first obs of the next episode (restarting lanes)
   if (restart) {  // next episode from its pre-drawn slot: a fresh Boat (boat_env.py:152-198)
@@ -1530,37 +1531,12 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   A.at_e<float>(A.ur() + 44, eo4) = (float)reward;
   A.at_e<uint8_t>(A.ur() + 48, (uint32_t)e) = ended ? 1 : 0;
   A.at_e<uint8_t>(A.ur() + 49, (uint32_t)e) = term;
-  // obs rows through LDS, stored as float4 (64 rows x 44 B = 176 float4)
+  // obs rows through LDS, stored as float4 (64 rows x 44 B = 176 float4); a
+  // restarting env's row is its new episode's first obs
 #pragma unroll
-  for (int k = 0; k < SACENV_OBS_DIM; ++k) l.obs[lane * SACENV_OBS_DIM + k] = o.v[k];
+  for (int k = 0; k < SACENV_OBS_DIM; ++k) l.obs[lane * SACENV_OBS_DIM + k] = restart ? fo.v[k] : o.v[k];
   __syncthreads();
   const int64_t row0 = (int64_t)ob * kWave * SACENV_OBS_DIM;
-#ifdef SACENV_FINAL_NARROW
-  if (__ballot(restart) != 0ull) {
-    __syncthreads();
-    if (restart)
-#pragma unroll
-      for (int k = 0; k < SACENV_OBS_DIM; ++k) l.obs[lane * SACENV_OBS_DIM + k] = fo.v[k];
-    __syncthreads();
-  }
-  if (false) {
-#else
-#ifdef SACENV_DIAG_NO_FINAL
-  if (false) {
-#else
-  if (__ballot(restart) != 0ull) {  // uniform
-#endif
-#endif
-    // final_obs block of the wave = this step's obs rows: the terminal obs of
-    // every env that ended (main.py:72 reset, boat_env.py:121); other rows of
-    // the block carry this step's obs (final_obs is valid where done)
-    store_obs_block(l.obs, A.final_obs() + row0, lane);
-    __syncthreads();
-    if (restart)
-#pragma unroll
-      for (int k = 0; k < SACENV_OBS_DIM; ++k) l.obs[lane * SACENV_OBS_DIM + k] = fo.v[k];
-    __syncthreads();
-  }
   store_obs_block(l.obs, A.obs() + row0, lane);
 
 #ifdef SACENV_STAMPS
