@@ -11,13 +11,13 @@ all-gather over RCCL that pools transitions for a shared replay buffer).
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
 Timing: W untimed steps, then exactly K steps bracketed by barrier +
-synchronize; value = all envs x K / max-over-ranks time. Every 64 steps the
+synchronize; value = all envs x K / max-over-ranks time. Every 128 steps the
 slot refill (k_refill: the RNG draws and spline fits of the episodes that
 replace the ended ones) runs as its own launch INSIDE the timed region. At
-N=1 the 64-step segments are replayed from hipGraphs (launch-bound
+N=1 the 128-step segments are replayed from hipGraphs (launch-bound
 otherwise). Roofline: SURVEY.md §8(d) algorithmic 222 B per boat env-step x
 envs per launch, over k_step's average launch duration from HIP events on
-the kernel's stream around the 64-launch segments of the timed region (the
+the kernel's stream around the 128-launch segments of the timed region (the
 refills in between excluded; they are in ms_per_step); `traffic` = HBM bytes
 per launch from the committed rocprofv3 PMC passes (tools/pmc.sh).
 cpu_baseline: the numpy float64 oracle (oracle/boat_oracle.py, a port of the
@@ -44,8 +44,8 @@ METRIC_MIXED = ("env-steps/sec (whole node), mixed batch boat_env exp-6 + toy_pa
                 "32 768 envs each/GPU")
 HBM_PEAK = 8.0e12             # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 EPISODE_STEPS = 500
-SEG = 64               # step launches per refill (sacenv _lib.REFILL_PERIOD); one graph per segment
-ACTION_STEPS = 512     # the pre-generated action table cycles every 512 steps (8 segments)
+SEG = 128              # step launches per refill (sacenv _lib.REFILL_PERIOD); one graph per segment
+ACTION_STEPS = 512     # the pre-generated action table cycles every 512 steps (4 segments)
 
 
 def parse():
@@ -273,7 +273,7 @@ def main():
     el_max = float(t.item())
 
     # k_step average launch duration from HIP events on the stream the kernel
-    # runs on, around 64-launch graph segments (refills excluded). N=1: the
+    # runs on, around 128-launch graph segments (refills excluded). N=1: the
     # segments of the timed region itself. N>1: the timed region also holds
     # the all-gathers, so k_step-only segments are replayed and timed after it.
     if not use_graph:

@@ -40,8 +40,8 @@ extern "C" {
 #define SACENV_MT_N 624        /* MT19937 words per env (numpy legacy RNG) */
 #define SACENV_MAX_KNOTS 16    /* wind.fixed_points upper bound */
 #define SACENV_N_COUNTERS 5    /* info-dict termination counters, boat_env.py:24-32 */
-#define SACENV_SLOTS 65        /* episode slots per env in autoreset mode (active + 64 ahead) */
-#define SACENV_REFILL_PERIOD 64 /* autoreset: at most this many step launches between refills */
+#define SACENV_SLOTS 129       /* episode slots per env in autoreset mode (active + 128 ahead) */
+#define SACENV_REFILL_PERIOD 128 /* autoreset: at most this many step launches between refills */
 #define SACENV_RECORD_BYTES 50 /* packed per-env step record (see layout.record) */
 
 /* termination codes; 1..5 follow the info-dict key order boat_env.py:24-32,

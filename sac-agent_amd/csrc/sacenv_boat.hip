@@ -3,11 +3,11 @@
 // The step launch (k_step) runs owner waves only: one lane per env, 64
 // consecutive envs per wave, BoatEnv.step (boat_env.py:67-115) on float64
 // SoA state. In autoreset mode an env that ends (terminated or truncated)
-// starts its next episode at once from a PRE-DRAWN slot (SLOTS = 65 per env:
-// the active episode + 64 ahead), so no RNG or spline work ever sits on the
+// starts its next episode at once from a PRE-DRAWN slot (SLOTS = 129 per env:
+// the active episode + 128 ahead), so no RNG or spline work ever sits on the
 // step's path, and the step keeps no refill bookkeeping beyond the episode
 // counter `cons`.
-// The refill launches (at least every 64 steps): k_need_masks marks the envs
+// The refill launches (at least every 128 steps): k_need_masks marks the envs
 // whose ring is short (fill < cons + SLOTS); k_refill ranks them from those
 // masks (DPP scans, no atomics) and, one wave per env, draws
 // the replacement episodes from the env's own numpy-legacy MT19937 stream

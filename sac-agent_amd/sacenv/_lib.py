@@ -16,8 +16,8 @@ OBS_DIM = 11
 MT_N = 624
 MAX_KNOTS = 16
 N_COUNTERS = 5
-SLOTS = 65
-REFILL_PERIOD = 64  # autoreset: step launches allowed between sacenv_boat_refill calls
+SLOTS = 129
+REFILL_PERIOD = 128  # autoreset: step launches allowed between sacenv_boat_refill calls
 STATUS_SLOT_UNDERFLOW = 1
 RECORD_BYTES = 50
 

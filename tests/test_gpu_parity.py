@@ -128,7 +128,7 @@ def test_wind_tables_vs_reference(name, gpu, built_lib):
 def test_rng_draws_bit_exact_across_many_resets(autoreset, gpu, built_lib):
     """Knots/start-y of 150 consecutive Boats per env == numpy RandomState (crosses
     many 624-word MT blocks, incl. windows straddling a block end). In autoreset
-    mode the draws happen up to 64 episodes ahead; the sequence is the same."""
+    mode the draws happen up to 128 episodes ahead; the sequence is the same."""
     from sacenv import VecBoatEnv
     seeds = np.array([0, 5, 99, 2**32 - 1], np.uint64)
     env = VecBoatEnv({"base_settings": {"experiment": 6}}, len(seeds), seeds=seeds, device=gpu,
@@ -167,10 +167,10 @@ def test_spline_g_on_device(gpu, built_lib):
 
 def test_autoreset_every_step_one_step_episodes(gpu, built_lib):
     """|action| > 10.5 breaks the rudder on the first step: every env ends in every
-    launch, the worst case for the slot ring (64 episodes consumed between two
-    refills, then 64 drawn per env by one refill wave). Draws must stay exact."""
+    launch, the worst case for the slot ring (128 episodes consumed between two
+    refills, then 128 drawn per env by one refill wave). Draws must stay exact."""
     from sacenv import VecBoatEnv
-    E, S = 70, 140
+    E, S = 70, 270
     seeds = np.arange(E, dtype=np.uint64) * 7 + 3
     env = VecBoatEnv({"base_settings": {"experiment": 6, "test_mode": 0}}, E, seeds=seeds,
                      device=gpu, autoreset=True, n_helpers=5, record_knots=True)
@@ -191,7 +191,7 @@ def test_autoreset_every_step_one_step_episodes(gpu, built_lib):
 
 
 @pytest.mark.parametrize("period", [1, 7, 32])
-def test_refill_schedule_any_period_up_to_64(period, gpu, built_lib):
+def test_refill_schedule_any_period_up_to_128(period, gpu, built_lib):
     """Refills placed by hand (auto_refill off) every `period` steps, once doubled,
     give the same episodes as the oracle; a ring that runs dry sets the status bit."""
     from sacenv import VecBoatEnv, _lib

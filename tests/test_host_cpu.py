@@ -69,7 +69,7 @@ def test_argument_errors_without_gpu(built_lib):
     p.n_knots = 16
     p.n_envs = 1 << 17
     assert built_lib.sacenv_boat_step(ctypes.byref(p), 1, 1, None) == -4
-    p.n_envs = 1 << 16
+    p.n_envs = 1 << 15
     assert built_lib.sacenv_boat_step(ctypes.byref(p), None, None, None) == -1
 
 
