@@ -117,7 +117,7 @@ typedef struct SacenvBoatLayout {
   int64_t s_x, s_y, s_r, v_x, v_y, v_r, rudder, t, ep_reward; /* f64 [n_pad] */
   int64_t wind_coef;          /* f64 [2 curves][y0 m0 y1 m1][n_pad]: the active episode's spline piece of
                                  the interval of the next step's wind sample (a copy of its slot's
-                                 wind_knots; a new episode starts from (y(0), 0, 0, 0)) */
+                                 wind_knots; a new episode starts with y0 = y(0), exact at t = 0) */
   int64_t wind0_next;         /* f64 [2][n_pad] autoreset: the next episode's curve values at grid
                                  index 0 (copy, refreshed in each episode's first step) */
   int64_t start_y_next;       /* i32 [n_pad] autoreset: Boat.s_y_start of the next episode (same) */

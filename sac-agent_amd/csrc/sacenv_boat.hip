@@ -1298,8 +1298,8 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   // from the lane's copy of its spline piece (wind_coef, loaded with the
   // state). The copy is refreshed from the active slot at the end of a step
   // whose successor enters the next knot interval, and in an episode's first
-  // step (a new episode starts with the degenerate piece (y(0), 0, 0, 0),
-  // exact at t = 0): the few lanes that refresh issue their scattered slot
+  // step (a new episode starts with y0 = y(0) in the piece, exact at t = 0
+  // whatever the other fields hold): the few lanes that refresh issue their scattered slot
   // loads here and store the piece at the end.
   double cf[kCoef];
 #pragma unroll
@@ -1508,15 +1508,11 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
     A.i32e(U_CONS, eo4) = cons_out;
   }
   A.f64e(U_EP, eo) = ep;
-  if (restart && nc > 0) {  // the new episode's degenerate piece: y(0) at t = 0
+  if (restart && nc > 0) {  // the new episode's first wind: the piece's y0 = y(0); at
+    // t = 0 the piece is exactly y0 whatever (finite) m0, y1, m1 it still holds
 #pragma unroll
     for (int c = 0; c < 2; ++c)
-      if (c < nc) {
-        A.f64e(U_COEF + 32 * c, eo) = hdr_refresh ? y0g[c] : y0c[c];  // (y0, m0, y1, m1) = (y(0), 0, 0, 0)
-        A.f64e(U_COEF + 32 * c + 8, eo) = 0.0;
-        A.f64e(U_COEF + 32 * c + 16, eo) = 0.0;
-        A.f64e(U_COEF + 32 * c + 24, eo) = 0.0;
-      }
+      if (c < nc) A.f64e(U_COEF + 32 * c, eo) = hdr_refresh ? y0g[c] : y0c[c];
   } else if (refresh) {
 #pragma unroll
     for (int k = 0; k < kCoef; ++k)
@@ -1574,6 +1570,7 @@ __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, Arena A, Tai
     toy_wave(M.p[1], M.a[1], b - M.nb[0], lane);
   }
 }
+
 
 
 __global__ void __launch_bounds__(kWave) k_toy_init(SacenvToyParams p, ToyArena T, const int32_t* __restrict__ ids,
