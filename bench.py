@@ -66,6 +66,8 @@ def parse():
     ap.add_argument("--mixed-envs", type=int, default=32768, help="envs per type per GPU (--mixed)")
     ap.add_argument("--no-autoreset", action="store_true",
                     help="diagnostic: no in-kernel auto-reset (ended envs keep stepping)")
+    ap.add_argument("--rollout", type=int, default=0,
+                    help="K > 0: open-loop K-step rollouts (sacenv_boat_rollout), a separate line")
     ap.add_argument("--episode-steps", type=int, default=EPISODE_STEPS,
                     help="truncation length (0 = none)")
     return ap.parse_args()
@@ -155,6 +157,76 @@ def load_traffic(n_envs: int, experiment: int):
     return None
 
 
+def bench_rollout(args, env, actions, rank, world, dev):
+    """SURVEY.md §7.6 K-step fused rollout: K steps of an open-loop action sequence per
+    launch (state in registers), every step's record (+ terminal obs) written out."""
+    K = args.rollout
+    if SEG % K:
+        raise SystemExit(f"--rollout K must divide {SEG}")
+    N = env.num_envs
+    recs = torch.empty((K, 50 * env.n_pad), dtype=torch.uint8, device=dev)
+    fin = torch.empty((K, env.n_pad, 11), dtype=torch.float32, device=dev)
+    st = torch.cuda.current_stream(dev)
+    seg_events = []
+
+    def run(n_steps, k, timed=False):
+        done = 0
+        while done < n_steps:
+            if timed:
+                ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                ea.record(st)
+            env.rollout(actions[k % ACTION_STEPS: k % ACTION_STEPS + K], recs, fin)
+            if timed:
+                eb.record(st)
+                seg_events.append((ea, eb))
+            k += K
+            done += K
+            if k % SEG == 0:
+                env.refill()
+        return k
+
+    k = run(args.warmup // SEG * SEG or SEG, 0)
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    steps = max(SEG, args.steps // SEG * SEG)
+    t0 = time.perf_counter()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(st)
+    run(steps, k, timed=True)
+    ev1.record(st)
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device=dev)
+    if world > 1:
+        import torch.distributed as dist
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el_max = float(t.item())
+    kern_s = sum(a.elapsed_time(b) for a, b in seg_events) * 1e-3 / (K * len(seg_events))
+    bytes_env = 4 + 50 + 152 / K
+    if rank == 0:
+        print(json.dumps({
+            "metric": "env-steps/sec (whole node), boat_env exp-6 open-loop K-step rollout, "
+                      "65 536 envs/GPU",
+            "value": world * N * steps / el_max, "unit": "env-steps/s", "n_gpus": world,
+            "steps": steps, "warmup": args.warmup, "ms_per_step": el_max / steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic: U(-1,1) f32 actions, per-env MT19937 wind/start draws",
+            "config": {"workload": f"boat_env exp {args.experiment}, {N} envs/GPU, open-loop actions, "
+                                   f"{K} steps per sacenv_boat_rollout launch, every step's record "
+                                   f"and terminal obs written, refill every {SEG} steps",
+                       "rollout_k": K, "envs_per_gpu": N, "parallelism": f"env-dp{world}"},
+            "roofline": {"bound": "hbm", "achieved": bytes_env * N / kern_s / 1e9, "peak": HBM_PEAK / 1e9,
+                         "unit": "GB/s", "frac": bytes_env * N / kern_s / HBM_PEAK,
+                         "bytes_per_env_step": bytes_env, "kernel": "k_rollout",
+                         "kernel_avg_us_per_step": kern_s * 1e6,
+                         "note": "algorithmic bytes: action 4 + record 50 per step, state r+w 152 per K"},
+            "cpu_baseline": None}), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     rank, world, dev = init_dist(args.gpus)
@@ -210,6 +282,8 @@ def main():
                     dist.all_gather_into_tensor(out, st)
                 gather_done[b].record(gather_stream)
 
+    if args.rollout:
+        return bench_rollout(args, env, actions, rank, world, dev)
     use_graph = world == 1 and not args.no_graph
     graphs = []
 

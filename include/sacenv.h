@@ -205,6 +205,18 @@ int sacenv_boat_reset_explicit(const SacenvBoatParams *p, void *arena, const int
  * work on the step's path); sacenv_boat_refill replaces them. */
 int sacenv_boat_step(const SacenvBoatParams *p, void *arena, const float *action, void *stream);
 
+/* n_steps sacenv_boat_step calls fused into one launch (open-loop action
+ * sequences; SURVEY.md §7.6 K-step rollout): actions is device f32
+ * [n_steps][n_envs]; step k's record (the layout.record format, 50 n_pad
+ * bytes) goes to records + k * 50 n_pad and, when final_obs is not NULL, the
+ * terminal obs of the envs that auto-reset in step k to final_obs +
+ * k * 11 n_pad. The carried state stays in registers between the steps.
+ * Results equal n_steps step calls bit for bit; counts as n_steps step
+ * launches for the refill contract (autoreset: n_steps <= SACENV_REFILL_PERIOD,
+ * with a refill at most SACENV_REFILL_PERIOD launches before the last step). */
+int sacenv_boat_rollout(const SacenvBoatParams *p, void *arena, const float *actions, int32_t n_steps,
+                        void *records, float *final_obs, void *stream);
+
 /* Autoreset mode: draw (RNG, Boat.__init__ boat_env.py:144-201 / Wind
  * wind.py:26-99) and spline-fit the replacement episodes of every env that
  * ended since the previous refill, topping its slot ring up to SLOTS

@@ -1246,7 +1246,10 @@ __host__ __device__ inline bool t_from_index(double dt) {
 // Each dynamics field is stored as soon as it is final, so the write traffic
 // drains while the wave still computes (measured: -0.15 us/step against
 // staging every output for 16-B stores at the end).
-#define EARLY_STORE(u, v) (A.f64e(u, eo) = (v))
+#define EARLY_STORE(u, v)              \
+  do {                                 \
+    if (!kRoll) A.f64e(u, eo) = (v);   \
+  } while (0)
 
 // 64 obs rows (2816 B) from LDS to a 16-B aligned row block: 3 float4 stores
 __device__ __forceinline__ void store_obs_block(const float* lds_rows, float* dst_rows, int lane) {
@@ -1260,9 +1263,14 @@ __device__ __forceinline__ void store_obs_block(const float* lds_rows, float* ds
 }
 
 // One owner wave: BoatEnv.step for 64 consecutive envs, one per lane.
+// kRoll: n_steps steps in one launch (sacenv_boat_rollout) with the state in
+// registers, step k's record to rec + k * 50 n_pad and its terminal obs to
+// fin + k * 11 n_pad; the state is loaded once and stored once.
+template <bool kRoll>
 __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Arena& A, const Tail& T,
                                            const float* __restrict__ action, OwnerLds& l, int ob,
-                                           int lane) {
+                                           int lane, int n_steps = 1, char* roll_rec = nullptr,
+                                           float* roll_fin = nullptr) {
 #ifdef SACENV_STAMPS
   const uint64_t st_real0 = __builtin_amdgcn_s_memrealtime();
   uint64_t st_loaded = 0, st_computed = 0;
@@ -1285,7 +1293,9 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   const int e = ob * kWave + lane;
   const uint32_t eo = (uint32_t)e * 8u, eo4 = (uint32_t)e * 4u;  // per-lane byte offsets
   const bool active = e < p.n_envs;
-  const float act = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(action) + (active ? eo4 : 0u));
+  // the (first) action, in flight with the state loads
+  const char* const abase = reinterpret_cast<const char*>(action) + (active ? eo4 : 0u);
+  float act_cur = *reinterpret_cast<const float*>(abase);
   const bool t_idx = t_from_index(p.dt);
   const int nc = p.use_wind_table ? 0 : n_curves(p.experiment);  // spline curves of the wind
   owner_load(A, l, ob, lane, t_idx, 9 + 4 * nc);
@@ -1293,7 +1303,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   double v_x = l.f[3][lane], v_y = l.f[4][lane], v_r = l.f[5][lane];
   double rudder = l.f[6][lane], t = l.f[7][lane], ep = l.f[8][lane];
   int32_t index = l.idx[lane];
-  const int cons = p.autoreset ? l.cons[lane] : 0;
+  int cons = p.autoreset ? l.cons[lane] : 0;
   // Wind.get_wind(index) (wind.py:20-24, IndexError guard) of this step. Curves:
   // from the lane's copy of its spline piece (wind_coef, loaded with the
   // state). The copy is refreshed from the active slot at the end of a step
@@ -1304,6 +1314,19 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   double cf[kCoef];
 #pragma unroll
   for (int k = 0; k < kCoef; ++k) cf[k] = k < 4 * nc ? l.f[9 + k][lane] : 0.0;
+  // rollout: the next pre-drawn episode's y(0) and start y, carried in registers
+  double y0c[2] = {0.0, 0.0};
+  int32_t syc = 0;
+  if (kRoll && p.autoreset) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+      if (c < nc) y0c[c] = A.f64e(U_W0N + 8 * c, eo);
+    if (p.experiment == 2) syc = A.i32e(U_SYN, eo4);
+  }
+  for (int ks = 0; ks < (kRoll ? n_steps : 1); ++ks) {
+  const float act = act_cur;
+  if (kRoll && ks + 1 < n_steps)  // the next step's action, a step ahead
+    act_cur = *reinterpret_cast<const float*>(abase + (int64_t)(ks + 1) * p.n_envs * 4);
   const int wi = index > p.wind_len - 1 ? p.wind_len - 1 : index;
   double wv = 0.0, wa = 0.0;
   bool refresh = false;
@@ -1343,27 +1366,28 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
     }
   }
   // autoreset: the next pre-drawn episode's curve values at grid index 0 and
-  // start y, read speculatively from their lane-coalesced copies, which a
-  // lane refreshes from the slot ring in the first step of each episode
-  double y0c[2] = {0.0, 0.0}, y0g[2];  // copy / gathered (hdr lanes): selected at the end
-  int32_t syc = 0, syg = 0;
+  // start y. Lanes in an episode's first step gather them from the slot ring
+  // and refresh their lane-coalesced copies; the others read the copies. One
+  // load per lane into one register either way (a select between two loaded
+  // registers would make the branch wait for its load to merge them).
+  double y0n[2];  // (no zero fill: a register write after the other side's load waits for it)
+  int32_t syn = 0;
 #ifndef SACENV_DIAG_NO_REFRESH
   const bool hdr_refresh = p.autoreset && index == 0;
 #else
   const bool hdr_refresh = false;
 #endif
-  if (p.autoreset) {
+  if (hdr_refresh) {
+    const int ns = (cons + 1) % kSlots;
 #pragma unroll
     for (int c = 0; c < 2; ++c)
-      if (c < nc) y0c[c] = A.f64e(U_W0N + 8 * c, eo);
-    if (p.experiment == 2) syc = A.i32e(U_SYN, eo4);
-    if (hdr_refresh) {
-      const int ns = (cons + 1) % kSlots;
+      if (c < nc) y0n[c] = A.wy0(ns, c, e);
+    if (p.experiment == 2) syn = A.i32e(U_STARTY + 4 * ns, eo4);
+  } else if (p.autoreset) {
 #pragma unroll
-      for (int c = 0; c < 2; ++c)
-        if (c < nc) y0g[c] = A.wy0(ns, c, e);
-      if (p.experiment == 2) syg = A.i32e(U_STARTY + 4 * ns, eo4);
-    }
+    for (int c = 0; c < 2; ++c)
+      if (c < nc) y0n[c] = kRoll ? y0c[c] : A.f64e(U_W0N + 8 * c, eo);
+    if (p.experiment == 2) syn = kRoll ? syc : A.i32e(U_SYN, eo4);
   }
   OWNER_STAMP(st_loaded);
   const double r_mx = T.r_mx, r_my = T.r_my, r_iz = T.r_iz, r_nd = T.r_nd, r_w = T.r_w;
@@ -1424,7 +1448,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   EARLY_STORE(U_SR, s_r);
   EARLY_STORE(U_SX, s_x);
   EARLY_STORE(U_SY, s_y);
-  A.i32e(U_IDX, eo4) = index;
+  if (!kRoll) A.i32e(U_IDX, eo4) = index;
 
   Obs o = make_obs(p, oc, s_x, v_x, a_x, s_y, v_y, a_y, s_r, v_r, a_r, rudder, (double)fuel);
 
@@ -1461,6 +1485,10 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   const bool ended = term != SACENV_TERM_NONE;
 
   OWNER_STAMP(st_computed);
+  // this step's outputs: the arena's record, or the rollout's step-ks record
+  char* const R = kRoll ? roll_rec + (int64_t)ks * 50 * A.np : A.b + A.ur() * A.np;
+  float* const fin = kRoll ? (roll_fin != nullptr ? roll_fin + (int64_t)ks * A.np * SACENV_OBS_DIM : nullptr)
+                           : A.final_obs();
   if (p.out_flags & SACENV_OUT_REWARD64) A.at_e<double>(A.ur() + 126, eo) = reward;
   if (p.out_flags & SACENV_OUT_ACCEL) {
     A.at_e<double>(A.ur() + 102, eo) = a_x;
@@ -1472,11 +1500,11 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   // terminal obs of the envs that auto-reset (main.py:72 reset, boat_env.py:121):
   // per-lane stores (measured 0.13 us/step cheaper than a 2.8-KB block store per
   // restarting wave with two extra barriers)
-  if (restart) store_obs(A.final_obs() + (int64_t)e * SACENV_OBS_DIM, o);
+  if (restart && fin != nullptr) store_obs(fin + (int64_t)e * SACENV_OBS_DIM, o);
   int cons_out = cons;
   Obs fo;  // first obs of the next episode (restarting lanes)
   if (restart) {  // next episode from its pre-drawn slot: a fresh Boat (boat_env.py:152-198)
-    const double sy0 = p.experiment == 2 ? (double)(hdr_refresh ? syg : syc) : 0.0;  // :166-169
+    const double sy0 = p.experiment == 2 ? (double)syn : 0.0;  // :166-169
     s_x = 0.0, s_y = sy0, s_r = 0.0, v_x = 0.0, v_y = 0.0, v_r = 0.0, rudder = 0.0;
     t = 0.0, ep = 0.0;  // :122
     index = 0;
@@ -1495,11 +1523,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   // the dynamics' fields went out as they were computed; what is left: the
   // fresh state of restarting envs (same lane, same address: the later store
   // wins), ep_reward, the next wind, and the record
-#ifdef SACENV_DIAG_NO_RESTORE
-  if (false) {
-#else
-  if (restart) {
-#endif
+  if (!kRoll && restart) {
     A.f64e(U_SX, eo) = s_x, A.f64e(U_SY, eo) = s_y, A.f64e(U_SR, eo) = s_r;
     A.f64e(U_VX, eo) = v_x, A.f64e(U_VY, eo) = v_y, A.f64e(U_VR, eo) = v_r;
     A.f64e(U_RUD, eo) = rudder;
@@ -1507,33 +1531,68 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
     A.i32e(U_IDX, eo4) = index;
     A.i32e(U_CONS, eo4) = cons_out;
   }
-  A.f64e(U_EP, eo) = ep;
-  if (restart && nc > 0) {  // the new episode's first wind: the piece's y0 = y(0); at
-    // t = 0 the piece is exactly y0 whatever (finite) m0, y1, m1 it still holds
+  if (!kRoll) {
+    A.f64e(U_EP, eo) = ep;
+    if (restart && nc > 0) {  // the new episode's first wind: the piece's y0 = y(0); at
+      // t = 0 the piece is exactly y0 whatever (finite) m0, y1, m1 it still holds
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
-      if (c < nc) A.f64e(U_COEF + 32 * c, eo) = hdr_refresh ? y0g[c] : y0c[c];
-  } else if (refresh) {
+      for (int c = 0; c < 2; ++c)
+        if (c < nc) A.f64e(U_COEF + 32 * c, eo) = y0n[c];
+    } else if (refresh) {
 #pragma unroll
-    for (int k = 0; k < kCoef; ++k)
-      if (k < 4 * nc) A.f64e(U_COEF + 8 * k, eo) = rq[k];
+      for (int k = 0; k < kCoef; ++k)
+        if (k < 4 * nc) A.f64e(U_COEF + 8 * k, eo) = rq[k];
+    }
+    if (hdr_refresh) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+        if (c < nc) A.f64e(U_W0N + 8 * c, eo) = y0n[c];
+      if (p.experiment == 2) A.i32e(U_SYN, eo4) = syn;
+    }
+  } else {  // the same updates, in registers
+    if (restart) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+        if (c < nc) cf[4 * c] = y0n[c];
+    } else if (refresh) {
+#pragma unroll
+      for (int k = 0; k < kCoef; ++k) cf[k] = rq[k];
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) y0c[c] = y0n[c];
+    syc = syn;
+    cons = cons_out;
   }
-  if (hdr_refresh) {
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-      if (c < nc) A.f64e(U_W0N + 8 * c, eo) = y0g[c];
-    if (p.experiment == 2) A.i32e(U_SYN, eo4) = syg;
-  }
-  A.at_e<float>(A.ur() + 44, eo4) = (float)reward;
-  A.at_e<uint8_t>(A.ur() + 48, (uint32_t)e) = ended ? 1 : 0;
-  A.at_e<uint8_t>(A.ur() + 49, (uint32_t)e) = term;
+  *reinterpret_cast<float*>(R + 44 * A.np + eo4) = (float)reward;
+  *reinterpret_cast<uint8_t*>(R + 48 * A.np + e) = ended ? 1 : 0;
+  *reinterpret_cast<uint8_t*>(R + 49 * A.np + e) = term;
   // obs rows through LDS, stored as float4 (64 rows x 44 B = 176 float4); a
   // restarting env's row is its new episode's first obs
 #pragma unroll
   for (int k = 0; k < SACENV_OBS_DIM; ++k) l.obs[lane * SACENV_OBS_DIM + k] = restart ? fo.v[k] : o.v[k];
   __syncthreads();
   const int64_t row0 = (int64_t)ob * kWave * SACENV_OBS_DIM;
-  store_obs_block(l.obs, A.obs() + row0, lane);
+  store_obs_block(l.obs, reinterpret_cast<float*>(R) + row0, lane);
+  if (kRoll) __syncthreads();  // l.obs is rewritten by the next step
+  }  // steps
+  if (kRoll) {  // the carried state, once
+    A.f64e(U_SX, eo) = s_x, A.f64e(U_SY, eo) = s_y, A.f64e(U_SR, eo) = s_r;
+    A.f64e(U_VX, eo) = v_x, A.f64e(U_VY, eo) = v_y, A.f64e(U_VR, eo) = v_r;
+    A.f64e(U_RUD, eo) = rudder;
+    if (!t_idx) A.f64e(U_T, eo) = t;
+    A.f64e(U_EP, eo) = ep;
+    A.i32e(U_IDX, eo4) = index;
+    if (p.autoreset) A.i32e(U_CONS, eo4) = cons;
+#pragma unroll
+    for (int k = 0; k < kCoef; ++k)
+      if (k < 4 * nc) A.f64e(U_COEF + 8 * k, eo) = cf[k];
+    if (p.autoreset) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+        if (c < nc) A.f64e(U_W0N + 8 * c, eo) = y0c[c];
+      if (p.experiment == 2) A.i32e(U_SYN, eo4) = syc;
+    }
+  }
 
 #ifdef SACENV_STAMPS
 #ifndef SACENV_STAMPS_LIGHT
@@ -1560,7 +1619,7 @@ __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, Arena A, Tai
   const int lane = threadIdx.x;
   int b = (int)blockIdx.x;
   if (!kMixed || b < nb_boat) {
-    owner_wave(vreg_params(p), A, vreg_tail(T), action, slds, b, lane);
+    owner_wave<false>(vreg_params(p), A, vreg_tail(T), action, slds, b, lane);
     return;
   }
   b -= nb_boat;
@@ -1572,6 +1631,15 @@ __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, Arena A, Tai
 }
 
 
+
+// n_steps BoatEnv.step launches fused: open-loop actions
+// [n_steps][n_envs], state in registers between the steps
+__global__ void __launch_bounds__(kWave) k_rollout(SacenvBoatParams p, Arena A, Tail T,
+                                                   const float* __restrict__ action, int n_steps,
+                                                   char* __restrict__ rec, float* __restrict__ fin) {
+  __shared__ OwnerLds slds;
+  owner_wave<true>(vreg_params(p), A, vreg_tail(T), action, slds, blockIdx.x, threadIdx.x, n_steps, rec, fin);
+}
 
 __global__ void __launch_bounds__(kWave) k_toy_init(SacenvToyParams p, ToyArena T, const int32_t* __restrict__ ids,
                                                     int n, int zero_counters) {
@@ -1768,6 +1836,18 @@ int sacenv_boat_step(const SacenvBoatParams* p, void* arena, const float* action
   const int nb_boat = (int)(pad64(p->n_envs) / kWave);
   hipLaunchKernelGGL(k_step<false>, dim3(nb_boat), dim3(kWave), 0, (hipStream_t)stream, *p,
                      make_arena(*p, arena), make_tail(*p, arena), action, nb_boat, MixedToys{});
+  return launch_status();
+}
+
+int sacenv_boat_rollout(const SacenvBoatParams* p, void* arena, const float* actions, int32_t n_steps,
+                        void* records, float* final_obs, void* stream) {
+  int rc = check_params(p);
+  if (rc) return rc;
+  if (arena == nullptr || actions == nullptr || records == nullptr) return SACENV_E_NULL;
+  if (n_steps < 1 || (p->autoreset && n_steps > SACENV_REFILL_PERIOD)) return SACENV_E_SIZE;
+  const int nb_boat = (int)(pad64(p->n_envs) / kWave);
+  hipLaunchKernelGGL(k_rollout, dim3(nb_boat), dim3(kWave), 0, (hipStream_t)stream, *p, make_arena(*p, arena),
+                     make_tail(*p, arena), actions, n_steps, static_cast<char*>(records), final_obs);
   return launch_status();
 }
 

@@ -103,7 +103,7 @@ class ReplayLayout(C.Structure):
 
 EXPORTS = ("sacenv_abi_version", "sacenv_error_string", "sacenv_boat_layout",
            "sacenv_boat_init", "sacenv_boat_reset", "sacenv_boat_reset_explicit",
-           "sacenv_boat_step", "sacenv_boat_refill", "sacenv_boat_wind_eval", "sacenv_toy_layout", "sacenv_toy_init",
+           "sacenv_boat_step", "sacenv_boat_rollout", "sacenv_boat_refill", "sacenv_boat_wind_eval", "sacenv_toy_layout", "sacenv_toy_init",
            "sacenv_toy_reset", "sacenv_toy_step", "sacenv_mixed_step", "sacenv_replay_layout",
            "sacenv_replay_init", "sacenv_replay_store", "sacenv_replay_sample",
            "sacenv_compact_done", "sacenv_boat_reset_list")
@@ -138,6 +138,7 @@ def load(path: str | None = None):
         "sacenv_boat_reset_explicit": (C.c_int, [P, _p, _p, _i32, _p, _p, _p]),
         "sacenv_boat_step": (C.c_int, [P, _p, _p, _p]),
         "sacenv_boat_refill": (C.c_int, [P, _p, _p]),
+        "sacenv_boat_rollout": (C.c_int, [P, _p, _p, _i32, _p, _p, _p]),
         "sacenv_boat_wind_eval": (C.c_int, [P, _p, _p, _p, _i32, _p, _p, _p]),
         "sacenv_toy_layout": (C.c_int, [TP, C.POINTER(ToyLayout)]),
         "sacenv_toy_init": (C.c_int, [TP, _p, _p]),

@@ -216,6 +216,38 @@ class VecBoatEnv:
         _lib.check(self.lib.sacenv_boat_step(self._pp, self._ptr, actions.data_ptr(), self.stream))
         self._after_step()
 
+    def rollout(self, actions, records=None, final_obs=None):
+        """``K`` steps in one launch for an open-loop action sequence ``actions``
+        [K, N] (f32, device): the same results as K ``step`` calls, bit for bit.
+        Returns ``records`` (u8 [K, 50 n_pad], step k's packed record; views via
+        ``record_views``) and ``final_obs`` (f32 [K, n_pad, 11] or None: terminal
+        obs where step k's done is set). The env's own record is not written."""
+        a = torch.as_tensor(actions, device=self.device)
+        if a.dtype != torch.float32:
+            a = a.to(torch.float32)
+        K = int(a.shape[0])
+        a = a.reshape(K, self.num_envs).contiguous()
+        if self.autoreset and K > _lib.REFILL_PERIOD:
+            raise ValueError(f"rollout of more than {_lib.REFILL_PERIOD} steps in autoreset mode")
+        if self.autoreset and self.auto_refill and self._since_refill + K > _lib.REFILL_PERIOD:
+            self.refill()
+        if records is None:
+            records = torch.empty((K, RECORD_BYTES * self.n_pad), dtype=torch.uint8, device=self.device)
+        _lib.check(self.lib.sacenv_boat_rollout(
+            self._pp, self._ptr, a.data_ptr(), K, records.data_ptr(),
+            None if final_obs is None else final_obs.data_ptr(), self.stream))
+        self._keep_roll = a
+        if self.autoreset:
+            self._since_refill += K
+        return records, final_obs
+
+    def record_views(self, rec: torch.Tensor):
+        """(obs [N, 11], reward [N], done [N], term [N]) views of one packed record."""
+        NP, N = self.n_pad, self.num_envs
+        obs = rec[: 44 * NP].view(torch.float32).view(NP, _lib.OBS_DIM)[:N]
+        return (obs, rec[44 * NP: 48 * NP].view(torch.float32)[:N], rec[48 * NP: 49 * NP][:N],
+                rec[49 * NP: 50 * NP][:N])
+
     def _after_step(self) -> None:
         if self.autoreset:
             self._since_refill += 1

@@ -608,6 +608,41 @@ def test_wind_piece_cache_across_intervals_and_episodes(exp, autoreset, gpu, bui
     assert crossed > 0
 
 
+@pytest.mark.parametrize("exp,tmax", [(6, 2500.0), (4, 20.0), (2, 2500.0), (3, 2500.0)])
+def test_rollout_equals_sequential_steps(exp, tmax, gpu, built_lib):
+    """sacenv_boat_rollout (K steps in one launch, state in registers) gives the records,
+    terminal obs, counters and final state of K step() calls bit for bit, through
+    auto-resets, wind-interval crossings (t_max 20: 11 steps per knot interval) and
+    timeouts; then keeps matching across a refill."""
+    from sacenv import VecBoatEnv
+    N, K = 777, 40
+    cfg = {"base_settings": {"experiment": exp, "test_mode": 0, "t_max": tmax},
+           "boat_env": {"track_width": 30}}
+    kw = dict(seed=11, device=gpu, autoreset=True, max_episode_steps=23, n_helpers=64)
+    a_env, b_env = VecBoatEnv(cfg, N, **kw), VecBoatEnv(cfg, N, **kw)
+    g = torch.Generator(device=gpu)
+    g.manual_seed(exp)
+    for rep in range(5):   # 200 steps: crosses a refill (period 128)
+        acts = torch.rand((K, N), generator=g, device=gpu) * 2 - 1
+        acts[:, ::7] *= 12.0   # some rudders break at once
+        fin = torch.zeros((K, a_env.n_pad, 11), dtype=torch.float32, device=gpu)
+        recs, _ = a_env.rollout(acts, final_obs=fin)
+        for k in range(K):
+            o, r, d, info = b_env.step(acts[k])
+            ro, rr, rd, rt = a_env.record_views(recs[k])
+            torch.testing.assert_close(ro, o, rtol=0, atol=0)
+            torch.testing.assert_close(rr, r, rtol=0, atol=0)
+            assert torch.equal(rd, d) and torch.equal(rt, info["term"]), (rep, k)
+            done = d.bool()
+            if done.any():
+                torch.testing.assert_close(fin[k, :N][done], info["final_obs"][done], rtol=0, atol=0)
+        for name in ("s_x", "s_y", "s_r", "v_x", "v_y", "v_r", "rudder", "ep_reward", "index", "cons"):
+            assert torch.equal(getattr(a_env, name), getattr(b_env, name)), (rep, name)
+        assert torch.equal(a_env.counters, b_env.counters)
+    a_env.check_status()
+    b_env.check_status()
+
+
 # ---------------------------------------------------------------- recorder (§8(f) rank 3)
 
 def test_vec_recorder_reproduces_reference_episode_csv(tmp_path, gpu, built_lib):
