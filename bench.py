@@ -252,46 +252,37 @@ def main():
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
     actions = (torch.rand((ACTION_STEPS, N), generator=g, device=dev, dtype=torch.float32) * 2 - 1)
+    pool = None
     if world > 1:
         import torch.distributed as dist
-        # Step k's packed records are copied to a staging buffer and all-gathered on a
-        # side stream while step k+1 runs (the env step needs only the local obs; the
-        # pooled records feed the shared replay buffer). Double-buffered: step k+2
-        # reuses step k's staging buffer after that gather has completed.
-        gather_stream = torch.cuda.Stream(device=dev)
-        stage = [[torch.empty_like(e.record) for e in envs] for _ in range(2)]
-        gathered = [[torch.empty(world * e.record.numel(), dtype=torch.uint8, device=dev)
-                     for e in envs] for _ in range(2)]
-        gather_done = [torch.cuda.Event(), torch.cuda.Event()]
-        for ev in gather_done:
-            ev.record(torch.cuda.current_stream(dev))
+        from sacenv.dist import SegmentPool
+        # Pooling (obs, reward, done, term) for the shared replay buffer: each
+        # step's packed records are copied into row j of a [SEG][record] staging
+        # buffer (graph-captured with the steps) and ONE all-gather per segment
+        # pools them on a side stream while the next segment steps (fewer,
+        # larger collectives: 420 MB per rank at 65 536 envs).
+        pool = SegmentPool(sum(e.record.numel() for e in envs), SEG, dev)
+    pooling = {"on": pool is not None}
 
     def step_eager(k: int):
         stepper(actions[k % ACTION_STEPS])
+        if pooling["on"]:
+            pool.push([e.record for e in envs])  # flushes at the segment's end
         if (k + 1) % SEG == 0:
             refill()
-        if world > 1:
-            b = k % 2
-            cur = torch.cuda.current_stream(dev)
-            cur.wait_event(gather_done[b])
-            for e, st in zip(envs, stage[b]):
-                st.copy_(e.record)
-            gather_stream.wait_stream(cur)
-            with torch.cuda.stream(gather_stream):
-                for st, out in zip(stage[b], gathered[b]):
-                    dist.all_gather_into_tensor(out, st)
-                gather_done[b].record(gather_stream)
 
     if args.rollout:
         return bench_rollout(args, env, actions, rank, world, dev)
-    use_graph = world == 1 and not args.no_graph
+    use_graph = not args.no_graph
     graphs = []
 
-    def capture(k0: int) -> torch.cuda.CUDAGraph:
+    def capture(k0: int, buf: int = -1) -> torch.cuda.CUDAGraph:
         gr = torch.cuda.CUDAGraph()
         with torch.cuda.graph(gr):
-            for k in range(k0, k0 + SEG):
+            for j, k in enumerate(range(k0, k0 + SEG)):
                 stepper(actions[k % ACTION_STEPS])
+                if buf >= 0:
+                    pool.stage_row(j, [e.record for e in envs], buf)
         return gr
 
     if use_graph:
@@ -301,9 +292,13 @@ def main():
             for k in range(3):
                 step_eager(k)
         torch.cuda.current_stream(dev).wait_stream(s)
+        if pool is not None:
+            pool.fill = 0
         refill()
         torch.cuda.synchronize(dev)
-        graphs = [capture(base) for base in range(0, ACTION_STEPS, SEG)]
+        # N>1: one graph per (segment of the action table, staging buffer)
+        graphs = [[capture(base, b) for b in ((0, 1) if world > 1 else (-1,))]
+                  for base in range(0, ACTION_STEPS, SEG)]
 
     st = torch.cuda.current_stream(dev)
     seg_events = []
@@ -313,20 +308,28 @@ def main():
         done = 0
         while done < n_steps:
             if use_graph and k % SEG == 0 and n_steps - done >= SEG:
+                if pooling["on"]:
+                    pool.begin()
                 if timed:
                     ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     ea.record(st)
-                graphs[(k % ACTION_STEPS) // SEG].replay()
+                gset = graphs[(k % ACTION_STEPS) // SEG]
+                gset[pool.buf if pooling["on"] else 0].replay()
                 if timed:
                     eb.record(st)
                     seg_events.append((ea, eb))
                 refill()
+                if pooling["on"]:
+                    pool.fill = SEG
+                    pool.flush()
                 k += SEG
                 done += SEG
             else:
                 step_eager(k)
                 k += 1
                 done += 1
+        if timed and pooling["on"]:
+            pool.flush()  # a partial segment's records are pooled inside the timed region
         return k
 
     k = run(args.warmup, 0)
@@ -336,7 +339,9 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     ev0.record(st)
+    g0 = pool.flushes if pool is not None else 0
     k = run(args.steps, k, timed=True)
+    gathers_timed = (pool.flushes if pool is not None else 0) - g0
     ev1.record(st)
     torch.cuda.synchronize(dev)
     barrier(world)
@@ -350,19 +355,22 @@ def main():
     # runs on, around 128-launch graph segments (refills excluded). N=1: the
     # segments of the timed region itself. N>1: the timed region also holds
     # the all-gathers, so k_step-only segments are replayed and timed after it.
-    if not use_graph:
+    if world > 1 or not use_graph:
         k0 = (k + SEG - 1) // SEG * SEG
         while k < k0:  # align to a segment boundary (refill after the last eager step)
             step_eager(k)
             k += 1
-        graphs = [capture(base) for base in range(0, ACTION_STEPS, SEG)]
+        torch.cuda.synchronize(dev)
+        pooling["on"] = False  # k_step alone: no staging copies, no collective
+        graphs = [[capture(base)] for base in range(0, ACTION_STEPS, SEG)]
         use_graph = True
+        seg_events.clear()
         run(SEG, k)
         torch.cuda.synchronize(dev)
         run(max(SEG, args.kernel_launches // SEG * SEG), k, timed=True)
         torch.cuda.synchronize(dev)
         kern_src = (f"HIP events around {len(seg_events)} graph-replayed {SEG}-launch k_step segments "
-                    "after the timed region (no collective; refills between segments excluded)")
+                    "after the timed region (no staging copy, no collective; refills between segments excluded)")
     else:
         kern_src = (f"HIP events around the {len(seg_events)} graph-replayed {SEG}-launch k_step "
                     "segments of the timed region (refills between segments excluded)")
@@ -398,10 +406,13 @@ def main():
                    "experiment": args.experiment, "envs_per_gpu": per_gpu_envs,
                    "global_envs": world * per_gpu_envs,
                    "episode_steps": EPISODE_STEPS, "parallelism": f"env-dp{world}",
-                   "collective": ("all_gather (obs,reward,done,term) 50 B/env/step, RCCL on a side "
-                                  "stream overlapped with the next step") if world > 1 else None,
-                   "launch": (f"hipGraph segments of {SEG} k_step launches + the 2 refill launches"
-                              if world == 1 and not args.no_graph else "eager"),
+                   "collective": (f"all_gather of the (obs,reward,done,term) records, 50 B/env/step: "
+                                  f"one {'RCCL' if dist.get_backend() == 'nccl' else dist.get_backend()} all_gather per {SEG}-step segment ({gathers_timed} in the "
+                                  "timed region) on a side stream, overlapped with the next segment")
+                   if world > 1 else None,
+                   "launch": (f"hipGraph segments of {SEG} k_step launches" +
+                              (" (+ a record copy into the pooling buffer per step)" if world > 1 else "") +
+                              " + the 2 refill launches" if not args.no_graph else "eager"),
                    "refill": f"k_refill + k_refill_fit every {SEG} steps, inside the timed region" if autoreset else None},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK,

@@ -3,8 +3,9 @@
 Envs are independent (no cross-env term in BoatEnv.step), so each rank owns
 a contiguous block of global env ids [rank*N, (rank+1)*N) and seeds every env
 by its GLOBAL id: results do not depend on the world size. The only
-collective is one all-gather per step of the packed per-env record that the
-step kernel already writes contiguously (VecBoatEnv.record):
+collective is the all-gather of the packed per-env record that the step
+kernel already writes contiguously (VecBoatEnv.record), per step
+(``gather_records``) or per segment of steps (``SegmentPool``):
 
     [ obs f32 N x 11 | reward f32 N | done u8 N | term u8 N ]  = 50 B/env
 
@@ -71,3 +72,93 @@ def gather_records(record: torch.Tensor, out: torch.Tensor | None = None, group=
         chunks = list(out.chunk(world))
         dist.all_gather(chunks, record, group=group)
     return out
+
+
+class SegmentPool:
+    """Pools a segment of steps' records with ONE all-gather.
+
+    Step j of a segment copies the packed record(s) into row j of a staging
+    buffer [seg][record_bytes] (graph-capturable: a device copy); ``flush``
+    all-gathers the filled rows on a side stream, so the next segment steps
+    while xGMI moves this one. Gathered layout: [world][n_steps][record_bytes]
+    (``step_records`` slices it back per step). Two staging buffers alternate;
+    ``begin`` makes the stepping stream wait for the gather that last used the
+    buffer about to be refilled. Fewer, larger collectives than one per step:
+    at 65 536 envs a segment of 128 steps is 420 MB per rank.
+    """
+
+    def __init__(self, record_bytes: int, seg: int, device, group=None, n_buffers: int = 2):
+        import torch.distributed as dist
+        self.rb, self.seg, self.group = int(record_bytes), int(seg), group
+        self.world = dist.get_world_size(group)
+        self.device = torch.device(device)
+        self.stage = [torch.empty(self.seg * self.rb, dtype=torch.uint8, device=self.device)
+                      for _ in range(n_buffers)]
+        self.gathered = [torch.empty(self.world * self.seg * self.rb, dtype=torch.uint8, device=self.device)
+                         for _ in range(n_buffers)]
+        self.cuda = self.device.type == "cuda"
+        self.side = torch.cuda.Stream(device=self.device) if self.cuda else None
+        self.done = [None] * n_buffers
+        self.buf, self.fill, self.flushes = 0, 0, 0
+        self.last = None  # (gathered buffer, n_steps) of the latest flush
+
+    def _cur(self):
+        return torch.cuda.current_stream(self.device) if self.cuda else None
+
+    def begin(self) -> None:
+        """Before writing row 0 of the current buffer: its previous gather is done."""
+        if self.fill == 0 and self.done[self.buf] is not None:
+            self._cur().wait_event(self.done[self.buf])
+
+    def stage_row(self, j: int, records, buf: int | None = None) -> None:
+        """Copy one step's packed record(s) (uint8 tensors, concatenated) into row j."""
+        b = self.buf if buf is None else buf
+        off = j * self.rb
+        for r in records:
+            n = r.numel()
+            self.stage[b][off: off + n].copy_(r)
+            off += n
+        if off != (j + 1) * self.rb:
+            raise ValueError("records do not fill one row")
+
+    def push(self, records) -> None:
+        """Stage the next step (eager use); flushes when the segment is full."""
+        self.begin()
+        self.stage_row(self.fill, records)
+        self.fill += 1
+        if self.fill == self.seg:
+            self.flush()
+
+    def flush(self, n_steps: int | None = None):
+        """All-gather the current buffer's first n_steps rows (default: the filled ones)."""
+        n = self.fill if n_steps is None else int(n_steps)
+        if n == 0:
+            return None
+        b = self.buf
+        src = self.stage[b][: n * self.rb]
+        out = self.gathered[b][: self.world * n * self.rb]
+        if self.cuda:
+            self.side.wait_stream(self._cur())
+            with torch.cuda.stream(self.side):
+                gather_records(src, out, self.group)
+                ev = torch.cuda.Event()
+                ev.record(self.side)
+            self.done[b] = ev
+        else:
+            gather_records(src, out, self.group)
+        self.buf, self.fill = (b + 1) % len(self.stage), 0
+        self.flushes += 1
+        self.last = (out, n)
+        return out
+
+    def wait(self) -> None:
+        """The stepping stream waits for every gather in flight."""
+        if self.cuda:
+            for ev in self.done:
+                if ev is not None:
+                    self._cur().wait_event(ev)
+
+    def step_records(self, gathered: torch.Tensor, n_steps: int, k: int) -> torch.Tensor:
+        """Step k's pooled record [world * record_bytes], rank order (a copy)."""
+        g = gathered.view(self.world, n_steps, self.rb)
+        return g[:, k].reshape(-1).clone()

@@ -97,3 +97,50 @@ def test_record_layout_roundtrip():
     assert torch.equal(o, obs) and d.tolist() == [0, 1, 0, 0, 1] and t.tolist() == [0, 4, 0, 0, 6]
     with pytest.raises(ValueError):
         lay.views(torch.zeros(10, dtype=torch.uint8))
+
+
+def _seg_worker(rank, world, port, seg, q):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "sac-agent_amd"))
+    from sacenv.dist import SegmentPool, gather_records
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rb = 50 * 3
+        pool = SegmentPool(rb, seg, "cpu")
+        rng = np.random.default_rng(rank)
+        per_step, pooled = [], []
+        for k in range(STEPS):
+            rec = torch.from_numpy(rng.integers(0, 256, rb, dtype=np.uint8))
+            per_step.append(gather_records(rec.clone()))
+            pool.push([rec[:100], rec[100:]])  # two record parts fill one row
+            if pool.last is not None:
+                out, n = pool.last
+                pooled += [pool.step_records(out, n, j) for j in range(n)]
+                pool.last = None
+        out = pool.flush()  # the partial last segment
+        if out is not None:
+            n = pool.last[1]
+            pooled += [pool.step_records(out, n, j) for j in range(n)]
+        ok = len(pooled) == STEPS and all(torch.equal(a, b) for a, b in zip(pooled, per_step))
+        q.put((rank, ok, pool.flushes))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,seg", [(2, 8), (2, 7), (3, 16)])
+def test_segment_pool_equals_per_step_gathers(world, seg):
+    """SegmentPool (one all-gather per segment, as bench.py at N>1) pools the
+    same per-step records as one all-gather per step, partial segments too."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_seg_worker, args=(r, world, port, seg, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert all(ok for _, ok, _ in res), res
+    assert all(f == -(-STEPS // seg) for _, _, f in res), res
