@@ -68,6 +68,9 @@ def parse():
                     help="diagnostic: no in-kernel auto-reset (ended envs keep stepping)")
     ap.add_argument("--rollout", type=int, default=0,
                     help="K > 0: open-loop K-step rollouts (sacenv_boat_rollout), a separate line")
+    ap.add_argument("--pooling", choices=("gather", "none"), default="gather",
+                    help="N>1: all-gather the records per 128-step segment (configs[3]), or none "
+                         "(sharded per-GPU replay, SURVEY.md §8(e)'s alternative to measure)")
     ap.add_argument("--episode-steps", type=int, default=EPISODE_STEPS,
                     help="truncation length (0 = none)")
     return ap.parse_args()
@@ -255,6 +258,7 @@ def main():
     pool = None
     if world > 1:
         import torch.distributed as dist
+    if world > 1 and args.pooling == "gather":
         from sacenv.dist import SegmentPool
         # Pooling (obs, reward, done, term) for the shared replay buffer: each
         # step's packed records are copied into row j of a [SEG][record] staging
@@ -409,7 +413,8 @@ def main():
                    "collective": (f"all_gather of the (obs,reward,done,term) records, 50 B/env/step: "
                                   f"one {'RCCL' if dist.get_backend() == 'nccl' else dist.get_backend()} all_gather per {SEG}-step segment ({gathers_timed} in the "
                                   "timed region) on a side stream, overlapped with the next segment")
-                   if world > 1 else None,
+                   if pool is not None else (
+                       "none: sharded per-GPU replay (--pooling none)" if world > 1 else None),
                    "launch": (f"hipGraph segments of {SEG} k_step launches" +
                               (" (+ a record copy into the pooling buffer per step)" if world > 1 else "") +
                               " + the 2 refill launches" if not args.no_graph else "eager"),
