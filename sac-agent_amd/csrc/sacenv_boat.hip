@@ -1188,50 +1188,10 @@ struct MixedToys {
 // next (6 load instructions instead of 13). Outputs are stored per lane as
 // soon as they are final (EARLY_STORE); the obs rows go out through LDS as
 // float4 (64 rows x 44 B = 176 float4).
-constexpr int kF64 = 17;  // s_x s_y s_r v_x v_y v_r rudder t ep_reward | wind_coef[8]
 constexpr int kCoef = 8;  // wind_coef fields: 2 curves x (y0, y1, m0, m1)
 struct OwnerLds {
-  double f[kF64][kWave];
-  int32_t idx[kWave], cons[kWave];
-  float reward[kWave];
-  uint8_t done[kWave], term[kWave];
-  float obs[kWave * SACENV_OBS_DIM];
+  float obs[kWave * SACENV_OBS_DIM];  // the wave's obs rows, stored as float4
 };
-
-
-// wave-wide 16-B gathers of the owner's SoA inputs into LDS: fields 0..nf-1
-// (the state, then the wind piece of nc curves) two fields per instruction,
-// field 16 with index and cons: at most 9 load instructions
-__device__ __forceinline__ void owner_load(const Arena& A, OwnerLds& l, int ob, int lane, bool t_idx, int nf) {
-  const int half = lane >> 5, c = lane & 31;
-  const int64_t e0 = (int64_t)ob * kWave;
-  // uniform row base + 32-bit per-lane offset (field 2q+half, envs e0+2c, e0+2c+1)
-  const char* row = A.b + e0 * 8;
-  const uint32_t lo = (uint32_t)half * 8u * (uint32_t)A.np + (uint32_t)c * 16u;
-  f4v v[9];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const int fi = 2 * q + half;
-    v[q] = f4v{0.f, 0.f, 0.f, 0.f};
-    if (fi < nf && !(fi == 7 && t_idx))  // field 7 = t is derived from the index when exact
-      v[q] = *reinterpret_cast<const f4v*>(row + (int64_t)(16 * q) * A.np + lo);
-  }
-  {  // lanes 0-31: field 16; 32-47: index; 48-63: cons (4 envs per lane)
-    const uint32_t np = (uint32_t)A.np, j = (uint32_t)(lane & 15);
-    const uint32_t off = lane < 32 ? 128u * np + (uint32_t)e0 * 8u + (uint32_t)c * 16u
-                                   : (lane < 48 ? (uint32_t)U_IDX : (uint32_t)U_CONS) * np + (uint32_t)e0 * 4u + j * 16u;
-    v[8] = f4v{0.f, 0.f, 0.f, 0.f};
-    if (lane >= 32 || nf > 16) v[8] = *reinterpret_cast<const f4v*>(A.b + off);
-  }
-#pragma unroll
-  for (int q = 0; q < 8; ++q)
-    if (2 * q < nf) *reinterpret_cast<f4v*>(&l.f[2 * q + half][2 * c]) = v[q];
-  if (lane < 32)
-    *reinterpret_cast<f4v*>(&l.f[16][2 * c]) = v[8];
-  else
-    *reinterpret_cast<f4v*>((lane < 48 ? l.idx : l.cons) + 4 * (lane & 15)) = v[8];
-  __syncthreads();
-}
 
 // t += dt (boat_env.py:69) accumulates exactly when dt = m * 2^e with m < 2^22:
 // every partial sum k*dt (k <= 2^31) is then a double, so t == index * dt
@@ -1298,12 +1258,17 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   float act_cur = *reinterpret_cast<const float*>(abase);
   const bool t_idx = t_from_index(p.dt);
   const int nc = p.use_wind_table ? 0 : n_curves(p.experiment);  // spline curves of the wind
-  owner_load(A, l, ob, lane, t_idx, 9 + 4 * nc);
-  double s_x = l.f[0][lane], s_y = l.f[1][lane], s_r = l.f[2][lane];
-  double v_x = l.f[3][lane], v_y = l.f[4][lane], v_r = l.f[5][lane];
-  double rudder = l.f[6][lane], t = l.f[7][lane], ep = l.f[8][lane];
-  int32_t index = l.idx[lane];
-  int cons = p.autoreset ? l.cons[lane] : 0;
+  // per-lane 8-B loads straight into registers, coalesced over the wave's
+  // 512-B rows; the wind piece and index first, as the wind is evaluated
+  // first (measured 0.16 us/step faster than 16-B loads staged through LDS)
+  int32_t index = A.i32e(U_IDX, eo4);
+  double cf[kCoef];
+#pragma unroll
+  for (int k = 0; k < kCoef; ++k) cf[k] = k < 4 * nc ? A.f64e(U_COEF + 8 * k, eo) : 0.0;
+  double s_x = A.f64e(U_SX, eo), s_y = A.f64e(U_SY, eo), s_r = A.f64e(U_SR, eo);
+  double v_x = A.f64e(U_VX, eo), v_y = A.f64e(U_VY, eo), v_r = A.f64e(U_VR, eo);
+  double rudder = A.f64e(U_RUD, eo), t = t_idx ? 0.0 : A.f64e(U_T, eo), ep = A.f64e(U_EP, eo);
+  int cons = p.autoreset ? A.i32e(U_CONS, eo4) : 0;
   // Wind.get_wind(index) (wind.py:20-24, IndexError guard) of this step. Curves:
   // from the lane's copy of its spline piece (wind_coef, loaded with the
   // state). The copy is refreshed from the active slot at the end of a step
@@ -1311,9 +1276,6 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   // step (a new episode starts with y0 = y(0) in the piece, exact at t = 0
   // whatever the other fields hold): the few lanes that refresh issue their scattered slot
   // loads here and store the piece at the end.
-  double cf[kCoef];
-#pragma unroll
-  for (int k = 0; k < kCoef; ++k) cf[k] = k < 4 * nc ? l.f[9 + k][lane] : 0.0;
   // rollout: the next pre-drawn episode's y(0) and start y, carried in registers
   double y0c[2] = {0.0, 0.0};
   int32_t syc = 0;
