@@ -186,8 +186,15 @@ struct Arena {
   __device__ __forceinline__ T& at_e(int64_t unit, uint32_t off) const {
     return *reinterpret_cast<T*>(b + unit * np + off);
   }
-  __device__ __forceinline__ double& f64e(int u, uint32_t eo) const { return at_e<double>(u, eo); }
-  __device__ __forceinline__ int32_t& i32e(int u, uint32_t eo4) const { return at_e<int32_t>(u, eo4); }
+  // the per-env fields below U_WIND: the whole byte offset in 32 bits (u < 708
+  // and n_pad * 33 024 < 2^32 by check_params), so each access is one VALU add
+  // on the lane offset and an SGPR-base load/store
+  template <class T>
+  __device__ __forceinline__ T& at_s(int u, uint32_t off) const {
+    return *reinterpret_cast<T*>(b + ((uint32_t)u * (uint32_t)np + off));
+  }
+  __device__ __forceinline__ double& f64e(int u, uint32_t eo) const { return at_s<double>(u, eo); }
+  __device__ __forceinline__ int32_t& i32e(int u, uint32_t eo4) const { return at_s<int32_t>(u, eo4); }
 };
 
 __host__ inline Arena make_arena(const SacenvBoatParams& p, void* base) {
@@ -1262,13 +1269,21 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   // 512-B rows; the wind piece and index first, as the wind is evaluated
   // first (measured 0.16 us/step faster than 16-B loads staged through LDS)
   int32_t index = A.i32e(U_IDX, eo4);
+  int cons = p.autoreset ? A.i32e(U_CONS, eo4) : 0;  // (early: the refresh gathers' slot)
   double cf[kCoef];
 #pragma unroll
-  for (int k = 0; k < kCoef; ++k) cf[k] = k < 4 * nc ? A.f64e(U_COEF + 8 * k, eo) : 0.0;
+  for (int k = 0; k < kCoef; ++k) cf[k] = 0.0;
+  if (nc > 0) {  // two uniform branches, not one per field
+#pragma unroll
+    for (int k = 0; k < 4; ++k) cf[k] = A.f64e(U_COEF + 8 * k, eo);
+    if (nc > 1) {
+#pragma unroll
+      for (int k = 4; k < 8; ++k) cf[k] = A.f64e(U_COEF + 8 * k, eo);
+    }
+  }
   double s_x = A.f64e(U_SX, eo), s_y = A.f64e(U_SY, eo), s_r = A.f64e(U_SR, eo);
   double v_x = A.f64e(U_VX, eo), v_y = A.f64e(U_VY, eo), v_r = A.f64e(U_VR, eo);
   double rudder = A.f64e(U_RUD, eo), t = t_idx ? 0.0 : A.f64e(U_T, eo), ep = A.f64e(U_EP, eo);
-  int cons = p.autoreset ? A.i32e(U_CONS, eo4) : 0;
   // Wind.get_wind(index) (wind.py:20-24, IndexError guard) of this step. Curves:
   // from the lane's copy of its spline piece (wind_coef, loaded with the
   // state). The copy is refreshed from the active slot at the end of a step
