@@ -176,6 +176,21 @@ struct Arena {
     const double2 a = *reinterpret_cast<const double2*>(base), b = *reinterpret_cast<const double2*>(base + next);
     q[0] = a.x, q[1] = a.y, q[2] = b.x, q[3] = b.y;  // memory order: y0, m0, y1, m1
   }
+  // piece() for lanes with `use`; the others read the ring's first line (a
+  // fixed address: one cache line per wave), so the load needs no branch
+  __device__ __forceinline__ void piece_if(bool use, int slot, int c, int k, int e, double (&q)[4]) const {
+    const char* base = reinterpret_cast<const char*>(wind_knots()) + (use ? wko(slot, c, k, e) : 0u);
+#ifdef SACENV_SLOT_MAJOR
+    const uint32_t next = (uint32_t)np * 16u;
+#else
+    const uint32_t next = 16u;
+#endif
+    const double2 a = *reinterpret_cast<const double2*>(base), b = *reinterpret_cast<const double2*>(base + next);
+    q[0] = a.x, q[1] = a.y, q[2] = b.x, q[3] = b.y;
+  }
+  __device__ __forceinline__ const double* wy0p(int slot, int c, int e) const {
+    return reinterpret_cast<const double*>(reinterpret_cast<const char*>(wind_knots()) + wko(slot, c, 0, e));
+  }
   __device__ __forceinline__ double wy0(int slot, int c, int e) const {
     return *reinterpret_cast<const double*>(reinterpret_cast<const char*>(wind_knots()) + wko(slot, c, 0, e));
   }
@@ -1233,7 +1248,12 @@ __device__ __forceinline__ void store_obs_block(const float* lds_rows, float* ds
 // kRoll: n_steps steps in one launch (sacenv_boat_rollout) with the state in
 // registers, step k's record to rec + k * 50 n_pad and its terminal obs to
 // fin + k * 11 n_pad; the state is loaded once and stored once.
-template <bool kRoll>
+// kNc: spline curves of the wind (0: constants or the shared table; 1: exp
+// 4/5; 2: exp 6); kTIdx: t derived from the index (t_from_index). Both are
+// launch constants; as template arguments the step carries no code (and no
+// loads whose pending registers the waitcnt pass must respect) of the other
+// wind kinds.
+template <bool kRoll, int kNc, bool kTIdx>
 __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Arena& A, const Tail& T,
                                            const float* __restrict__ action, OwnerLds& l, int ob,
                                            int lane, int n_steps = 1, char* roll_rec = nullptr,
@@ -1263,8 +1283,8 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   // the (first) action, in flight with the state loads
   const char* const abase = reinterpret_cast<const char*>(action) + (active ? eo4 : 0u);
   float act_cur = *reinterpret_cast<const float*>(abase);
-  const bool t_idx = t_from_index(p.dt);
-  const int nc = p.use_wind_table ? 0 : n_curves(p.experiment);  // spline curves of the wind
+  constexpr bool t_idx = kTIdx;
+  constexpr int nc = kNc;  // spline curves of the wind
   // per-lane 8-B loads straight into registers, coalesced over the wave's
   // 512-B rows; the wind piece and index first, as the wind is evaluated
   // first (measured 0.16 us/step faster than 16-B loads staged through LDS)
@@ -1284,6 +1304,10 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   double s_x = A.f64e(U_SX, eo), s_y = A.f64e(U_SY, eo), s_r = A.f64e(U_SR, eo);
   double v_x = A.f64e(U_VX, eo), v_y = A.f64e(U_VY, eo), v_r = A.f64e(U_VR, eo);
   double rudder = A.f64e(U_RUD, eo), t = t_idx ? 0.0 : A.f64e(U_T, eo), ep = A.f64e(U_EP, eo);
+  // keep the whole load burst ahead of the first computation: the scheduler
+  // would otherwise hoist the refresh-address math (index, cons) above the
+  // state loads and wait for those two first
+  __builtin_amdgcn_sched_barrier(0);
   // Wind.get_wind(index) (wind.py:20-24, IndexError guard) of this step. Curves:
   // from the lane's copy of its spline piece (wind_coef, loaded with the
   // state). The copy is refreshed from the active slot at the end of a step
@@ -1314,7 +1338,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   } else {
     const double tt = knot_coord(p, wi).t;
     const double c0 = spline_piece(cf[0], cf[2], cf[1], cf[3], tt);  // cf: y0 m0 y1 m1
-    if (p.experiment == 6) {
+    if (nc == 2) {  // exp 6 (the only two-curve experiment)
       wv = c0;
       wa = spline_piece(cf[4], cf[6], cf[5], cf[7], tt);
     } else if (p.experiment == 4) {
@@ -1330,14 +1354,17 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
 #ifdef SACENV_DIAG_NO_REFRESH  // timing diagnostics only
     refresh = false;
 #endif
-    if (refresh) {  // the piece of the next step's interval, stored at the end
-      // (own registers, read only there: no merge copy that would wait here)
+    {  // the piece of the next step's interval for refreshing lanes, stored at
+      // the end (own registers, read only there). Unconditional loads, the
+      // other lanes reading one fixed line: with no branch around them the
+      // waitcnt pass can count the loads in flight (a load under a divergent
+      // branch made the first use of every earlier load wait for all of them)
       const int slot = cons % kSlots;
 #pragma unroll
       for (int c = 0; c < 2; ++c)
         if (c < nc) {
           double q[4];
-          A.piece(slot, c, jn, e, q);
+          A.piece_if(refresh, slot, c, jn, e, q);
           rq[4 * c] = q[0], rq[4 * c + 1] = q[1], rq[4 * c + 2] = q[2], rq[4 * c + 3] = q[3];
         }
     }
@@ -1345,26 +1372,27 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   // autoreset: the next pre-drawn episode's curve values at grid index 0 and
   // start y. Lanes in an episode's first step gather them from the slot ring
   // and refresh their lane-coalesced copies; the others read the copies. One
-  // load per lane into one register either way (a select between two loaded
-  // registers would make the branch wait for its load to merge them).
-  double y0n[2];  // (no zero fill: a register write after the other side's load waits for it)
+  // unconditional load per value from a per-lane address (no branch: see the
+  // refresh loads above; no select between two loaded registers either).
+  double y0n[2];
   int32_t syn = 0;
 #ifndef SACENV_DIAG_NO_REFRESH
   const bool hdr_refresh = p.autoreset && index == 0;
 #else
   const bool hdr_refresh = false;
 #endif
-  if (hdr_refresh) {
+  {
     const int ns = (cons + 1) % kSlots;
 #pragma unroll
     for (int c = 0; c < 2; ++c)
-      if (c < nc) y0n[c] = A.wy0(ns, c, e);
-    if (p.experiment == 2) syn = A.i32e(U_STARTY + 4 * ns, eo4);
-  } else if (p.autoreset) {
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-      if (c < nc) y0n[c] = kRoll ? y0c[c] : A.f64e(U_W0N + 8 * c, eo);
-    if (p.experiment == 2) syn = kRoll ? syc : A.i32e(U_SYN, eo4);
+      if (c < nc) {
+        const double v = *(hdr_refresh ? A.wy0p(ns, c, e) : &A.f64e(U_W0N + 8 * c, eo));
+        y0n[c] = kRoll && !hdr_refresh ? y0c[c] : v;  // rollout: the copy is in registers
+      }
+    if (nc == 0 && p.experiment == 2) {
+      const int32_t v = *(hdr_refresh ? &A.i32e(U_STARTY + 4 * ns, eo4) : &A.i32e(U_SYN, eo4));
+      syn = kRoll && !hdr_refresh ? syc : v;
+    }
   }
   OWNER_STAMP(st_loaded);
   const double r_mx = T.r_mx, r_my = T.r_my, r_iz = T.r_iz, r_nd = T.r_nd, r_w = T.r_w;
@@ -1588,7 +1616,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
 // The step launch. Grid: nb_boat owner waves, then (kMixed) the waves of
 // each toy arena: heterogeneous workgroups of one launch, selected by
 // uniform block-index ranges.
-template <bool kMixed>
+template <bool kMixed, int kNc, bool kTIdx>
 __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, Arena A, Tail T,
                                                 const float* __restrict__ action, int nb_boat,
                                                 MixedToys M) {
@@ -1596,7 +1624,7 @@ __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, Arena A, Tai
   const int lane = threadIdx.x;
   int b = (int)blockIdx.x;
   if (!kMixed || b < nb_boat) {
-    owner_wave<false>(vreg_params(p), A, vreg_tail(T), action, slds, b, lane);
+    owner_wave<false, kNc, kTIdx>(vreg_params(p), A, vreg_tail(T), action, slds, b, lane);
     return;
   }
   b -= nb_boat;
@@ -1611,11 +1639,12 @@ __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, Arena A, Tai
 
 // n_steps BoatEnv.step launches fused: open-loop actions
 // [n_steps][n_envs], state in registers between the steps
+template <int kNc, bool kTIdx>
 __global__ void __launch_bounds__(kWave) k_rollout(SacenvBoatParams p, Arena A, Tail T,
                                                    const float* __restrict__ action, int n_steps,
                                                    char* __restrict__ rec, float* __restrict__ fin) {
   __shared__ OwnerLds slds;
-  owner_wave<true>(vreg_params(p), A, vreg_tail(T), action, slds, blockIdx.x, threadIdx.x, n_steps, rec, fin);
+  owner_wave<true, kNc, kTIdx>(vreg_params(p), A, vreg_tail(T), action, slds, blockIdx.x, threadIdx.x, n_steps, rec, fin);
 }
 
 __global__ void __launch_bounds__(kWave) k_toy_init(SacenvToyParams p, ToyArena T, const int32_t* __restrict__ ids,
@@ -1806,13 +1835,28 @@ int sacenv_boat_reset_explicit(const SacenvBoatParams* p, void* arena, const int
   return launch_status();
 }
 
+// the step kernels' wind kind and t rule (owner_wave's template arguments)
+static int owner_curves(const SacenvBoatParams& p) { return p.use_wind_table ? 0 : n_curves(p.experiment); }
+#define SACENV_OWNER_DISPATCH(p, LAUNCH)                                  \
+  switch (owner_curves(p) * 2 + (t_from_index((p).dt) ? 1 : 0)) {         \
+    case 0: LAUNCH(0, false); break;                                      \
+    case 1: LAUNCH(0, true); break;                                       \
+    case 2: LAUNCH(1, false); break;                                      \
+    case 3: LAUNCH(1, true); break;                                       \
+    case 4: LAUNCH(2, false); break;                                      \
+    default: LAUNCH(2, true); break;                                      \
+  }
+
 int sacenv_boat_step(const SacenvBoatParams* p, void* arena, const float* action, void* stream) {
   int rc = check_params(p);
   if (rc) return rc;
   if (arena == nullptr || action == nullptr) return SACENV_E_NULL;
   const int nb_boat = (int)(pad64(p->n_envs) / kWave);
-  hipLaunchKernelGGL(k_step<false>, dim3(nb_boat), dim3(kWave), 0, (hipStream_t)stream, *p,
-                     make_arena(*p, arena), make_tail(*p, arena), action, nb_boat, MixedToys{});
+#define SACENV_LAUNCH(NC, TI)                                                                         \
+  hipLaunchKernelGGL((k_step<false, NC, TI>), dim3(nb_boat), dim3(kWave), 0, (hipStream_t)stream, *p, \
+                     make_arena(*p, arena), make_tail(*p, arena), action, nb_boat, MixedToys{})
+  SACENV_OWNER_DISPATCH(*p, SACENV_LAUNCH)
+#undef SACENV_LAUNCH
   return launch_status();
 }
 
@@ -1823,8 +1867,12 @@ int sacenv_boat_rollout(const SacenvBoatParams* p, void* arena, const float* act
   if (arena == nullptr || actions == nullptr || records == nullptr) return SACENV_E_NULL;
   if (n_steps < 1 || (p->autoreset && n_steps > SACENV_REFILL_PERIOD)) return SACENV_E_SIZE;
   const int nb_boat = (int)(pad64(p->n_envs) / kWave);
-  hipLaunchKernelGGL(k_rollout, dim3(nb_boat), dim3(kWave), 0, (hipStream_t)stream, *p, make_arena(*p, arena),
-                     make_tail(*p, arena), actions, n_steps, static_cast<char*>(records), final_obs);
+#define SACENV_LAUNCH(NC, TI)                                                                            \
+  hipLaunchKernelGGL((k_rollout<NC, TI>), dim3(nb_boat), dim3(kWave), 0, (hipStream_t)stream, *p,        \
+                     make_arena(*p, arena), make_tail(*p, arena), actions, n_steps, static_cast<char*>(records), \
+                     final_obs)
+  SACENV_OWNER_DISPATCH(*p, SACENV_LAUNCH)
+#undef SACENV_LAUNCH
   return launch_status();
 }
 
@@ -1913,8 +1961,10 @@ int sacenv_mixed_step(const SacenvBoatParams* bp, void* boat_arena, const float*
     nb += nb_boat;
   }
   if (nb == 0) return SACENV_OK;
-  hipLaunchKernelGGL(k_step<true>, dim3(nb), dim3(kWave), 0, (hipStream_t)stream, p, A, T, boat_action, nb_boat,
-                     M);
+#define SACENV_LAUNCH(NC, TI) \
+  hipLaunchKernelGGL((k_step<true, NC, TI>), dim3(nb), dim3(kWave), 0, (hipStream_t)stream, p, A, T, boat_action, nb_boat, M)
+  SACENV_OWNER_DISPATCH(p, SACENV_LAUNCH)
+#undef SACENV_LAUNCH
   return launch_status();
 }
 
