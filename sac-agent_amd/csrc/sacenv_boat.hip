@@ -1386,8 +1386,10 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
 #pragma unroll
     for (int c = 0; c < 2; ++c)
       if (c < nc) {
-        const double v = *(hdr_refresh ? A.wy0p(ns, c, e) : &A.f64e(U_W0N + 8 * c, eo));
-        y0n[c] = kRoll && !hdr_refresh ? y0c[c] : v;  // rollout: the copy is in registers
+        // (rollout: the copy is in registers; other lanes read the ring's first line)
+        const double v = *(hdr_refresh ? A.wy0p(ns, c, e)
+                                       : (kRoll ? A.wind_knots() : &A.f64e(U_W0N + 8 * c, eo)));
+        y0n[c] = kRoll && !hdr_refresh ? y0c[c] : v;
       }
     if (nc == 0 && p.experiment == 2) {
       const int32_t v = *(hdr_refresh ? &A.i32e(U_STARTY + 4 * ns, eo4) : &A.i32e(U_SYN, eo4));
