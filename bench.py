@@ -417,8 +417,8 @@ def main():
                        "none: sharded per-GPU replay (--pooling none)" if world > 1 else None),
                    "launch": (f"hipGraph segments of {SEG} k_step launches" +
                               (" (+ a record copy into the pooling buffer per step)" if world > 1 else "") +
-                              " + the 2 refill launches" if not args.no_graph else "eager"),
-                   "refill": f"k_refill + k_refill_fit every {SEG} steps, inside the timed region" if autoreset else None},
+                              " + the 3 refill launches" if not args.no_graph else "eager"),
+                   "refill": f"k_need_masks + k_refill + k_refill_fit every {SEG} steps, inside the timed region" if autoreset else None},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK,
                      "traffic": None if traffic is None else traffic["hbm_bytes_per_launch"],
