@@ -125,6 +125,10 @@ def load(path: str | None = None):
         raise SacenvError(
             f"libsacenv.so not found at {p}: build it with `python __graft_entry__.py build` "
             "(hipcc --offload-arch=gfx950). The env has no CPU fallback.")
+    # torch first: it brings its own HIP runtime, and the library must bind to
+    # that same one (loaded before torch, the library's HIP calls found no
+    # device on the MI355X box)
+    import torch  # noqa: F401
     lib = C.CDLL(p)
     P = C.POINTER(BoatParams)
     TP = C.POINTER(ToyParams)

@@ -380,3 +380,14 @@ def test_replay_sampling_algorithm_matches_reference():
         # stream state after the draw: the same words consumed as numpy (both twist lazily)
         assert mt.pos == int(g("pos_after")), c
         assert mt.key == [int(x) for x in g("key_after")], c
+
+
+def test_library_binds_after_torch():
+    """_lib.load() imports torch before the CDLL, so the library binds to torch's HIP
+    runtime (smoke() loads the library before anything imports torch; bound to
+    /opt/rocm's runtime first, its HIP calls found no device on the GPU box)."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, 'sac-agent_amd'); from sacenv import _lib; "
+            "assert 'torch' not in sys.modules; _lib.load(); assert 'torch' in sys.modules")
+    subprocess.run([sys.executable, "-c", code], check=True, cwd=ROOT)
