@@ -282,7 +282,9 @@ def main():
 
     def capture(k0: int, buf: int = -1) -> torch.cuda.CUDAGraph:
         gr = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(gr):
+        # thread_local: a collective library thread querying its events while this
+        # thread captures must not invalidate the capture
+        with torch.cuda.graph(gr, capture_error_mode="thread_local"):
             for j, k in enumerate(range(k0, k0 + SEG)):
                 stepper(actions[k % ACTION_STEPS])
                 if buf >= 0:
