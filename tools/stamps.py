@@ -2,9 +2,8 @@
 
 Builds sac-agent_amd/build/libsacenv_stamps.so (never loaded by the product
 path), runs the bench workload for a few hundred steps and prints, per
-owner wave: load phase (start -> all loads back), compute phase, store phase
-(shader-clock cycles), plus wave start skew and end spread (100 MHz
-realtime ticks -> us). The accel output region carries the stamps in this
+owner wave: load phase (start -> all loads back), compute phase, store phase,
+plus wave start skew and end spread (100 MHz realtime ticks -> us). The accel output region carries the stamps in this
 build, so its values are not accelerations.
 """
 import os
@@ -36,28 +35,22 @@ def main():
     N = int(os.environ.get("STAMP_ENVS", "65536"))
     tm = int(os.environ.get("STAMP_TEST_MODE", "0"))
     env = VecBoatEnv({"base_settings": {"experiment": 6, "test_mode": tm}}, N, device="cuda",
-                     max_episode_steps=int(os.environ.get("STAMP_EPISODE", "500")),
-                     n_helpers=int(os.environ.get("STAMP_HELPERS", "256")))
+                     max_episode_steps=int(os.environ.get("STAMP_EPISODE", "500")))
     env.reset()
     acts = torch.rand(500, N, device="cuda") * 2 - 1
     nw = env.n_pad // 64
     acc_off = env.layout.accel
     raw = env.arena[acc_off: acc_off + nw * 4 * 8].view(torch.float64).view(nw, 4)
-    nh = int(env.params.n_helpers)
-    r64 = env.layout.reward64
-    hraw = env.arena[r64: r64 + 2 * nh * 12 * 8].view(torch.float64).view(2 * nh, 12)
-    rows, hrows = [], []
-    for k in range(300):
+    rows = []
+    for k in range(300):  # (VecBoatEnv refills the slot ring by itself every 128 steps)
         env.step_async(acts[k % 500])
         if k >= 100 and k % 10 == 0:
             torch.cuda.synchronize()
             rows.append(raw.cpu().numpy().copy())
-            hrows.append(hraw.cpu().numpy().copy())
-    r = np.stack(rows)           # [samples, waves, 2]  realtime start/end
-    h = np.stack(hrows)          # [samples, 2 nh, 4]   start/end/items/phase
+    r = np.stack(rows)           # [samples, waves, 4]  realtime start/end, loaded, computed
     t0 = r[..., 0].min(1)
     owner_end = (r[..., 1].max(1) - t0) / 100.0
-    print(f"N={N} owner waves={nw} helpers={nh}x2 test_mode={tm}")
+    print(f"N={N} owner waves={nw} test_mode={tm}")
     print(f"owner span (first owner start -> last owner end) us: median {np.median(owner_end):.2f} "
           f"p90 {np.percentile(owner_end, 90):.2f}")
     light = "LIGHT" in os.environ.get("STAMP_DEFINES", "")
@@ -66,29 +59,6 @@ def main():
         print(f"    owner {nm:16s} us median {np.median(d):6.2f} p90 {np.percentile(d, 90):6.2f}")
     skew = (r[..., 0] - t0[:, None]) / 100.0
     print(f"owner start skew us: median {np.median(skew):.2f} max {skew.max():.2f}")
-    for ph, name in ((0, "phase A (draw)"), (1, "phase B (fit)")):
-        sel = h[:, :, 3] == ph
-        hs = h[:, sel[0]]
-        busy = hs[..., 2] > 0
-        start = (hs[..., 0] - t0[:, None]) / 100.0
-        end = (hs[..., 1] - t0[:, None]) / 100.0
-        last = np.where(busy, end, -1).max(1)
-        print(f"{name}: busy waves/launch median {np.median(busy.sum(1)):.0f}, items max "
-              f"{hs[..., 2].max():.0f}; start median {np.median(start):.2f} us; "
-              f"last busy end median {np.median(last):.2f} p90 {np.percentile(last, 90):.2f} us; "
-              f"busy wave duration median {np.median(np.where(busy, end - start, np.nan)[busy]):.2f} us")
-        names = (() if light else ("epoch", "masks+scan", "rank walk -> e", "pos/key -> knots", "stores/end")
-                 if ph == 0 else ("epoch", "count", "list+raw y", "fit+stores/end"))
-        if not names:
-            continue
-        b = hs[busy]                                   # [items, 12]
-        marks = [b[:, 0]] + [b[:, 4 + i] for i in range(len(names) - 1)] + [b[:, 1]]
-        for i, nm in enumerate(names):
-            d = (marks[i + 1] - marks[i]) / 100.0
-            print(f"    {nm:18s} us median {np.median(d):6.2f} p90 {np.percentile(d, 90):6.2f}")
-    allend = np.maximum(owner_end, ((h[..., 1].max(1)) - t0) / 100.0)
-    print(f"whole launch span median {np.median(allend):.2f} us")
-
 
 if __name__ == "__main__":
     main()
