@@ -608,15 +608,17 @@ def test_wind_piece_cache_across_intervals_and_episodes(exp, autoreset, gpu, bui
     assert crossed > 0
 
 
-@pytest.mark.parametrize("exp,tmax", [(6, 2500.0), (4, 20.0), (2, 2500.0), (3, 2500.0)])
-def test_rollout_equals_sequential_steps(exp, tmax, gpu, built_lib):
+@pytest.mark.parametrize("exp,tmax,dt", [(6, 2500.0, 0.25), (4, 20.0, 0.25), (2, 2500.0, 0.25),
+                                         (3, 2500.0, 0.25), (6, 20.0, 0.1)])
+def test_rollout_equals_sequential_steps(exp, tmax, dt, gpu, built_lib):
     """sacenv_boat_rollout (K steps in one launch, state in registers) gives the records,
     terminal obs, counters and final state of K step() calls bit for bit, through
     auto-resets, wind-interval crossings (t_max 20: 11 steps per knot interval) and
-    timeouts; then keeps matching across a refill."""
+    timeouts; then keeps matching across a refill. Covers every step-kernel instantiation:
+    2, 1 and 0 wind curves, t from the index (dt 0.25) and t carried (dt 0.1)."""
     from sacenv import VecBoatEnv
     N, K = 777, 40
-    cfg = {"base_settings": {"experiment": exp, "test_mode": 0, "t_max": tmax},
+    cfg = {"base_settings": {"experiment": exp, "test_mode": 0, "t_max": tmax, "dt": dt},
            "boat_env": {"track_width": 30}}
     kw = dict(seed=11, device=gpu, autoreset=True, max_episode_steps=23, n_helpers=64)
     a_env, b_env = VecBoatEnv(cfg, N, **kw), VecBoatEnv(cfg, N, **kw)
@@ -636,7 +638,8 @@ def test_rollout_equals_sequential_steps(exp, tmax, gpu, built_lib):
             done = d.bool()
             if done.any():
                 torch.testing.assert_close(fin[k, :N][done], info["final_obs"][done], rtol=0, atol=0)
-        for name in ("s_x", "s_y", "s_r", "v_x", "v_y", "v_r", "rudder", "ep_reward", "index", "cons"):
+        names = ("s_x", "s_y", "s_r", "v_x", "v_y", "v_r", "rudder", "ep_reward", "index", "cons")
+        for name in names + (("t",) if dt == 0.1 else ()):
             assert torch.equal(getattr(a_env, name), getattr(b_env, name)), (rep, name)
         assert torch.equal(a_env.counters, b_env.counters)
     a_env.check_status()
