@@ -1,6 +1,5 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?
-echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log
-exit $rc
+timeout -k 10 900 bash tools/pmc.sh > gpurun_out/pmc_run.log 2>&1 || { tail -30 gpurun_out/pmc_run.log; exit 1; }
+tail -3 gpurun_out/pmc_run.log | cut -c1-300
