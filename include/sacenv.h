@@ -207,7 +207,7 @@ int sacenv_boat_step(const SacenvBoatParams *p, void *arena, const float *action
 
 /* n_steps sacenv_boat_step calls fused into one launch: replaces n_steps
  * calls of BoatEnv.step (environment/boat_env.py:67-115) with known actions,
- * the open-loop loop of main.py:79-81 when the policy is scripted (SURVEY.md
+ * the loop of main.py:70-114 when the actions are known ahead (SURVEY.md
  * §7.6 K-step rollout). actions is device f32
  * [n_steps][n_envs]; step k's record (the layout.record format, 50 n_pad
  * bytes) goes to records + k * 50 n_pad and, when final_obs is not NULL, the
