@@ -334,6 +334,17 @@ int sacenv_replay_init(const SacenvReplayParams *p, void *arena, uint32_t seed, 
 int sacenv_replay_store(const SacenvReplayParams *p, void *arena, int64_t n, const float *state,
                         const float *action, const void *reward, const float *new_state,
                         const float *final_state, const uint8_t *code, void *stream);
+/* store_transition for the n envs of one env step (main.py:81-88): as
+ * sacenv_replay_store, and last_term[i] (u8, caller-owned device array of n,
+ * zero-initialised = info['termination'] == '') carries env i's
+ * info['termination'] across steps and resets like the reference's info dict
+ * (boat_env.py:24-32,84-105,120-126): codes 1..5 overwrite it, 0 and 6
+ * (truncation) keep it, and terminal = (terminal_mask >> last_term[i]) & 1.
+ * last_term == NULL is sacenv_replay_store. */
+int sacenv_replay_store_env(const SacenvReplayParams *p, void *arena, int64_t n, const float *state,
+                            const float *action, const void *reward, const float *new_state,
+                            const float *final_state, const uint8_t *code, uint8_t *last_term,
+                            void *stream);
 /* sample_buffer(batch) (buffer.py:24-35): indices (i64) and the gathered rows.
  * Any output but idx may be NULL. An empty buffer is an error (SACENV_E_SIZE:
  * np.random.choice(0, n) raises) detected on the host from `stored`. */

@@ -93,13 +93,16 @@ __global__ void __launch_bounds__(256) k_rb_store(SacenvReplayParams p, RB r, in
                                                   const void* __restrict__ reward,
                                                   const float* __restrict__ new_state,
                                                   const float* __restrict__ final_state,
-                                                  const uint8_t* __restrict__ code) {
+                                                  const uint8_t* __restrict__ code,
+                                                  uint8_t* __restrict__ last_term) {
   const int64_t M = p.mem_size, c0 = *r.cntr();
   const int64_t first = n > M ? n - M : 0;
   const uint32_t rows = (uint32_t)(n - first);
   const uint32_t base = (uint32_t)((c0 + first) % M);  // ring row of stored row 0
   const uint32_t D = (uint32_t)p.obs_dim, A = (uint32_t)p.act_dim, Mu = (uint32_t)M;
-  const uint32_t nD = rows * D, nA = rows * A, total = nD + nA + rows;
+  const uint32_t nD = rows * D, nA = rows * A, stored = nD + nA + rows;
+  // with last_term, rows a later row overwrites still update their env's byte
+  const uint32_t total = stored + (last_term != nullptr ? (uint32_t)first : 0u);
   for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < total; q += gridDim.x * blockDim.x) {
     if (q < nD) {
       const uint32_t j = q / D, k = q - j * D;
@@ -114,15 +117,26 @@ __global__ void __launch_bounds__(256) k_rb_store(SacenvReplayParams p, RB r, in
       uint32_t row = base + j;
       row = row >= Mu ? row - Mu : row;
       r.action()[(int64_t)row * A + k] = action[(first + j) * (int64_t)A + k];
-    } else {
+    } else if (q < stored) {
       const uint32_t j = q - nD - nA;
       uint32_t row = base + j;
       row = row >= Mu ? row - Mu : row;
       const int64_t i = first + j;
       r.reward()[row] = p.reward_f32 ? (double)static_cast<const float*>(reward)[i]
                                      : static_cast<const double*>(reward)[i];
-      const uint32_t cd = code[i];
+      uint32_t cd = code[i];
+      if (last_term != nullptr) {
+        // main.py:83 tests info['termination'], which only the termination
+        // chain writes (boat_env.py:84-105) and reset never clears (:120-126):
+        // codes 1..5 overwrite env i's last termination, others keep it
+        if (cd >= 1u && cd <= 5u) last_term[i] = (uint8_t)cd;
+        else cd = last_term[i];
+      }
       r.terminal()[row] = (uint8_t)((p.terminal_mask >> (cd < 31 ? cd : 31)) & 1u);
+    } else {
+      const int64_t i = q - stored;  // a row the ring drops: only its env's byte
+      const uint32_t cd = code[i];
+      if (cd >= 1u && cd <= 5u) last_term[i] = (uint8_t)cd;
     }
   }
 }
@@ -242,25 +256,33 @@ int sacenv_replay_init(const SacenvReplayParams* p, void* arena, uint32_t seed, 
   return status();
 }
 
-int sacenv_replay_store(const SacenvReplayParams* p, void* arena, int64_t n, const float* state,
-                        const float* action, const void* reward, const float* new_state,
-                        const float* final_state, const uint8_t* code, void* stream) {
+int sacenv_replay_store_env(const SacenvReplayParams* p, void* arena, int64_t n, const float* state,
+                            const float* action, const void* reward, const float* new_state,
+                            const float* final_state, const uint8_t* code, uint8_t* last_term,
+                            void* stream) {
   int rc = check_replay(p);
   if (rc) return rc;
   if (n < 0) return SACENV_E_SIZE;
   if (n == 0) return SACENV_OK;
   if (!arena || !state || !action || !reward || !new_state || !code) return SACENV_E_NULL;
   const int64_t rows = n > p->mem_size ? p->mem_size : n;
-  const int64_t total = rows * ((int64_t)p->obs_dim + p->act_dim + 1);
+  const int64_t total = rows * ((int64_t)p->obs_dim + p->act_dim + 1) + (last_term ? n - rows : 0);
   if (total >= (1LL << 32)) return SACENV_E_SIZE;  // 32-bit element index per call
   int64_t blocks = (total + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   const RB r = make_rb(*p, arena);
   hipLaunchKernelGGL(k_rb_store, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *p, r, n, state,
-                     action, reward, new_state, final_state, code);
+                     action, reward, new_state, final_state, code, last_term);
   if ((rc = status())) return rc;
   hipLaunchKernelGGL(k_rb_advance, dim3(1), dim3(kWave), 0, (hipStream_t)stream, r, n);
   return status();
+}
+
+int sacenv_replay_store(const SacenvReplayParams* p, void* arena, int64_t n, const float* state,
+                        const float* action, const void* reward, const float* new_state,
+                        const float* final_state, const uint8_t* code, void* stream) {
+  return sacenv_replay_store_env(p, arena, n, state, action, reward, new_state, final_state, code,
+                                 nullptr, stream);
 }
 
 int sacenv_replay_sample(const SacenvReplayParams* p, void* arena, int32_t batch, int64_t stored,

@@ -105,7 +105,7 @@ EXPORTS = ("sacenv_abi_version", "sacenv_error_string", "sacenv_boat_layout",
            "sacenv_boat_init", "sacenv_boat_reset", "sacenv_boat_reset_explicit",
            "sacenv_boat_step", "sacenv_boat_rollout", "sacenv_boat_refill", "sacenv_boat_wind_eval", "sacenv_toy_layout", "sacenv_toy_init",
            "sacenv_toy_reset", "sacenv_toy_step", "sacenv_mixed_step", "sacenv_replay_layout",
-           "sacenv_replay_init", "sacenv_replay_store", "sacenv_replay_sample",
+           "sacenv_replay_init", "sacenv_replay_store", "sacenv_replay_store_env", "sacenv_replay_sample",
            "sacenv_compact_done", "sacenv_boat_reset_list")
 
 _LIB = None
@@ -154,6 +154,7 @@ def load(path: str | None = None):
         "sacenv_replay_layout": (C.c_int, [RP, C.POINTER(ReplayLayout)]),
         "sacenv_replay_init": (C.c_int, [RP, _p, C.c_uint32, _p]),
         "sacenv_replay_store": (C.c_int, [RP, _p, _i64, _p, _p, _p, _p, _p, _p, _p]),
+        "sacenv_replay_store_env": (C.c_int, [RP, _p, _i64, _p, _p, _p, _p, _p, _p, _p, _p]),
         "sacenv_replay_sample": (C.c_int, [RP, _p, _i32, _i64, _p, _p, _p, _p, _p, _p, _p]),
     }
     for name, (res, args) in sig.items():

@@ -11,6 +11,13 @@ kernel already writes contiguously (VecBoatEnv.record), per step
 
 so the gather needs no packing kernel. Over RCCL (backend "nccl") this is
 ``all_gather_into_tensor``; gloo (CPU tests) falls back to list all_gather.
+
+The shared replay buffer consumes whole transitions (s, a, r, s', terminal)
+(main.py:83-88, agent/buffer.py:13-22), so the pooled row of a step is the
+record plus the step's action and the terminal-obs region
+(``TransitionLayout``): for an env that ended (and auto-reset) the record's
+obs is already the NEXT episode's first obs, and s' is ``final_obs``.
+``TransitionStream`` turns consecutive pooled rows back into transitions.
 """
 from __future__ import annotations
 
@@ -58,6 +65,84 @@ class RecordLayout:
         """Global (obs [world*n,11], reward, done, term), in global env-id order."""
         parts = [self.views(gathered[r * self.nbytes:(r + 1) * self.nbytes]) for r in range(world)]
         return tuple(torch.cat([p[i] for p in parts]) for i in range(4))
+
+
+@dataclass(frozen=True)
+class TransitionLayout:
+    """One rank's pooled row for one step: the packed record (n_pad rows, the
+    kernel's layout), the step's action (f32 x n) and the terminal-obs region
+    (f32 x 11 x n_pad; rows valid where done):
+
+        [ record 50 n_pad | action 4 n | final_obs 44 n_pad ]
+    """
+    n: int       # envs per rank
+    n_pad: int   # the arena's padded row count (n rounded up to 64)
+
+    @property
+    def nbytes(self) -> int:
+        return (RECORD_BYTES + 44) * self.n_pad + 4 * self.n
+
+    def parts(self, record: torch.Tensor, action: torch.Tensor, final_obs_bytes: torch.Tensor):
+        """The uint8 tensors that fill one row, in order (``SegmentPool.stage_row``)."""
+        a = action.reshape(-1)
+        if a.dtype != torch.float32 or a.numel() != self.n:
+            raise ValueError("action must be f32 with one value per env")
+        parts = [record, a.view(torch.uint8), final_obs_bytes]
+        if sum(p.numel() for p in parts) != self.nbytes:
+            raise ValueError("record / final_obs regions do not match the layout")
+        return parts
+
+    def views(self, row: torch.Tensor):
+        """(obs [n,11], reward [n], done [n], term [n], action [n], final_obs [n,11])."""
+        n, NP = self.n, self.n_pad
+        if row.dtype != torch.uint8 or row.numel() != self.nbytes:
+            raise ValueError("row must be uint8 of TransitionLayout.nbytes")
+        rec = row[: RECORD_BYTES * NP]
+        obs = rec[: 44 * NP].view(torch.float32).view(NP, 11)[:n]
+        reward = rec[44 * NP: 48 * NP].view(torch.float32)[:n]
+        done, term = rec[48 * NP: 49 * NP][:n], rec[49 * NP: 50 * NP][:n]
+        o = RECORD_BYTES * NP
+        action = row[o: o + 4 * n].view(torch.float32)
+        fin = row[o + 4 * n:].view(torch.float32).view(NP, 11)[:n]
+        return obs, reward, done, term, action, fin
+
+    def pack(self, obs, reward, done, term, action, final_obs) -> torch.Tensor:
+        """Host-side packing (tests, and hosts without the kernel's buffers)."""
+        row = torch.zeros(self.nbytes, dtype=torch.uint8, device=obs.device)
+        o, r, d, t, a, f = self.views(row)
+        o.copy_(obs.to(torch.float32))
+        r.copy_(reward.to(torch.float32))
+        d.copy_(done.to(torch.uint8))
+        t.copy_(term.to(torch.uint8))
+        a.copy_(action.to(torch.float32).reshape(-1))
+        f.copy_(final_obs.to(torch.float32))
+        return row
+
+    def unpack_gathered(self, gathered: torch.Tensor, world: int):
+        """Global (obs, reward, done, term, action, final_obs) in global env-id order."""
+        parts = [self.views(gathered[r * self.nbytes:(r + 1) * self.nbytes]) for r in range(world)]
+        return tuple(torch.cat([p[i] for p in parts]) for i in range(6))
+
+
+class TransitionStream:
+    """Pooled rows of consecutive steps -> (s, a, r, s', code) of every global env.
+
+    ``s`` is the obs the action was taken on: the previous step's pooled obs
+    (for an env that ended last step, already its new episode's first obs), or
+    the reset obs for the first step. ``s'`` is the step's obs, or the terminal
+    obs for envs that ended (done) this step. ``code`` is the term code (the
+    replay buffer derives terminal from it, main.py:83-88)."""
+
+    def __init__(self, layout: TransitionLayout, world: int, reset_obs: torch.Tensor):
+        self.layout, self.world = layout, int(world)
+        self.prev = reset_obs.to(torch.float32).clone()
+
+    def push(self, gathered_row: torch.Tensor):
+        obs, reward, done, term, action, fin = self.layout.unpack_gathered(gathered_row, self.world)
+        s = self.prev
+        s_next = torch.where(done.bool()[:, None], fin, obs)
+        self.prev = obs.clone()
+        return s, action.clone(), reward.clone(), s_next, term.clone()
 
 
 def gather_records(record: torch.Tensor, out: torch.Tensor | None = None, group=None) -> torch.Tensor:

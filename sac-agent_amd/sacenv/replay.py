@@ -5,8 +5,8 @@ Two front ends over one C-ABI arena (libsacenv.so, gfx950):
 * ``DeviceReplayBuffer``: batched and device-resident. ``store_batch`` appends
   the transitions of all envs of a step (one launch). ``store_env_step`` takes a
   ``VecBoatEnv`` step directly: the new_state of an env that auto-reset is its
-  terminal obs (``info['final_obs']``), and terminal = reached_goal
-  (main.py:83-88). ``sample`` returns device tensors. Sampling follows
+  terminal obs (``info['final_obs']``), and terminal = the env's last
+  termination is reached_goal (main.py:83-88, with the info dict's persistence). ``sample`` returns device tensors. Sampling follows
   ``np.random.choice`` on the buffer's own MT19937 stream, seeded like
   ``np.random.seed(seed)``.
 * ``ReplayBuffer``: the drop-in for ``agent.buffer.ReplayBuffer``. It has the
@@ -62,6 +62,7 @@ class DeviceReplayBuffer:
         self.mt_key = view(L.mt_key, torch.int32, _lib.MT_N)
         self.mt_pos = view(L.mt_pos, torch.int32, 1)
         self.mem_cntr = 0                        # host mirror (buffer.py:6)
+        self._last_term = {}                     # id(env) -> u8 [num_envs] info['termination'] codes
         _lib.check(self.lib.sacenv_replay_init(self._pp, self.arena.data_ptr(), int(seed) & 0xFFFFFFFF,
                                                self.stream))
 
@@ -73,10 +74,13 @@ class DeviceReplayBuffer:
         t = torch.as_tensor(x, device=self.device)
         return t.to(dtype).contiguous() if t.dtype != dtype else t.contiguous()
 
-    def store_batch(self, state, action, reward, new_state, code, final_state=None) -> None:
+    def store_batch(self, state, action, reward, new_state, code, final_state=None,
+                    last_term=None) -> None:
         """Append n transitions (rows in order, buffer.py:13-22). ``code`` is u8:
         terminal = (terminal_mask >> code) & 1; rows with code != 0 take new_state
-        from ``final_state`` if it is given."""
+        from ``final_state`` if it is given. ``last_term`` (u8 [n] device tensor, in/out):
+        row i's terminal follows env i's persistent last termination instead
+        (``sacenv_replay_store_env``; see ``store_env_step``)."""
         s = self._dev(state, torch.float32)
         n = s.shape[0]
         a = self._dev(action, torch.float32).reshape(n, -1)
@@ -86,16 +90,38 @@ class DeviceReplayBuffer:
         fs = None if final_state is None else self._dev(final_state, torch.float32)
         if a.shape[1] != self.n_actions or s.shape != ns.shape:
             raise ValueError("transition shapes do not match the buffer")
-        _lib.check(self.lib.sacenv_replay_store(
+        lt = None
+        if last_term is not None:
+            lt = last_term
+            if (lt.dtype != torch.uint8 or lt.device != self.device or lt.numel() != n
+                    or not lt.is_contiguous()):
+                raise ValueError("last_term must be a contiguous u8 device tensor with one byte per row")
+        _lib.check(self.lib.sacenv_replay_store_env(
             self._pp, self.arena.data_ptr(), n, s.data_ptr(), a.data_ptr(), r.data_ptr(), ns.data_ptr(),
-            None if fs is None else fs.data_ptr(), c.data_ptr(), self.stream))
+            None if fs is None else fs.data_ptr(), c.data_ptr(), None if lt is None else lt.data_ptr(),
+            self.stream))
         self._keep = (s, a, r, ns, c, fs)
         self.mem_cntr += n
 
-    def store_env_step(self, prev_obs, actions, env) -> None:
+    def store_env_step(self, prev_obs, actions, env, reference_terminal: bool = True) -> None:
         """The transitions of one ``VecBoatEnv.step``: (prev_obs, actions, reward,
-        obs or final_obs for envs that ended, term code)."""
-        self.store_batch(prev_obs, actions, env.reward, env.obs, env.term, final_state=env.final_obs)
+        obs or final_obs for envs that ended, terminal).
+
+        ``reference_terminal`` (default, parity with main.py:83-88): terminal is
+        ``info['termination'] == 'reached_goal'``, where ``info['termination']``
+        is the env's LAST termination -- the reference's info dict keeps it
+        across steps and resets (boat_env.py:24-32,120-126), so after a goal
+        episode every transition is stored terminal until another ending
+        overwrites it. The buffer keeps that byte per env. ``False``: terminal
+        only on the step that reached the goal (the evident intent)."""
+        last = None
+        if reference_terminal:
+            last = self._last_term.get(id(env))
+            if last is None or last.numel() != env.num_envs:
+                last = torch.zeros(env.num_envs, dtype=torch.uint8, device=self.device)
+                self._last_term[id(env)] = last
+        self.store_batch(prev_obs, actions, env.reward, env.obs, env.term, final_state=env.final_obs,
+                         last_term=last)
 
     def sample(self, batch_size: int):
         """sample_buffer (buffer.py:24-35) on device: (states, actions, rewards, states_, dones, idx)."""

@@ -113,6 +113,7 @@ class VecToyEnv:
         self.done = view(L.done, torch.uint8, NP)[:N]
         self.term = view(L.term, torch.uint8, NP)[:N]
         self.final_obs = view(L.final_obs, torch.float32, NP, 2)[:N]
+        self.final_obs_bytes = self.arena[L.final_obs: L.final_obs + 8 * NP]
         # gym-style metadata: open-loop envs take no action
         self.action_space = Box(low=0, high=0, shape=(0,), dtype=np.float32)
         self.observation_space = Box(low=-np.inf, high=np.inf, shape=(2,), dtype=np.float32)

@@ -105,6 +105,8 @@ class VecBoatEnv:
         self.done = view(L.done, torch.uint8, NP)[:N]
         self.term = view(L.term, torch.uint8, NP)[:N]
         self.final_obs = view(L.final_obs, torch.float32, NP, _lib.OBS_DIM)[:N]
+        # the terminal-obs region as raw bytes (n_pad rows): a pooled transition's s'
+        self.final_obs_bytes = self.arena[L.final_obs: L.final_obs + 4 * _lib.OBS_DIM * NP]
         self.final_ep_reward = view(L.final_ep_reward, f64, NP)[:N]
         self.accel = view(L.accel, f64, 3, NP)[:, :N]
         self.reward64 = view(L.reward64, f64, NP)[:N]

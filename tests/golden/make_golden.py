@@ -24,6 +24,12 @@ Fixture kinds
     The reference ``ReplayBuffer`` (``agent/buffer.py:3-35``): stored
     transitions, then ``sample_buffer`` under a seeded global numpy stream
     (batches and the RNG state after sampling), at several fill levels.
+``main_loop_goal.npz``
+    ``main.py:70-91``'s loop around the reference ``BoatEnv`` and ``ReplayBuffer``:
+    the transitions it stores, with ``terminal = info['termination'] ==
+    'reached_goal'`` (``main.py:83-88``). ``info['termination']`` persists
+    across steps and resets (``boat_env.py:24-32,120-126``), so after a goal
+    episode later steps are stored terminal until another ending overwrites it.
 ``recorded_exp<k>.npz``
     The reference's own recorded runs under
     ``ressources/settings_visualized/experiment_setting_<k>/`` converted from
@@ -260,8 +266,53 @@ def run_replay():
     print(f"{path}: {list(cases)}")
 
 
+def run_main_loop(n_steps=700, seeds=SEEDS, action_seed=21):
+    """main.py:70-91 with a reference ReplayBuffer: what the loop stores."""
+    be = H.boat_env_module()
+    from agent.buffer import ReplayBuffer  # reference module
+    cfg = H.load_config({"base_settings": {"experiment": 6, "test_mode": 0},
+                         "boat_env": {"goal_line": 100, "track_width": 30}})
+    E, S = len(seeds), n_steps
+    actions = np.random.default_rng(action_seed).uniform(-1.0, 1.0, (E, S)).astype(np.float32)
+    out = {k: [] for k in ("state", "new_state", "action", "reward", "terminal", "term", "done")}
+    for e, seed in enumerate(seeds):
+        np.random.seed(int(seed))
+        env = be.BoatEnv(cfg, types.SimpleNamespace(experiment_dir=tempfile.mkdtemp()))
+        rb = ReplayBuffer(S, (11,), 1)
+        observation = env.reset()
+        terms, dones = [], []
+        for k in range(S):
+            action = np.array([float(actions[e, k])], dtype=np.float64)
+            observation_, reward, done, info = env.step(action)
+            rb.store_transition(observation, action, reward, observation_,
+                                info["termination"] == "reached_goal")     # main.py:83-88
+            terms.append(TERM_CODES[info["termination"]] if done else 0)
+            dones.append(bool(done))
+            observation = env.reset() if done else observation_          # main.py:72
+        out["state"].append(rb.state_memory)
+        out["new_state"].append(rb.new_state_memory)
+        out["action"].append(rb.action_memory)
+        out["reward"].append(rb.reward_memory)
+        out["terminal"].append(rb.terminal_memory)
+        out["term"].append(terms)
+        out["done"].append(dones)
+    flat = {k: np.asarray(v) for k, v in out.items()}
+    flat["term"] = flat["term"].astype(np.uint8)
+    flat["done"] = flat["done"].astype(np.uint8)
+    flat["seeds"], flat["actions"] = np.asarray(seeds, np.uint64), actions
+    flat.update(_cfg_vector(cfg))
+    path = os.path.join(HERE, "main_loop_goal.npz")
+    np.savez_compressed(path, **flat)
+    t = flat["term"]
+    print(f"{path}: E={E} S={S} terms={np.bincount(t.ravel(), minlength=6).tolist()} "
+          f"terminal={int(flat['terminal'].sum())} goal_steps={int((t == 1).sum())}")
+
+
 def main():
     import sys
+    if sys.argv[1:] == ["main_loop"]:
+        run_main_loop()
+        return
     if sys.argv[1:] == ["toys"]:
         run_toys()
         return
@@ -270,6 +321,7 @@ def main():
         return
     run_toys()
     run_replay()
+    run_main_loop()
     for exp in range(1, 7):
         run_seeded(f"exp{exp}_uniform", {"base_settings": {"experiment": exp, "test_mode": 0}},
                    400, "uniform", action_seed=100 + exp)

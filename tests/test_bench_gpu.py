@@ -1,0 +1,39 @@
+"""The driver's exact round-end bench command on the GPU (round 1 died on it).
+
+Runs ``python bench.py --gpus 1 --steps 20 --warmup 5`` as a child process
+(with a 1-second CPU-baseline budget) and checks the JSON line: rc 0, whole
+segments executed, ``roofline`` and ``cpu_baseline`` present, and the timed
+steps fit in the wall time of the run.
+"""
+import json
+import os
+import subprocess
+import sys
+import time
+
+import pytest
+
+from conftest import ROOT
+
+
+@pytest.mark.gpu
+def test_driver_bench_command():
+    t0 = time.perf_counter()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "20",
+                        "--warmup", "5", "--cpu-seconds", "1"],
+                       capture_output=True, text=True, timeout=600, cwd=ROOT)
+    wall = time.perf_counter() - t0
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+    d = json.loads(line)
+    assert d["steps"] == 128 and d["warmup"] == 128 and d["n_gpus"] == 1
+    assert d["value"] > 0 and d["unit"] == "env-steps/s"
+    assert d["ms_per_step"] * d["steps"] * 1e-3 <= wall
+    rf = d["roofline"]
+    assert rf["bound"] == "hbm" and 0 < rf["frac"] < 1 and rf["kernel_avg_us"] > 0
+    # the timed step includes its refill: never faster than the kernel alone
+    assert rf["step_us_incl_refill"] >= rf["kernel_avg_us"]
+    cb = d["cpu_baseline"]
+    assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] == "port" and cb["one_core"] > 0
+    with open(os.path.join(ROOT, "BASELINE.json")) as f:
+        assert d["metric"] == json.load(f)["metric"]

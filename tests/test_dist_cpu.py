@@ -144,3 +144,84 @@ def test_segment_pool_equals_per_step_gathers(world, seg):
         assert p.exitcode == 0
     assert all(ok for _, ok, _ in res), res
     assert all(f == -(-STEPS // seg) for _, _, f in res), res
+
+
+def _transition_worker(rank, world, port, seg, q):
+    import sys
+    for p in (os.path.join(ROOT, "sac-agent_amd"), os.path.join(ROOT, "oracle")):
+        sys.path.insert(0, p)
+    from boat_oracle import OracleConfig, OracleVecBoat
+    from sacenv.dist import SegmentPool, TransitionLayout, TransitionStream, shard
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        off, n = shard(rank, world, N_PER_RANK)
+        seeds = np.arange(off, off + n, dtype=np.uint64) + 100
+        # a short track and truncation: envs end (OOB, rudder, truncation) every few steps
+        ora = OracleVecBoat(OracleConfig(experiment=6, track_width=60.0), seeds, max_episode_steps=9)
+        reset_obs = torch.from_numpy(ora.reset()).to(torch.float32)
+        lay = TransitionLayout(n, 64)     # the kernel pads rows to 64
+        pool = SegmentPool(lay.nbytes, seg, "cpu")
+        g_reset = torch.empty(world * n, 11)
+        dist.all_gather(list(g_reset.chunk(world)), reset_obs)
+        stream = TransitionStream(lay, world, g_reset)
+        acts = np.random.default_rng(0).uniform(-1, 1, (STEPS, world * N_PER_RANK)).astype(np.float32)
+        out = []
+
+        def drain():
+            if pool.last is not None:
+                g, m = pool.last
+                out.extend(stream.push(pool.step_records(g, m, j)) for j in range(m))
+                pool.last = None
+
+        for k in range(STEPS):
+            r = ora.step(acts[k, off:off + n])
+            t = lambda x: torch.from_numpy(np.asarray(x))  # noqa: E731
+            row = lay.pack(t(r["reset_obs"]), t(r["reward"]), t(r["done"]), t(r["term"]),
+                           t(acts[k, off:off + n]), t(r["obs"]))
+            pool.push(lay.parts(row[: 50 * 64], row[50 * 64: 50 * 64 + 4 * n].view(torch.float32),
+                                row[50 * 64 + 4 * n:]))
+            drain()
+        pool.flush()
+        drain()
+        if rank == 0:
+            q.put([[x.numpy().copy() for x in tr] for tr in out])
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,seg", [(2, 8), (2, 5)])
+def test_pooled_transitions_equal_single_process(world, seg):
+    """N>1 pooling carries whole transitions (main.py:83-88, buffer.py:13-22): the
+    pooled (s, a, r, s', code) of every global env equal a single-process run,
+    including envs that ended (s' = the terminal obs, not the next episode's)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from boat_oracle import OracleConfig, OracleVecBoat
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_transition_worker, args=(r, world, port, seg, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    pooled = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert len(pooled) == STEPS
+    seeds = np.arange(world * N_PER_RANK, dtype=np.uint64) + 100
+    ora = OracleVecBoat(OracleConfig(experiment=6, track_width=60.0), seeds, max_episode_steps=9)
+    s = ora.reset().astype(np.float32)
+    acts = np.random.default_rng(0).uniform(-1, 1, (STEPS, world * N_PER_RANK)).astype(np.float32)
+    ended = 0
+    for k in range(STEPS):
+        r = ora.step(acts[k])
+        ps, pa, pr, pn, pc = pooled[k]
+        np.testing.assert_array_equal(ps, s)
+        np.testing.assert_array_equal(pa, acts[k])
+        np.testing.assert_array_equal(pr, r["reward"].astype(np.float32))
+        np.testing.assert_array_equal(pn, r["obs"].astype(np.float32))   # terminal obs where done
+        np.testing.assert_array_equal(pc, r["term"])
+        ended += int(r["done"].sum())
+        s = r["reset_obs"].astype(np.float32)
+    assert ended > STEPS // 2   # the ended-env rows were exercised

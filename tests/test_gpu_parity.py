@@ -434,7 +434,8 @@ def test_replay_dropin_matches_reference_buffer(case, gpu, built_lib):
 
 def test_replay_store_env_step_uses_final_obs(gpu, built_lib):
     """Batched path: transitions of a VecBoatEnv step; envs that auto-reset store their
-    terminal obs as new_state and terminal = reached_goal only (main.py:83-88)."""
+    terminal obs as new_state; reference_terminal=False: terminal = this step reached
+    the goal."""
     from sacenv import VecBoatEnv
     from sacenv.replay import DeviceReplayBuffer
     cfg = {"base_settings": {"experiment": 6, "test_mode": 1}, "boat_env": {"goal_line": 40}}
@@ -446,7 +447,7 @@ def test_replay_store_env_step_uses_final_obs(gpu, built_lib):
     done_any = goal_any = False
     for k in range(steps):
         env.step(a)
-        rb.store_env_step(obs, a.view(-1, 1), env)
+        rb.store_env_step(obs, a.view(-1, 1), env, reference_terminal=False)
         d = env.done.bool()
         row0 = k * 512
         torch.cuda.synchronize()
@@ -464,6 +465,32 @@ def test_replay_store_env_step_uses_final_obs(gpu, built_lib):
     want = np.random.RandomState(5).choice(min(rb.mem_cntr, rb.mem_size), 1024)
     np.testing.assert_array_equal(idx.cpu().numpy(), want)
     assert torch.equal(st, rb.state_memory[idx]) and torch.equal(ns, rb.new_state_memory[idx])
+
+
+def test_replay_store_env_step_reference_terminal_vs_main_loop(gpu, built_lib):
+    """main.py:70-91 around the reference env + ReplayBuffer (main_loop_goal.npz): the
+    device buffer holds the same rows, terminal following the env's persistent
+    info['termination'] (sacenv_replay_store_env's last_term byte per env)."""
+    from sacenv import VecBoatEnv
+    from sacenv.replay import DeviceReplayBuffer
+    z = golden("main_loop_goal.npz")
+    E, S = z["term"].shape
+    env = VecBoatEnv(_cfg_dict(z), E, seeds=z["seeds"], device=gpu, autoreset=True, n_helpers=8)
+    rb = DeviceReplayBuffer(E * S, (11,), 1, device=gpu, seed=1)
+    obs = env.reset().clone()
+    acts = torch.from_numpy(np.ascontiguousarray(z["actions"].T)).to(gpu)
+    for k in range(S):
+        env.step(acts[k])
+        rb.store_env_step(obs, acts[k].view(-1, 1), env)
+        obs = env.obs.clone()
+    torch.cuda.synchronize()
+    assert rb.mem_cntr == E * S
+    view = lambda t: t.cpu().numpy().reshape(S, E, *t.shape[1:]).swapaxes(0, 1)  # noqa: E731
+    np.testing.assert_array_equal(view(rb.terminal_memory).astype(bool), z["terminal"])
+    np.testing.assert_allclose(view(rb.state_memory), z["state"], rtol=0, atol=OBS_TOL)
+    np.testing.assert_allclose(view(rb.new_state_memory), z["new_state"], rtol=0, atol=OBS_TOL)
+    np.testing.assert_array_equal(view(rb.action_memory), z["action"])
+    np.testing.assert_allclose(view(rb.reward_memory), z["reward"], rtol=0, atol=STATE_TOL)
 
 
 # ---------------------------------------------------------------- done compaction + device-list reset

@@ -104,3 +104,30 @@ def test_toy_oracle_matches_reference_scripts(kind, name):
     """The toy oracle reproduces the signals the reference scripts record, bit for bit."""
     from toy_oracle import script_signals
     np.testing.assert_array_equal(script_signals(kind), golden(name)["signals"])
+
+
+def test_oracle_main_loop_terminal_persistence():
+    """main.py:70-91 around the reference env and ReplayBuffer (main_loop_goal.npz):
+    the stored (s, a, r, s', terminal) rows, terminal following the persistent
+    info['termination'] (goal, then later episodes stored terminal until a
+    different ending)."""
+    from boat_oracle import MainLoopTerminal
+    z = golden("main_loop_goal.npz")
+    o = OracleVecBoat(config_from_fixture(z), z["seeds"])
+    s = o.reset()
+    E, S = z["term"].shape
+    term_rule = MainLoopTerminal(E)
+    for k in range(S):
+        r = o.step(z["actions"][:, k])
+        np.testing.assert_array_equal(r["term"], z["term"][:, k], err_msg=f"step {k}")
+        np.testing.assert_array_equal(term_rule(r["term"]), z["terminal"][:, k], err_msg=f"step {k}")
+        np.testing.assert_allclose(s, z["state"][:, k], rtol=0, atol=1e-12)
+        np.testing.assert_allclose(r["obs"], z["new_state"][:, k], rtol=0, atol=1e-12)
+        np.testing.assert_allclose(r["reward"], z["reward"][:, k], rtol=0, atol=1e-10)
+        np.testing.assert_array_equal(z["actions"][:, k].astype(np.float64), z["action"][:, k, 0])
+        s = r["reset_obs"]
+    t = z["term"]
+    # the fixture exercises the quirk: goals, a later non-goal ending, terminal rows
+    # on steps that are not goals
+    assert (t == 1).sum() > 0 and ((t >= 2) & (t <= 5)).sum() > 0
+    assert (z["terminal"] & (t != 1)).sum() > 0

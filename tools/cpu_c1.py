@@ -1,4 +1,4 @@
-"""the CPU restatement at N=1 (exp 1), one core and all cores.
+"""the CPU restatement at N=1, one core and all cores.
 
 C1 is the reference's own CPU-runnable case: one env per process.
 * 1 core: oracle/boat_oracle.py with one env, pinned to one CPU
@@ -6,12 +6,14 @@ C1 is the reference's own CPU-runnable case: one env per process.
 * all cores: one such process per CPU of this process's affinity set (capped by
   ``--max-procs``: the GPU box gives a job 16 CPUs while ``nproc`` shows the host's).
 Actions U(-1,1) float64 from ``np.random.default_rng(rank)``; auto-reset on done or
-every 500 steps, as in §8(d). Each process runs for a fixed wall time.
+every 500 steps, as in §8(d). Each process runs for a fixed wall time. C1 is exp 1;
+``--experiments 1,6`` adds the bench's experiment (exp 6 resets draw wind splines,
+as the reference's do).
 
 Test / measurement infrastructure: this imports the oracle and is never part of the
 product path. Prints one JSON line.
 
-    python tools/cpu_c1.py [--seconds 10] [--max-procs 16]
+    python tools/cpu_c1.py [--seconds 10] [--max-procs 16] [--experiments 1,6]
 """
 from __future__ import annotations
 
@@ -28,7 +30,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run(rank: int, cpu: int, seconds: float, q) -> None:
+def _run(rank: int, cpu: int, seconds: float, experiment: int, q) -> None:
     os.environ["OMP_NUM_THREADS"] = "1"
     try:
         os.sched_setaffinity(0, {cpu})
@@ -36,7 +38,7 @@ def _run(rank: int, cpu: int, seconds: float, q) -> None:
         pass
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from boat_oracle import OracleConfig, OracleVecBoat
-    ora = OracleVecBoat(OracleConfig(experiment=1, test_mode=0), [rank], max_episode_steps=500)
+    ora = OracleVecBoat(OracleConfig(experiment=experiment, test_mode=0), [rank], max_episode_steps=500)
     ora.reset()
     rng = np.random.default_rng(rank)
     acts = rng.uniform(-1.0, 1.0, (4096, 1))
@@ -52,10 +54,10 @@ def _run(rank: int, cpu: int, seconds: float, q) -> None:
     q.put((rank, steps, el))
 
 
-def _leg(cpus, seconds):
+def _leg(cpus, seconds, experiment):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_run, args=(r, c, seconds, q)) for r, c in enumerate(cpus)]
+    ps = [ctx.Process(target=_run, args=(r, c, seconds, experiment, q)) for r, c in enumerate(cpus)]
     for p in ps:
         p.start()
     res = [q.get(timeout=seconds * 10 + 120) for _ in ps]
@@ -80,15 +82,19 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=10.0)
     ap.add_argument("--max-procs", type=int, default=16)
+    ap.add_argument("--experiments", default="1")
     a = ap.parse_args(argv)
     cpus = sorted(os.sched_getaffinity(0))
     allc = cpus[:max(1, a.max_procs)]
-    one = _leg(cpus[:1], a.seconds)
-    many = _leg(allc, a.seconds)
+    legs = {}
+    for e in (int(x) for x in a.experiments.split(",")):
+        legs[str(e)] = {"one_core": {"env_steps_per_s": _leg(cpus[:1], a.seconds, e), "procs": 1},
+                        "all_cores": {"env_steps_per_s": _leg(allc, a.seconds, e), "procs": len(allc)}}
+    first = legs[sorted(legs)[0]]
     print(json.dumps({
-        "config": "C1: exp 1, 1 env per process, oracle/boat_oracle.py (numpy f64)",
-        "one_core": {"env_steps_per_s": one, "procs": 1},
-        "all_cores": {"env_steps_per_s": many, "procs": len(allc)},
+        "config": "C1: 1 env per process, oracle/boat_oracle.py (numpy f64), per experiment",
+        "experiments": legs,
+        "one_core": first["one_core"], "all_cores": first["all_cores"],
         "os_cpu_count": os.cpu_count(), "affinity_cpus": len(cpus), "cpu_model": _cpu_model(),
         "numpy": np.__version__, "python": platform.python_version(),
         "note": "the reference BoatEnv itself: 13 385 env-steps/s on 1 core, 101 354 on 8 "
