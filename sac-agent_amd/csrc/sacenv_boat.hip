@@ -150,49 +150,35 @@ struct Arena {
   __device__ __forceinline__ int32_t* refill_list(int k) const { return i32(U_LIST + 4 * k); }
   // element index of (env, slot, curve, knot) in knots_raw; x2 (+1) in wind_knots
   __device__ __forceinline__ int64_t wix(int slot, int c, int k, int e) const {
-#ifdef SACENV_SLOT_MAJOR  // A/B layout switch (same field sizes): [slot][curve][knot][env]
-    return ((int64_t)(slot * 2 + c) * nk + k) * np + e;
-#else
     return (((int64_t)e * kSlots + slot) * 2 + c) * nk + k;
-#endif
   }
-  // byte offset of knot k's (y, m) pair: 32-bit (check_params bounds the
-  // region below 4 GiB), so the step's gathers use SGPR base + VGPR offset
-  __device__ __forceinline__ uint32_t wko(int slot, int c, int k, int e) const {
-#ifdef SACENV_SLOT_MAJOR
-    return (((uint32_t)(slot * 2 + c) * (uint32_t)nk + (uint32_t)k) * (uint32_t)np + (uint32_t)e) * 16u;
-#else
-    return ((((uint32_t)e * (uint32_t)kSlots + (uint32_t)slot) * 2u + (uint32_t)c) * (uint32_t)nk + (uint32_t)k) * 16u;
-#endif
+  // The slot ring of a wave's 64 envs is one contiguous block: its base is
+  // uniform (64-bit, scalar registers) and a lane's (y, m) offset inside it
+  // stays 32-bit (< 64 x 33 KB), so the step's gathers keep the SGPR-base
+  // addressing mode at any env count.
+  __device__ __forceinline__ const char* wk_wave(int e0) const {
+    return reinterpret_cast<const char*>(wind_knots()) + (int64_t)e0 * (int64_t)kSlots * 32 * nk;
   }
-  // (y, m) of knot k and k+1: 32 contiguous bytes
+  __device__ __forceinline__ uint32_t wko_l(int slot, int c, int k, int l) const {
+    return ((((uint32_t)l * (uint32_t)kSlots + (uint32_t)slot) * 2u + (uint32_t)c) * (uint32_t)nk + (uint32_t)k) * 16u;
+  }
+  // (y, m) of knot k and k+1 of env e: 32 contiguous bytes
   __device__ __forceinline__ void piece(int slot, int c, int k, int e, double (&q)[4]) const {
-    const char* base = reinterpret_cast<const char*>(wind_knots()) + wko(slot, c, k, e);
-#ifdef SACENV_SLOT_MAJOR
-    const uint32_t next = (uint32_t)np * 16u;
-#else
-    const uint32_t next = 16u;
-#endif
-    const double2 a = *reinterpret_cast<const double2*>(base), b = *reinterpret_cast<const double2*>(base + next);
+    const char* base = wk_wave(e & ~63) + wko_l(slot, c, k, e & 63);
+    const double2 a = *reinterpret_cast<const double2*>(base), b = *reinterpret_cast<const double2*>(base + 16);
     q[0] = a.x, q[1] = a.y, q[2] = b.x, q[3] = b.y;  // memory order: y0, m0, y1, m1
   }
-  // piece() for lanes with `use`; the others read the ring's first line (a
-  // fixed address: one cache line per wave), so the load needs no branch
-  __device__ __forceinline__ void piece_if(bool use, int slot, int c, int k, int e, double (&q)[4]) const {
-    const char* base = reinterpret_cast<const char*>(wind_knots()) + (use ? wko(slot, c, k, e) : 0u);
-#ifdef SACENV_SLOT_MAJOR
-    const uint32_t next = (uint32_t)np * 16u;
-#else
-    const uint32_t next = 16u;
-#endif
-    const double2 a = *reinterpret_cast<const double2*>(base), b = *reinterpret_cast<const double2*>(base + next);
+  // piece() for lane `lane` of the wave whose ring block starts at wbase, for
+  // lanes with `use`; the others read the block's first line (a fixed address:
+  // one cache line per wave), so the load needs no branch
+  __device__ __forceinline__ void piece_if(bool use, const char* wbase, int slot, int c, int k, int lane,
+                                           double (&q)[4]) const {
+    const char* base = wbase + (use ? wko_l(slot, c, k, lane) : 0u);
+    const double2 a = *reinterpret_cast<const double2*>(base), b = *reinterpret_cast<const double2*>(base + 16);
     q[0] = a.x, q[1] = a.y, q[2] = b.x, q[3] = b.y;
   }
-  __device__ __forceinline__ const double* wy0p(int slot, int c, int e) const {
-    return reinterpret_cast<const double*>(reinterpret_cast<const char*>(wind_knots()) + wko(slot, c, 0, e));
-  }
-  __device__ __forceinline__ double wy0(int slot, int c, int e) const {
-    return *reinterpret_cast<const double*>(reinterpret_cast<const char*>(wind_knots()) + wko(slot, c, 0, e));
+  __device__ __forceinline__ const double* wy0p(const char* wbase, int slot, int c, int lane) const {
+    return reinterpret_cast<const double*>(wbase + wko_l(slot, c, 0, lane));
   }
   // Per-lane accesses as uniform base + 32-bit byte offset: the compiler then
   // uses the SGPR-base addressing mode (no 64-bit address arithmetic in VALU).
@@ -201,8 +187,8 @@ struct Arena {
   __device__ __forceinline__ T& at_e(int64_t unit, uint32_t off) const {
     return *reinterpret_cast<T*>(b + unit * np + off);
   }
-  // the per-env fields below U_WIND: the whole byte offset in 32 bits (u < 708
-  // and n_pad * 33 024 < 2^32 by check_params), so each access is one VALU add
+  // the per-env fields below U_WIND: the whole byte offset in 32 bits (u < 720
+  // and n_pad <= 2^22 by check_params), so each access is one VALU add
   // on the lane offset and an SGPR-base load/store
   template <class T>
   __device__ __forceinline__ T& at_s(int u, uint32_t off) const {
@@ -328,6 +314,32 @@ __device__ __forceinline__ void wind_at(const SacenvBoatParams& p, const Arena& 
   }
 }
 
+// sin(x) for |x| <= 1.25 with no argument reduction: x + x^3 P(x^2), P the
+// Taylor series through x^21 (truncation < 1e-20, below half an ulp), about
+// 12 FMAs against ocml's reduction + two polynomials + select. Waves with any
+// lane beyond the bound take ocml's sin (a uniform branch).
+__device__ __forceinline__ double sin_reduced(double x) {
+  constexpr double kBound = 1.25;
+  if (__ballot(!(fabs(x) <= kBound)) != 0ull) return sin(x);
+  const double z = x * x;
+  double q = -1.9572941063391262e-20;  // -1/21!
+  q = fma(q, z, 8.22063524662432950e-18);   // 1/19!
+  q = fma(q, z, -2.8114572543455206e-15);   // -1/17!
+  q = fma(q, z, 7.6471637318198164e-13);    // 1/15!
+  q = fma(q, z, -1.6059043836821613e-10);   // -1/13!
+  q = fma(q, z, 2.5052108385441720e-08);    // 1/11!
+  q = fma(q, z, -2.7557319223985893e-06);   // -1/9!
+  q = fma(q, z, 1.9841269841269841e-04);    // 1/7!
+  q = fma(q, z, -8.3333333333333333e-03);   // -1/5!
+  q = fma(q, z, 1.6666666666666666e-01);    // 1/3! (sign below)
+  return fma(-(x * z), q, x);
+}
+#ifdef SACENV_SIN_POLY
+#define SACENV_SIN_SMALL(x) sin_reduced(x)
+#else
+#define SACENV_SIN_SMALL(x) sin(x)
+#endif
+
 // x / c for a per-launch constant c, from r = RN(1/c): Markstein's correction
 // step returns the correctly rounded quotient, i.e. the same double as IEEE
 // division, in 3 dependent FLOPs instead of the ~10 of a full fp64 divide.
@@ -373,6 +385,40 @@ __device__ __forceinline__ Obs make_obs(const SacenvBoatParams& p, const ObsCons
 }
 
 typedef float f4v __attribute__((ext_vector_type(4)));
+
+// Cache policy of the step's output stores. Default SACENV_ST_SC1:
+// write-through (sc1: the line leaves the XCD L2, so the launch ends with no
+// dirty lines to write back; measured 0.21 us/step faster than plain stores);
+// the obs rows (16-B stores, no sc1 atomic form) go nontemporal. A/B builds:
+// SACENV_ST_PLAIN, SACENV_ST_NT, SACENV_OBS_PLAIN.
+#if !defined(SACENV_ST_PLAIN) && !defined(SACENV_ST_NT) && !defined(SACENV_ST_SC1)
+#define SACENV_ST_SC1 1
+#endif
+template <class T>
+__device__ __forceinline__ void st_out(T& ref, T v) {
+#if defined(SACENV_ST_SC1)
+  __hip_atomic_store(&ref, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#elif defined(SACENV_ST_NT)
+  __builtin_nontemporal_store(v, &ref);
+#else
+  ref = v;
+#endif
+}
+template <class T>
+__device__ __forceinline__ void st_rec(T& ref, T v) {  // reward / done / term bytes
+#ifdef SACENV_REC_PLAIN
+  ref = v;
+#else
+  st_out(ref, v);
+#endif
+}
+__device__ __forceinline__ void st_out4(f4v* ptr, f4v v) {
+#if (defined(SACENV_ST_NT) || defined(SACENV_ST_SC1)) && !defined(SACENV_OBS_PLAIN)
+  __builtin_nontemporal_store(v, ptr);
+#else
+  *ptr = v;
+#endif
+}
 
 __device__ __forceinline__ void store_obs(float* dst, const Obs& o) {
 #pragma unroll
@@ -1228,9 +1274,9 @@ __host__ __device__ inline bool t_from_index(double dt) {
 // Each dynamics field is stored as soon as it is final, so the write traffic
 // drains while the wave still computes (measured: -0.15 us/step against
 // staging every output for 16-B stores at the end).
-#define EARLY_STORE(u, v)              \
-  do {                                 \
-    if (!kRoll) A.f64e(u, eo) = (v);   \
+#define EARLY_STORE(u, v)                      \
+  do {                                         \
+    if (!kRoll) st_out(A.f64e(u, eo), (v));    \
   } while (0)
 
 // 64 obs rows (2816 B) from LDS to a 16-B aligned row block: 3 float4 stores
@@ -1240,7 +1286,7 @@ __device__ __forceinline__ void store_obs_block(const float* lds_rows, float* ds
   for (int i = 0; i < 3; ++i) {
     const uint32_t q = (uint32_t)lane + kWave * i;
     if (q < kWave * SACENV_OBS_DIM / 4)
-      *reinterpret_cast<f4v*>(reinterpret_cast<char*>(dst_rows) + q * 16u) = src[q];
+      st_out4(reinterpret_cast<f4v*>(reinterpret_cast<char*>(dst_rows) + q * 16u), src[q]);
   }
 }
 
@@ -1279,6 +1325,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
 #endif
   const int e = ob * kWave + lane;
   const uint32_t eo = (uint32_t)e * 8u, eo4 = (uint32_t)e * 4u;  // per-lane byte offsets
+  const char* const wbase = A.wk_wave(ob * kWave);  // the wave's slot-ring block (uniform)
   const bool active = e < p.n_envs;
   // the (first) action, in flight with the state loads
   const char* const abase = reinterpret_cast<const char*>(action) + (active ? eo4 : 0u);
@@ -1364,7 +1411,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
       for (int c = 0; c < 2; ++c)
         if (c < nc) {
           double q[4];
-          A.piece_if(refresh, slot, c, jn, e, q);
+          A.piece_if(refresh, wbase, slot, c, jn, lane, q);
           rq[4 * c] = q[0], rq[4 * c + 1] = q[1], rq[4 * c + 2] = q[2], rq[4 * c + 3] = q[3];
         }
     }
@@ -1387,7 +1434,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
     for (int c = 0; c < 2; ++c)
       if (c < nc) {
         // (rollout: the copy is in registers; other lanes read the ring's first line)
-        const double v = *(hdr_refresh ? A.wy0p(ns, c, e)
+        const double v = *(hdr_refresh ? A.wy0p(wbase, ns, c, lane)
                                        : (kRoll ? A.wind_knots() : &A.f64e(U_W0N + 8 * c, eo)));
         y0n[c] = kRoll && !hdr_refresh ? y0c[c] : v;
       }
@@ -1415,7 +1462,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   const double F_R = v_x * v_x * p.c_r_front * 0.5 * p.rho * p.boat_area_front;
   const double v_x_w = v_x * p.one_minus_wf;
   const double J = p.n_rpm != 0.0 ? div_c(v_x_w, p.n_times_d, r_nd) : 0.0;  // :222-224
-  const double F_T = sin(J) * p.n_squared * p.rho * p.d_pow4 * p.one_minus_td;
+  const double F_T = SACENV_SIN_SMALL(J) * p.n_squared * p.rho * p.d_pow4 * p.one_minus_td;
   const double F_C = v_y * p.m_plus_my * v_r;
   const double F_W = (wv * wv * wsign * p.c_r_front * 0.5 * p.rho * p.boat_area_front) * cwa;
   const double a_x = div_c(-F_R + F_T + F_C + F_W, p.m_plus_mx, r_mx);
@@ -1425,7 +1472,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   // eom_transverse :241-265 (new v_x)
   const double vys = (double)((v_y > 0.0) - (v_y < 0.0));
   const double F_R2 = v_y * v_y * p.c_r_side * 0.5 * p.rho * p.boat_area_side * vys;
-  const double sin_rud = sin(rudder);
+  const double sin_rud = SACENV_SIN_SMALL(rudder);
   const double F_RU = sin_rud * (v_x * v_x * p.c_r_front * 0.5 * p.rho * p.rudder_area);
   const double F_C2 = v_x * p.m_plus_mx * v_r;
   const double F_W2 = (wv * wv * wsign * p.c_r_side * 0.5 * p.rho * p.boat_area_side) * swa;
@@ -1443,6 +1490,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   EARLY_STORE(U_VR, v_r);
 
   // get_kinematics :283-306
+#ifdef SACENV_KIN_ATAN2  // the reference's expressions (A/B builds)
   const double v = sqrt(v_x * v_x + v_y * v_y);
   const double drift = atan2(v_x, v_y);
   s_r = v_r * p.dt + s_r;
@@ -1451,11 +1499,23 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   sincos(dir, &sd, &cd);
   s_x = (sd * v) * p.dt + s_x;
   s_y = (cd * v) * p.dt + s_y;
+#else
+  // drift = atan2(v_x, v_y) has sin = v_x / v, cos = v_y / v, so
+  // sin(drift - s_r) v = v_x cos s_r - v_y sin s_r and
+  // cos(drift - s_r) v = v_y cos s_r + v_x sin s_r: no atan2, sqrt or division
+  // (122 fewer VALU; -0.26 us/step). Same parity class as the ocml/libm
+  // differences: the increments agree to a few ulp of v dt.
+  s_r = v_r * p.dt + s_r;
+  double ssr, csr;
+  sincos(s_r, &ssr, &csr);
+  s_x = (v_x * csr - v_y * ssr) * p.dt + s_x;
+  s_y = (v_y * csr + v_x * ssr) * p.dt + s_y;
+#endif
   index = index + 1;
   EARLY_STORE(U_SR, s_r);
   EARLY_STORE(U_SX, s_x);
   EARLY_STORE(U_SY, s_y);
-  if (!kRoll) A.i32e(U_IDX, eo4) = index;
+  if (!kRoll) st_out(A.i32e(U_IDX, eo4), index);
 
   Obs o = make_obs(p, oc, s_x, v_x, a_x, s_y, v_y, a_y, s_r, v_r, a_r, rudder, (double)fuel);
 
@@ -1531,30 +1591,30 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   // fresh state of restarting envs (same lane, same address: the later store
   // wins), ep_reward, the next wind, and the record
   if (!kRoll && restart) {
-    A.f64e(U_SX, eo) = s_x, A.f64e(U_SY, eo) = s_y, A.f64e(U_SR, eo) = s_r;
-    A.f64e(U_VX, eo) = v_x, A.f64e(U_VY, eo) = v_y, A.f64e(U_VR, eo) = v_r;
-    A.f64e(U_RUD, eo) = rudder;
-    if (!t_idx) A.f64e(U_T, eo) = t;
-    A.i32e(U_IDX, eo4) = index;
-    A.i32e(U_CONS, eo4) = cons_out;
+    st_out(A.f64e(U_SX, eo), s_x), st_out(A.f64e(U_SY, eo), s_y), st_out(A.f64e(U_SR, eo), s_r);
+    st_out(A.f64e(U_VX, eo), v_x), st_out(A.f64e(U_VY, eo), v_y), st_out(A.f64e(U_VR, eo), v_r);
+    st_out(A.f64e(U_RUD, eo), rudder);
+    if (!t_idx) st_out(A.f64e(U_T, eo), t);
+    st_out(A.i32e(U_IDX, eo4), index);
+    st_out(A.i32e(U_CONS, eo4), cons_out);
   }
   if (!kRoll) {
-    A.f64e(U_EP, eo) = ep;
+    st_out(A.f64e(U_EP, eo), ep);
     if (restart && nc > 0) {  // the new episode's first wind: the piece's y0 = y(0); at
       // t = 0 the piece is exactly y0 whatever (finite) m0, y1, m1 it still holds
 #pragma unroll
       for (int c = 0; c < 2; ++c)
-        if (c < nc) A.f64e(U_COEF + 32 * c, eo) = y0n[c];
+        if (c < nc) st_out(A.f64e(U_COEF + 32 * c, eo), y0n[c]);
     } else if (refresh) {
 #pragma unroll
       for (int k = 0; k < kCoef; ++k)
-        if (k < 4 * nc) A.f64e(U_COEF + 8 * k, eo) = rq[k];
+        if (k < 4 * nc) st_out(A.f64e(U_COEF + 8 * k, eo), rq[k]);
     }
     if (hdr_refresh) {
 #pragma unroll
       for (int c = 0; c < 2; ++c)
-        if (c < nc) A.f64e(U_W0N + 8 * c, eo) = y0n[c];
-      if (p.experiment == 2) A.i32e(U_SYN, eo4) = syn;
+        if (c < nc) st_out(A.f64e(U_W0N + 8 * c, eo), y0n[c]);
+      if (p.experiment == 2) st_out(A.i32e(U_SYN, eo4), syn);
     }
   } else {  // the same updates, in registers
     if (restart) {
@@ -1570,17 +1630,26 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
     syc = syn;
     cons = cons_out;
   }
-  *reinterpret_cast<float*>(R + 44 * A.np + eo4) = (float)reward;
-  *reinterpret_cast<uint8_t*>(R + 48 * A.np + e) = ended ? 1 : 0;
-  *reinterpret_cast<uint8_t*>(R + 49 * A.np + e) = term;
+  st_rec(*reinterpret_cast<float*>(R + 44 * A.np + eo4), (float)reward);
+  st_rec(*reinterpret_cast<uint8_t*>(R + 48 * A.np + e), (uint8_t)(ended ? 1 : 0));
+  st_rec(*reinterpret_cast<uint8_t*>(R + 49 * A.np + e), term);
   // obs rows through LDS, stored as float4 (64 rows x 44 B = 176 float4); a
   // restarting env's row is its new episode's first obs
 #pragma unroll
   for (int k = 0; k < SACENV_OBS_DIM; ++k) l.obs[lane * SACENV_OBS_DIM + k] = restart ? fo.v[k] : o.v[k];
-  __syncthreads();
+  // the rows are this wave's own LDS: a wave's LDS accesses run in issue order,
+  // so only the compiler must keep the stores ahead of the loads (no workgroup
+  // barrier: a step workgroup may hold several owner waves, or toy waves)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const int64_t row0 = (int64_t)ob * kWave * SACENV_OBS_DIM;
   store_obs_block(l.obs, reinterpret_cast<float*>(R) + row0, lane);
-  if (kRoll) __syncthreads();  // l.obs is rewritten by the next step
+  if (kRoll) {  // l.obs is rewritten by the next step
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
   }  // steps
   if (kRoll) {  // the carried state, once
     A.f64e(U_SX, eo) = s_x, A.f64e(U_SY, eo) = s_y, A.f64e(U_SR, eo) = s_r;
@@ -1618,15 +1687,32 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
 // The step launch. Grid: nb_boat owner waves, then (kMixed) the waves of
 // each toy arena: heterogeneous workgroups of one launch, selected by
 // uniform block-index ranges.
+// kStepWaves waves per workgroup (A/B builds: SACENV_STEP_WAVES); with
+// SACENV_STEP_LDS the workgroup declares that many bytes of LDS so that at
+// most one workgroup fits a CU (one wave per SIMD).
+#ifndef SACENV_STEP_WAVES
+#define SACENV_STEP_WAVES 1
+#endif
+constexpr int kStepWaves = SACENV_STEP_WAVES;
+struct StepLds {
+  OwnerLds w[kStepWaves];
+#ifdef SACENV_STEP_LDS
+  char pad[SACENV_STEP_LDS - sizeof(OwnerLds) * kStepWaves];
+#endif
+};
 template <bool kMixed, int kNc, bool kTIdx>
-__global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, Arena A, Tail T,
+__global__ void __launch_bounds__(kWave * kStepWaves) k_step(SacenvBoatParams p, Arena A, Tail T,
                                                 const float* __restrict__ action, int nb_boat,
                                                 MixedToys M) {
-  __shared__ OwnerLds slds;
-  const int lane = threadIdx.x;
-  int b = (int)blockIdx.x;
+  __shared__ StepLds slds;
+  const int lane = threadIdx.x & (kWave - 1), wv = kStepWaves > 1 ? (int)(threadIdx.x >> 6) : 0;
+  int b = (int)blockIdx.x * kStepWaves + wv;
+#ifdef SACENV_STEP_LDS
+  if (threadIdx.x == 0xFFFF) slds.pad[lane] = 0;  // keeps the pad allocated
+#endif
   if (!kMixed || b < nb_boat) {
-    owner_wave<false, kNc, kTIdx>(vreg_params(p), A, vreg_tail(T), action, slds, b, lane);
+    if (kStepWaves > 1 && b >= nb_boat) return;
+    owner_wave<false, kNc, kTIdx>(vreg_params(p), A, vreg_tail(T), action, slds.w[wv], b, lane);
     return;
   }
   b -= nb_boat;
@@ -1694,8 +1780,6 @@ int check_params(const SacenvBoatParams* p) {
   if (p->experiment < 1 || p->experiment > 6) return SACENV_E_EXPERIMENT;
   if (p->n_envs <= 0 || p->n_envs > (1 << 22) || p->wind_len <= 0) return SACENV_E_SIZE;  // 32-bit offsets
   if (n_curves(p->experiment) > 0 && (p->n_knots < 4 || p->n_knots > kMaxK)) return SACENV_E_KNOTS;
-  // 32-bit byte offsets into wind_knots (Arena::wko): n_pad x SLOTS x 2 curves x knots x 16 B
-  if (pad64(p->n_envs) * kSlots * 2 * 16 * (p->n_knots > 1 ? p->n_knots : 1) >= (1LL << 32)) return SACENV_E_SIZE;
   if (p->n_knots < 2 || p->n_knots > kMaxK) return SACENV_E_KNOTS;
   if (n_curves(p->experiment) > 0 && !p->use_wind_table && p->wind_len < 2) return SACENV_E_SIZE;
   if (p->start_y_half < 1) return SACENV_E_RANGE;
@@ -1854,8 +1938,9 @@ int sacenv_boat_step(const SacenvBoatParams* p, void* arena, const float* action
   if (rc) return rc;
   if (arena == nullptr || action == nullptr) return SACENV_E_NULL;
   const int nb_boat = (int)(pad64(p->n_envs) / kWave);
+  const int grid = (nb_boat + kStepWaves - 1) / kStepWaves;
 #define SACENV_LAUNCH(NC, TI)                                                                         \
-  hipLaunchKernelGGL((k_step<false, NC, TI>), dim3(nb_boat), dim3(kWave), 0, (hipStream_t)stream, *p, \
+  hipLaunchKernelGGL((k_step<false, NC, TI>), dim3(grid), dim3(kWave * kStepWaves), 0, (hipStream_t)stream, *p, \
                      make_arena(*p, arena), make_tail(*p, arena), action, nb_boat, MixedToys{})
   SACENV_OWNER_DISPATCH(*p, SACENV_LAUNCH)
 #undef SACENV_LAUNCH
@@ -1970,8 +2055,9 @@ int sacenv_mixed_step(const SacenvBoatParams* bp, void* boat_arena, const float*
     nb += nb_boat;
   }
   if (nb == 0) return SACENV_OK;
+  const int grid = (nb + kStepWaves - 1) / kStepWaves;
 #define SACENV_LAUNCH(NC, TI) \
-  hipLaunchKernelGGL((k_step<true, NC, TI>), dim3(nb), dim3(kWave), 0, (hipStream_t)stream, p, A, T, boat_action, nb_boat, M)
+  hipLaunchKernelGGL((k_step<true, NC, TI>), dim3(grid), dim3(kWave * kStepWaves), 0, (hipStream_t)stream, p, A, T, boat_action, nb_boat, M)
   SACENV_OWNER_DISPATCH(p, SACENV_LAUNCH)
 #undef SACENV_LAUNCH
   return launch_status();

@@ -183,6 +183,7 @@ class MixedBatch:
             if a.dtype != torch.float32:
                 a = a.to(torch.float32)
             a = a.reshape(b.num_envs).contiguous()
+            b.check_actions(a)
             self._keep = a
         _lib.check(self.lib.sacenv_mixed_step(
             b._pp if b is not None else None, b.arena.data_ptr() if b is not None else None,

@@ -63,6 +63,8 @@ class VecBoatEnv:
         self.device = torch.device(device if device is not None else "cuda")
         if self.device.type != "cuda":
             raise RuntimeError("VecBoatEnv runs on a GPU (HIP); no CPU path")
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.env_id_offset = int(env_id_offset)
         self.autoreset = bool(autoreset)
         self.auto_refill = bool(auto_refill)
@@ -213,8 +215,21 @@ class VecBoatEnv:
         self._keep = (ids, sy, kn)  # alive until the stream has consumed them
         return self.obs
 
+    def check_actions(self, actions: torch.Tensor) -> None:
+        """The kernel reads num_envs f32 values from the pointer: refuse anything else
+        (a wrong tensor would otherwise be an out-of-bounds device read)."""
+        if not isinstance(actions, torch.Tensor):
+            raise TypeError("actions must be a torch tensor on the env's device")
+        if actions.dtype != torch.float32 or not actions.is_contiguous():
+            raise ValueError("actions must be a contiguous float32 tensor")
+        if actions.numel() != self.num_envs:
+            raise ValueError(f"actions must hold num_envs={self.num_envs} values, got {actions.numel()}")
+        if actions.device != self.device:
+            raise ValueError(f"actions are on {actions.device}, the env on {self.device}")
+
     def step_async(self, actions: torch.Tensor) -> None:
         """Enqueue one step; ``actions`` is a contiguous f32 device tensor of N values."""
+        self.check_actions(actions)
         _lib.check(self.lib.sacenv_boat_step(self._pp, self._ptr, actions.data_ptr(), self.stream))
         self._after_step()
 

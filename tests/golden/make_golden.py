@@ -30,6 +30,13 @@ Fixture kinds
     'reached_goal'`` (``main.py:83-88``). ``info['termination']`` persists
     across steps and resets (``boat_env.py:24-32,120-126``), so after a goal
     episode later steps are stored terminal until another ending overwrites it.
+``sac_learn.npz``
+    The reference ``ContinuousAgent`` (``agent/continuous_agent.py:9-154``, networks
+    ``networks/networks.py:14-133``) built under ``torch.manual_seed(0)`` on the CPU,
+    then ``learn()`` on fixed 1 024-row batches (``sample_buffer`` returns them) with
+    the policy's ``Normal.sample``/``rsample`` drawing recorded standard normals
+    (``loc + eps * scale``): the losses of each call and every network's weights
+    after the calls.
 ``recorded_exp<k>.npz``
     The reference's own recorded runs under
     ``ressources/settings_visualized/experiment_setting_<k>/`` converted from
@@ -308,8 +315,79 @@ def run_main_loop(n_steps=700, seeds=SEEDS, action_seed=21):
           f"terminal={int(flat['terminal'].sum())} goal_steps={int((t == 1).sum())}")
 
 
+def run_sac_learn(n_calls=2, batch=1024, seed=0):
+    """ContinuousAgent.learn (continuous_agent.py:96-154) on fixed batches and noise."""
+    import torch
+    H.install_standins()
+    import torch.nn.functional as F
+    from agent.continuous_agent import ContinuousAgent  # reference module
+    cfg = H.load_config()
+    env = types.SimpleNamespace(action_space=sys_modules_box()(low=-1, high=1, dtype=np.float32))
+    torch.manual_seed(seed)
+    agent = ContinuousAgent(cfg, tempfile.mkdtemp(), (11,), env)
+    rng = np.random.default_rng(seed + 17)
+    batches = []
+    for _ in range(n_calls):
+        batches.append(dict(
+            state=rng.uniform(0, 1, (batch, 11)),
+            action=rng.uniform(-1, 1, (batch, 1)),
+            reward=rng.standard_normal(batch) * 3,
+            new_state=rng.uniform(0, 1, (batch, 11)),
+            done=rng.random(batch) < 0.1))
+    Normal = torch.distributions.Normal
+    orig = (Normal.sample, Normal.rsample, F.mse_loss)
+    eps_log, mse_log = [], []
+    gen = torch.Generator().manual_seed(seed + 99)
+
+    def sample(self, sample_shape=torch.Size()):
+        with torch.no_grad():
+            eps = torch.randn(self._extended_shape(sample_shape), generator=gen)
+            eps_log.append(eps.numpy().copy())
+            return self.loc + eps * self.scale
+
+    def rsample(self, sample_shape=torch.Size()):
+        eps = torch.randn(self._extended_shape(sample_shape), generator=gen)
+        eps_log.append(eps.numpy().copy())
+        return self.loc + eps * self.scale
+
+    def mse(a, b, *args, **kw):
+        out = orig[2](a, b, *args, **kw)
+        mse_log.append(float(out))
+        return out
+
+    Normal.sample, Normal.rsample, F.mse_loss = sample, rsample, mse
+    try:
+        for b in batches:
+            agent.memory.mem_cntr = agent.batch_size
+            agent.memory.sample_buffer = (lambda bs, b=b: (b["state"], b["action"], b["reward"],
+                                                           b["new_state"], b["done"]))
+            agent.learn()
+    finally:
+        Normal.sample, Normal.rsample, F.mse_loss = orig
+    out = {"n_calls": n_calls, "seed": seed, "eps": np.asarray(eps_log, np.float32),
+           "mse": np.asarray(mse_log, np.float64)}
+    for i, b in enumerate(batches):
+        for k, v in b.items():
+            out[f"b{i}_{k}"] = v
+    for name in ("actor", "critic_1", "critic_2", "value", "target_value"):
+        for k, v in getattr(agent, name).state_dict().items():
+            out[f"w_{name}.{k}"] = v.numpy()
+    out.update({f"cfg_{k}": np.asarray(v) for k, v in cfg["agent"].items()})
+    path = os.path.join(HERE, "sac_learn.npz")
+    np.savez_compressed(path, **out)
+    print(f"{path}: calls={n_calls} eps={out['eps'].shape} mse={out['mse'].tolist()}")
+
+
+def sys_modules_box():
+    import sys
+    return sys.modules["gym.spaces"].Box
+
+
 def main():
     import sys
+    if sys.argv[1:] == ["sac"]:
+        run_sac_learn()
+        return
     if sys.argv[1:] == ["main_loop"]:
         run_main_loop()
         return
@@ -322,6 +400,7 @@ def main():
     run_toys()
     run_replay()
     run_main_loop()
+    run_sac_learn()
     for exp in range(1, 7):
         run_seeded(f"exp{exp}_uniform", {"base_settings": {"experiment": exp, "test_mode": 0}},
                    400, "uniform", action_seed=100 + exp)

@@ -328,6 +328,20 @@ def test_bad_config_raises(gpu, built_lib):
         VecBoatEnv({"base_settings": {"experiment": 6}, "wind": {"fixed_points": 3}}, 4, device=gpu)
 
 
+def test_step_async_refuses_bad_action_tensors(gpu, built_lib):
+    """The kernel reads num_envs f32 values: wrong dtype, length, layout or device
+    raise before the launch instead of reading out of bounds."""
+    from sacenv import VecBoatEnv
+    env = VecBoatEnv({"base_settings": {"experiment": 6}}, 100, device=gpu)
+    env.step_async(torch.zeros(100, device=gpu))
+    for bad in (torch.zeros(99, device=gpu), torch.zeros(100, device=gpu, dtype=torch.float64),
+                torch.zeros(200, device=gpu)[::2], torch.zeros(100)):
+        with pytest.raises(ValueError):
+            env.step_async(bad)
+    with pytest.raises(TypeError):
+        env.step_async([0.0] * 100)
+
+
 # ---------------------------------------------------------------- toy envs (A17, A18)
 
 def _toy_env(kind, n, **kw):
@@ -490,7 +504,8 @@ def test_replay_store_env_step_reference_terminal_vs_main_loop(gpu, built_lib):
     np.testing.assert_allclose(view(rb.state_memory), z["state"], rtol=0, atol=OBS_TOL)
     np.testing.assert_allclose(view(rb.new_state_memory), z["new_state"], rtol=0, atol=OBS_TOL)
     np.testing.assert_array_equal(view(rb.action_memory), z["action"])
-    np.testing.assert_allclose(view(rb.reward_memory), z["reward"], rtol=0, atol=STATE_TOL)
+    # the batched path stores the f32 reward the step writes (rewards reach ~1000)
+    np.testing.assert_allclose(view(rb.reward_memory), z["reward"], rtol=1e-6, atol=STATE_TOL)
 
 
 # ---------------------------------------------------------------- done compaction + device-list reset
@@ -732,3 +747,95 @@ def test_vec_sac_training_loop_runs_on_device(gpu, built_lib):
     out = mod.main(["--envs", "2048", "--iters", "20"])
     assert out["env_steps_per_s"] > 0 and out["losses"] is not None
     assert all(np.isfinite(out["losses"]))
+
+
+# ---------------------------------------------------------------- configs at their stated sizes
+
+def _subsample_run(env_factory, cfg, N, S, max_steps, pick, seed_base, act_seed):
+    """Step a VecBoatEnv of N envs S steps with U(-1,1) actions; check the picked envs
+    against the oracle run on just their seeds (term bit-exact, obs/state to tolerance)."""
+    rng = np.random.default_rng(act_seed)
+    seeds = np.arange(N, dtype=np.uint64) + seed_base
+    env = env_factory(seeds)
+    env.reset()
+    ora = OracleVecBoat(cfg, seeds[pick], max_episode_steps=max_steps)
+    ora.reset()
+    ended = trunc = 0
+    for k in range(S):
+        a = rng.uniform(-1, 1, N).astype(np.float32)
+        o, r, d, info = env.step(torch.from_numpy(a).to(env.device))
+        ro = ora.step(a[pick])
+        torch.cuda.synchronize()
+        term = info["term"].cpu().numpy()[pick]
+        np.testing.assert_array_equal(term, ro["term"], err_msg=f"step {k}")
+        np.testing.assert_allclose(o.cpu().numpy()[pick], ro["reset_obs"], rtol=OBS_TOL, atol=OBS_TOL)
+        dd = ro["done"].astype(bool)
+        if dd.any():
+            np.testing.assert_allclose(info["final_obs"].cpu().numpy()[pick][dd], ro["obs"][dd],
+                                       rtol=OBS_TOL, atol=OBS_TOL)
+        for f in ("s_x", "s_y", "v_x", "v_y", "s_r"):
+            assert np.abs(getattr(env, f).cpu().numpy()[pick] - getattr(ora, f)).max() <= STATE_TOL, f
+        ended += int(dd.sum())
+        trunc += int((term == 6).sum())
+    return ended, trunc
+
+
+def test_c2_exp1_4096_envs_500_step_episodes(gpu, built_lib):
+    """BASELINE configs[1] at its size: exp 1, 4 096 envs, episodes
+    truncated at 500 steps, auto-reset; 256 envs checked against the oracle over 620
+    steps (early endings and the step-500 truncation)."""
+    from sacenv import VecBoatEnv
+    N = 4096
+    pick = np.sort(np.random.default_rng(2).choice(N, 256, replace=False))
+    mk = lambda seeds: VecBoatEnv({"base_settings": {"experiment": 1, "test_mode": 0}}, N,  # noqa: E731
+                                  seeds=seeds, device=gpu, max_episode_steps=500)
+    ended, trunc = _subsample_run(mk, OracleConfig(experiment=1), N, 620, 500, pick, 77, 5)
+    assert trunc > 0 and ended > trunc
+
+
+def test_envs_beyond_130k_per_gpu(gpu, built_lib):
+    """131 072 envs on one GPU (round 1 capped n_pad at 130 048 by 32-bit slot-ring
+    offsets): the last owner waves, past the old cap, match the oracle."""
+    from sacenv import VecBoatEnv
+    N = 131072
+    rng = np.random.default_rng(3)
+    pick = np.sort(np.concatenate([rng.choice(130048, 64, replace=False), np.arange(N - 64, N)]))
+    mk = lambda seeds: VecBoatEnv({"base_settings": {"experiment": 6, "test_mode": 0}}, N,  # noqa: E731
+                                  seeds=seeds, device=gpu, max_episode_steps=30)
+    ended, _ = _subsample_run(mk, OracleConfig(experiment=6), N, 70, 30, pick, 9, 6)
+    assert ended >= 128
+
+
+def test_c5_mixed_32768_each_vs_oracles(gpu, built_lib):
+    """BASELINE configs[4] at its size: boat exp 6 + parachute + car, 32 768 envs each,
+    ONE launch per step; a boat subsample vs the boat oracle, every toy env vs the toy
+    oracle (auto-reset + truncation)."""
+    from sacenv import VecBoatEnv
+    from sacenv.toys import MixedBatch
+    from toy_oracle import OracleToy
+    N, S = 32768, 260
+    rng = np.random.default_rng(4)
+    seeds = np.arange(N, dtype=np.uint64) + 500
+    boat = VecBoatEnv({"base_settings": {"experiment": 6, "test_mode": 0}}, N, seeds=seeds, device=gpu,
+                      max_episode_steps=120)
+    par, car = _toy_env(1, N, max_episode_steps=110), _toy_env(2, N, max_episode_steps=130)
+    mix = MixedBatch(boat, [par, car])
+    boat.reset()
+    pick = np.sort(rng.choice(N, 192, replace=False))
+    ora = OracleVecBoat(OracleConfig(experiment=6), seeds[pick], max_episode_steps=120)
+    ora.reset()
+    toys = [OracleToy(1, N, max_episode_steps=110), OracleToy(2, N, max_episode_steps=130)]
+    for k in range(S):
+        a = rng.uniform(-1, 1, N).astype(np.float32)
+        mix.step_async(torch.from_numpy(a).to(gpu))
+        ro = ora.step(a[pick])
+        tr = [t.step() for t in toys]
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(boat.term.cpu().numpy()[pick], ro["term"], err_msg=f"step {k}")
+        np.testing.assert_allclose(boat.obs.cpu().numpy()[pick], ro["reset_obs"], rtol=OBS_TOL, atol=OBS_TOL)
+        assert np.abs(boat.s_x.cpu().numpy()[pick] - ora.s_x).max() <= STATE_TOL
+        for env, r in ((par, tr[0]), (car, tr[1])):
+            np.testing.assert_array_equal(env.term.cpu().numpy(), r["term"], err_msg=f"step {k}")
+            np.testing.assert_allclose(env.obs.cpu().numpy(), r["obs"], rtol=1e-6, atol=1e-5)
+            np.testing.assert_allclose(env.state.cpu().numpy(), r["state"], rtol=0, atol=1e-5)
+    assert boat.counters.cpu().numpy().sum() > 0

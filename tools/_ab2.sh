@@ -1,0 +1,3 @@
+set -o pipefail
+VARIANTS="base sk wg4 wg2 wg4f" BENCH_ARGS="--steps 2048 --warmup 512 --no-cpu-baseline" bash tools/ab.sh || exit 1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -15 gpurun_out/pytest_gpu.log
