@@ -67,7 +67,7 @@ def test_argument_errors_without_gpu(built_lib):
     assert built_lib.sacenv_boat_refill(ctypes.byref(p), 1, None) == -6
     # 32-bit byte offsets into wind_knots: n_pad x SLOTS x 2 x knots x 16 B < 2**32
     p.n_knots = 16
-    p.n_envs = 1 << 17
+    p.n_envs = (1 << 22) + 1  # 32-bit per-env field offsets (no slot-ring cap since round 2)
     assert built_lib.sacenv_boat_step(ctypes.byref(p), 1, 1, None) == -4
     p.n_envs = 1 << 15
     assert built_lib.sacenv_boat_step(ctypes.byref(p), None, None, None) == -1
