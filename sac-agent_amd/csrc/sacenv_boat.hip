@@ -334,10 +334,54 @@ __device__ __forceinline__ double sin_reduced(double x) {
   q = fma(q, z, 1.6666666666666666e-01);    // 1/3! (sign below)
   return fma(-(x * z), q, x);
 }
-#ifdef SACENV_SIN_POLY
+#ifndef SACENV_SIN_OCML  // A/B builds: ocml's sin everywhere (measured 0.13 us/step slower)
 #define SACENV_SIN_SMALL(x) sin_reduced(x)
 #else
 #define SACENV_SIN_SMALL(x) sin(x)
+#endif
+
+// sin and cos of x for |x| <= 1e5: k = rint(x 2/pi), r = x - k pi/2 by fma in
+// three Cody-Waite terms (each fma rounds once: r within ~1 ulp), Taylor
+// polynomials on |r| <= pi/4 (sin through r^17, cos through r^16: truncation
+// below 1e-17) and the quadrant swap. About 35 VALU against ocml's
+// double-double reduction + two polynomials. Waves with any lane beyond the
+// bound (or NaN) take ocml's sincos (a uniform branch).
+__device__ __forceinline__ void sincos_cw(double x, double* sp, double* cp) {
+  if (__ballot(!(fabs(x) <= 1.0e5)) != 0ull) {
+    sincos(x, sp, cp);
+    return;
+  }
+  const double k = rint(x * 0.6366197723675814);
+  double r = fma(-k, 1.5707963267948966, x);
+  r = fma(-k, 6.123233995736766e-17, r);
+  r = fma(-k, -1.4973849048591698e-33, r);
+  const double z = r * r;
+  double ps = 2.8114572543455206e-15;          // 1/17!
+  ps = fma(ps, z, -7.647163731819816e-13);     // -1/15!
+  ps = fma(ps, z, 1.6059043836821613e-10);     // 1/13!
+  ps = fma(ps, z, -2.505210838544172e-08);     // -1/11!
+  ps = fma(ps, z, 2.7557319223985893e-06);     // 1/9!
+  ps = fma(ps, z, -1.984126984126984e-04);     // -1/7!
+  ps = fma(ps, z, 8.333333333333333e-03);      // 1/5!
+  ps = fma(ps, z, -1.6666666666666666e-01);    // -1/3!
+  const double sr = fma(r * z, ps, r);
+  double pc = 4.779477332387385e-14;           // 1/16!
+  pc = fma(pc, z, -1.1470745597729725e-11);    // -1/14!
+  pc = fma(pc, z, 2.08767569878681e-09);       // 1/12!
+  pc = fma(pc, z, -2.755731922398589e-07);     // -1/10!
+  pc = fma(pc, z, 2.48015873015873e-05);       // 1/8!
+  pc = fma(pc, z, -1.388888888888889e-03);     // -1/6!
+  pc = fma(pc, z, 4.1666666666666664e-02);     // 1/4!
+  const double cr = 1.0 - fma(-(z * z), pc, 0.5 * z);
+  const int q = (int)k;
+  const double a = (q & 1) ? cr : sr, b = (q & 1) ? sr : cr;  // sin, cos of r + (q&1) pi/2
+  *sp = (q & 2) ? -a : a;
+  *cp = ((q + 1) & 2) ? -b : b;
+}
+#ifndef SACENV_SINCOS_OCML
+#define SACENV_SINCOS(x, s, c) sincos_cw(x, s, c)
+#else
+#define SACENV_SINCOS(x, s, c) sincos(x, s, c)
 #endif
 
 // x / c for a per-launch constant c, from r = RN(1/c): Markstein's correction
@@ -1456,7 +1500,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   const bool first = index == 0;  // integrator counter == 0 (control_blocks.py:21-22)
   const double wsign = (double)((wv > 0.0) - (wv < 0.0));
   double swa, cwa;
-  sincos(wa, &swa, &cwa);
+  SACENV_SINCOS(wa, &swa, &cwa);
 
   // eom_longitudinal :213-239
   const double F_R = v_x * v_x * p.c_r_front * 0.5 * p.rho * p.boat_area_front;
@@ -1507,7 +1551,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
   // differences: the increments agree to a few ulp of v dt.
   s_r = v_r * p.dt + s_r;
   double ssr, csr;
-  sincos(s_r, &ssr, &csr);
+  SACENV_SINCOS(s_r, &ssr, &csr);
   s_x = (v_x * csr - v_y * ssr) * p.dt + s_x;
   s_y = (v_y * csr + v_x * ssr) * p.dt + s_y;
 #endif

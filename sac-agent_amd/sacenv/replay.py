@@ -36,6 +36,8 @@ class DeviceReplayBuffer:
         self.device = torch.device(device if device is not None else "cuda")
         if self.device.type != "cuda":
             raise RuntimeError("DeviceReplayBuffer runs on a GPU (HIP); no CPU path")
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         shape = (int(input_shape),) if np.isscalar(input_shape) else tuple(int(d) for d in input_shape)
         self.input_shape = shape
         self.mem_size = int(max_size)

@@ -91,6 +91,8 @@ class VecToyEnv:
         self.device = torch.device(device if device is not None else "cuda")
         if self.device.type != "cuda":
             raise RuntimeError("VecToyEnv runs on a GPU (HIP); no CPU path")
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.autoreset = bool(autoreset)
         self.params = make_toy_params(self.kind, config, N, autoreset=autoreset,
                                       max_episode_steps=max_episode_steps)
