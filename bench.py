@@ -52,6 +52,7 @@ HBM_PEAK = 8.0e12             # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 EPISODE_STEPS = 500
 SEG = 128              # step launches per refill (sacenv _lib.REFILL_PERIOD); one graph per segment
 ACTION_STEPS = 512     # the pre-generated action table cycles every 512 steps (4 segments)
+TRANS_ROW = "58-B/env transition row (s' f32x11, reward, action, obs3_next, done, term)"
 
 
 def metric_name(args) -> str:
@@ -226,15 +227,18 @@ def load_traffic(n_envs: int, experiment: int):
 # ---------------------------------------------------------------- workload
 class Workload:
     """What the timing loop drives: ``stepper(actions_row)`` enqueues one step of
-    every env of the rank, ``refill()`` the slot refill, ``rows(k)`` the uint8
-    parts of step k's pooled row (N>1), ``envs`` the env objects."""
+    every env of the rank, ``pooled_step(k, row)`` step k writing its pooled
+    transition row (N>1; ``row_bytes`` per step), ``refill()`` the slot refill,
+    ``envs`` the env objects."""
 
-    def __init__(self, envs, stepper, refill, actions, rows, per_gpu_envs, bytes_per_launch):
+    def __init__(self, envs, stepper, refill, actions, pooled_step, row_bytes, per_gpu_envs,
+                 bytes_per_launch):
         self.envs, self.stepper, self.refill, self.actions = envs, stepper, refill, actions
-        self.rows, self.per_gpu_envs, self.bytes_per_launch = rows, per_gpu_envs, bytes_per_launch
+        self.pooled_step, self._row_bytes = pooled_step, int(row_bytes)
+        self.per_gpu_envs, self.bytes_per_launch = per_gpu_envs, bytes_per_launch
 
     def row_bytes(self) -> int:
-        return sum(p.numel() for p in self.rows(0))
+        return self._row_bytes
 
 
 def make_workload(args, rank: int, dev) -> Workload:
@@ -255,22 +259,33 @@ def make_workload(args, rank: int, dev) -> Workload:
         toys = [ParachuteEnv(num_envs=N, device=dev, max_episode_steps=args.episode_steps),
                 CarEnv(num_envs=N, device=dev, max_episode_steps=args.episode_steps)]
         envs += toys
-        stepper = MixedBatch(env, toys).step_async
+        mixed = MixedBatch(env, toys)
+        stepper = mixed.step_async
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
     actions = torch.rand((ACTION_STEPS, N), generator=g, device=dev, dtype=torch.float32) * 2 - 1
     lay = TransitionLayout(N, env.n_pad)
+    toy_bytes = [t.record.numel() + t.final_obs_bytes.numel() for t in toys]
+    row_bytes = lay.nbytes + sum(toy_bytes)
 
-    def rows(k: int):
-        # the boat's full transition (record | action | terminal obs), then each toy's
-        # record and terminal obs (open-loop toys take no action)
-        parts = lay.parts(env.record, actions[k % ACTION_STEPS], env.final_obs_bytes)
-        for t in toys:
-            parts += [t.record, t.final_obs_bytes]
-        return parts
+    def pooled_step(k: int, row: torch.Tensor):
+        # the boat's transition row, written by the step launch itself into the
+        # pooling buffer (sacenv_boat_step_pooled / sacenv_mixed_step_pooled);
+        # the toys' records and terminal obs copied behind it (open-loop toys
+        # take no action, and a fresh toy's first obs is fixed)
+        a = actions[k % ACTION_STEPS]
+        if toys:
+            mixed.step_async(a, row[: lay.nbytes])
+            o = lay.nbytes
+            for t in toys:
+                for part in (t.record, t.final_obs_bytes):
+                    row[o: o + part.numel()].copy_(part)
+                    o += part.numel()
+        else:
+            env.step_pooled_async(a, row[: lay.nbytes])
 
     bytes_launch = BYTES_PER_ENV_STEP * N + (sum(TOY_BYTES.values()) * N if args.mixed else 0)
-    return Workload(envs, stepper, refill, actions, rows, N * len(envs), bytes_launch)
+    return Workload(envs, stepper, refill, actions, pooled_step, row_bytes, N * len(envs), bytes_launch)
 
 
 # ---------------------------------------------------------------- timing loop
@@ -294,9 +309,10 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
         # thread captures must not invalidate the capture
         with torch.cuda.graph(gr, capture_error_mode="thread_local"):
             for j, k in enumerate(range(k0, k0 + SEG)):
-                wl.stepper(wl.actions[k % ACTION_STEPS])
                 if with_pool:
-                    pool.stage_row(j, wl.rows(k), buf)
+                    wl.pooled_step(k, pool.row(j, buf))
+                else:
+                    wl.stepper(wl.actions[k % ACTION_STEPS])
         return gr
 
     graphs = None
@@ -330,9 +346,10 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
             gset[p.buf if p is not None else 0].replay()
         else:
             for j, k in enumerate(range(k0, k0 + SEG)):
-                wl.stepper(wl.actions[k % ACTION_STEPS])
                 if p is not None:
-                    p.stage_row(j, wl.rows(k))
+                    wl.pooled_step(k, p.row(j))
+                else:
+                    wl.stepper(wl.actions[k % ACTION_STEPS])
         if timed:
             eb.record(st)
             seg_events.append((ea, eb))
@@ -424,14 +441,16 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
                    "experiment": args.experiment, "envs_per_gpu": wl.per_gpu_envs,
                    "global_envs": world * wl.per_gpu_envs,
                    "episode_steps": args.episode_steps, "parallelism": f"env-dp{world}",
-                   "collective": (f"all_gather of each step's full transitions (record 50 B + action 4 B + "
-                                  f"terminal obs 44 B per env, {wl.row_bytes()} B per rank-step): one "
+                   "collective": (f"all_gather of each step's full transitions (the {TRANS_ROW} written by the "
+                                  f"step kernel, {wl.row_bytes()} B per rank-step): one "
                                   f"{backend} all_gather per {SEG}-step segment ({gathers_timed} in the "
                                   "timed region) on a side stream, overlapped with the next segment")
                    if pool is not None else (
                        "none: sharded per-GPU replay (--pooling none)" if world > 1 else None),
                    "launch": (f"hipGraph segments of {SEG} k_step launches" +
-                              (" (+ the pooled-row copies per step)" if pool is not None else "") +
+                              (" (sacenv_boat_step_pooled: the step writes its pooled row)"
+                               if pool is not None and not args.mixed else
+                               " (+ the pooled-row copies per step)" if pool is not None else "") +
                               " + the 3 refill launches" if use_graph else "eager"),
                    "refill": (f"k_need_masks + k_refill + k_refill_fit after every {SEG}-step segment, "
                               "inside the timed region") if not args.no_autoreset else None},

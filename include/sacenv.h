@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SACENV_ABI_VERSION 9
+#define SACENV_ABI_VERSION 10
 #define SACENV_OBS_DIM 11      /* Boat.return_state, boat_env.py:308-323 */
 #define SACENV_MT_N 624        /* MT19937 words per env (numpy legacy RNG) */
 #define SACENV_MAX_KNOTS 16    /* wind.fixed_points upper bound */
@@ -43,6 +43,7 @@ extern "C" {
 #define SACENV_SLOTS 129       /* episode slots per env in autoreset mode (active + 128 ahead) */
 #define SACENV_REFILL_PERIOD 128 /* autoreset: at most this many step launches between refills */
 #define SACENV_RECORD_BYTES 50 /* packed per-env step record (see layout.record) */
+#define SACENV_TRANS_BYTES 58  /* per-env transition row of sacenv_boat_step_pooled */
 
 /* termination codes; 1..5 follow the info-dict key order boat_env.py:24-32,
  * the chain's priority stays goal > oob > fuel > timeout > rudder (:84-105). */
@@ -205,6 +206,26 @@ int sacenv_boat_reset_explicit(const SacenvBoatParams *p, void *arena, const int
  * work on the step's path); sacenv_boat_refill replaces them. */
 int sacenv_boat_step(const SacenvBoatParams *p, void *arena, const float *action, void *stream);
 
+/* sacenv_boat_step that also writes the step's transitions for a pooled
+ * replay buffer (main.py:81-88 -> agent/buffer.py:13-22) to
+ * the device row `trans` (SACENV_TRANS_BYTES x n_pad bytes, 16-B aligned):
+ *   s'       f32 [n_pad][11]  obs after the step, BEFORE any auto-reset (the
+ *                             terminal obs of envs that ended)
+ *   reward   f32 [n_pad]
+ *   action   f32 [n_pad]      the step's action
+ *   obs3_next f32 [n_pad]     envs that auto-reset: obs[3] (normalised s_y)
+ *                             of the new episode's first obs (its other
+ *                             entries are fixed by the config: the first obs
+ *                             of a fresh Boat, boat_env.py:152-198)
+ *   done     u8  [n_pad]
+ *   term     u8  [n_pad]
+ * The previous step's transition row gives each env's s: s' of that row, or
+ * for envs that ended there the fresh-Boat obs with obs3_next. 58 B per env
+ * instead of the record + action + terminal obs (98 B), written by the step
+ * launch itself (no copy launches). */
+int sacenv_boat_step_pooled(const SacenvBoatParams *p, void *arena, const float *action, void *trans,
+                            void *stream);
+
 /* n_steps sacenv_boat_step calls fused into one launch: replaces n_steps
  * calls of BoatEnv.step (environment/boat_env.py:67-115) with known actions,
  * the loop of main.py:70-114 when the actions are known ahead (SURVEY.md
@@ -292,6 +313,11 @@ int sacenv_toy_step(const SacenvToyParams *p, void *arena, void *stream);
 int sacenv_mixed_step(const SacenvBoatParams *bp, void *boat_arena, const float *boat_action,
                       const SacenvToyParams *toy_params, void *const *toy_arenas, int32_t n_toys,
                       void *stream);
+/* sacenv_mixed_step whose boat waves also write the boat's transition row
+ * (sacenv_boat_step_pooled's format) to trans; bp must not be NULL. */
+int sacenv_mixed_step_pooled(const SacenvBoatParams *bp, void *boat_arena, const float *boat_action,
+                             const SacenvToyParams *toy_params, void *const *toy_arenas, int32_t n_toys,
+                             void *trans, void *stream);
 
 /* ------------------------------------------------------------------------
  * Device replay buffer: agent/buffer.py:3-35 ReplayBuffer (SURVEY.md §8(f)

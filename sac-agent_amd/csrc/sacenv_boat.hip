@@ -1347,7 +1347,7 @@ template <bool kRoll, int kNc, bool kTIdx>
 __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Arena& A, const Tail& T,
                                            const float* __restrict__ action, OwnerLds& l, int ob,
                                            int lane, int n_steps = 1, char* roll_rec = nullptr,
-                                           float* roll_fin = nullptr) {
+                                           float* roll_fin = nullptr, char* trans = nullptr) {
 #ifdef SACENV_STAMPS
   const uint64_t st_real0 = __builtin_amdgcn_s_memrealtime();
   uint64_t st_loaded = 0, st_computed = 0;
@@ -1694,6 +1694,25 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& p, const Aren
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
+  if (!kRoll && trans != nullptr) {  // the pooled transition row (sacenv_boat_step_pooled)
+    // s' = the pre-reset obs: only restarting lanes' LDS rows differ from it
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (restart) {
+#pragma unroll
+      for (int k = 0; k < SACENV_OBS_DIM; ++k) l.obs[lane * SACENV_OBS_DIM + k] = o.v[k];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    store_obs_block(l.obs, reinterpret_cast<float*>(trans) + row0, lane);
+    st_rec(*reinterpret_cast<float*>(trans + 44 * A.np + eo4), (float)reward);
+    st_rec(*reinterpret_cast<float*>(trans + 48 * A.np + eo4), act);
+    st_rec(*reinterpret_cast<float*>(trans + 52 * A.np + eo4), restart ? fo.v[3] : 0.0f);
+    st_rec(*reinterpret_cast<uint8_t*>(trans + 56 * A.np + e), (uint8_t)(ended ? 1 : 0));
+    st_rec(*reinterpret_cast<uint8_t*>(trans + 57 * A.np + e), term);
+  }
   }  // steps
   if (kRoll) {  // the carried state, once
     A.f64e(U_SX, eo) = s_x, A.f64e(U_SY, eo) = s_y, A.f64e(U_SR, eo) = s_r;
@@ -1747,7 +1766,7 @@ struct StepLds {
 template <bool kMixed, int kNc, bool kTIdx>
 __global__ void __launch_bounds__(kWave * kStepWaves) k_step(SacenvBoatParams p, Arena A, Tail T,
                                                 const float* __restrict__ action, int nb_boat,
-                                                MixedToys M) {
+                                                MixedToys M, char* __restrict__ trans) {
   __shared__ StepLds slds;
   const int lane = threadIdx.x & (kWave - 1), wv = kStepWaves > 1 ? (int)(threadIdx.x >> 6) : 0;
   int b = (int)blockIdx.x * kStepWaves + wv;
@@ -1756,7 +1775,8 @@ __global__ void __launch_bounds__(kWave * kStepWaves) k_step(SacenvBoatParams p,
 #endif
   if (!kMixed || b < nb_boat) {
     if (kStepWaves > 1 && b >= nb_boat) return;
-    owner_wave<false, kNc, kTIdx>(vreg_params(p), A, vreg_tail(T), action, slds.w[wv], b, lane);
+    owner_wave<false, kNc, kTIdx>(vreg_params(p), A, vreg_tail(T), action, slds.w[wv], b, lane, 1,
+                                  nullptr, nullptr, trans);
     return;
   }
   b -= nb_boat;
@@ -1977,7 +1997,7 @@ static int owner_curves(const SacenvBoatParams& p) { return p.use_wind_table ? 0
     default: LAUNCH(2, true); break;                                      \
   }
 
-int sacenv_boat_step(const SacenvBoatParams* p, void* arena, const float* action, void* stream) {
+static int boat_step(const SacenvBoatParams* p, void* arena, const float* action, char* trans, void* stream) {
   int rc = check_params(p);
   if (rc) return rc;
   if (arena == nullptr || action == nullptr) return SACENV_E_NULL;
@@ -1985,10 +2005,21 @@ int sacenv_boat_step(const SacenvBoatParams* p, void* arena, const float* action
   const int grid = (nb_boat + kStepWaves - 1) / kStepWaves;
 #define SACENV_LAUNCH(NC, TI)                                                                         \
   hipLaunchKernelGGL((k_step<false, NC, TI>), dim3(grid), dim3(kWave * kStepWaves), 0, (hipStream_t)stream, *p, \
-                     make_arena(*p, arena), make_tail(*p, arena), action, nb_boat, MixedToys{})
+                     make_arena(*p, arena), make_tail(*p, arena), action, nb_boat, MixedToys{}, trans)
   SACENV_OWNER_DISPATCH(*p, SACENV_LAUNCH)
 #undef SACENV_LAUNCH
   return launch_status();
+}
+
+int sacenv_boat_step(const SacenvBoatParams* p, void* arena, const float* action, void* stream) {
+  return boat_step(p, arena, action, nullptr, stream);
+}
+
+int sacenv_boat_step_pooled(const SacenvBoatParams* p, void* arena, const float* action, void* trans,
+                            void* stream) {
+  if (trans == nullptr) return SACENV_E_NULL;
+  if ((reinterpret_cast<uintptr_t>(trans) & 15u) != 0u) return SACENV_E_RANGE;  // float4 row stores
+  return boat_step(p, arena, action, static_cast<char*>(trans), stream);
 }
 
 int sacenv_boat_rollout(const SacenvBoatParams* p, void* arena, const float* actions, int32_t n_steps,
@@ -2068,9 +2099,9 @@ int sacenv_toy_step(const SacenvToyParams* p, void* arena, void* stream) {
   return launch_status();
 }
 
-int sacenv_mixed_step(const SacenvBoatParams* bp, void* boat_arena, const float* boat_action,
+static int mixed_step(const SacenvBoatParams* bp, void* boat_arena, const float* boat_action,
                       const SacenvToyParams* toy_params, void* const* toy_arenas, int32_t n_toys,
-                      void* stream) {
+                      char* trans, void* stream) {
   int rc;
   if (n_toys < 0 || n_toys > 2) return SACENV_E_SIZE;
   if (n_toys > 0 && (toy_params == nullptr || toy_arenas == nullptr)) return SACENV_E_NULL;
@@ -2101,10 +2132,25 @@ int sacenv_mixed_step(const SacenvBoatParams* bp, void* boat_arena, const float*
   if (nb == 0) return SACENV_OK;
   const int grid = (nb + kStepWaves - 1) / kStepWaves;
 #define SACENV_LAUNCH(NC, TI) \
-  hipLaunchKernelGGL((k_step<true, NC, TI>), dim3(grid), dim3(kWave * kStepWaves), 0, (hipStream_t)stream, p, A, T, boat_action, nb_boat, M)
+  hipLaunchKernelGGL((k_step<true, NC, TI>), dim3(grid), dim3(kWave * kStepWaves), 0, (hipStream_t)stream, p, A, T, boat_action, nb_boat, M, trans)
   SACENV_OWNER_DISPATCH(p, SACENV_LAUNCH)
 #undef SACENV_LAUNCH
   return launch_status();
+}
+
+int sacenv_mixed_step(const SacenvBoatParams* bp, void* boat_arena, const float* boat_action,
+                      const SacenvToyParams* toy_params, void* const* toy_arenas, int32_t n_toys,
+                      void* stream) {
+  return mixed_step(bp, boat_arena, boat_action, toy_params, toy_arenas, n_toys, nullptr, stream);
+}
+
+int sacenv_mixed_step_pooled(const SacenvBoatParams* bp, void* boat_arena, const float* boat_action,
+                             const SacenvToyParams* toy_params, void* const* toy_arenas, int32_t n_toys,
+                             void* trans, void* stream) {
+  if (bp == nullptr || trans == nullptr) return SACENV_E_NULL;
+  if ((reinterpret_cast<uintptr_t>(trans) & 15u) != 0u) return SACENV_E_RANGE;
+  return mixed_step(bp, boat_arena, boat_action, toy_params, toy_arenas, n_toys, static_cast<char*>(trans),
+                    stream);
 }
 
 int sacenv_boat_wind_eval(const SacenvBoatParams* p, const void* arena, const int32_t* env_ids,

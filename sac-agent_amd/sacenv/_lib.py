@@ -11,7 +11,7 @@ import os
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # .../sac-agent_amd
 LIB_PATH = os.environ.get("SACENV_LIB", os.path.join(PKG_ROOT, "build", "libsacenv.so"))
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 OBS_DIM = 11
 MT_N = 624
 MAX_KNOTS = 16
@@ -20,6 +20,7 @@ SLOTS = 129
 REFILL_PERIOD = 128  # autoreset: step launches allowed between sacenv_boat_refill calls
 STATUS_SLOT_UNDERFLOW = 1
 RECORD_BYTES = 50
+TRANS_BYTES = 58  # sacenv_boat_step_pooled's per-env transition row
 
 TERM_NONE, TERM_REACHED_GOAL, TERM_OUT_OF_BOUNDS, TERM_OUT_OF_FUEL, \
     TERM_RUDDER_BROKEN, TERM_TIMEOUT, TERM_TRUNCATED = range(7)
@@ -103,8 +104,8 @@ class ReplayLayout(C.Structure):
 
 EXPORTS = ("sacenv_abi_version", "sacenv_error_string", "sacenv_boat_layout",
            "sacenv_boat_init", "sacenv_boat_reset", "sacenv_boat_reset_explicit",
-           "sacenv_boat_step", "sacenv_boat_rollout", "sacenv_boat_refill", "sacenv_boat_wind_eval", "sacenv_toy_layout", "sacenv_toy_init",
-           "sacenv_toy_reset", "sacenv_toy_step", "sacenv_mixed_step", "sacenv_replay_layout",
+           "sacenv_boat_step", "sacenv_boat_step_pooled", "sacenv_boat_rollout", "sacenv_boat_refill", "sacenv_boat_wind_eval", "sacenv_toy_layout", "sacenv_toy_init",
+           "sacenv_toy_reset", "sacenv_toy_step", "sacenv_mixed_step", "sacenv_mixed_step_pooled", "sacenv_replay_layout",
            "sacenv_replay_init", "sacenv_replay_store", "sacenv_replay_store_env", "sacenv_replay_sample",
            "sacenv_compact_done", "sacenv_boat_reset_list")
 
@@ -141,6 +142,7 @@ def load(path: str | None = None):
         "sacenv_boat_reset": (C.c_int, [P, _p, _p, _i32, _p]),
         "sacenv_boat_reset_explicit": (C.c_int, [P, _p, _p, _i32, _p, _p, _p]),
         "sacenv_boat_step": (C.c_int, [P, _p, _p, _p]),
+        "sacenv_boat_step_pooled": (C.c_int, [P, _p, _p, _p, _p]),
         "sacenv_boat_refill": (C.c_int, [P, _p, _p]),
         "sacenv_boat_rollout": (C.c_int, [P, _p, _p, _i32, _p, _p, _p]),
         "sacenv_boat_wind_eval": (C.c_int, [P, _p, _p, _p, _i32, _p, _p, _p]),
@@ -149,6 +151,7 @@ def load(path: str | None = None):
         "sacenv_toy_reset": (C.c_int, [TP, _p, _p, _i32, _p]),
         "sacenv_toy_step": (C.c_int, [TP, _p, _p]),
         "sacenv_mixed_step": (C.c_int, [P, _p, _p, TP, C.POINTER(_p), _i32, _p]),
+        "sacenv_mixed_step_pooled": (C.c_int, [P, _p, _p, TP, C.POINTER(_p), _i32, _p, _p]),
         "sacenv_compact_done": (C.c_int, [_p, _i32, _p, _p, _p]),
         "sacenv_boat_reset_list": (C.c_int, [P, _p, _p, _p, _p]),
         "sacenv_replay_layout": (C.c_int, [RP, C.POINTER(ReplayLayout)]),

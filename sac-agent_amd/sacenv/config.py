@@ -186,5 +186,19 @@ def observation_bounds():
     return low, high
 
 
-__all__ = ["BoatConfig", "make_params", "spline_g", "observation_bounds", "t_from_index"]
+def first_obs_template(cfg: BoatConfig) -> np.ndarray:
+    """Boat.return_state of a fresh Boat (boat_env.py:152-198, :308-326) as the step
+    kernel writes it (f32): every state value 0 but fuel = fuel0; entry 3 is
+    (s_y + W) / 2W = 0.5 at s_y = 0 (experiment 2 starts at its start y: the
+    pooled transition row carries that entry as obs3_next)."""
+    rud0 = np.float32((0.0 + np.pi / 3) * (1.0 / (np.pi / 3 - (-np.pi / 3))))
+    with np.errstate(invalid="ignore", divide="ignore"):
+        fuel = np.float64(cfg.fuel) / np.float64(cfg.fuel) if cfg.fuel else np.float64(np.nan)
+    t = np.zeros(11, np.float32)
+    t[3], t[9], t[10] = 0.5, rud0, np.float32(fuel)
+    return t
+
+
+__all__ = ["BoatConfig", "make_params", "spline_g", "observation_bounds", "t_from_index",
+           "first_obs_template"]
 _ = fields  # keep dataclasses import explicit for readers

@@ -13,11 +13,13 @@ so the gather needs no packing kernel. Over RCCL (backend "nccl") this is
 ``all_gather_into_tensor``; gloo (CPU tests) falls back to list all_gather.
 
 The shared replay buffer consumes whole transitions (s, a, r, s', terminal)
-(main.py:83-88, agent/buffer.py:13-22), so the pooled row of a step is the
-record plus the step's action and the terminal-obs region
-(``TransitionLayout``): for an env that ended (and auto-reset) the record's
-obs is already the NEXT episode's first obs, and s' is ``final_obs``.
-``TransitionStream`` turns consecutive pooled rows back into transitions.
+(main.py:83-88, agent/buffer.py:13-22). The record alone cannot form them:
+for an env that ended (and auto-reset) its obs is already the NEXT episode's
+first obs. The pooled row of a step is the transition row the step kernel
+writes itself (``sacenv_boat_step_pooled``, ``TransitionLayout``: s' before
+the reset, reward, action, done, term and the one obs entry a fresh Boat does
+not fix, 58 B per env); ``TransitionStream`` turns consecutive pooled rows
+back into (s, a, r, s', code).
 """
 from __future__ import annotations
 
@@ -25,6 +27,7 @@ from dataclasses import dataclass
 
 import torch
 
+from ._lib import TRANS_BYTES
 from .vec_env import RECORD_BYTES
 
 
@@ -69,57 +72,41 @@ class RecordLayout:
 
 @dataclass(frozen=True)
 class TransitionLayout:
-    """One rank's pooled row for one step: the packed record (n_pad rows, the
-    kernel's layout), the step's action (f32 x n) and the terminal-obs region
-    (f32 x 11 x n_pad; rows valid where done):
+    """One rank's pooled row for one step, as ``sacenv_boat_step_pooled`` writes it
+    (SACENV_TRANS_BYTES = 58 per env, per-field arrays of n_pad entries):
 
-        [ record 50 n_pad | action 4 n | final_obs 44 n_pad ]
+        [ s' f32 [n_pad][11] | reward f32 | action f32 | obs3_next f32 | done u8 | term u8 ]
+
+    s' is the obs BEFORE any auto-reset (the terminal obs of envs that ended);
+    the next transition's s of such an env is the fresh-Boat obs
+    (``first_obs_template``) with entry 3 = obs3_next.
     """
     n: int       # envs per rank
     n_pad: int   # the arena's padded row count (n rounded up to 64)
 
     @property
     def nbytes(self) -> int:
-        return (RECORD_BYTES + 44) * self.n_pad + 4 * self.n
-
-    def parts(self, record: torch.Tensor, action: torch.Tensor, final_obs_bytes: torch.Tensor):
-        """The uint8 tensors that fill one row, in order (``SegmentPool.stage_row``)."""
-        a = action.reshape(-1)
-        if a.dtype != torch.float32 or a.numel() != self.n:
-            raise ValueError("action must be f32 with one value per env")
-        parts = [record, a.view(torch.uint8), final_obs_bytes]
-        if sum(p.numel() for p in parts) != self.nbytes:
-            raise ValueError("record / final_obs regions do not match the layout")
-        return parts
+        return TRANS_BYTES * self.n_pad
 
     def views(self, row: torch.Tensor):
-        """(obs [n,11], reward [n], done [n], term [n], action [n], final_obs [n,11])."""
+        """(s' [n,11], reward [n], action [n], obs3_next [n], done [n], term [n])."""
         n, NP = self.n, self.n_pad
         if row.dtype != torch.uint8 or row.numel() != self.nbytes:
             raise ValueError("row must be uint8 of TransitionLayout.nbytes")
-        rec = row[: RECORD_BYTES * NP]
-        obs = rec[: 44 * NP].view(torch.float32).view(NP, 11)[:n]
-        reward = rec[44 * NP: 48 * NP].view(torch.float32)[:n]
-        done, term = rec[48 * NP: 49 * NP][:n], rec[49 * NP: 50 * NP][:n]
-        o = RECORD_BYTES * NP
-        action = row[o: o + 4 * n].view(torch.float32)
-        fin = row[o + 4 * n:].view(torch.float32).view(NP, 11)[:n]
-        return obs, reward, done, term, action, fin
+        f = lambda a, b: row[a * NP: b * NP].view(torch.float32)[:n]  # noqa: E731
+        s_next = row[: 44 * NP].view(torch.float32).view(NP, 11)[:n]
+        return (s_next, f(44, 48), f(48, 52), f(52, 56), row[56 * NP: 57 * NP][:n],
+                row[57 * NP: 58 * NP][:n])
 
-    def pack(self, obs, reward, done, term, action, final_obs) -> torch.Tensor:
+    def pack(self, s_next, reward, action, obs3_next, done, term) -> torch.Tensor:
         """Host-side packing (tests, and hosts without the kernel's buffers)."""
-        row = torch.zeros(self.nbytes, dtype=torch.uint8, device=obs.device)
-        o, r, d, t, a, f = self.views(row)
-        o.copy_(obs.to(torch.float32))
-        r.copy_(reward.to(torch.float32))
-        d.copy_(done.to(torch.uint8))
-        t.copy_(term.to(torch.uint8))
-        a.copy_(action.to(torch.float32).reshape(-1))
-        f.copy_(final_obs.to(torch.float32))
+        row = torch.zeros(self.nbytes, dtype=torch.uint8, device=s_next.device)
+        for dst, src in zip(self.views(row), (s_next, reward, action, obs3_next, done, term)):
+            dst.copy_(src.reshape(dst.shape).to(dst.dtype))
         return row
 
     def unpack_gathered(self, gathered: torch.Tensor, world: int):
-        """Global (obs, reward, done, term, action, final_obs) in global env-id order."""
+        """Global (s', reward, action, obs3_next, done, term) in global env-id order."""
         parts = [self.views(gathered[r * self.nbytes:(r + 1) * self.nbytes]) for r in range(world)]
         return tuple(torch.cat([p[i] for p in parts]) for i in range(6))
 
@@ -127,22 +114,27 @@ class TransitionLayout:
 class TransitionStream:
     """Pooled rows of consecutive steps -> (s, a, r, s', code) of every global env.
 
-    ``s`` is the obs the action was taken on: the previous step's pooled obs
-    (for an env that ended last step, already its new episode's first obs), or
-    the reset obs for the first step. ``s'`` is the step's obs, or the terminal
-    obs for envs that ended (done) this step. ``code`` is the term code (the
-    replay buffer derives terminal from it, main.py:83-88)."""
+    ``s`` is the obs the action was taken on: the previous step's s', or for an
+    env that ended there the first obs of its new episode (``first_obs``, the
+    fresh-Boat template, with entry 3 = that row's obs3_next); the reset obs
+    for the first step. ``s'`` is the step's obs before any auto-reset.
+    ``code`` is the term code (the replay buffer derives terminal from it,
+    main.py:83-88)."""
 
-    def __init__(self, layout: TransitionLayout, world: int, reset_obs: torch.Tensor):
+    def __init__(self, layout: TransitionLayout, world: int, reset_obs: torch.Tensor,
+                 first_obs: torch.Tensor):
         self.layout, self.world = layout, int(world)
         self.prev = reset_obs.to(torch.float32).clone()
+        self.first = first_obs.to(torch.float32).to(self.prev.device).reshape(1, -1)
 
     def push(self, gathered_row: torch.Tensor):
-        obs, reward, done, term, action, fin = self.layout.unpack_gathered(gathered_row, self.world)
+        s_next, reward, action, obs3, done, term = self.layout.unpack_gathered(gathered_row, self.world)
         s = self.prev
-        s_next = torch.where(done.bool()[:, None], fin, obs)
-        self.prev = obs.clone()
-        return s, action.clone(), reward.clone(), s_next, term.clone()
+        d = done.bool()[:, None]
+        fresh = self.first.expand_as(s_next).clone()
+        fresh[:, 3] = obs3
+        self.prev = torch.where(d, fresh, s_next)
+        return s, action.clone(), reward.clone(), s_next.clone(), term.clone()
 
 
 def gather_records(record: torch.Tensor, out: torch.Tensor | None = None, group=None) -> torch.Tensor:
@@ -194,6 +186,11 @@ class SegmentPool:
         """Before writing row 0 of the current buffer: its previous gather is done."""
         if self.fill == 0 and self.done[self.buf] is not None:
             self._cur().wait_event(self.done[self.buf])
+
+    def row(self, j: int, buf: int | None = None) -> torch.Tensor:
+        """Row j of the current (or given) staging buffer, for kernels that write it."""
+        b = self.buf if buf is None else buf
+        return self.stage[b][j * self.rb:(j + 1) * self.rb]
 
     def stage_row(self, j: int, records, buf: int | None = None) -> None:
         """Copy one step's packed record(s) (uint8 tensors, concatenated) into row j."""

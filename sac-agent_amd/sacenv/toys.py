@@ -177,7 +177,9 @@ class MixedBatch:
     def num_envs(self) -> int:
         return (self.boat.num_envs if self.boat is not None else 0) + sum(t.num_envs for t in self.toys)
 
-    def step_async(self, boat_actions=None) -> None:
+    def step_async(self, boat_actions=None, trans_row=None) -> None:
+        """One heterogeneous launch; ``trans_row`` (boat only): the boat's pooled
+        transition row as ``VecBoatEnv.step_pooled_async`` writes it."""
         b = self.boat
         stream = (b if b is not None else self.toys[0]).stream
         if b is not None:
@@ -187,9 +189,19 @@ class MixedBatch:
             a = a.reshape(b.num_envs).contiguous()
             b.check_actions(a)
             self._keep = a
-        _lib.check(self.lib.sacenv_mixed_step(
-            b._pp if b is not None else None, b.arena.data_ptr() if b is not None else None,
-            a.data_ptr() if b is not None else None, self._tp, self._ta, len(self.toys), stream))
+        if trans_row is not None:
+            if b is None:
+                raise ValueError("a transition row needs the boat env")
+            if (trans_row.dtype != torch.uint8 or trans_row.device != b.device or not trans_row.is_contiguous()
+                    or trans_row.numel() != _lib.TRANS_BYTES * b.n_pad):
+                raise ValueError("trans_row must be a contiguous uint8 device tensor of TRANS_BYTES * n_pad bytes")
+            _lib.check(self.lib.sacenv_mixed_step_pooled(
+                b._pp, b.arena.data_ptr(), a.data_ptr(), self._tp, self._ta, len(self.toys),
+                trans_row.data_ptr(), stream))
+        else:
+            _lib.check(self.lib.sacenv_mixed_step(
+                b._pp if b is not None else None, b.arena.data_ptr() if b is not None else None,
+                a.data_ptr() if b is not None else None, self._tp, self._ta, len(self.toys), stream))
         if b is not None:
             b._after_step()
 

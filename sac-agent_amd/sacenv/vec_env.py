@@ -233,6 +233,26 @@ class VecBoatEnv:
         _lib.check(self.lib.sacenv_boat_step(self._pp, self._ptr, actions.data_ptr(), self.stream))
         self._after_step()
 
+    def step_pooled_async(self, actions: torch.Tensor, trans_row: torch.Tensor) -> None:
+        """``step_async`` that also writes the step's transition row (s', reward,
+        action, obs3_next, done, term; ``sacenv_boat_step_pooled``) into ``trans_row``,
+        a 16-B aligned uint8 device tensor of ``_lib.TRANS_BYTES * n_pad`` bytes
+        (e.g. a row of a pooling buffer: no copy launches)."""
+        self.check_actions(actions)
+        if (trans_row.dtype != torch.uint8 or trans_row.device != self.device
+                or trans_row.numel() != _lib.TRANS_BYTES * self.n_pad or not trans_row.is_contiguous()):
+            raise ValueError("trans_row must be a contiguous uint8 device tensor of TRANS_BYTES * n_pad bytes")
+        _lib.check(self.lib.sacenv_boat_step_pooled(self._pp, self._ptr, actions.data_ptr(),
+                                                    trans_row.data_ptr(), self.stream))
+        self._after_step()
+
+    def first_obs_template(self) -> torch.Tensor:
+        """The first obs of a fresh Boat (boat_env.py:152-198 -> return_state) as the
+        kernel writes it, f32 [11]; entry 3 (normalised s_y) depends on the start y in
+        experiment 2 (the transition row's obs3_next carries it)."""
+        from .config import first_obs_template
+        return torch.from_numpy(first_obs_template(self.cfg))
+
     def rollout(self, actions, records=None, final_obs=None):
         """``K`` steps in one launch for an open-loop action sequence ``actions``
         [K, N] (f32, device): the same results as K ``step`` calls, bit for bit.

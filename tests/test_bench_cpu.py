@@ -46,11 +46,13 @@ def _workload(bench, rank):
     actions = torch.rand((bench.ACTION_STEPS, N_ENVS), generator=torch.Generator().manual_seed(rank))
     lay = TransitionLayout(N_ENVS, N_PAD)
 
-    def rows(k):
-        return lay.parts(env.record, actions[k % bench.ACTION_STEPS], env.final_obs_bytes)
+    def pooled_step(k, row):
+        assert row.numel() == lay.nbytes
+        env.step_async(actions[k % bench.ACTION_STEPS])
+        row.fill_((env.steps * 3 + rank) % 255)
 
-    return env, bench.Workload([env], env.step_async, env.refill, actions, rows, N_ENVS,
-                               bench.BYTES_PER_ENV_STEP * N_ENVS)
+    return env, bench.Workload([env], env.step_async, env.refill, actions, pooled_step, lay.nbytes,
+                               N_ENVS, bench.BYTES_PER_ENV_STEP * N_ENVS)
 
 
 def _run(rank, world, argv):
@@ -131,7 +133,7 @@ def test_driver_command_world2_gloo_segment_pooling():
     assert out["value"] > 0
     assert "1 in the timed region" in out["config"]["collective"]
     assert "gloo" in out["config"]["collective"]
-    # the row holds record + action + terminal obs
-    assert f"{(50 + 44) * N_PAD + 4 * N_ENVS} B per rank-step" in out["config"]["collective"]
+    # the row is the step kernel's 58-B/env transition row
+    assert f"{58 * N_PAD} B per rank-step" in out["config"]["collective"]
     for _, _, steps, refills in res:
         assert steps % 128 == 0 and refills == steps // 128

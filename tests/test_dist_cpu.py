@@ -151,6 +151,7 @@ def _transition_worker(rank, world, port, seg, q):
     for p in (os.path.join(ROOT, "sac-agent_amd"), os.path.join(ROOT, "oracle")):
         sys.path.insert(0, p)
     from boat_oracle import OracleConfig, OracleVecBoat
+    from sacenv.config import BoatConfig, first_obs_template
     from sacenv.dist import SegmentPool, TransitionLayout, TransitionStream, shard
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -164,7 +165,8 @@ def _transition_worker(rank, world, port, seg, q):
         pool = SegmentPool(lay.nbytes, seg, "cpu")
         g_reset = torch.empty(world * n, 11)
         dist.all_gather(list(g_reset.chunk(world)), reset_obs)
-        stream = TransitionStream(lay, world, g_reset)
+        first = torch.from_numpy(first_obs_template(BoatConfig.from_any({"boat_env": {"track_width": 60}})))
+        stream = TransitionStream(lay, world, g_reset, first)
         acts = np.random.default_rng(0).uniform(-1, 1, (STEPS, world * N_PER_RANK)).astype(np.float32)
         out = []
 
@@ -177,10 +179,11 @@ def _transition_worker(rank, world, port, seg, q):
         for k in range(STEPS):
             r = ora.step(acts[k, off:off + n])
             t = lambda x: torch.from_numpy(np.asarray(x))  # noqa: E731
-            row = lay.pack(t(r["reset_obs"]), t(r["reward"]), t(r["done"]), t(r["term"]),
-                           t(acts[k, off:off + n]), t(r["obs"]))
-            pool.push(lay.parts(row[: 50 * 64], row[50 * 64: 50 * 64 + 4 * n].view(torch.float32),
-                                row[50 * 64 + 4 * n:]))
+            # what sacenv_boat_step_pooled writes: s' before the reset, and the new
+            # episode's obs[3] where an env restarted
+            row = lay.pack(t(r["obs"]), t(r["reward"]), t(acts[k, off:off + n]),
+                           t(r["reset_obs"][:, 3]), t(r["done"]), t(r["term"]))
+            pool.push([row])
             drain()
         pool.flush()
         drain()
@@ -194,7 +197,8 @@ def _transition_worker(rank, world, port, seg, q):
 def test_pooled_transitions_equal_single_process(world, seg):
     """N>1 pooling carries whole transitions (main.py:83-88, buffer.py:13-22): the
     pooled (s, a, r, s', code) of every global env equal a single-process run,
-    including envs that ended (s' = the terminal obs, not the next episode's)."""
+    including envs that ended (s' = the terminal obs, and the next s = the new
+    episode's first obs rebuilt from the fresh-Boat template + obs3_next)."""
     import sys
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from boat_oracle import OracleConfig, OracleVecBoat

@@ -839,3 +839,65 @@ def test_c5_mixed_32768_each_vs_oracles(gpu, built_lib):
             np.testing.assert_allclose(env.obs.cpu().numpy(), r["obs"], rtol=1e-6, atol=1e-5)
             np.testing.assert_allclose(env.state.cpu().numpy(), r["state"], rtol=0, atol=1e-5)
     assert boat.counters.cpu().numpy().sum() > 0
+
+
+# ---------------------------------------------------------------- pooled transition rows (§8(e))
+
+@pytest.mark.parametrize("exp", [2, 6])
+def test_step_pooled_row_equals_step_outputs(exp, gpu, built_lib):
+    """sacenv_boat_step_pooled = sacenv_boat_step (arena bit-identical) + the transition
+    row: s' = the pre-reset obs (final_obs where done), reward, action, done, term,
+    obs3_next = the new episode's obs[3]; TransitionStream rebuilds each next s
+    (the returned obs) exactly from consecutive rows."""
+    from sacenv import VecBoatEnv, _lib
+    from sacenv.dist import TransitionLayout, TransitionStream
+    cfg = {"base_settings": {"experiment": exp, "test_mode": 0}, "boat_env": {"track_width": 30}}
+    N = 3000
+    a_env = VecBoatEnv(cfg, N, seed=11, device=gpu, max_episode_steps=40, n_helpers=64)
+    b_env = VecBoatEnv(cfg, N, seed=11, device=gpu, max_episode_steps=40, n_helpers=64)
+    a_env.reset()
+    obs0 = b_env.reset().clone()
+    lay = TransitionLayout(N, b_env.n_pad)
+    row = torch.empty(lay.nbytes, dtype=torch.uint8, device=gpu)
+    stream = TransitionStream(lay, 1, obs0, b_env.first_obs_template())
+    g = torch.Generator(device=gpu)
+    g.manual_seed(5)
+    ended = 0
+    for k in range(150):
+        act = torch.rand(N, generator=g, device=gpu) * 2 - 1
+        a_env.step_async(act)
+        b_env.step_pooled_async(act, row)
+        torch.cuda.synchronize()
+        assert torch.equal(a_env.arena, b_env.arena), f"step {k}"
+        s_next, rew, ac, obs3, done, term = lay.views(row)
+        d = a_env.done.bool()
+        assert torch.equal(done, a_env.done) and torch.equal(term, a_env.term)
+        assert torch.equal(rew, a_env.reward) and torch.equal(ac, act)
+        assert torch.equal(s_next[d], a_env.final_obs[d]) and torch.equal(s_next[~d], a_env.obs[~d])
+        assert torch.equal(obs3[d], a_env.obs[d][:, 3])
+        s, a2, r2, sn, code = stream.push(row)
+        assert torch.equal(stream.prev, a_env.obs), f"step {k}: rebuilt next s"
+        ended += int(d.sum())
+    assert ended > 1000
+
+
+def test_mixed_step_pooled_boat_row(gpu, built_lib):
+    """The mixed launch writes the same boat transition row as the boat's own pooled step."""
+    from sacenv import VecBoatEnv, _lib
+    from sacenv.toys import MixedBatch
+    cfg = {"base_settings": {"experiment": 6, "test_mode": 0}}
+    b1 = VecBoatEnv(cfg, 1000, seed=2, device=gpu, max_episode_steps=17, n_helpers=16)
+    b2 = VecBoatEnv(cfg, 1000, seed=2, device=gpu, max_episode_steps=17, n_helpers=16)
+    mix = MixedBatch(b1, [_toy_env(1, 500, max_episode_steps=9)])
+    r1 = torch.empty(_lib.TRANS_BYTES * b1.n_pad, dtype=torch.uint8, device=gpu)
+    r2 = torch.empty_like(r1)
+    g = torch.Generator(device=gpu)
+    g.manual_seed(1)
+    for k in range(40):
+        a = torch.rand(1000, generator=g, device=gpu) * 2 - 1
+        mix.step_async(a, r1)
+        b2.step_pooled_async(a, r2)
+        torch.cuda.synchronize()
+        assert torch.equal(r1, r2), f"step {k}"
+    with pytest.raises(ValueError):
+        b2.step_pooled_async(a, r2[:-16])
