@@ -1,9 +1,14 @@
 """Reduce tools/pmc.sh's rocprofv3 output to per-launch figures for k_step.
 
-Writes gpurun_out/pmc_k_step.json: mean duration from the kernel trace, and
-per-launch FETCH_SIZE / WRITE_SIZE / TCC hit rate from the PMC passes. HBM
-bytes follow MI355X_MICROARCH.md's HBM section: FETCH_SIZE (reported in KB)
-is doubled on gfx950 (128-B requests tallied at 64 B), WRITE_SIZE taken as is.
+Writes gpurun_out/pmc_k_step.json:
+* the kernel trace's mean duration of k_step;
+* per-launch counter means for k_step and for the calibration kernels of
+  tools/probes/fetch_calib (k_calib8: k_step's 8-B/lane access pattern with
+  known bytes: 10 485 760 read, 7 864 320 written per launch);
+* HBM-side bytes per launch from the read requests split by size
+  (32 x RDREQ_32B + 64 x RDREQ_64B + 128 x RDREQ_128B) and from WRITE_SIZE,
+  each scaled by the calibration kernel's known/measured ratio, next to the
+  guide's FETCH_SIZE x 2 convention (MI355X_MICROARCH.md, HBM section).
 """
 import csv
 import glob
@@ -12,6 +17,7 @@ import os
 import sys
 
 KERNEL = "k_step"
+CALIB = {"k_calib8": (10485760.0, 7864320.0), "k_calib16": (10485760.0, 7864320.0)}
 
 
 def rows(pattern):
@@ -22,25 +28,62 @@ def rows(pattern):
     return out
 
 
+def means(prefix, out_dir, name):
+    by = {}
+    for d in sorted(glob.glob(os.path.join(out_dir, prefix + "*"))):
+        for r in rows(os.path.join(d, "**", "*counter_collection.csv")):
+            kn = r.get("Kernel_Name", "")
+            if name in kn and (name != KERNEL or "k_step<false" in kn or "k_stepILb0E" in kn):
+                by.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in by.items()}
+
+
+def read_bytes(m):
+    if "TCC_EA0_RDREQ_128B_sum" not in m:
+        return None
+    return (128 * m["TCC_EA0_RDREQ_128B_sum"] + 64 * m.get("TCC_EA0_RDREQ_64B_sum", 0.0)
+            + 32 * m.get("TCC_EA0_RDREQ_32B_sum", 0.0))
+
+
 def main(out_dir):
     res = {"kernel": KERNEL}
     st = [r for r in rows(os.path.join(out_dir, "prof_trace", "**", "*kernel_stats.csv"))
-          if KERNEL in r.get("Name", "")]
+          if KERNEL in r.get("Name", "") and "true" not in r.get("Name", "")]
     if st:
-        r = st[0]
-        res["trace_calls"] = int(r["Calls"])
-        res["trace_avg_ns"] = float(r["AverageNs"])
-        res["trace_min_ns"] = float(r.get("MinNs", "nan"))
-        res["trace_max_ns"] = float(r.get("MaxNs", "nan"))
-    for i in (1, 2, 3):
-        rr = [r for r in rows(os.path.join(out_dir, f"prof_pmc{i}", "**", "*counter_collection.csv"))
-              if KERNEL in r.get("Kernel_Name", "")]
-        by = {}
-        for r in rr:
-            by.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
-        for name, v in by.items():
-            res[name + "_mean"] = sum(v) / len(v)
-            res[name + "_n"] = len(v)
+        r = max(st, key=lambda x: int(x["Calls"]))
+        res.update(trace_kernel=r["Name"], trace_calls=int(r["Calls"]), trace_avg_ns=float(r["AverageNs"]),
+                   trace_min_ns=float(r.get("MinNs", "nan")), trace_max_ns=float(r.get("MaxNs", "nan")))
+    k = means("prof_pmc", out_dir, KERNEL)
+    res["counters_per_launch"] = k
+    cal = {n: means("calib_pmc", out_dir, n) for n in CALIB}
+    res["calibration"] = {}
+    for n, (rb, wb) in CALIB.items():
+        m = cal[n]
+        rd = read_bytes(m)
+        wr = m.get("WRITE_SIZE", 0.0) * 1024.0
+        res["calibration"][n] = {
+            "known_read_bytes": rb, "known_write_bytes": wb,
+            "sized_read_bytes": rd, "fetch_size_bytes": m.get("FETCH_SIZE", 0.0) * 1024.0,
+            "write_size_bytes": wr,
+            "read_scale": rb / rd if rd else None, "write_scale": wb / wr if wr else None}
+    c8 = res["calibration"]["k_calib8"]
+    rd = read_bytes(k)
+    wr = k.get("WRITE_SIZE", 0.0) * 1024.0
+    if rd is not None and wr:
+        rs = c8["read_scale"] or 1.0
+        ws = c8["write_scale"] or 1.0
+        res["hbm_read_bytes_per_launch"] = rd * rs
+        res["hbm_write_bytes_per_launch"] = wr * ws
+        res["hbm_bytes_per_launch"] = rd * rs + wr * ws
+        res["hbm_bytes_method"] = ("read: 32/64/128-B request counts x size; write: WRITE_SIZE; each x the "
+                                   "k_calib8 known/measured ratio (same 8-B/lane pattern)")
+        res["guide_fetch_x2_bytes"] = 2.0 * k.get("FETCH_SIZE", 0.0) * 1024.0
+    if "TCC_HIT_sum" in k:
+        h, mi = k["TCC_HIT_sum"], k.get("TCC_MISS_sum", 0.0)
+        res["l2_hit_rate"] = h / (h + mi) if h + mi else None
+    if "SQ_WAVES" in k and k["SQ_WAVES"]:
+        w = k["SQ_WAVES"]
+        res["per_wave"] = {n[3:]: v / w for n, v in k.items() if n.startswith("SQ_") and n != "SQ_WAVES"}
     bench = os.path.join(out_dir, "prof_trace_bench.json")
     if os.path.exists(bench):
         d = json.loads(open(bench).read().strip().splitlines()[-1])
@@ -48,15 +91,6 @@ def main(out_dir):
         res["experiment"] = d["config"]["experiment"]
         res["bench_kernel_avg_us"] = d["roofline"]["kernel_avg_us"]
         res["algorithmic_bytes_per_launch"] = d["roofline"]["bytes_per_launch"]
-    if "FETCH_SIZE_mean" in res and "WRITE_SIZE_mean" in res:
-        fetch = 2.0 * res["FETCH_SIZE_mean"] * 1024.0
-        write = res["WRITE_SIZE_mean"] * 1024.0
-        res["hbm_fetch_bytes_per_launch"] = fetch
-        res["hbm_write_bytes_per_launch"] = write
-        res["hbm_bytes_per_launch"] = fetch + write
-    if "TCC_HIT_sum_mean" in res:
-        h, m = res["TCC_HIT_sum_mean"], res.get("TCC_MISS_sum_mean", 0.0)
-        res["l2_hit_rate"] = h / (h + m) if h + m else None
     json.dump(res, open(os.path.join(out_dir, "pmc_k_step.json"), "w"), indent=1)
     print(json.dumps(res, indent=1))
 
