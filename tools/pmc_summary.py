@@ -48,7 +48,8 @@ def read_bytes(m):
 def main(out_dir):
     res = {"kernel": KERNEL}
     st = [r for r in rows(os.path.join(out_dir, "prof_trace", "**", "*kernel_stats.csv"))
-          if KERNEL in r.get("Name", "") and "true" not in r.get("Name", "")]
+          if KERNEL in r.get("Name", "") and "k_step<true" not in r.get("Name", "")
+          and "k_stepILb1E" not in r.get("Name", "")]
     if st:
         r = max(st, key=lambda x: int(x["Calls"]))
         res.update(trace_kernel=r["Name"], trace_calls=int(r["Calls"]), trace_avg_ns=float(r["AverageNs"]),
