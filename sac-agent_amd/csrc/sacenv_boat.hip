@@ -314,6 +314,20 @@ __device__ __forceinline__ void wind_at(const SacenvBoatParams& p, const Arena& 
   }
 }
 
+// a * b + c with c a compile-time constant: one VOP3 v_fma_f64 reading c from
+// a scalar register pair (two SALU moves, off the VALU). Written as plain
+// fma(), the compiler builds each 64-bit coefficient in the accumulator with
+// two v_mov_b32 and a v_fmac: three VALU per polynomial term instead of one.
+__device__ __forceinline__ double fma_sc(double a, double b, double c) {
+#ifndef SACENV_FMA_PLAIN
+  double r;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+  return r;
+#else
+  return fma(a, b, c);
+#endif
+}
+
 // sin(x) for |x| <= 1.25 with no argument reduction: x + x^3 P(x^2), P the
 // Taylor series through x^21 (truncation < 1e-20, below half an ulp), about
 // 12 FMAs against ocml's reduction + two polynomials + select. Waves with any
@@ -322,16 +336,15 @@ __device__ __forceinline__ double sin_reduced(double x) {
   constexpr double kBound = 1.25;
   if (__ballot(!(fabs(x) <= kBound)) != 0ull) return sin(x);
   const double z = x * x;
-  double q = -1.9572941063391262e-20;  // -1/21!
-  q = fma(q, z, 8.22063524662432950e-18);   // 1/19!
-  q = fma(q, z, -2.8114572543455206e-15);   // -1/17!
-  q = fma(q, z, 7.6471637318198164e-13);    // 1/15!
-  q = fma(q, z, -1.6059043836821613e-10);   // -1/13!
-  q = fma(q, z, 2.5052108385441720e-08);    // 1/11!
-  q = fma(q, z, -2.7557319223985893e-06);   // -1/9!
-  q = fma(q, z, 1.9841269841269841e-04);    // 1/7!
-  q = fma(q, z, -8.3333333333333333e-03);   // -1/5!
-  q = fma(q, z, 1.6666666666666666e-01);    // 1/3! (sign below)
+  double q = fma_sc(z, -1.9572941063391262e-20, 8.22063524662432950e-18);  // -1/21!, 1/19!
+  q = fma_sc(q, z, -2.8114572543455206e-15);   // -1/17!
+  q = fma_sc(q, z, 7.6471637318198164e-13);    // 1/15!
+  q = fma_sc(q, z, -1.6059043836821613e-10);   // -1/13!
+  q = fma_sc(q, z, 2.5052108385441720e-08);    // 1/11!
+  q = fma_sc(q, z, -2.7557319223985893e-06);   // -1/9!
+  q = fma_sc(q, z, 1.9841269841269841e-04);    // 1/7!
+  q = fma_sc(q, z, -8.3333333333333333e-03);   // -1/5!
+  q = fma_sc(q, z, 1.6666666666666666e-01);    // 1/3! (sign below)
   return fma(-(x * z), q, x);
 }
 #ifndef SACENV_SIN_OCML  // A/B builds: ocml's sin everywhere (measured 0.13 us/step slower)
@@ -343,9 +356,8 @@ __device__ __forceinline__ double sin_reduced(double x) {
 // sin and cos of x for |x| <= 1e5: k = rint(x 2/pi), r = x - k pi/2 by fma in
 // three Cody-Waite terms (each fma rounds once: r within ~1 ulp), Taylor
 // polynomials on |r| <= pi/4 (sin through r^17, cos through r^16: truncation
-// below 1e-17) and the quadrant swap. About 35 VALU against ocml's
-// double-double reduction + two polynomials. Waves with any lane beyond the
-// bound (or NaN) take ocml's sincos (a uniform branch).
+// below 1e-17) and the quadrant swap. Waves with any lane beyond the bound
+// (or NaN) take ocml's sincos (a uniform branch).
 __device__ __forceinline__ void sincos_cw(double x, double* sp, double* cp) {
   if (__ballot(!(fabs(x) <= 1.0e5)) != 0ull) {
     sincos(x, sp, cp);
@@ -356,22 +368,20 @@ __device__ __forceinline__ void sincos_cw(double x, double* sp, double* cp) {
   r = fma(-k, 6.123233995736766e-17, r);
   r = fma(-k, -1.4973849048591698e-33, r);
   const double z = r * r;
-  double ps = 2.8114572543455206e-15;          // 1/17!
-  ps = fma(ps, z, -7.647163731819816e-13);     // -1/15!
-  ps = fma(ps, z, 1.6059043836821613e-10);     // 1/13!
-  ps = fma(ps, z, -2.505210838544172e-08);     // -1/11!
-  ps = fma(ps, z, 2.7557319223985893e-06);     // 1/9!
-  ps = fma(ps, z, -1.984126984126984e-04);     // -1/7!
-  ps = fma(ps, z, 8.333333333333333e-03);      // 1/5!
-  ps = fma(ps, z, -1.6666666666666666e-01);    // -1/3!
+  double ps = fma_sc(z, 2.8114572543455206e-15, -7.647163731819816e-13);  // 1/17!, -1/15!
+  ps = fma_sc(ps, z, 1.6059043836821613e-10);     // 1/13!
+  ps = fma_sc(ps, z, -2.505210838544172e-08);     // -1/11!
+  ps = fma_sc(ps, z, 2.7557319223985893e-06);     // 1/9!
+  ps = fma_sc(ps, z, -1.984126984126984e-04);     // -1/7!
+  ps = fma_sc(ps, z, 8.333333333333333e-03);      // 1/5!
+  ps = fma_sc(ps, z, -1.6666666666666666e-01);    // -1/3!
   const double sr = fma(r * z, ps, r);
-  double pc = 4.779477332387385e-14;           // 1/16!
-  pc = fma(pc, z, -1.1470745597729725e-11);    // -1/14!
-  pc = fma(pc, z, 2.08767569878681e-09);       // 1/12!
-  pc = fma(pc, z, -2.755731922398589e-07);     // -1/10!
-  pc = fma(pc, z, 2.48015873015873e-05);       // 1/8!
-  pc = fma(pc, z, -1.388888888888889e-03);     // -1/6!
-  pc = fma(pc, z, 4.1666666666666664e-02);     // 1/4!
+  double pc = fma_sc(z, 4.779477332387385e-14, -1.1470745597729725e-11);  // 1/16!, -1/14!
+  pc = fma_sc(pc, z, 2.08767569878681e-09);       // 1/12!
+  pc = fma_sc(pc, z, -2.755731922398589e-07);     // -1/10!
+  pc = fma_sc(pc, z, 2.48015873015873e-05);       // 1/8!
+  pc = fma_sc(pc, z, -1.388888888888889e-03);     // -1/6!
+  pc = fma_sc(pc, z, 4.1666666666666664e-02);     // 1/4!
   const double cr = 1.0 - fma(-(z * z), pc, 0.5 * z);
   const int q = (int)k;
   const double a = (q & 1) ? cr : sr, b = (q & 1) ? sr : cr;  // sin, cos of r + (q&1) pi/2
@@ -383,6 +393,7 @@ __device__ __forceinline__ void sincos_cw(double x, double* sp, double* cp) {
 #else
 #define SACENV_SINCOS(x, s, c) sincos(x, s, c)
 #endif
+
 
 // x / c for a per-launch constant c, from r = RN(1/c): Markstein's correction
 // step returns the correctly rounded quotient, i.e. the same double as IEEE
