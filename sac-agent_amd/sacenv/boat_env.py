@@ -109,6 +109,13 @@ class BoatEnv:
         self.action_space = Box(low=-1, high=1, dtype=np.float32)
         self.low_state, self.high_state = observation_bounds()
         self.observation_space = Box(low=self.low_state, high=self.high_state, dtype=np.float32)
+        # one pinned host round trip per step: the action in, then one packed copy
+        # out (obs f32 x 11 | reward f64 | term u8) instead of three blocking reads
+        dev = self._vec.device
+        self._act_host = torch.empty(1, dtype=torch.float32).pin_memory()
+        self._act_dev = torch.empty(1, dtype=torch.float32, device=dev)
+        self._out_dev = torch.empty(53, dtype=torch.uint8, device=dev)
+        self._out_host = torch.empty(53, dtype=torch.uint8).pin_memory()
         self._new_boat()                         # boat_env.py:15
         self.boat = _BoatView(self)
 
@@ -146,13 +153,21 @@ class BoatEnv:
     def step(self, action):
         """boat_env.py:67-115 -> (state, reward, done, info)."""
         self.action = action
-        a = np.asarray(action, dtype=np.float32).reshape(-1)[:1]
-        self._vec.step_async(torch.from_numpy(a).to(self._vec.device))
-        torch.cuda.synchronize(self._vec.device)
+        v = self._vec
+        self._act_host[0] = float(np.asarray(action, dtype=np.float32).reshape(-1)[0])
+        self._act_dev.copy_(self._act_host, non_blocking=True)
+        v.step_async(self._act_dev)
+        out = self._out_dev
+        out[:44].copy_(v.obs[0].view(torch.uint8))
+        out[44:52].copy_(v.reward64[:1].view(torch.uint8))
+        out[52:].copy_(v.term[:1])
+        self._out_host.copy_(out, non_blocking=True)
+        torch.cuda.current_stream(v.device).synchronize()
         self._hs = None
-        obs = self._vec.obs[0].cpu().numpy().astype(np.float64)
-        self.reward = float(self._vec.reward64[0].item())
-        code = int(self._vec.term[0].item())
+        h = self._out_host.numpy()
+        obs = h[:44].view(np.float32).astype(np.float64)
+        self.reward = float(h[44:52].view(np.float64)[0])
+        code = int(h[52])
         done = code != _lib.TERM_NONE
         if done and code <= _lib.TERM_TIMEOUT:
             name = _lib.TERM_NAMES[code]
