@@ -1767,7 +1767,8 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
 // uniform block-index ranges.
 // kStepWaves waves per workgroup (A/B builds: SACENV_STEP_WAVES); with
 // SACENV_STEP_LDS the workgroup declares that many bytes of LDS so that at
-// most one workgroup fits a CU (one wave per SIMD).
+// most one workgroup fits a CU (one wave per SIMD). Measured: 2 waves 6.29 us,
+// 2 waves one-per-CU 6.04, 4 waves 6.09-6.12, against 5.33-5.35 for one.
 #ifndef SACENV_STEP_WAVES
 #define SACENV_STEP_WAVES 1
 #endif
