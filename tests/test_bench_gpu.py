@@ -37,3 +37,27 @@ def test_driver_bench_command():
     assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] == "port" and cb["one_core"] > 0
     with open(os.path.join(ROOT, "BASELINE.json")) as f:
         assert d["metric"] == json.load(f)["metric"]
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_gloo_on_one_device():
+    """The N>1 bench path (segment pooling of the kernel-written transition rows, max-over-
+    ranks timing) as two processes sharing the one GPU over gloo, under the launcher the
+    driver uses (torch.distributed.run). RCCL needs one device per rank; the driver's
+    8-GPU run is the RCCL one."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, SACENV_BENCH_BACKEND="gloo", SACENV_BENCH_ONE_DEVICE="1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "2", "--steps", "20", "--warmup", "5", "--envs", "8192"],
+                       capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert d["n_gpus"] == 2 and d["steps"] == 128 and d["value"] > 0
+    assert d["config"]["global_envs"] == 2 * 8192
+    assert "gloo all_gather per 128-step segment (1 in the timed region)" in d["config"]["collective"]
+    assert "58-B/env transition row" in d["config"]["collective"]
