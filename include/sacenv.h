@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SACENV_ABI_VERSION 10
+#define SACENV_ABI_VERSION 11
 #define SACENV_OBS_DIM 11      /* Boat.return_state, boat_env.py:308-323 */
 #define SACENV_MT_N 624        /* MT19937 words per env (numpy legacy RNG) */
 #define SACENV_MAX_KNOTS 16    /* wind.fixed_points upper bound */
@@ -44,6 +44,7 @@ extern "C" {
 #define SACENV_REFILL_PERIOD 128 /* autoreset: at most this many step launches between refills */
 #define SACENV_RECORD_BYTES 50 /* packed per-env step record (see layout.record) */
 #define SACENV_TRANS_BYTES 58  /* per-env transition row of sacenv_boat_step_pooled */
+#define SACENV_PAIR_STRIDE 16  /* bytes between envs in the paired f64 state fields */
 
 /* termination codes; 1..5 follow the info-dict key order boat_env.py:24-32,
  * the chain's priority stays goal > oob > fuel > timeout > rudder (:84-105). */
@@ -115,11 +116,14 @@ typedef struct SacenvBoatParams {
 typedef struct SacenvBoatLayout {
   int64_t total_bytes;
   int64_t n_pad;
-  int64_t s_x, s_y, s_r, v_x, v_y, v_r, rudder, t, ep_reward; /* f64 [n_pad] */
-  int64_t wind_coef;          /* f64 [2 curves][y0 m0 y1 m1][n_pad]: the active episode's spline piece of
-                                 the interval of the next step's wind sample (a copy of its slot's
-                                 wind_knots; a new episode starts with y0 = y(0), exact at t = 0) */
-  int64_t wind0_next;         /* f64 [2][n_pad] autoreset: the next episode's curve values at grid
+  /* Paired f64 fields: stored as 16-B pairs per env, [n_pad][2], env e's element at
+   * offset + 16 e: (s_x, s_y) (s_r, v_x) (v_y, v_r) (rudder, ep_reward). t is f64 [n_pad]. */
+  int64_t s_x, s_y, s_r, v_x, v_y, v_r, rudder, t, ep_reward;
+  int64_t wind_coef;          /* f64 pairs [2 curves][(y0, m0), (y1, m1)][n_pad][2]: the active episode's
+                                 spline piece of the interval of the next step's wind sample (a copy of
+                                 its slot's wind_knots; a new episode starts with y0 = y(0), exact at
+                                 t = 0) */
+  int64_t wind0_next;         /* f64 [n_pad][2] autoreset: the next episode's curve values at grid
                                  index 0 (copy, refreshed in each episode's first step) */
   int64_t start_y_next;       /* i32 [n_pad] autoreset: Boat.s_y_start of the next episode (same) */
   int64_t index;              /* i32 [n_pad] steps since reset; fuel = fuel0 - index */

@@ -53,11 +53,17 @@ constexpr double kPi = 3.141592653589793;  // np.pi
 // every wave's loads over up to 33 rows. U_COEF follows the carried state
 // directly: fields 0..16 are loaded as one run (owner_load).
 constexpr int U_SX = 0, U_SY = 8, U_SR = 16, U_VX = 24, U_VY = 32, U_VR = 40, U_RUD = 48,
-              U_T = 56, U_EP = 64, U_COEF = 72, U_W0N = 136, U_IDX = 152,
+              U_EP = 56, U_COEF = 64, U_W0N = 128, U_T = 144, U_IDX = 152,
               U_CONS = 156, U_FILL = 160, U_MTPOS = 164, U_SYN = 168, U_STARTY = 172,
               U_CNT = U_STARTY + 4 * kSlots,
               U_LIST = U_CNT + 4 * SACENV_N_COUNTERS, U_WIND = U_LIST + 12;
 constexpr int U_MT_BYTES = 4 * kMtN;
+// The f64 fields below U_PAIRED are stored as 16-B pairs per env, [n_pad][2]:
+// (s_x, s_y) (s_r, v_x) (v_y, v_r) (rudder, ep_reward), the spline piece as
+// (y0, m0) (y1, m1) per curve, and the two next-episode y0. A field's pair
+// block starts at (u & ~15) * n_pad and it is element (u & 8) / 8 of each
+// pair, so the step moves them with 16-B per-lane loads and stores.
+constexpr int U_PAIRED = 144;
 constexpr int64_t kWindUnits = 16LL * kSlots;  // f64 x 2 curves x slots, per knot
 
 __host__ __device__ inline int64_t pad64(int64_t n) { return (n + 63) / 64 * 64; }
@@ -66,15 +72,17 @@ __host__ __device__ inline int64_t align256(int64_t x) { return (x + 255) / 256 
 __host__ __device__ inline void compute_layout(int n, int nk, int L, int use_table, SacenvBoatLayout* o) {
   const int64_t np = pad64(n), nw = np / 64;
   o->n_pad = np;
-  o->s_x = U_SX * np;
-  o->s_y = U_SY * np;
-  o->s_r = U_SR * np;
-  o->v_x = U_VX * np;
-  o->v_y = U_VY * np;
-  o->v_r = U_VR * np;
-  o->rudder = U_RUD * np;
+  // paired fields: the offset of env 0's element; consecutive envs are 16 B apart
+  auto pair_off = [np](int u) { return (int64_t)(u & ~15) * np + (u & 8); };
+  o->s_x = pair_off(U_SX);
+  o->s_y = pair_off(U_SY);
+  o->s_r = pair_off(U_SR);
+  o->v_x = pair_off(U_VX);
+  o->v_y = pair_off(U_VY);
+  o->v_r = pair_off(U_VR);
+  o->rudder = pair_off(U_RUD);
   o->t = U_T * np;
-  o->ep_reward = U_EP * np;
+  o->ep_reward = pair_off(U_EP);
   o->wind_coef = U_COEF * np;
   o->wind0_next = U_W0N * np;
   o->start_y_next = U_SYN * np;
@@ -194,7 +202,11 @@ struct Arena {
   __device__ __forceinline__ T& at_s(int u, uint32_t off) const {
     return *reinterpret_cast<T*>(b + ((uint32_t)u * (uint32_t)np + off));
   }
-  __device__ __forceinline__ double& f64e(int u, uint32_t eo) const { return at_s<double>(u, eo); }
+  __device__ __forceinline__ double& f64e(int u, uint32_t eo) const {
+    return u < U_PAIRED ? at_s<double>(u & ~15, 2u * eo + (uint32_t)(u & 8)) : at_s<double>(u, eo);
+  }
+  // the pair whose block starts at unit u (16-aligned, < U_PAIRED)
+  __device__ __forceinline__ double2& f64p(int u, uint32_t eo) const { return at_s<double2>(u, 2u * eo); }
   __device__ __forceinline__ int32_t& i32e(int u, uint32_t eo4) const { return at_s<int32_t>(u, eo4); }
 };
 
@@ -472,6 +484,21 @@ __device__ __forceinline__ void st_out4(f4v* ptr, f4v v) {
   __builtin_nontemporal_store(v, ptr);
 #else
   *ptr = v;
+#endif
+}
+
+// a 16-B pair of the paired state (block unit u): with the default policy a
+// write-through buffer store (sc1, aux bit 4); there is no 16-B sc1 atomic form
+typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_pair(char* base, int u, uint32_t np, uint32_t eo, double a, double b) {
+  const uint32_t off = (uint32_t)u * np + 2u * eo;
+#if defined(SACENV_ST_SC1)
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, make_double2(a, b)), r, off, 0, 16);
+#elif defined(SACENV_ST_NT)
+  __builtin_nontemporal_store(make_double2(a, b), reinterpret_cast<double2*>(base + off));
+#else
+  *reinterpret_cast<double2*>(base + off) = make_double2(a, b);
 #endif
 }
 
@@ -856,20 +883,21 @@ __device__ __forceinline__ Obs fresh_state(const SacenvBoatParams& p, const Aren
                                            int32_t start_y, int slot) {
   const double s_y = p.experiment == 2 ? (double)start_y : 0.0;  // :166-169
   const int nc = p.use_wind_table ? 0 : n_curves(p.experiment);
+  const uint32_t eo = (uint32_t)e * 8u;
   for (int c = 0; c < nc; ++c) {
     double q[4];
     A.piece(slot, c, 0, e, q);
-    for (int k = 0; k < 4; ++k) A.f64(U_COEF + 32 * c + 8 * k)[e] = q[k];
+    for (int k = 0; k < 4; ++k) A.f64e(U_COEF + 32 * c + 8 * k, eo) = q[k];
   }
-  A.f64(U_SX)[e] = 0.0;
-  A.f64(U_SY)[e] = s_y;
-  A.f64(U_SR)[e] = 0.0;
-  A.f64(U_VX)[e] = 0.0;
-  A.f64(U_VY)[e] = 0.0;
-  A.f64(U_VR)[e] = 0.0;
-  A.f64(U_RUD)[e] = 0.0;
-  A.f64(U_T)[e] = 0.0;
-  A.f64(U_EP)[e] = 0.0;  // :122
+  A.f64e(U_SX, eo) = 0.0;
+  A.f64e(U_SY, eo) = s_y;
+  A.f64e(U_SR, eo) = 0.0;
+  A.f64e(U_VX, eo) = 0.0;
+  A.f64e(U_VY, eo) = 0.0;
+  A.f64e(U_VR, eo) = 0.0;
+  A.f64e(U_RUD, eo) = 0.0;
+  A.f64e(U_T, eo) = 0.0;
+  A.f64e(U_EP, eo) = 0.0;  // :122
   A.i32(U_IDX)[e] = 0;
   return make_obs(p, obs_const(T), 0.0, 0.0, 0.0, s_y, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, (double)p.fuel0);
 }
@@ -1333,6 +1361,10 @@ __host__ __device__ inline bool t_from_index(double dt) {
   do {                                         \
     if (!kRoll) st_out(A.f64e(u, eo), (v));    \
   } while (0)
+#define EARLY_STORE2(u, v0, v1)                                     \
+  do {                                                              \
+    if (!kRoll) st_pair(A.b, (u), (uint32_t)A.np, eo, (v0), (v1));  \
+  } while (0)
 
 // 64 obs rows (2816 B) from LDS to a 16-B aligned row block: 3 float4 stores
 __device__ __forceinline__ void store_obs_block(const float* lds_rows, float* dst_rows, int lane) {
@@ -1395,17 +1427,25 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   double cf[kCoef];
 #pragma unroll
   for (int k = 0; k < kCoef; ++k) cf[k] = 0.0;
-  if (nc > 0) {  // two uniform branches, not one per field
+  if (nc > 0) {  // two uniform branches, not one per field; 16-B pairs (y0, m0), (y1, m1)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) cf[k] = A.f64e(U_COEF + 8 * k, eo);
+    for (int k = 0; k < 4; k += 2) {
+      const double2 q = A.f64p(U_COEF + 8 * k, eo);
+      cf[k] = q.x, cf[k + 1] = q.y;
+    }
     if (nc > 1) {
 #pragma unroll
-      for (int k = 4; k < 8; ++k) cf[k] = A.f64e(U_COEF + 8 * k, eo);
+      for (int k = 4; k < 8; k += 2) {
+        const double2 q = A.f64p(U_COEF + 8 * k, eo);
+        cf[k] = q.x, cf[k + 1] = q.y;
+      }
     }
   }
-  double s_x = A.f64e(U_SX, eo), s_y = A.f64e(U_SY, eo), s_r = A.f64e(U_SR, eo);
-  double v_x = A.f64e(U_VX, eo), v_y = A.f64e(U_VY, eo), v_r = A.f64e(U_VR, eo);
-  double rudder = A.f64e(U_RUD, eo), t = t_idx ? 0.0 : A.f64e(U_T, eo), ep = A.f64e(U_EP, eo);
+  const double2 p_sxy = A.f64p(U_SX, eo), p_srvx = A.f64p(U_SR, eo), p_vyvr = A.f64p(U_VY, eo);
+  const double2 p_rudep = A.f64p(U_RUD, eo);
+  double s_x = p_sxy.x, s_y = p_sxy.y, s_r = p_srvx.x;
+  double v_x = p_srvx.y, v_y = p_vyvr.x, v_r = p_vyvr.y;
+  double rudder = p_rudep.x, t = t_idx ? 0.0 : A.f64e(U_T, eo), ep = p_rudep.y;
   // keep the whole load burst ahead of the first computation: the scheduler
   // would otherwise hoist the refresh-address math (index, cons) above the
   // state loads and wait for those two first
@@ -1511,7 +1551,6 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   const int32_t fuel = p.fuel0 - (index + 1);
   if (p.test_mode == 0) rudder = rudder + div_c((double)act, 10.0, 0.1);  // action / 10
   if (!t_idx) EARLY_STORE(U_T, t);
-  EARLY_STORE(U_RUD, rudder);
   const bool first = index == 0;  // integrator counter == 0 (control_blocks.py:21-22)
   const double wsign = (double)((wv > 0.0) - (wv < 0.0));
   double swa, cwa;
@@ -1526,7 +1565,6 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   const double F_W = (wv * wv * wsign * p.c_r_front * 0.5 * p.rho * p.boat_area_front) * cwa;
   const double a_x = div_c(-F_R + F_T + F_C + F_W, p.m_plus_mx, r_mx);
   v_x = first ? 3.0 : a_x * p.dt + v_x;
-  EARLY_STORE(U_VX, v_x);
 
   // eom_transverse :241-265 (new v_x)
   const double vys = (double)((v_y > 0.0) - (v_y < 0.0));
@@ -1537,7 +1575,6 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   const double F_W2 = (wv * wv * wsign * p.c_r_side * 0.5 * p.rho * p.boat_area_side) * swa;
   const double a_y = div_c(-F_R2 + F_RU + F_C2 + F_W2, p.m_plus_my, r_my);
   v_y = first ? 0.0 : a_y * p.dt + v_y;
-  EARLY_STORE(U_VY, v_y);
 
   // eom_yawning :267-281
   const double vrs = (double)((v_r > 0.0) - (v_r < 0.0));
@@ -1546,7 +1583,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   const double M_rud = v_x * v_x * p.c_r_side * 0.5 * p.rho * p.rudder_area * sin_rud * (p.boat_b / 2) * vxs;
   const double a_r = div_c(-M_hull + M_rud, p.i_plus_iz, r_iz);
   v_r = first ? 0.0 : a_r * p.dt + v_r;
-  EARLY_STORE(U_VR, v_r);
+  EARLY_STORE2(U_VY, v_y, v_r);
 
   // get_kinematics :283-306
 #ifdef SACENV_KIN_ATAN2  // the reference's expressions (A/B builds)
@@ -1571,9 +1608,8 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   s_y = (v_y * csr + v_x * ssr) * p.dt + s_y;
 #endif
   index = index + 1;
-  EARLY_STORE(U_SR, s_r);
-  EARLY_STORE(U_SX, s_x);
-  EARLY_STORE(U_SY, s_y);
+  EARLY_STORE2(U_SX, s_x, s_y);
+  EARLY_STORE2(U_SR, s_r, v_x);
   if (!kRoll) st_out(A.i32e(U_IDX, eo4), index);
 
   Obs o = make_obs(p, oc, s_x, v_x, a_x, s_y, v_y, a_y, s_r, v_r, a_r, rudder, (double)fuel);
@@ -1650,15 +1686,15 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   // fresh state of restarting envs (same lane, same address: the later store
   // wins), ep_reward, the next wind, and the record
   if (!kRoll && restart) {
-    st_out(A.f64e(U_SX, eo), s_x), st_out(A.f64e(U_SY, eo), s_y), st_out(A.f64e(U_SR, eo), s_r);
-    st_out(A.f64e(U_VX, eo), v_x), st_out(A.f64e(U_VY, eo), v_y), st_out(A.f64e(U_VR, eo), v_r);
-    st_out(A.f64e(U_RUD, eo), rudder);
+    EARLY_STORE2(U_SX, s_x, s_y);
+    EARLY_STORE2(U_SR, s_r, v_x);
+    EARLY_STORE2(U_VY, v_y, v_r);
     if (!t_idx) st_out(A.f64e(U_T, eo), t);
     st_out(A.i32e(U_IDX, eo4), index);
     st_out(A.i32e(U_CONS, eo4), cons_out);
   }
   if (!kRoll) {
-    st_out(A.f64e(U_EP, eo), ep);
+    EARLY_STORE2(U_RUD, rudder, ep);
     if (restart && nc > 0) {  // the new episode's first wind: the piece's y0 = y(0); at
       // t = 0 the piece is exactly y0 whatever (finite) m0, y1, m1 it still holds
 #pragma unroll
@@ -1666,8 +1702,8 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
         if (c < nc) st_out(A.f64e(U_COEF + 32 * c, eo), y0n[c]);
     } else if (refresh) {
 #pragma unroll
-      for (int k = 0; k < kCoef; ++k)
-        if (k < 4 * nc) st_out(A.f64e(U_COEF + 8 * k, eo), rq[k]);
+      for (int k = 0; k < kCoef; k += 2)
+        if (k < 4 * nc) EARLY_STORE2(U_COEF + 8 * k, rq[k], rq[k + 1]);
     }
     if (hdr_refresh) {
 #pragma unroll

@@ -86,9 +86,14 @@ class VecBoatEnv:
             return self.arena[off: off + cnt * esz].view(dtype).view(*shape)
 
         f64, i32 = torch.float64, torch.int32
-        # carried state (SoA views, first N entries of each n_pad array)
+
+        def pair_view(off):  # paired f64 fields: [n_pad][2] blocks, env stride 16 B
+            k = (off % 16) // 8
+            return view(off - 8 * k, f64, NP, 2)[:N, k]
+
+        # carried state (strided views of the paired fields, first N envs)
         for name in ("s_x", "s_y", "s_r", "v_x", "v_y", "v_r", "rudder", "ep_reward"):
-            setattr(self, name, view(getattr(L, name), f64, NP)[:N])
+            setattr(self, name, pair_view(getattr(L, name)))
         self._t_view = view(L.t, f64, NP)[:N]
         self._t_from_index = t_from_index(float(self.cfg.dt))
         self.index = view(L.index, i32, NP)[:N]

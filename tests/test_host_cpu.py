@@ -140,8 +140,11 @@ def test_arena_layout(built_lib, n):
     assert np_ % 64 == 0 and n <= np_ < n + 64
     nk = 8
     S = _lib.SLOTS
-    sizes = {"s_x": 8, "s_y": 8, "s_r": 8, "v_x": 8, "v_y": 8, "v_r": 8, "rudder": 8, "t": 8,
-             "ep_reward": 8, "wind_coef": 64, "wind0_next": 16, "start_y_next": 4,
+    # paired f64 fields: [n_pad][2] blocks, the second element 8 B after the first
+    for a, b in (("s_x", "s_y"), ("s_r", "v_x"), ("v_y", "v_r"), ("rudder", "ep_reward")):
+        assert getattr(L, b) == getattr(L, a) + 8, (a, b)
+    sizes = {"s_x": 16, "s_r": 16, "v_y": 16, "rudder": 16, "t": 8,
+             "wind_coef": 64, "wind0_next": 16, "start_y_next": 4,
              "index": 4, "cons": 4, "fill": 4, "mt_pos": 4,
              "start_y": 4 * S, "counters": 20, "refill_list": 12, "wind_knots": 32 * S * nk,
              "knots_raw": 16 * S * nk, "mt_key": 2496, "obs": 44, "reward": 4, "done": 1, "term": 1,
