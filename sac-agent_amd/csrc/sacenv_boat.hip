@@ -1369,11 +1369,20 @@ __host__ __device__ inline bool t_from_index(double dt) {
 // 64 obs rows (2816 B) from LDS to a 16-B aligned row block: 3 float4 stores
 __device__ __forceinline__ void store_obs_block(const float* lds_rows, float* dst_rows, int lane) {
   const f4v* src = reinterpret_cast<const f4v*>(lds_rows);
+#ifndef SACENV_OBS_NT  // write-through 16-B buffer stores (sc1, aux bit 4): 0.13 us/step
+  // faster than nontemporal ones, which leave the rows dirty in L2 for the boundary
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(dst_rows, 0, 0x7fffffff, 0x00020000);
+#endif
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     const uint32_t q = (uint32_t)lane + kWave * i;
-    if (q < kWave * SACENV_OBS_DIM / 4)
+    if (q < kWave * SACENV_OBS_DIM / 4) {
+#ifndef SACENV_OBS_NT
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, src[q]), r, q * 16u, 0, 16);
+#else
       st_out4(reinterpret_cast<f4v*>(reinterpret_cast<char*>(dst_rows) + q * 16u), src[q]);
+#endif
+    }
   }
 }
 
