@@ -479,7 +479,7 @@ __device__ __forceinline__ void st_rec(T& ref, T v) {  // reward / done / term b
   st_out(ref, v);
 #endif
 }
-__device__ __forceinline__ void st_out4(f4v* ptr, f4v v) {
+[[maybe_unused]] __device__ __forceinline__ void st_out4(f4v* ptr, f4v v) {  // SACENV_OBS_NT A/B
 #if (defined(SACENV_ST_NT) || defined(SACENV_ST_SC1)) && !defined(SACENV_OBS_PLAIN)
   __builtin_nontemporal_store(v, ptr);
 #else
