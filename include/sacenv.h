@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SACENV_ABI_VERSION 11
+#define SACENV_ABI_VERSION 12
 #define SACENV_OBS_DIM 11      /* Boat.return_state, boat_env.py:308-323 */
 #define SACENV_MT_N 624        /* MT19937 words per env (numpy legacy RNG) */
 #define SACENV_MAX_KNOTS 16    /* wind.fixed_points upper bound */
@@ -381,6 +381,75 @@ int sacenv_replay_store_env(const SacenvReplayParams *p, void *arena, int64_t n,
 int sacenv_replay_sample(const SacenvReplayParams *p, void *arena, int32_t batch, int64_t stored,
                          int64_t *idx, float *state, float *action, double *reward,
                          float *new_state, uint8_t *terminal, void *stream);
+
+/* ------------------------------------------------------------------------
+ * SAC agent on the device: the batched
+ * policy of ContinuousAgent.choose_action (agent/continuous_agent.py:57-61)
+ * and one ContinuousAgent.learn (:96-154) over the five networks of
+ * networks/networks.py:14-133 (actor, critic 1, critic 2, value, target
+ * value: 256-256 MLPs, f32), as fp32 MFMA kernels (v_mfma_f32_16x16x4_f32).
+ *
+ * All five networks, the four Adam states and the kernel-side transposes of
+ * the 256x256 layers live in one caller-owned f32 WEIGHTS buffer of
+ * sacenv_sac_layout()->total_floats floats. Net n starts at layout.net[n]
+ * (0 actor, 1 critic 1, 2 critic 2, 3 value, 4 target value); inside a net
+ * the tensors sit at layout.tensor[shape][k] (shape 0 actor, 1 critic,
+ * 2 value; k = fc1.weight [256][in], fc1.bias, fc2.weight [256][256],
+ * fc2.bias, head-0 weight [256], head-0 bias, head-1 weight, head-1 bias;
+ * -1 where absent): the torch layout of nn.Linear, so the host can view each
+ * parameter in place. Adam's exp_avg / exp_avg_sq of net n < 4 start at
+ * adam_m[n] / adam_v[n] with the same inner offsets. After the host writes
+ * weights, sacenv_sac_sync() refreshes the transposes; learn keeps them.
+ * `scratch` is a device buffer of layout.scratch_bytes (no contents kept
+ * between calls). Same conventions as above: device pointers, host params,
+ * stream-ordered, graph-capturable, 0 or an SACENV_E_* / hipError_t. */
+
+#define SACENV_SAC_HIDDEN 256   /* layer1_size = layer2_size (original_config.yaml:18-19) */
+
+typedef struct SacenvSacParams {
+  int32_t obs_dim;       /* input_dims[0] (11 for the boat), 1..15 */
+  int32_t n_actions;     /* 1 (the boat's action_space.shape) */
+  int32_t hidden;        /* SACENV_SAC_HIDDEN */
+  int32_t batch;         /* learn batch (batch_size), a multiple of 256 */
+  /* Python floats of the reference; the kernels cast them to f32 where torch does */
+  double max_action;     /* action_space.high[0] (base_agent.py:15-17) */
+  double gamma;          /* agent.gamma */
+  double tau;            /* agent.tvn_parameter_modulation_tau */
+  double reward_scale;   /* agent.reward_scale */
+  double lr_actor;       /* agent.learning_rate_alpha */
+  double lr_critic;      /* agent.learning_rate_beta (critics, value) */
+  double adam_beta1, adam_beta2, adam_eps;  /* torch.optim.Adam defaults 0.9, 0.999, 1e-8 */
+} SacenvSacParams;
+
+typedef struct SacenvSacLayout {
+  int64_t total_floats;
+  int64_t net[5];
+  int64_t adam_m[4];
+  int64_t adam_v[4];
+  int64_t w2t[4];          /* fc2.weight transposed [in][out] of nets 0..3 */
+  int64_t net_floats[3];   /* floats of one net per shape */
+  int64_t tensor[3][8];
+  int64_t scratch_bytes;
+} SacenvSacLayout;
+
+int sacenv_sac_layout(const SacenvSacParams *p, SacenvSacLayout *out);
+/* rebuild the kernel-side transposes from the weights (after the host wrote them) */
+int sacenv_sac_sync(const SacenvSacParams *p, float *weights, void *stream);
+/* choose_action for n observations [n][obs_dim]: action = tanh(mean + eps*std)
+ * * max_action with the given standard normal draws eps [n] (networks.py:47-70,
+ * reparameterize=False); log_prob [n] may be NULL. */
+int sacenv_sac_act(const SacenvSacParams *p, const float *weights, const float *obs, int32_t n,
+                   const float *eps, float *action, float *log_prob, void *stream);
+/* one learn() on a sampled batch (state, new_state f32 [batch][obs_dim],
+ * action f32 [batch], reward f64 [batch] as sample_buffer returns it, done u8
+ * [batch]) with the policy draws of its sample() (eps1) and rsample() (eps2),
+ * f32 [batch]. adam_step = the optimizers' step count after this call (1 on
+ * the first). losses (device f32 [4], may be NULL) <- value, actor, critic 1,
+ * critic 2 losses. */
+int sacenv_sac_learn(const SacenvSacParams *p, float *weights, void *scratch, const float *state,
+                     const float *action, const double *reward, const float *new_state,
+                     const uint8_t *done, const float *eps1, const float *eps2, int32_t adam_step,
+                     float *losses, void *stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,856 @@
+// sacenv_sac.hip — the SAC agent on gfx950.
+//
+// ContinuousAgent.choose_action (agent/continuous_agent.py:57-61) for N
+// observations at once, and ContinuousAgent.learn (:96-154) over the five
+// networks of networks/networks.py:14-133, as fp32 MFMA kernels
+// (v_mfma_f32_16x16x4_f32: f32 in, f32 accumulate, an fmaf chain per output).
+//
+// learn() in four launches. Every gradient of one learn() is taken at the
+// parameters the call starts with: the value step (:121-125) changes only the
+// value net, which neither the actor loss nor the critic loss reads; the
+// critics step after the actor loss (:127-137 vs :139-150); the value-phase
+// gradients that reach actor and critics are zeroed before their own losses
+// (:133, :139-140). So the four losses are independent and the kernels run
+// them side by side:
+//
+//   phase 0 (row blocks x 5 roles): actor forward + both policy draws, value
+//     forward, target forward (value_, done-masked), critic 1 / 2 forward on
+//     the stored actions.
+//   phase 1 (x 4): critic c at the sample() actions (value target) and at the
+//     rsample() actions with dq/da (actor loss); critic c's own loss backward
+//     (q_hat = scale * reward + gamma * value_).
+//   phase 2 (x 2): actor backward (min of the critics, tanh-squashed Normal
+//     log-prob), value backward (value_target = min q - log_prob).
+//   phase 3: weight gradients as batch reductions (dW = dZ^T H on MFMA), Adam
+//     (torch.optim.Adam, foreach form) on the four optimised nets, the target
+//     soft update (:63-77), the transposes, and the four losses.
+//
+// Row blocks are 16 batch rows per 256-thread workgroup. A dense layer of a
+// row block is Y^T = W X^T: wave w owns output features [64w, 64w + 64) as
+// four 16x16 tiles; the weights are the MFMA A operand straight from L2
+// (float4 per lane), the activations the B operand from LDS ([row][feature],
+// 4-float pad). k runs in blocks of 16 with lane (i, kq) supplying
+// k = 16 kb + 4 kq + s in step s — the same permutation on both operands, so
+// each lane reads one float4 of each per block. Activations that phase 3
+// reduces over the batch are stored feature-major [256][B].
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+
+#include "sacenv.h"
+
+namespace {
+
+constexpr int kH = SACENV_SAC_HIDDEN;
+constexpr int kRows = 16;      // batch rows per row-block workgroup
+constexpr int kThreads = 256;  // 4 waves
+constexpr int kSP = kH + 4;    // LDS row stride of an activation tile (floats)
+constexpr int kXP = 20;        // LDS row stride of the padded input tile
+constexpr float kLogSqrt2Pi = 0.91893853320467274f;  // math.log(math.sqrt(2 * math.pi))
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------- layout
+
+struct NetOff {
+  int64_t t[8];  // w1, b1, w2, b2, wh0, bh0, wh1, bh1 (-1 absent)
+  int64_t size;
+};
+
+__host__ __device__ inline NetOff net_off(int in_dim, int nh) {
+  NetOff o;
+  int64_t p = 0;
+  auto take = [&](int k, int64_t n) {
+    o.t[k] = p;
+    p += (n + 3) & ~int64_t(3);  // every tensor 16-B aligned
+  };
+  take(0, (int64_t)kH * in_dim);
+  take(1, kH);
+  take(2, (int64_t)kH * kH);
+  take(3, kH);
+  take(4, kH);
+  take(5, 1);
+  if (nh > 1) {
+    take(6, kH);
+    take(7, 1);
+  } else {
+    o.t[6] = o.t[7] = -1;
+  }
+  o.size = p;
+  return o;
+}
+
+enum Shape { kActorShape = 0, kCriticShape = 1, kValueShape = 2 };
+__host__ __device__ inline int net_shape(int n) { return n == 0 ? kActorShape : (n <= 2 ? kCriticShape : kValueShape); }
+__host__ __device__ inline int net_in(int n, int D) { return net_shape(n) == kCriticShape ? D + 1 : D; }
+
+// per-row fields of the scratch, f32 [B] each
+enum RowField {
+  F_MU, F_SR, F_SIG, F_TL, F_A1, F_LP1, F_A2, F_X2, F_LP2,   // actor forward + draws
+  F_V, F_VN,                                                 // value, value_ (done-masked target)
+  F_QC1, F_QC2,                                              // critics at the stored actions
+  F_Q1A1, F_Q2A1, F_Q1A2, F_Q2A2, F_DA1, F_DA2,              // critics at the draws, dq/da at a2
+  F_GMU, F_GSR, F_GC1, F_GC2, F_GV,                          // head-output gradients
+  F_LV, F_LA, F_LC1, F_LC2,                                  // per-row loss terms
+  F_COUNT
+};
+
+struct NetAct {   // feature-major [kH][B] activations of one optimised net
+  float* h1t;
+  float* h2t;
+  float* dz1t;
+  float* dz2t;
+};
+
+struct SacArgs {
+  float* P;            // weights buffer
+  const float* s;      // state [B][D]
+  const float* act;    // action [B]
+  const double* rew;   // reward [B]
+  const float* s2;     // new_state [B][D]
+  const uint8_t* done;
+  const float* eps1;
+  const float* eps2;
+  float* rows;         // row fields [F_COUNT][B]
+  float* losses;
+  NetAct na[4];        // actor, critic 1, critic 2, value
+  int64_t net[5], am[4], av[4], w2t[4];
+  NetOff off[3];
+  int B, D;
+  float max_action, gamma, scale, inv_b;
+  // Adam (torch.optim.Adam foreach form), scalars as torch casts them
+  float lerp_w, b2, omb2, bc2s, eps, nstep_actor, nstep_critic;
+  float tau, omtau;
+};
+
+__device__ __forceinline__ float* rowf(const SacArgs& a, int f) { return a.rows + (int64_t)f * a.B; }
+
+// ---------------------------------------------------------------- LDS tiles
+
+struct RowLds {
+  float x[kRows * kXP];
+  float h1[kRows * kSP];
+  float h2[kRows * kSP];
+  float z[kRows * kSP];
+  float g0[kRows], g1[kRows];
+};
+
+// X[j][k] = src[row0 + j][k] (k < D), acol[row0 + j] at k = D, zero to 16
+__device__ __forceinline__ void load_x(float* xl, const float* __restrict__ src, int D, int row0, int nrows,
+                                       const float* __restrict__ acol, int tid) {
+  const int j = tid >> 4, k = tid & 15;
+  float v = 0.f;
+  if (j < nrows) {
+    if (k < D)
+      v = src[(int64_t)(row0 + j) * D + k];
+    else if (k == D && acol != nullptr)
+      v = acol[row0 + j];
+  }
+  xl[j * kXP + k] = v;
+}
+
+// feature-major [kH][B] rows row0..row0+15 -> LDS tile
+__device__ __forceinline__ void load_tile_t(float* hl, const float* __restrict__ gT, int B, int row0, int tid) {
+  const int j = tid & 15, fg = tid >> 4;
+#pragma unroll 4
+  for (int q = 0; q < 16; ++q) {
+    const int f = fg * 16 + q;
+    hl[j * kSP + f] = gT[(int64_t)f * B + row0 + j];
+  }
+}
+
+__device__ __forceinline__ void store_tile_t(const float* hl, float* __restrict__ gT, int B, int row0, int tid) {
+  const int j = tid & 15, fg = tid >> 4;
+#pragma unroll 4
+  for (int q = 0; q < 16; ++q) {
+    const int f = fg * 16 + q;
+    gT[(int64_t)f * B + row0 + j] = hl[j * kSP + f];
+  }
+}
+
+// ---------------------------------------------------------------- dense layer on MFMA
+
+// acc[t] <- W[64w + 16t + ..][:] . X^T for the 16 rows of xl. FC1: W is
+// [kH][kin] (kin <= 16, scalar loads); else [kH][kH] (float4 loads).
+template <bool FC1>
+__device__ __forceinline__ void layer(const float* __restrict__ W, int kin, const float* xl, int xs, int lane,
+                                      int w, f4 acc[4]) {
+  const int i = lane & 15, kq = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
+  constexpr int KB = FC1 ? 1 : kH / 16;
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb) {
+    const f4 b = *reinterpret_cast<const f4*>(xl + i * xs + 16 * kb + 4 * kq);
+    f4 av[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int n = 64 * w + 16 * t + i;
+      if (FC1) {
+        const float* wp = W + n * kin;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int k = 4 * kq + s;
+          av[t][s] = k < kin ? wp[k] : 0.f;
+        }
+      } else {
+        av[t] = *reinterpret_cast<const f4*>(W + n * kH + 16 * kb + 4 * kq);
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t][s], b[s], acc[t], 0, 0, 0);
+  }
+}
+
+// forward epilogue: y = relu(acc + bias) -> LDS tile (and feature-major global)
+// lane (j = row, kq) holds features 64w + 16t + 4kq + r
+__device__ __forceinline__ void epi_fwd(const f4 acc[4], const float* __restrict__ bias, float* yl, int lane, int w,
+                                        float* __restrict__ gT, int B, int row0) {
+  const int j = lane & 15, kq = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int n0 = 64 * w + 16 * t + 4 * kq;
+    const f4 bb = *reinterpret_cast<const f4*>(bias + n0);
+    f4 y;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) y[r] = fmaxf(acc[t][r] + bb[r], 0.f);
+    *reinterpret_cast<f4*>(yl + j * kSP + n0) = y;
+    if (gT != nullptr)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) gT[(int64_t)(n0 + r) * B + row0 + j] = y[r];
+  }
+}
+
+// backward epilogue: dz = acc * [h > 0] (relu backward on the stored output)
+__device__ __forceinline__ void epi_bwd(const f4 acc[4], const float* hl, float* zl, int lane, int w,
+                                        float* __restrict__ gT, int B, int row0) {
+  const int j = lane & 15, kq = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int n0 = 64 * w + 16 * t + 4 * kq;
+    const f4 h = *reinterpret_cast<const f4*>(hl + j * kSP + n0);
+    f4 z;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) z[r] = h[r] > 0.f ? acc[t][r] : 0.f;
+    if (zl != nullptr) *reinterpret_cast<f4*>(zl + j * kSP + n0) = z;
+    if (gT != nullptr)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) gT[(int64_t)(n0 + r) * B + row0 + j] = z[r];
+  }
+}
+
+// sum_f w[f * ws] * h[row][f] for row = tid >> 4, in all 16 lanes of the row
+__device__ __forceinline__ float row_dot(const float* hl, const float* __restrict__ wv, int ws, int tid) {
+  const int j = tid >> 4, part = tid & 15;
+  float s = 0.f;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int f = q * 16 + part;
+    s = fmaf(wv[f * ws], hl[j * kSP + f], s);
+  }
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o, 16);
+  return s;
+}
+
+// two-layer trunk on the input tile in l.x: h1, h2 in LDS (and optionally global)
+__device__ __forceinline__ void trunk(const float* __restrict__ Pn, const NetOff& o, int kin, RowLds& l, int tid,
+                                      float* h1t, float* h2t, int B, int row0) {
+  const int lane = tid & 63, w = tid >> 6;
+  f4 acc[4];
+  layer<true>(Pn + o.t[0], kin, l.x, kXP, lane, w, acc);
+  epi_fwd(acc, Pn + o.t[1], l.h1, lane, w, h1t, B, row0);
+  __syncthreads();
+  layer<false>(Pn + o.t[2], kH, l.h1, kSP, lane, w, acc);
+  epi_fwd(acc, Pn + o.t[3], l.h2, lane, w, h2t, B, row0);
+  __syncthreads();
+}
+
+// head backward: dz2 = (wh0 g0 + wh1 g1) * [h2 > 0] -> dz2t; dz1 = (W2^T dz2) * [h1 > 0]
+// -> dz1t (and LDS l.h2 when keep_dz1). g0/g1 per row in l.g0/l.g1.
+__device__ __forceinline__ void head_backward(const float* __restrict__ Pn, const NetOff& o,
+                                              const float* __restrict__ w2t, RowLds& l, int tid, float* dz2t,
+                                              float* dz1t, int B, int row0, bool keep_dz1) {
+  const int lane = tid & 63, w = tid >> 6;
+  const float* wh0 = Pn + o.t[4];
+  const float* wh1 = o.t[6] >= 0 ? Pn + o.t[6] : nullptr;
+  for (int e = tid; e < kRows * kH; e += kThreads) {
+    const int j = e >> 8, f = e & (kH - 1);
+    float g = wh0[f] * l.g0[j];
+    if (wh1 != nullptr) g = g + wh1[f] * l.g1[j];
+    l.z[j * kSP + f] = l.h2[j * kSP + f] > 0.f ? g : 0.f;
+  }
+  __syncthreads();
+  if (dz2t != nullptr) store_tile_t(l.z, dz2t, B, row0, tid);
+  f4 acc[4];
+  layer<false>(w2t, kH, l.z, kSP, lane, w, acc);
+  __syncthreads();  // every wave has read l.z / l.h2 before l.h2 is overwritten
+  epi_bwd(acc, l.h1, keep_dz1 ? l.h2 : nullptr, lane, w, dz1t, B, row0);
+  __syncthreads();
+}
+
+// tanh-squashed Normal draw (networks.py:47-70): x = mean + eps * std,
+// action = tanh(x) * max_action, log_prob with the tanh correction
+__device__ __forceinline__ float policy_sigma(float sr, float& tl) {
+  tl = tanhf(sr);
+  const float ls = -5.f + 3.5f * (tl + 1.f);  // LOG_STD_MIN + 0.5 (MAX - MIN) (tanh + 1)
+  return expf(ls);
+}
+__device__ __forceinline__ void policy_draw(float mu, float sig, float eps, float M, float& x, float& act, float& lp) {
+  x = mu + eps * sig;
+  act = tanhf(x) * M;
+  const float u = x - mu;
+  lp = -(u * u) / (2.f * (sig * sig)) - logf(sig) - kLogSqrt2Pi;
+  lp = lp - logf(1.f - act * act + 1e-6f);
+}
+
+// ---------------------------------------------------------------- phase roles
+
+__device__ void role_actor_fwd(const SacArgs& a, RowLds& l, int tid, int row0) {
+  const float* Pn = a.P + a.net[0];
+  const NetOff& o = a.off[kActorShape];
+  load_x(l.x, a.s, a.D, row0, kRows, nullptr, tid);
+  __syncthreads();
+  trunk(Pn, o, a.D, l, tid, a.na[0].h1t, a.na[0].h2t, a.B, row0);
+  const float mu = row_dot(l.h2, Pn + o.t[4], 1, tid) + Pn[o.t[5]];
+  const float sr = row_dot(l.h2, Pn + o.t[6], 1, tid) + Pn[o.t[7]];
+  if ((tid & 15) == 0) {
+    const int r = row0 + (tid >> 4);
+    float tl;
+    const float sig = policy_sigma(sr, tl);
+    float x1, a1, lp1, x2, a2, lp2;
+    policy_draw(mu, sig, a.eps1[r], a.max_action, x1, a1, lp1);
+    policy_draw(mu, sig, a.eps2[r], a.max_action, x2, a2, lp2);
+    rowf(a, F_MU)[r] = mu;
+    rowf(a, F_SR)[r] = sr;
+    rowf(a, F_SIG)[r] = sig;
+    rowf(a, F_TL)[r] = tl;
+    rowf(a, F_A1)[r] = a1;
+    rowf(a, F_LP1)[r] = lp1;
+    rowf(a, F_A2)[r] = a2;
+    rowf(a, F_X2)[r] = x2;
+    rowf(a, F_LP2)[r] = lp2;
+  }
+}
+
+// value(state) (storing the activations) or target_value(new_state) -> value_
+__device__ void role_value_fwd(const SacArgs& a, RowLds& l, int tid, int row0, bool target) {
+  const int n = target ? 4 : 3;
+  const float* Pn = a.P + a.net[n];
+  const NetOff& o = a.off[kValueShape];
+  load_x(l.x, target ? a.s2 : a.s, a.D, row0, kRows, nullptr, tid);
+  __syncthreads();
+  trunk(Pn, o, a.D, l, tid, target ? nullptr : a.na[3].h1t, target ? nullptr : a.na[3].h2t, a.B, row0);
+  const float v = row_dot(l.h2, Pn + o.t[4], 1, tid) + Pn[o.t[5]];
+  if ((tid & 15) == 0) {
+    const int r = row0 + (tid >> 4);
+    if (target)
+      rowf(a, F_VN)[r] = a.done[r] ? 0.f : v;  // value_[done] = 0.0 (:111)
+    else
+      rowf(a, F_V)[r] = v;
+  }
+}
+
+// critic c (1, 2) on [state, acol]; returns q in the row's lanes
+__device__ float critic_fwd(const SacArgs& a, RowLds& l, int tid, int row0, int c, const float* acol, bool store) {
+  const float* Pn = a.P + a.net[c];
+  const NetOff& o = a.off[kCriticShape];
+  load_x(l.x, a.s, a.D, row0, kRows, acol, tid);
+  __syncthreads();
+  trunk(Pn, o, a.D + 1, l, tid, store ? a.na[c].h1t : nullptr, store ? a.na[c].h2t : nullptr, a.B, row0);
+  return row_dot(l.h2, Pn + o.t[4], 1, tid) + Pn[o.t[5]];
+}
+
+__device__ void role_critic_stored(const SacArgs& a, RowLds& l, int tid, int row0, int c) {
+  const float q = critic_fwd(a, l, tid, row0, c, a.act, true);
+  if ((tid & 15) == 0) rowf(a, c == 1 ? F_QC1 : F_QC2)[row0 + (tid >> 4)] = q;
+}
+
+// critic c at the sample() actions (value target, :113-117) and at the
+// rsample() actions with dq/da through the critic (actor loss, :127-131)
+__device__ void role_critic_policy(const SacArgs& a, RowLds& l, int tid, int row0, int c) {
+  const float qa1 = critic_fwd(a, l, tid, row0, c, rowf(a, F_A1), false);
+  __syncthreads();
+  const float qa2 = critic_fwd(a, l, tid, row0, c, rowf(a, F_A2), false);
+  const float* Pn = a.P + a.net[c];
+  const NetOff& o = a.off[kCriticShape];
+  if ((tid & 15) == 0) l.g0[tid >> 4] = 1.f;
+  __syncthreads();
+  head_backward(Pn, o, a.P + a.w2t[c], l, tid, nullptr, nullptr, a.B, row0, true);
+  // dq/da = W1[:, D] . dz1
+  const float da = row_dot(l.h2, Pn + o.t[0] + a.D, a.D + 1, tid);
+  if ((tid & 15) == 0) {
+    const int r = row0 + (tid >> 4);
+    rowf(a, c == 1 ? F_Q1A1 : F_Q2A1)[r] = qa1;
+    rowf(a, c == 1 ? F_Q1A2 : F_Q2A2)[r] = qa2;
+    rowf(a, c == 1 ? F_DA1 : F_DA2)[r] = da;
+  }
+}
+
+// critic c's loss backward: 0.5 mse(q, q_hat), q_hat = scale r + gamma value_ (:141-146)
+__device__ void role_critic_loss(const SacArgs& a, RowLds& l, int tid, int row0, int c) {
+  const NetAct& na = a.na[c];
+  load_tile_t(l.h1, na.h1t, a.B, row0, tid);
+  load_tile_t(l.h2, na.h2t, a.B, row0, tid);
+  if (tid < kRows) {
+    const int r = row0 + tid;
+    const float q = rowf(a, c == 1 ? F_QC1 : F_QC2)[r];
+    const float qh = a.scale * (float)a.rew[r] + a.gamma * rowf(a, F_VN)[r];
+    const float d = q - qh;
+    const float g = d * a.inv_b;  // mse backward: (2 / B) (q - q_hat) * 0.5
+    l.g0[tid] = g;
+    rowf(a, c == 1 ? F_GC1 : F_GC2)[r] = g;
+    rowf(a, c == 1 ? F_LC1 : F_LC2)[r] = d * d;
+  }
+  __syncthreads();
+  head_backward(a.P + a.net[c], a.off[kCriticShape], a.P + a.w2t[c], l, tid, na.dz2t, na.dz1t, a.B, row0, false);
+}
+
+// actor loss backward: mean(log_prob - min(q1, q2)) at the rsample() draw (:127-135)
+__device__ void role_actor_bwd(const SacArgs& a, RowLds& l, int tid, int row0) {
+  const NetAct& na = a.na[0];
+  load_tile_t(l.h1, na.h1t, a.B, row0, tid);
+  load_tile_t(l.h2, na.h2t, a.B, row0, tid);
+  if (tid < kRows) {
+    const int r = row0 + tid;
+    const float ib = a.inv_b;
+    const float q1 = rowf(a, F_Q1A2)[r], q2 = rowf(a, F_Q2A2)[r];
+    // torch.min(q1, q2) backward: the smaller one, half each on a tie
+    const float dm = -ib;
+    const float g1 = q1 < q2 ? dm : (q1 == q2 ? 0.5f * dm : 0.f);
+    const float g2 = q2 < q1 ? dm : (q1 == q2 ? 0.5f * dm : 0.f);
+    const float M = a.max_action;
+    const float mu = rowf(a, F_MU)[r], sig = rowf(a, F_SIG)[r], tl = rowf(a, F_TL)[r];
+    const float x = rowf(a, F_X2)[r], act = rowf(a, F_A2)[r];
+    const float e2 = a.eps2[r];
+    const float th = tanhf(x);
+    const float u = x - mu, var = sig * sig;
+    // d/d action: -log(1 - a^2 + 1e-6) (log_prob term) and -min q
+    const float dact = ib * (2.f * act / (1.f - act * act + 1e-6f)) + (g1 * rowf(a, F_DA1)[r] + g2 * rowf(a, F_DA2)[r]);
+    const float dx = dact * M * (1.f - th * th) + ib * (-u / var);
+    const float dmu = dx + ib * (u / var);
+    const float dsig = dx * e2 + ib * (u * u * sig / (var * var) - 1.f / sig);
+    const float dsr = dsig * sig * 3.5f * (1.f - tl * tl);
+    l.g0[tid] = dmu;
+    l.g1[tid] = dsr;
+    rowf(a, F_GMU)[r] = dmu;
+    rowf(a, F_GSR)[r] = dsr;
+    rowf(a, F_LA)[r] = rowf(a, F_LP2)[r] - fminf(q1, q2);
+  }
+  __syncthreads();
+  head_backward(a.P + a.net[0], a.off[kActorShape], a.P + a.w2t[0], l, tid, na.dz2t, na.dz1t, a.B, row0, false);
+}
+
+// value loss backward: 0.5 mse(value, min q(sample()) - log_prob) (:113-124)
+__device__ void role_value_bwd(const SacArgs& a, RowLds& l, int tid, int row0) {
+  const NetAct& na = a.na[3];
+  load_tile_t(l.h1, na.h1t, a.B, row0, tid);
+  load_tile_t(l.h2, na.h2t, a.B, row0, tid);
+  if (tid < kRows) {
+    const int r = row0 + tid;
+    const float target = fminf(rowf(a, F_Q1A1)[r], rowf(a, F_Q2A1)[r]) - rowf(a, F_LP1)[r];
+    const float d = rowf(a, F_V)[r] - target;
+    const float g = d * a.inv_b;
+    l.g0[tid] = g;
+    rowf(a, F_GV)[r] = g;
+    rowf(a, F_LV)[r] = d * d;
+  }
+  __syncthreads();
+  head_backward(a.P + a.net[3], a.off[kValueShape], a.P + a.w2t[3], l, tid, na.dz2t, na.dz1t, a.B, row0, false);
+}
+
+__global__ void __launch_bounds__(kThreads) k_sac_rows(SacArgs a, int phase) {
+  __shared__ RowLds l;
+  const int tid = threadIdx.x;
+  const int nrb = a.B / kRows;
+  const int role = blockIdx.x / nrb, row0 = (blockIdx.x - role * nrb) * kRows;
+  if (phase == 0) {
+    if (role == 0) role_actor_fwd(a, l, tid, row0);
+    else if (role == 1) role_value_fwd(a, l, tid, row0, false);
+    else if (role == 2) role_value_fwd(a, l, tid, row0, true);
+    else role_critic_stored(a, l, tid, row0, role - 2);
+  } else if (phase == 1) {
+    if (role < 2) role_critic_policy(a, l, tid, row0, role + 1);
+    else role_critic_loss(a, l, tid, row0, role - 1);
+  } else {
+    if (role == 0) role_actor_bwd(a, l, tid, row0);
+    else role_value_bwd(a, l, tid, row0);
+  }
+}
+
+// ---------------------------------------------------------------- phase 3: gradients + Adam
+
+__device__ __forceinline__ void adam(const SacArgs& a, float nstep, float g, float& p, float& m, float& v) {
+  m = m + a.lerp_w * (g - m);            // exp_avg.lerp_(grad, 1 - beta1)
+  v = v * a.b2 + (a.omb2 * g) * g;       // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, 1 - beta2)
+  const float den = sqrtf(v) / a.bc2s + a.eps;
+  p = p + nstep * (m / den);             // param.addcdiv_(exp_avg, denom, -step_size)
+}
+
+__device__ __forceinline__ void update_elem(const SacArgs& a, int t, int64_t idx, float g) {
+  float* P = a.P + a.net[t];
+  float* M = a.P + a.am[t];
+  float* V = a.P + a.av[t];
+  float p = P[idx], m = M[idx], v = V[idx];
+  adam(a, t == 0 ? a.nstep_actor : a.nstep_critic, g, p, m, v);
+  P[idx] = p;
+  M[idx] = m;
+  V[idx] = v;
+  if (t == 3) {  // update_network_parameters(): tau * value + (1 - tau) * target
+    float* T = a.P + a.net[4];
+    T[idx] = a.tau * p + a.omtau * T[idx];
+  }
+}
+
+constexpr int kUpdLds = 4 * 32 * 33 > 256 * 17 ? 4 * 32 * 33 : 256 * 17;
+
+// fc2.weight gradient tile (32 out x 32 in) of net t: dW = dz2^T h1 over the
+// batch, each wave a quarter of the rows, then Adam and the transpose
+__device__ void fc2_tile(const SacArgs& a, int t, int ob, int ib, int tid, float* red) {
+  const int lane = tid & 63, w = tid >> 6, i = lane & 15, kq = lane >> 4;
+  const NetAct& na = a.na[t];
+  const int B = a.B, rq = B / 4, rbeg = w * rq;
+  const int o0 = 32 * ob, i0 = 32 * ib;
+  f4 acc[2][2];
+#pragma unroll
+  for (int so = 0; so < 2; ++so)
+#pragma unroll
+    for (int si = 0; si < 2; ++si) acc[so][si] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int r0 = rbeg; r0 < rbeg + rq; r0 += 16) {
+    f4 A[2], Bv[2];
+#pragma unroll
+    for (int so = 0; so < 2; ++so) A[so] = *reinterpret_cast<const f4*>(na.dz2t + (int64_t)(o0 + 16 * so + i) * B + r0 + 4 * kq);
+#pragma unroll
+    for (int si = 0; si < 2; ++si) Bv[si] = *reinterpret_cast<const f4*>(na.h1t + (int64_t)(i0 + 16 * si + i) * B + r0 + 4 * kq);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int so = 0; so < 2; ++so)
+#pragma unroll
+        for (int si = 0; si < 2; ++si)
+          acc[so][si] = __builtin_amdgcn_mfma_f32_16x16x4f32(A[so][s], Bv[si][s], acc[so][si], 0, 0, 0);
+  }
+  // lane holds dW[o = 16 so + 4 kq + r][i = 16 si + (lane & 15)]
+#pragma unroll
+  for (int so = 0; so < 2; ++so)
+#pragma unroll
+    for (int si = 0; si < 2; ++si)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[(w * 32 + 16 * so + 4 * kq + r) * 33 + 16 * si + i] = acc[so][si][r];
+  __syncthreads();
+  const int o = tid >> 3, ic = (tid & 7) * 4;
+  const int64_t w2 = a.off[net_shape(t)].t[2];
+  float* w2t = a.P + a.w2t[t];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int col = ic + c;
+    const float g = ((red[(0 * 32 + o) * 33 + col] + red[(1 * 32 + o) * 33 + col]) + red[(2 * 32 + o) * 33 + col]) +
+                    red[(3 * 32 + o) * 33 + col];
+    const int64_t idx = w2 + (int64_t)(o0 + o) * kH + i0 + col;
+    update_elem(a, t, idx, g);
+    w2t[(int64_t)(i0 + col) * kH + o0 + o] = a.P[a.net[t] + idx];
+  }
+}
+
+// fc1.weight / fc1.bias / fc2.bias / head weights of 32 features of net t
+// (and the head biases in block 0): batch reductions on the VALU
+__device__ void small_params(const SacArgs& a, int t, int ob, int tid, float* xs) {
+  const NetAct& na = a.na[t];
+  const int B = a.B, D = a.D, in = net_in(t, D);
+  const NetOff& o = a.off[net_shape(t)];
+  const int f = 32 * ob + (tid >> 3), part = tid & 7;
+  const float* g0 = rowf(a, t == 0 ? F_GMU : (t == 1 ? F_GC1 : (t == 2 ? F_GC2 : F_GV)));
+  const float* g1 = t == 0 ? rowf(a, F_GSR) : nullptr;
+  float sb2 = 0.f, sb1 = 0.f, sh0 = 0.f, sh1 = 0.f, sw[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) sw[k] = 0.f;
+  for (int c0 = 0; c0 < B; c0 += 256) {
+    __syncthreads();
+    {  // X rows c0 .. c0+255 of this net's input: state (+ the stored action for critics)
+      const int rr = tid;
+      for (int k = 0; k < 16; ++k) {
+        float v = 0.f;
+        if (k < D) v = a.s[(int64_t)(c0 + rr) * D + k];
+        else if (k == D && in > D) v = a.act[c0 + rr];
+        xs[rr * 17 + k] = v;
+      }
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int q = 0; q < 256; q += 32) {
+      const int rl = q + 4 * part, r = c0 + rl;
+      const f4 z2 = *reinterpret_cast<const f4*>(na.dz2t + (int64_t)f * B + r);
+      const f4 z1 = *reinterpret_cast<const f4*>(na.dz1t + (int64_t)f * B + r);
+      const f4 h2 = *reinterpret_cast<const f4*>(na.h2t + (int64_t)f * B + r);
+      const f4 ga = *reinterpret_cast<const f4*>(g0 + r);
+      f4 gb = f4{0.f, 0.f, 0.f, 0.f};
+      if (g1 != nullptr) gb = *reinterpret_cast<const f4*>(g1 + r);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        sb2 += z2[e];
+        sb1 += z1[e];
+        sh0 = fmaf(ga[e], h2[e], sh0);
+        sh1 = fmaf(gb[e], h2[e], sh1);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) sw[k] = fmaf(z1[e], xs[(rl + e) * 17 + k], sw[k]);
+      }
+    }
+  }
+#pragma unroll
+  for (int s = 4; s > 0; s >>= 1) {
+    sb2 += __shfl_xor(sb2, s, 8);
+    sb1 += __shfl_xor(sb1, s, 8);
+    sh0 += __shfl_xor(sh0, s, 8);
+    sh1 += __shfl_xor(sh1, s, 8);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) sw[k] += __shfl_xor(sw[k], s, 8);
+  }
+  if (part == 0) {
+    update_elem(a, t, o.t[3] + f, sb2);
+    update_elem(a, t, o.t[1] + f, sb1);
+    update_elem(a, t, o.t[4] + f, sh0);
+    if (o.t[6] >= 0) update_elem(a, t, o.t[6] + f, sh1);
+    for (int k = 0; k < in; ++k) update_elem(a, t, o.t[0] + (int64_t)f * in + k, sw[k]);
+  }
+  if (ob == 0) {  // head biases: sums of the head-output gradients
+    __syncthreads();
+    float s0 = 0.f, s1 = 0.f;
+    for (int r = tid; r < B; r += kThreads) {
+      s0 += g0[r];
+      if (g1 != nullptr) s1 += g1[r];
+    }
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) {
+      s0 += __shfl_xor(s0, s, 64);
+      s1 += __shfl_xor(s1, s, 64);
+    }
+    if ((tid & 63) == 0) {
+      xs[tid >> 6] = s0;
+      xs[4 + (tid >> 6)] = s1;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      update_elem(a, t, o.t[5], ((xs[0] + xs[1]) + xs[2]) + xs[3]);
+      if (o.t[7] >= 0) update_elem(a, t, o.t[7], ((xs[4] + xs[5]) + xs[6]) + xs[7]);
+    }
+  }
+}
+
+__device__ void reduce_losses(const SacArgs& a, int tid, float* xs) {
+  for (int q = 0; q < 4; ++q) {  // F_LV, F_LA, F_LC1, F_LC2 are consecutive
+    const float* v = rowf(a, F_LV + q);
+    float s = 0.f;
+    for (int r = tid; r < a.B; r += kThreads) s += v[r];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if ((tid & 63) == 0) xs[4 * q + (tid >> 6)] = s;
+  }
+  __syncthreads();
+  if (tid < 4 && a.losses != nullptr) {
+    const float s = ((xs[4 * tid] + xs[4 * tid + 1]) + xs[4 * tid + 2]) + xs[4 * tid + 3];
+    const float mean = s / (float)a.B;
+    a.losses[tid] = tid == 1 ? mean : 0.5f * mean;  // 0.5 * mse for value and critics
+  }
+}
+
+constexpr int kFc2Tiles = 8 * 8;  // 32x32 tiles of a 256x256 layer
+
+__global__ void __launch_bounds__(kThreads) k_sac_update(SacArgs a) {
+  __shared__ float sm[kUpdLds];
+  const int tid = threadIdx.x, b = blockIdx.x;
+  if (b < 4 * kFc2Tiles) {
+    const int t = b / kFc2Tiles, tile = b % kFc2Tiles;
+    fc2_tile(a, t, tile >> 3, tile & 7, tid, sm);
+  } else if (b < 4 * kFc2Tiles + 4 * 8) {
+    const int q = b - 4 * kFc2Tiles;
+    small_params(a, q >> 3, q & 7, tid, sm);
+  } else {
+    reduce_losses(a, tid, sm);
+  }
+}
+
+// fc2.weight -> [in][out] transposes of nets 0..3
+__global__ void __launch_bounds__(kThreads) k_sac_transpose(SacArgs a) {
+  const int t = blockIdx.y;
+  const float* w2 = a.P + a.net[t] + a.off[net_shape(t)].t[2];
+  float* w2t = a.P + a.w2t[t];
+  for (int e = blockIdx.x * kThreads + threadIdx.x; e < kH * kH; e += gridDim.x * kThreads) {
+    const int o = e >> 8, i = e & (kH - 1);
+    w2t[i * kH + o] = w2[e];
+  }
+}
+
+// choose_action for n rows: actor forward and the sample() draw
+__global__ void __launch_bounds__(kThreads) k_sac_act(SacArgs a, const float* __restrict__ obs, int n,
+                                                        const float* __restrict__ eps, float* __restrict__ out,
+                                                        float* __restrict__ logp) {
+  __shared__ RowLds l;
+  const int tid = threadIdx.x, row0 = blockIdx.x * kRows;
+  const int nrows = n - row0 < kRows ? n - row0 : kRows;
+  const float* Pn = a.P + a.net[0];
+  const NetOff& o = a.off[kActorShape];
+  load_x(l.x, obs, a.D, row0, nrows, nullptr, tid);
+  __syncthreads();
+  trunk(Pn, o, a.D, l, tid, nullptr, nullptr, 0, row0);
+  const float mu = row_dot(l.h2, Pn + o.t[4], 1, tid) + Pn[o.t[5]];
+  const float sr = row_dot(l.h2, Pn + o.t[6], 1, tid) + Pn[o.t[7]];
+  const int j = tid >> 4;
+  if ((tid & 15) == 0 && j < nrows) {
+    float tl, x, act, lp;
+    const float sig = policy_sigma(sr, tl);
+    policy_draw(mu, sig, eps[row0 + j], a.max_action, x, act, lp);
+    out[row0 + j] = act;
+    if (logp != nullptr) logp[row0 + j] = lp;
+  }
+}
+
+// ---------------------------------------------------------------- host side
+
+int check(const SacenvSacParams* p) {
+  if (p == nullptr) return SACENV_E_NULL;
+  if (p->hidden != kH || p->n_actions != 1 || p->obs_dim < 1 || p->obs_dim > 15) return SACENV_E_SIZE;
+  if (p->batch < 256 || p->batch % 256 != 0 || p->batch > (1 << 20)) return SACENV_E_SIZE;
+  return SACENV_OK;
+}
+
+void make_layout(const SacenvSacParams* p, SacenvSacLayout* L) {
+  const int D = p->obs_dim;
+  const NetOff sh[3] = {net_off(D, 2), net_off(D + 1, 1), net_off(D, 1)};
+  int64_t q = 0;
+  for (int n = 0; n < 5; ++n) {
+    L->net[n] = q;
+    q += sh[net_shape(n)].size;
+  }
+  for (int n = 0; n < 4; ++n) {
+    L->adam_m[n] = q;
+    q += sh[net_shape(n)].size;
+  }
+  for (int n = 0; n < 4; ++n) {
+    L->adam_v[n] = q;
+    q += sh[net_shape(n)].size;
+  }
+  for (int n = 0; n < 4; ++n) {
+    L->w2t[n] = q;
+    q += (int64_t)kH * kH;
+  }
+  L->total_floats = q;
+  for (int s = 0; s < 3; ++s) {
+    L->net_floats[s] = sh[s].size;
+    for (int k = 0; k < 8; ++k) L->tensor[s][k] = sh[s].t[k];
+  }
+  L->scratch_bytes = (int64_t)sizeof(float) * p->batch * (16 * (int64_t)kH + F_COUNT);
+}
+
+SacArgs make_args(const SacenvSacParams* p, float* weights) {
+  SacenvSacLayout L;
+  make_layout(p, &L);
+  SacArgs a{};
+  a.P = weights;
+  for (int n = 0; n < 5; ++n) a.net[n] = L.net[n];
+  for (int n = 0; n < 4; ++n) {
+    a.am[n] = L.adam_m[n];
+    a.av[n] = L.adam_v[n];
+    a.w2t[n] = L.w2t[n];
+  }
+  a.off[0] = net_off(p->obs_dim, 2);
+  a.off[1] = net_off(p->obs_dim + 1, 1);
+  a.off[2] = net_off(p->obs_dim, 1);
+  a.B = p->batch;
+  a.D = p->obs_dim;
+  a.max_action = (float)p->max_action;
+  a.gamma = (float)p->gamma;
+  a.scale = (float)p->reward_scale;
+  a.inv_b = 1.f / (float)p->batch;
+  a.tau = (float)p->tau;
+  a.omtau = (float)(1.0 - p->tau);
+  return a;
+}
+
+bool aligned16(const void* q) { return ((uintptr_t)q & 15u) == 0; }
+
+}  // namespace
+
+extern "C" int sacenv_sac_layout(const SacenvSacParams* p, SacenvSacLayout* out) {
+  if (p == nullptr || out == nullptr) return SACENV_E_NULL;
+  const int rc = check(p);
+  if (rc != SACENV_OK) return rc;
+  make_layout(p, out);
+  return SACENV_OK;
+}
+
+extern "C" int sacenv_sac_sync(const SacenvSacParams* p, float* weights, void* stream) {
+  const int rc = check(p);
+  if (rc != SACENV_OK) return rc;
+  if (weights == nullptr) return SACENV_E_NULL;
+  if (!aligned16(weights)) return SACENV_E_SIZE;
+  const SacArgs a = make_args(p, weights);
+  hipLaunchKernelGGL(k_sac_transpose, dim3(64, 4), dim3(kThreads), 0, (hipStream_t)stream, a);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sacenv_sac_act(const SacenvSacParams* p, const float* weights, const float* obs, int32_t n,
+                              const float* eps, float* action, float* log_prob, void* stream) {
+  if (p == nullptr) return SACENV_E_NULL;
+  if (p->hidden != kH || p->n_actions != 1 || p->obs_dim < 1 || p->obs_dim > 15) return SACENV_E_SIZE;
+  if (n < 0) return SACENV_E_SIZE;
+  if (n == 0) return SACENV_OK;
+  if (weights == nullptr || obs == nullptr || eps == nullptr || action == nullptr) return SACENV_E_NULL;
+  if (!aligned16(weights)) return SACENV_E_SIZE;
+  SacenvSacParams q = *p;
+  q.batch = 256;  // unused by the act kernel
+  const SacArgs a = make_args(&q, const_cast<float*>(weights));
+  const int blocks = (n + kRows - 1) / kRows;
+  hipLaunchKernelGGL(k_sac_act, dim3(blocks), dim3(kThreads), 0, (hipStream_t)stream, a, obs, (int)n, eps, action,
+                     log_prob);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sacenv_sac_learn(const SacenvSacParams* p, float* weights, void* scratch, const float* state,
+                                const float* action, const double* reward, const float* new_state,
+                                const uint8_t* done, const float* eps1, const float* eps2, int32_t adam_step,
+                                float* losses, void* stream) {
+  const int rc = check(p);
+  if (rc != SACENV_OK) return rc;
+  if (weights == nullptr || scratch == nullptr || state == nullptr || action == nullptr || reward == nullptr ||
+      new_state == nullptr || done == nullptr || eps1 == nullptr || eps2 == nullptr)
+    return SACENV_E_NULL;
+  if (adam_step < 1) return SACENV_E_RANGE;
+  if (!aligned16(weights) || !aligned16(scratch)) return SACENV_E_SIZE;
+  SacArgs a = make_args(p, weights);
+  a.s = state;
+  a.act = action;
+  a.rew = reward;
+  a.s2 = new_state;
+  a.done = done;
+  a.eps1 = eps1;
+  a.eps2 = eps2;
+  a.losses = losses;
+  float* scr = static_cast<float*>(scratch);
+  const int64_t tile = (int64_t)kH * p->batch;
+  for (int t = 0; t < 4; ++t) {
+    a.na[t].h1t = scr + (4 * t + 0) * tile;
+    a.na[t].h2t = scr + (4 * t + 1) * tile;
+    a.na[t].dz1t = scr + (4 * t + 2) * tile;
+    a.na[t].dz2t = scr + (4 * t + 3) * tile;
+  }
+  a.rows = scr + 16 * tile;
+  // torch.optim.Adam (_multi_tensor_adam): Python-float scalars, cast to f32 in the kernels
+  const double b1 = p->adam_beta1, b2 = p->adam_beta2;
+  const double bc1 = 1.0 - pow(b1, (double)adam_step), bc2 = 1.0 - pow(b2, (double)adam_step);
+  a.lerp_w = (float)(1.0 - b1);
+  a.b2 = (float)b2;
+  a.omb2 = (float)(1.0 - b2);
+  a.bc2s = (float)pow(bc2, 0.5);
+  a.eps = (float)p->adam_eps;
+  a.nstep_actor = (float)((p->lr_actor / bc1) * -1.0);
+  a.nstep_critic = (float)((p->lr_critic / bc1) * -1.0);
+  const int nrb = p->batch / kRows;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_sac_rows, dim3(5 * nrb), dim3(kThreads), 0, s, a, 0);
+  hipLaunchKernelGGL(k_sac_rows, dim3(4 * nrb), dim3(kThreads), 0, s, a, 1);
+  hipLaunchKernelGGL(k_sac_rows, dim3(2 * nrb), dim3(kThreads), 0, s, a, 2);
+  hipLaunchKernelGGL(k_sac_update, dim3(4 * kFc2Tiles + 4 * 8 + 1), dim3(kThreads), 0, s, a);
+  return (int)hipGetLastError();
+}

@@ -11,7 +11,7 @@ import os
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # .../sac-agent_amd
 LIB_PATH = os.environ.get("SACENV_LIB", os.path.join(PKG_ROOT, "build", "libsacenv.so"))
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 OBS_DIM = 11
 MT_N = 624
 MAX_KNOTS = 16
@@ -102,12 +102,29 @@ class ReplayLayout(C.Structure):
     _fields_ = [(n, _i64) for n in REPLAY_LAYOUT_FIELDS]
 
 
+SAC_HIDDEN = 256
+
+
+class SacParams(C.Structure):
+    _fields_ = [("obs_dim", _i32), ("n_actions", _i32), ("hidden", _i32), ("batch", _i32),
+                ("max_action", _d), ("gamma", _d), ("tau", _d), ("reward_scale", _d),
+                ("lr_actor", _d), ("lr_critic", _d), ("adam_beta1", _d), ("adam_beta2", _d),
+                ("adam_eps", _d)]
+
+
+class SacLayout(C.Structure):
+    _fields_ = [("total_floats", _i64), ("net", _i64 * 5), ("adam_m", _i64 * 4), ("adam_v", _i64 * 4),
+                ("w2t", _i64 * 4), ("net_floats", _i64 * 3), ("tensor", (_i64 * 8) * 3),
+                ("scratch_bytes", _i64)]
+
+
 EXPORTS = ("sacenv_abi_version", "sacenv_error_string", "sacenv_boat_layout",
            "sacenv_boat_init", "sacenv_boat_reset", "sacenv_boat_reset_explicit",
            "sacenv_boat_step", "sacenv_boat_step_pooled", "sacenv_boat_rollout", "sacenv_boat_refill", "sacenv_boat_wind_eval", "sacenv_toy_layout", "sacenv_toy_init",
            "sacenv_toy_reset", "sacenv_toy_step", "sacenv_mixed_step", "sacenv_mixed_step_pooled", "sacenv_replay_layout",
            "sacenv_replay_init", "sacenv_replay_store", "sacenv_replay_store_env", "sacenv_replay_sample",
-           "sacenv_compact_done", "sacenv_boat_reset_list")
+           "sacenv_compact_done", "sacenv_boat_reset_list", "sacenv_sac_layout", "sacenv_sac_sync",
+           "sacenv_sac_act", "sacenv_sac_learn")
 
 _LIB = None
 
@@ -159,6 +176,11 @@ def load(path: str | None = None):
         "sacenv_replay_store": (C.c_int, [RP, _p, _i64, _p, _p, _p, _p, _p, _p, _p]),
         "sacenv_replay_store_env": (C.c_int, [RP, _p, _i64, _p, _p, _p, _p, _p, _p, _p, _p]),
         "sacenv_replay_sample": (C.c_int, [RP, _p, _i32, _i64, _p, _p, _p, _p, _p, _p, _p]),
+        "sacenv_sac_layout": (C.c_int, [C.POINTER(SacParams), C.POINTER(SacLayout)]),
+        "sacenv_sac_sync": (C.c_int, [C.POINTER(SacParams), _p, _p]),
+        "sacenv_sac_act": (C.c_int, [C.POINTER(SacParams), _p, _p, _i32, _p, _p, _p, _p]),
+        "sacenv_sac_learn": (C.c_int, [C.POINTER(SacParams), _p, _p, _p, _p, _p, _p, _p, _p, _p, _i32,
+                                       _p, _p]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -188,6 +210,12 @@ def layout(params: BoatParams) -> BoatLayout:
 def toy_layout(params: ToyParams) -> ToyLayout:
     out = ToyLayout()
     check(load().sacenv_toy_layout(C.byref(params), C.byref(out)))
+    return out
+
+
+def sac_layout(params: SacParams) -> SacLayout:
+    out = SacLayout()
+    check(load().sacenv_sac_layout(C.byref(params), C.byref(out)))
     return out
 
 

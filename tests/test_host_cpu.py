@@ -34,7 +34,7 @@ def declared_functions():
 def test_library_exports_header(built_lib):
     from sacenv import _lib
     names = declared_functions()
-    assert len(names) == 24
+    assert len(names) == 28
     assert set(names) == set(_lib.EXPORTS)
     for n in names:
         assert hasattr(built_lib, n), n
@@ -109,7 +109,8 @@ def test_ctypes_structs_match_c_layout(tmp_path):
     from sacenv import _lib
     structs = {"SacenvBoatParams": _lib.BoatParams, "SacenvBoatLayout": _lib.BoatLayout,
                "SacenvToyParams": _lib.ToyParams, "SacenvToyLayout": _lib.ToyLayout,
-               "SacenvReplayParams": _lib.ReplayParams, "SacenvReplayLayout": _lib.ReplayLayout}
+               "SacenvReplayParams": _lib.ReplayParams, "SacenvReplayLayout": _lib.ReplayLayout,
+               "SacenvSacParams": _lib.SacParams, "SacenvSacLayout": _lib.SacLayout}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "sacenv.h"', "int main(void) {"]
     for cname, py in structs.items():
         lines.append(f'printf("{cname} sizeof %zu\\n", sizeof({cname}));')
@@ -394,3 +395,63 @@ def test_library_binds_after_torch():
     code = ("import sys; sys.path.insert(0, 'sac-agent_amd'); from sacenv import _lib; "
             "assert 'torch' not in sys.modules; _lib.load(); assert 'torch' in sys.modules")
     subprocess.run([sys.executable, "-c", code], check=True, cwd=ROOT)
+
+
+def _sac_params(**kw):
+    from sacenv import _lib
+    base = dict(obs_dim=11, n_actions=1, hidden=256, batch=1024, max_action=1.0, gamma=0.99, tau=0.005,
+                reward_scale=10.0, lr_actor=0.005, lr_critic=3e-4, adam_beta1=0.9, adam_beta2=0.999,
+                adam_eps=1e-8)
+    base.update(kw)
+    return _lib.SacParams(**base)
+
+
+def test_sac_layout(built_lib):
+    """The SAC weights buffer: torch-shaped tensors per net, 16-B aligned and disjoint,
+    Adam states and transposes after the five nets, scratch sized for the batch."""
+    from sacenv import _lib
+    L = _lib.sac_layout(_sac_params())
+    H, D = 256, 11
+    sizes = {0: [(H * D), H, H * H, H, H, 1, H, 1], 1: [H * (D + 1), H, H * H, H, H, 1, -1, -1],
+             2: [H * D, H, H * H, H, H, 1, -1, -1]}
+    for s in range(3):
+        spans = []
+        for k, n in enumerate(sizes[s]):
+            off = L.tensor[s][k]
+            if n < 0:
+                assert off == -1
+                continue
+            assert off % 4 == 0
+            spans.append((off, off + n))
+        spans.sort()
+        for (a0, a1), (b0, b1) in zip(spans, spans[1:]):
+            assert a1 <= b0
+        assert spans[-1][1] <= L.net_floats[s]
+    shapes = [0, 1, 1, 2, 2]
+    regions = [(L.net[n], L.net[n] + L.net_floats[shapes[n]]) for n in range(5)]
+    regions += [(L.adam_m[n], L.adam_m[n] + L.net_floats[shapes[n]]) for n in range(4)]
+    regions += [(L.adam_v[n], L.adam_v[n] + L.net_floats[shapes[n]]) for n in range(4)]
+    regions += [(L.w2t[n], L.w2t[n] + H * H) for n in range(4)]
+    regions.sort()
+    for (a0, a1), (b0, b1) in zip(regions, regions[1:]):
+        assert a1 <= b0 and a0 % 4 == 0
+    assert regions[-1][1] == L.total_floats
+    assert L.scratch_bytes == 4 * 1024 * (16 * H + 28)
+
+
+def test_sac_argument_errors_without_gpu(built_lib):
+    import ctypes
+    from sacenv import _lib
+    lay = _lib.SacLayout()
+    assert built_lib.sacenv_sac_layout(ctypes.byref(_sac_params(batch=1000)), ctypes.byref(lay)) == -4
+    assert built_lib.sacenv_sac_layout(ctypes.byref(_sac_params(hidden=128)), ctypes.byref(lay)) == -4
+    assert built_lib.sacenv_sac_layout(ctypes.byref(_sac_params(n_actions=2)), ctypes.byref(lay)) == -4
+    assert built_lib.sacenv_sac_layout(ctypes.byref(_sac_params(obs_dim=16)), ctypes.byref(lay)) == -4
+    assert built_lib.sacenv_sac_layout(None, ctypes.byref(lay)) == -1
+    p = _sac_params()
+    args = [None] * 9
+    assert built_lib.sacenv_sac_learn(ctypes.byref(p), *args, 1, None, None) == -1
+    assert built_lib.sacenv_sac_learn(ctypes.byref(p), *([16] * 9), 0, None, None) == -5
+    assert built_lib.sacenv_sac_learn(ctypes.byref(p), *([8] * 9), 1, None, None) == -4  # unaligned
+    assert built_lib.sacenv_sac_act(ctypes.byref(p), None, None, 4, None, None, None, None) == -1
+    assert built_lib.sacenv_sac_act(ctypes.byref(p), None, None, 0, None, None, None, None) == 0
