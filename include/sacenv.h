@@ -390,7 +390,7 @@ int sacenv_replay_sample(const SacenvReplayParams *p, void *arena, int32_t batch
  * value: 256-256 MLPs, f32), as fp32 MFMA kernels (v_mfma_f32_16x16x4_f32).
  *
  * All five networks, the four Adam states and the kernel-side transposes of
- * the 256x256 layers live in one caller-owned f32 WEIGHTS buffer of
+ * the 256x256 layers (kernel copies in MFMA fragment order) live in one caller-owned f32 WEIGHTS buffer of
  * sacenv_sac_layout()->total_floats floats. Net n starts at layout.net[n]
  * (0 actor, 1 critic 1, 2 critic 2, 3 value, 4 target value); inside a net
  * the tensors sit at layout.tensor[shape][k] (shape 0 actor, 1 critic,
@@ -399,7 +399,7 @@ int sacenv_replay_sample(const SacenvReplayParams *p, void *arena, int32_t batch
  * -1 where absent): the torch layout of nn.Linear, so the host can view each
  * parameter in place. Adam's exp_avg / exp_avg_sq of net n < 4 start at
  * adam_m[n] / adam_v[n] with the same inner offsets. After the host writes
- * weights, sacenv_sac_sync() refreshes the transposes; learn keeps them.
+ * weights, sacenv_sac_sync() refreshes the kernel copies; learn keeps them.
  * `scratch` is a device buffer of layout.scratch_bytes (no contents kept
  * between calls). Same conventions as above: device pointers, host params,
  * stream-ordered, graph-capturable, 0 or an SACENV_E_* / hipError_t. */
@@ -426,14 +426,15 @@ typedef struct SacenvSacLayout {
   int64_t net[5];
   int64_t adam_m[4];
   int64_t adam_v[4];
-  int64_t w2t[4];          /* fc2.weight transposed [in][out] of nets 0..3 */
+  int64_t w2f[5];          /* kernel copy of fc2.weight in MFMA fragment order, nets 0..4 */
+  int64_t w2tf[4];         /* the same of fc2.weight transposed, nets 0..3 */
   int64_t net_floats[3];   /* floats of one net per shape */
   int64_t tensor[3][8];
   int64_t scratch_bytes;
 } SacenvSacLayout;
 
 int sacenv_sac_layout(const SacenvSacParams *p, SacenvSacLayout *out);
-/* rebuild the kernel-side transposes from the weights (after the host wrote them) */
+/* rebuild the kernel copies of the 256x256 layers from the weights (after the host wrote them) */
 int sacenv_sac_sync(const SacenvSacParams *p, float *weights, void *stream);
 /* choose_action for n observations [n][obs_dim]: action = tanh(mean + eps*std)
  * * max_action with the given standard normal draws eps [n] (networks.py:47-70,

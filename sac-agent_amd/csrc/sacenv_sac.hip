@@ -13,12 +13,12 @@
 // (:133, :139-140). So the four losses are independent and the kernels run
 // them side by side:
 //
-//   phase 0 (row blocks x 5 roles): actor forward + both policy draws, value
-//     forward, target forward (value_, done-masked), critic 1 / 2 forward on
-//     the stored actions.
-//   phase 1 (x 4): critic c at the sample() actions (value target) and at the
-//     rsample() actions with dq/da (actor loss); critic c's own loss backward
-//     (q_hat = scale * reward + gamma * value_).
+//   phase 0 (row blocks x 4 roles): actor forward + both policy draws, value
+//     forward, critic 1 / 2 forward on the stored actions.
+//   phase 1 (x 6): critic c at the rsample() actions with dq/da (actor loss);
+//     critic c's own loss backward (target forward for value_, done-masked;
+//     q_hat = scale * reward + gamma * value_); critic c at the sample()
+//     actions (value target).
 //   phase 2 (x 2): actor backward (min of the critics, tanh-squashed Normal
 //     log-prob), value backward (value_target = min q - log_prob).
 //   phase 3: weight gradients as batch reductions (dW = dZ^T H on MFMA), Adam
@@ -84,10 +84,19 @@ enum Shape { kActorShape = 0, kCriticShape = 1, kValueShape = 2 };
 __host__ __device__ inline int net_shape(int n) { return n == 0 ? kActorShape : (n <= 2 ? kCriticShape : kValueShape); }
 __host__ __device__ inline int net_in(int n, int D) { return net_shape(n) == kCriticShape ? D + 1 : D; }
 
+// Fragment order of a 256x256 layer's kernel copy: element (n, k) of the
+// [out][in] matrix sits where lane (i = n % 16, kq = (k % 16) / 4) of the
+// 16x16 block (n / 16, k / 16) reads it as component k % 4 of its float4: one
+// A-fragment load is 1 KB contiguous (eight full 128-B lines) instead of 16
+// half-used lines of the [out][in] layout.
+__host__ __device__ inline int64_t swz(int n, int k) {
+  return ((int64_t)((n >> 4) * 16 + (k >> 4)) * 64 + ((k & 15) >> 2) * 16 + (n & 15)) * 4 + (k & 3);
+}
+
 // per-row fields of the scratch, f32 [B] each
 enum RowField {
   F_MU, F_SR, F_SIG, F_TL, F_A1, F_LP1, F_A2, F_X2, F_LP2,   // actor forward + draws
-  F_V, F_VN,                                                 // value, value_ (done-masked target)
+  F_V, F_VN_UNUSED,                                          // value; (value_ stays in the critic-loss role)
   F_QC1, F_QC2,                                              // critics at the stored actions
   F_Q1A1, F_Q2A1, F_Q1A2, F_Q2A2, F_DA1, F_DA2,              // critics at the draws, dq/da at a2
   F_GMU, F_GSR, F_GC1, F_GC2, F_GV,                          // head-output gradients
@@ -104,6 +113,7 @@ struct NetAct {   // feature-major [kH][B] activations of one optimised net
 
 struct SacArgs {
   float* P;            // weights buffer
+  unsigned long long* stamps;  // SACENV_SAC_STAMPS diagnostics: [phase][block][16] s_memrealtime
   const float* s;      // state [B][D]
   const float* act;    // action [B]
   const double* rew;   // reward [B]
@@ -114,7 +124,7 @@ struct SacArgs {
   float* rows;         // row fields [F_COUNT][B]
   float* losses;
   NetAct na[4];        // actor, critic 1, critic 2, value
-  int64_t net[5], am[4], av[4], w2t[4];
+  int64_t net[5], am[4], av[4], w2f[5], w2tf[4];
   NetOff off[3];
   int B, D;
   float max_action, gamma, scale, inv_b;
@@ -124,6 +134,23 @@ struct SacArgs {
 };
 
 __device__ __forceinline__ float* rowf(const SacArgs& a, int f) { return a.rows + (int64_t)f * a.B; }
+
+#ifdef SACENV_SAC_STAMPS  // timing diagnostics: wall clock (100 MHz) per block of each phase
+#define STAMP(a, ph, k)                                                                           \
+  do {                                                                                            \
+    if (threadIdx.x == 0)                                                                         \
+      (a).stamps[((int64_t)(ph) * 1024 + blockIdx.x) * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define STAMP(a, ph, k) \
+  do {                  \
+  } while (0)
+#endif
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS
+// operations, not for its global stores (__syncthreads() would drain those
+// too; nothing in these kernels reads its own global stores back)
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // ---------------------------------------------------------------- LDS tiles
 
@@ -152,11 +179,11 @@ __device__ __forceinline__ void load_x(float* xl, const float* __restrict__ src,
 // feature-major [kH][B] rows row0..row0+15 -> LDS tile
 __device__ __forceinline__ void load_tile_t(float* hl, const float* __restrict__ gT, int B, int row0, int tid) {
   const int j = tid & 15, fg = tid >> 4;
-#pragma unroll 4
-  for (int q = 0; q < 16; ++q) {
-    const int f = fg * 16 + q;
-    hl[j * kSP + f] = gT[(int64_t)f * B + row0 + j];
-  }
+  float v[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) v[q] = gT[(int64_t)(fg * 16 + q) * B + row0 + j];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) hl[j * kSP + fg * 16 + q] = v[q];
 }
 
 __device__ __forceinline__ void store_tile_t(const float* hl, float* __restrict__ gT, int B, int row0, int tid) {
@@ -171,48 +198,99 @@ __device__ __forceinline__ void store_tile_t(const float* hl, float* __restrict_
 // ---------------------------------------------------------------- dense layer on MFMA
 
 // acc[t] <- W[64w + 16t + ..][:] . X^T for the 16 rows of xl. FC1: W is
-// [kH][kin] (kin <= 16, scalar loads); else [kH][kH] (float4 loads).
-template <bool FC1>
-__device__ __forceinline__ void layer(const float* __restrict__ W, int kin, const float* xl, int xs, int lane,
-                                      int w, f4 acc[4]) {
+// [kH][kin] (kin <= 16, scalar loads); else [kH][kH] (float4 loads, issued
+// kPrefetch k-blocks ahead: one block is 16 MFMAs = ~0.25 us, an L2 round
+// trip ~1 us, and hipcc on its own pipelines one block ahead)
+#ifndef SACENV_SAC_PREFETCH
+#define SACENV_SAC_PREFETCH 8
+#endif
+constexpr int kPrefetch = SACENV_SAC_PREFETCH;
+
+// the first kPrefetch k-blocks of a 256x256 layer's A fragments, issued early
+struct WPre {
+  f4 v[kPrefetch][4];
+};
+__device__ __forceinline__ const f4* frag(const float* __restrict__ Wf, int w, int t, int kb, int lane) {
+  return reinterpret_cast<const f4*>(Wf + ((int64_t)((4 * w + t) * 16 + kb) * 64 + lane) * 4);
+}
+__device__ __forceinline__ void w_prefetch(const float* __restrict__ Wf, int lane, int w, WPre& p) {
+#pragma unroll
+  for (int kb = 0; kb < kPrefetch; ++kb)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) p.v[kb][t] = *frag(Wf, w, t, kb, lane);
+}
+
+// acc[t] <- W[64w + 16t + ..][:] . X^T for the 16 rows of xl (256 x 256 layer, W
+// in fragment order);
+// blocks kb >= kPrefetch are loaded kPrefetch blocks ahead of their MFMAs
+__device__ __forceinline__ void layer256(const float* __restrict__ W, const WPre& pre, const float* xl, int xs,
+                                         int lane, int w, f4 acc[4]) {
   const int i = lane & 15, kq = lane >> 4;
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
-  constexpr int KB = FC1 ? 1 : kH / 16;
+  constexpr int KB = kH / 16;
+  f4 av[KB][4];
 #pragma unroll
   for (int kb = 0; kb < KB; ++kb) {
-    const f4 b = *reinterpret_cast<const f4*>(xl + i * xs + 16 * kb + 4 * kq);
-    f4 av[4];
+    if (kb + kPrefetch < KB) {
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int n = 64 * w + 16 * t + i;
-      if (FC1) {
-        const float* wp = W + n * kin;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const int k = 4 * kq + s;
-          av[t][s] = k < kin ? wp[k] : 0.f;
-        }
-      } else {
-        av[t] = *reinterpret_cast<const f4*>(W + n * kH + 16 * kb + 4 * kq);
-      }
+      for (int t = 0; t < 4; ++t) av[kb + kPrefetch][t] = *frag(W, w, t, kb + kPrefetch, lane);
+      __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead (the scheduler sinks them)
     }
+    const f4 b = *reinterpret_cast<const f4*>(xl + i * xs + 16 * kb + 4 * kq);
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
-      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t][s], b[s], acc[t], 0, 0, 0);
+      for (int t = 0; t < 4; ++t) {
+        const float aw = kb < kPrefetch ? pre.v[kb < kPrefetch ? kb : 0][t][s] : av[kb][t][s];
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(aw, b[s], acc[t], 0, 0, 0);
+      }
   }
+}
+
+// fc1 (K = kin <= 16): A fragments of the four tiles, loaded early
+struct W1Pre {
+  f4 v[4];
+};
+__device__ __forceinline__ void w1_prefetch(const float* __restrict__ W, int kin, int lane, int w, W1Pre& p) {
+  const int i = lane & 15, kq = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const float* wp = W + (64 * w + 16 * t + i) * kin;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int k = 4 * kq + s;
+      p.v[t][s] = k < kin ? wp[k] : 0.f;
+    }
+  }
+}
+__device__ __forceinline__ void layer_fc1(const W1Pre& p, const float* xl, int xs, int lane, f4 acc[4]) {
+  const int i = lane & 15, kq = lane >> 4;
+  const f4 b = *reinterpret_cast<const f4*>(xl + i * xs + 4 * kq);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(p.v[t][s], b[s], acc[t], 0, 0, 0);
+}
+
+// a tile's bias slice, per lane (features 64w + 16t + 4kq .. +3)
+__device__ __forceinline__ void bias_prefetch(const float* __restrict__ bias, int lane, int w, f4 bv[4]) {
+  const int kq = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) bv[t] = *reinterpret_cast<const f4*>(bias + 64 * w + 16 * t + 4 * kq);
 }
 
 // forward epilogue: y = relu(acc + bias) -> LDS tile (and feature-major global)
 // lane (j = row, kq) holds features 64w + 16t + 4kq + r
-__device__ __forceinline__ void epi_fwd(const f4 acc[4], const float* __restrict__ bias, float* yl, int lane, int w,
+__device__ __forceinline__ void epi_fwd(const f4 acc[4], const f4 bv[4], float* yl, int lane, int w,
                                         float* __restrict__ gT, int B, int row0) {
   const int j = lane & 15, kq = lane >> 4;
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const int n0 = 64 * w + 16 * t + 4 * kq;
-    const f4 bb = *reinterpret_cast<const f4*>(bias + n0);
+    const f4 bb = bv[t];
     f4 y;
 #pragma unroll
     for (int r = 0; r < 4; ++r) y[r] = fmaxf(acc[t][r] + bb[r], 0.f);
@@ -256,23 +334,42 @@ __device__ __forceinline__ float row_dot(const float* hl, const float* __restric
 }
 
 // two-layer trunk on the input tile in l.x: h1, h2 in LDS (and optionally global)
+// input rows (state, + acol at column D) -> fc1 -> fc2 for the 16 rows: every
+// parameter load (fc1 fragments, biases, fc2's first k-blocks) is issued with
+// the input loads, before the first barrier
 __device__ __forceinline__ void trunk(const float* __restrict__ Pn, const NetOff& o, int kin, RowLds& l, int tid,
-                                      float* h1t, float* h2t, int B, int row0) {
+                                      float* h1t, float* h2t, int B, int row0, const float* __restrict__ src,
+                                      int D, const float* __restrict__ acol, const float* __restrict__ w2f,
+                                      const SacArgs* sa = nullptr, int ph = 0) {
   const int lane = tid & 63, w = tid >> 6;
+  W1Pre w1;
+  w1_prefetch(Pn + o.t[0], kin, lane, w, w1);
+  f4 b1[4], b2[4];
+  bias_prefetch(Pn + o.t[1], lane, w, b1);
+  bias_prefetch(Pn + o.t[3], lane, w, b2);
+  WPre w2;
+  w_prefetch(w2f, lane, w, w2);
+  load_x(l.x, src, D, row0, kRows, acol, tid);
+  lds_sync();
+  if (sa) STAMP(*sa, ph, 1);
   f4 acc[4];
-  layer<true>(Pn + o.t[0], kin, l.x, kXP, lane, w, acc);
-  epi_fwd(acc, Pn + o.t[1], l.h1, lane, w, h1t, B, row0);
-  __syncthreads();
-  layer<false>(Pn + o.t[2], kH, l.h1, kSP, lane, w, acc);
-  epi_fwd(acc, Pn + o.t[3], l.h2, lane, w, h2t, B, row0);
-  __syncthreads();
+  layer_fc1(w1, l.x, kXP, lane, acc);
+  epi_fwd(acc, b1, l.h1, lane, w, h1t, B, row0);
+  lds_sync();
+  if (sa) STAMP(*sa, ph, 2);
+  layer256(w2f, w2, l.h1, kSP, lane, w, acc);
+  if (sa) STAMP(*sa, ph, 3);
+  epi_fwd(acc, b2, l.h2, lane, w, h2t, B, row0);
+  lds_sync();
+  if (sa) STAMP(*sa, ph, 4);
 }
 
 // head backward: dz2 = (wh0 g0 + wh1 g1) * [h2 > 0] -> dz2t; dz1 = (W2^T dz2) * [h1 > 0]
+// (W2^T in fragment order: w2tf)
 // -> dz1t (and LDS l.h2 when keep_dz1). g0/g1 per row in l.g0/l.g1.
 __device__ __forceinline__ void head_backward(const float* __restrict__ Pn, const NetOff& o,
-                                              const float* __restrict__ w2t, RowLds& l, int tid, float* dz2t,
-                                              float* dz1t, int B, int row0, bool keep_dz1) {
+                                              const float* __restrict__ w2tf, const WPre& pre, RowLds& l, int tid,
+                                              float* dz2t, float* dz1t, int B, int row0, bool keep_dz1) {
   const int lane = tid & 63, w = tid >> 6;
   const float* wh0 = Pn + o.t[4];
   const float* wh1 = o.t[6] >= 0 ? Pn + o.t[6] : nullptr;
@@ -282,13 +379,13 @@ __device__ __forceinline__ void head_backward(const float* __restrict__ Pn, cons
     if (wh1 != nullptr) g = g + wh1[f] * l.g1[j];
     l.z[j * kSP + f] = l.h2[j * kSP + f] > 0.f ? g : 0.f;
   }
-  __syncthreads();
-  if (dz2t != nullptr) store_tile_t(l.z, dz2t, B, row0, tid);
+  lds_sync();
   f4 acc[4];
-  layer<false>(w2t, kH, l.z, kSP, lane, w, acc);
-  __syncthreads();  // every wave has read l.z / l.h2 before l.h2 is overwritten
+  layer256(w2tf, pre, l.z, kSP, lane, w, acc);
+  if (dz2t != nullptr) store_tile_t(l.z, dz2t, B, row0, tid);  // l.z stays until the next barrier
+  lds_sync();  // every wave has read l.z / l.h2 before l.h2 is overwritten
   epi_bwd(acc, l.h1, keep_dz1 ? l.h2 : nullptr, lane, w, dz1t, B, row0);
-  __syncthreads();
+  lds_sync();
 }
 
 // tanh-squashed Normal draw (networks.py:47-70): x = mean + eps * std,
@@ -311,9 +408,7 @@ __device__ __forceinline__ void policy_draw(float mu, float sig, float eps, floa
 __device__ void role_actor_fwd(const SacArgs& a, RowLds& l, int tid, int row0) {
   const float* Pn = a.P + a.net[0];
   const NetOff& o = a.off[kActorShape];
-  load_x(l.x, a.s, a.D, row0, kRows, nullptr, tid);
-  __syncthreads();
-  trunk(Pn, o, a.D, l, tid, a.na[0].h1t, a.na[0].h2t, a.B, row0);
+  trunk(Pn, o, a.D, l, tid, a.na[0].h1t, a.na[0].h2t, a.B, row0, a.s, a.D, nullptr, a.P + a.w2f[0]);
   const float mu = row_dot(l.h2, Pn + o.t[4], 1, tid) + Pn[o.t[5]];
   const float sr = row_dot(l.h2, Pn + o.t[6], 1, tid) + Pn[o.t[7]];
   if ((tid & 15) == 0) {
@@ -335,31 +430,29 @@ __device__ void role_actor_fwd(const SacArgs& a, RowLds& l, int tid, int row0) {
   }
 }
 
-// value(state) (storing the activations) or target_value(new_state) -> value_
-__device__ void role_value_fwd(const SacArgs& a, RowLds& l, int tid, int row0, bool target) {
+// value(state) (storing the activations) or target_value(new_state); v in the row's lanes
+__device__ float value_fwd(const SacArgs& a, RowLds& l, int tid, int row0, bool target) {
   const int n = target ? 4 : 3;
   const float* Pn = a.P + a.net[n];
   const NetOff& o = a.off[kValueShape];
-  load_x(l.x, target ? a.s2 : a.s, a.D, row0, kRows, nullptr, tid);
-  __syncthreads();
-  trunk(Pn, o, a.D, l, tid, target ? nullptr : a.na[3].h1t, target ? nullptr : a.na[3].h2t, a.B, row0);
+  trunk(Pn, o, a.D, l, tid, target ? nullptr : a.na[3].h1t, target ? nullptr : a.na[3].h2t, a.B, row0,
+        target ? a.s2 : a.s, a.D, nullptr, a.P + a.w2f[n], target ? nullptr : &a, 0);
   const float v = row_dot(l.h2, Pn + o.t[4], 1, tid) + Pn[o.t[5]];
-  if ((tid & 15) == 0) {
-    const int r = row0 + (tid >> 4);
-    if (target)
-      rowf(a, F_VN)[r] = a.done[r] ? 0.f : v;  // value_[done] = 0.0 (:111)
-    else
-      rowf(a, F_V)[r] = v;
-  }
+  if (!target) STAMP(a, 0, 5);
+  return v;
+}
+
+__device__ void role_value_fwd(const SacArgs& a, RowLds& l, int tid, int row0) {
+  const float v = value_fwd(a, l, tid, row0, false);
+  if ((tid & 15) == 0) rowf(a, F_V)[row0 + (tid >> 4)] = v;
 }
 
 // critic c (1, 2) on [state, acol]; returns q in the row's lanes
 __device__ float critic_fwd(const SacArgs& a, RowLds& l, int tid, int row0, int c, const float* acol, bool store) {
   const float* Pn = a.P + a.net[c];
   const NetOff& o = a.off[kCriticShape];
-  load_x(l.x, a.s, a.D, row0, kRows, acol, tid);
-  __syncthreads();
-  trunk(Pn, o, a.D + 1, l, tid, store ? a.na[c].h1t : nullptr, store ? a.na[c].h2t : nullptr, a.B, row0);
+  trunk(Pn, o, a.D + 1, l, tid, store ? a.na[c].h1t : nullptr, store ? a.na[c].h2t : nullptr, a.B, row0, a.s, a.D,
+        acol, a.P + a.w2f[c]);
   return row_dot(l.h2, Pn + o.t[4], 1, tid) + Pn[o.t[5]];
 }
 
@@ -368,49 +461,66 @@ __device__ void role_critic_stored(const SacArgs& a, RowLds& l, int tid, int row
   if ((tid & 15) == 0) rowf(a, c == 1 ? F_QC1 : F_QC2)[row0 + (tid >> 4)] = q;
 }
 
-// critic c at the sample() actions (value target, :113-117) and at the
-// rsample() actions with dq/da through the critic (actor loss, :127-131)
-__device__ void role_critic_policy(const SacArgs& a, RowLds& l, int tid, int row0, int c) {
+// critic c at the sample() actions: the value target's min q (:113-117)
+__device__ void role_critic_sample(const SacArgs& a, RowLds& l, int tid, int row0, int c) {
   const float qa1 = critic_fwd(a, l, tid, row0, c, rowf(a, F_A1), false);
-  __syncthreads();
+  if ((tid & 15) == 0) rowf(a, c == 1 ? F_Q1A1 : F_Q2A1)[row0 + (tid >> 4)] = qa1;
+}
+
+// critic c at the rsample() actions with dq/da through the critic (actor loss, :127-131)
+__device__ void role_critic_rsample(const SacArgs& a, RowLds& l, int tid, int row0, int c) {
   const float qa2 = critic_fwd(a, l, tid, row0, c, rowf(a, F_A2), false);
   const float* Pn = a.P + a.net[c];
   const NetOff& o = a.off[kCriticShape];
+  WPre pre;
+  w_prefetch(a.P + a.w2tf[c], tid & 63, tid >> 6, pre);
   if ((tid & 15) == 0) l.g0[tid >> 4] = 1.f;
-  __syncthreads();
-  head_backward(Pn, o, a.P + a.w2t[c], l, tid, nullptr, nullptr, a.B, row0, true);
+  lds_sync();
+  head_backward(Pn, o, a.P + a.w2tf[c], pre, l, tid, nullptr, nullptr, a.B, row0, true);
   // dq/da = W1[:, D] . dz1
   const float da = row_dot(l.h2, Pn + o.t[0] + a.D, a.D + 1, tid);
   if ((tid & 15) == 0) {
     const int r = row0 + (tid >> 4);
-    rowf(a, c == 1 ? F_Q1A1 : F_Q2A1)[r] = qa1;
     rowf(a, c == 1 ? F_Q1A2 : F_Q2A2)[r] = qa2;
     rowf(a, c == 1 ? F_DA1 : F_DA2)[r] = da;
   }
 }
 
 // critic c's loss backward: 0.5 mse(q, q_hat), q_hat = scale r + gamma value_ (:141-146)
+// (value_ = target_value(new_state), done-masked (:108-111), computed here: one
+// more layer for this role, one role fewer in phase 0 — 256 workgroups, one per CU)
 __device__ void role_critic_loss(const SacArgs& a, RowLds& l, int tid, int row0, int c) {
   const NetAct& na = a.na[c];
+  const float vt = value_fwd(a, l, tid, row0, true);
+  if ((tid & 15) == 0) {
+    const int j = tid >> 4;
+    l.g1[j] = a.done[row0 + j] ? 0.f : vt;  // value_[done] = 0.0
+  }
+  WPre pre;
+  w_prefetch(a.P + a.w2tf[c], tid & 63, tid >> 6, pre);
+  lds_sync();
   load_tile_t(l.h1, na.h1t, a.B, row0, tid);
   load_tile_t(l.h2, na.h2t, a.B, row0, tid);
   if (tid < kRows) {
     const int r = row0 + tid;
     const float q = rowf(a, c == 1 ? F_QC1 : F_QC2)[r];
-    const float qh = a.scale * (float)a.rew[r] + a.gamma * rowf(a, F_VN)[r];
+    const float qh = a.scale * (float)a.rew[r] + a.gamma * l.g1[tid];
     const float d = q - qh;
     const float g = d * a.inv_b;  // mse backward: (2 / B) (q - q_hat) * 0.5
     l.g0[tid] = g;
     rowf(a, c == 1 ? F_GC1 : F_GC2)[r] = g;
     rowf(a, c == 1 ? F_LC1 : F_LC2)[r] = d * d;
   }
-  __syncthreads();
-  head_backward(a.P + a.net[c], a.off[kCriticShape], a.P + a.w2t[c], l, tid, na.dz2t, na.dz1t, a.B, row0, false);
+  lds_sync();
+  head_backward(a.P + a.net[c], a.off[kCriticShape], a.P + a.w2tf[c], pre, l, tid, na.dz2t, na.dz1t, a.B, row0,
+                false);
 }
 
 // actor loss backward: mean(log_prob - min(q1, q2)) at the rsample() draw (:127-135)
 __device__ void role_actor_bwd(const SacArgs& a, RowLds& l, int tid, int row0) {
   const NetAct& na = a.na[0];
+  WPre pre;
+  w_prefetch(a.P + a.w2tf[0], tid & 63, tid >> 6, pre);
   load_tile_t(l.h1, na.h1t, a.B, row0, tid);
   load_tile_t(l.h2, na.h2t, a.B, row0, tid);
   if (tid < kRows) {
@@ -439,13 +549,15 @@ __device__ void role_actor_bwd(const SacArgs& a, RowLds& l, int tid, int row0) {
     rowf(a, F_GSR)[r] = dsr;
     rowf(a, F_LA)[r] = rowf(a, F_LP2)[r] - fminf(q1, q2);
   }
-  __syncthreads();
-  head_backward(a.P + a.net[0], a.off[kActorShape], a.P + a.w2t[0], l, tid, na.dz2t, na.dz1t, a.B, row0, false);
+  lds_sync();
+  head_backward(a.P + a.net[0], a.off[kActorShape], a.P + a.w2tf[0], pre, l, tid, na.dz2t, na.dz1t, a.B, row0, false);
 }
 
 // value loss backward: 0.5 mse(value, min q(sample()) - log_prob) (:113-124)
 __device__ void role_value_bwd(const SacArgs& a, RowLds& l, int tid, int row0) {
   const NetAct& na = a.na[3];
+  WPre pre;
+  w_prefetch(a.P + a.w2tf[3], tid & 63, tid >> 6, pre);
   load_tile_t(l.h1, na.h1t, a.B, row0, tid);
   load_tile_t(l.h2, na.h2t, a.B, row0, tid);
   if (tid < kRows) {
@@ -457,27 +569,30 @@ __device__ void role_value_bwd(const SacArgs& a, RowLds& l, int tid, int row0) {
     rowf(a, F_GV)[r] = g;
     rowf(a, F_LV)[r] = d * d;
   }
-  __syncthreads();
-  head_backward(a.P + a.net[3], a.off[kValueShape], a.P + a.w2t[3], l, tid, na.dz2t, na.dz1t, a.B, row0, false);
+  lds_sync();
+  head_backward(a.P + a.net[3], a.off[kValueShape], a.P + a.w2tf[3], pre, l, tid, na.dz2t, na.dz1t, a.B, row0, false);
 }
 
-__global__ void __launch_bounds__(kThreads) k_sac_rows(SacArgs a, int phase) {
+// one or two workgroups per CU: registers for kPrefetch k-blocks of weights in flight
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 2))) k_sac_rows(SacArgs a, int phase) {
   __shared__ RowLds l;
   const int tid = threadIdx.x;
   const int nrb = a.B / kRows;
   const int role = blockIdx.x / nrb, row0 = (blockIdx.x - role * nrb) * kRows;
+  STAMP(a, phase, 0);
   if (phase == 0) {
     if (role == 0) role_actor_fwd(a, l, tid, row0);
-    else if (role == 1) role_value_fwd(a, l, tid, row0, false);
-    else if (role == 2) role_value_fwd(a, l, tid, row0, true);
-    else role_critic_stored(a, l, tid, row0, role - 2);
-  } else if (phase == 1) {
-    if (role < 2) role_critic_policy(a, l, tid, row0, role + 1);
-    else role_critic_loss(a, l, tid, row0, role - 1);
+    else if (role == 1) role_value_fwd(a, l, tid, row0);
+    else role_critic_stored(a, l, tid, row0, role - 1);
+  } else if (phase == 1) {  // two-layer roles first; the one-layer ones share CUs
+    if (role < 2) role_critic_rsample(a, l, tid, row0, role + 1);
+    else if (role < 4) role_critic_loss(a, l, tid, row0, role - 1);
+    else role_critic_sample(a, l, tid, row0, role - 3);
   } else {
     if (role == 0) role_actor_bwd(a, l, tid, row0);
     else role_value_bwd(a, l, tid, row0);
   }
+  STAMP(a, phase, 15);
 }
 
 // ---------------------------------------------------------------- phase 3: gradients + Adam
@@ -504,7 +619,34 @@ __device__ __forceinline__ void update_elem(const SacArgs& a, int t, int64_t idx
   }
 }
 
-constexpr int kUpdLds = 4 * 32 * 33 > 256 * 17 ? 4 * 32 * 33 : 256 * 17;
+constexpr int kXChunk = 256;                // batch rows of X staged per pass (small_params)
+constexpr int kUpdLds = kXChunk * 17 > 4 * 32 * 33 ? kXChunk * 17 : 4 * 32 * 33;
+
+// C k-blocks of 16 rows: every load issued before the first MFMA (the update
+// launch runs one wave per SIMD: registers to spare, latency to hide)
+template <int C>
+__device__ __forceinline__ void fc2_chunk(const float* __restrict__ dz2t, const float* __restrict__ h1t, int B,
+                                          int r0, int o0, int i0, int i, int kq, f4 acc[2][2]) {
+  f4 A[C][2], Bv[C][2];
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const int r = r0 + 16 * c + 4 * kq;
+#pragma unroll
+    for (int so = 0; so < 2; ++so) A[c][so] = *reinterpret_cast<const f4*>(dz2t + (int64_t)(o0 + 16 * so + i) * B + r);
+#pragma unroll
+    for (int si = 0; si < 2; ++si) Bv[c][si] = *reinterpret_cast<const f4*>(h1t + (int64_t)(i0 + 16 * si + i) * B + r);
+  }
+  __builtin_amdgcn_sched_barrier(0);  // all loads in flight before the first MFMA
+#pragma unroll
+  for (int c = 0; c < C; ++c)
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int so = 0; so < 2; ++so)
+#pragma unroll
+        for (int si = 0; si < 2; ++si)
+          acc[so][si] = __builtin_amdgcn_mfma_f32_16x16x4f32(A[c][so][s], Bv[c][si][s], acc[so][si], 0, 0, 0);
+}
 
 // fc2.weight gradient tile (32 out x 32 in) of net t: dW = dz2^T h1 over the
 // batch, each wave a quarter of the rows, then Adam and the transpose
@@ -518,20 +660,10 @@ __device__ void fc2_tile(const SacArgs& a, int t, int ob, int ib, int tid, float
   for (int so = 0; so < 2; ++so)
 #pragma unroll
     for (int si = 0; si < 2; ++si) acc[so][si] = f4{0.f, 0.f, 0.f, 0.f};
-  for (int r0 = rbeg; r0 < rbeg + rq; r0 += 16) {
-    f4 A[2], Bv[2];
-#pragma unroll
-    for (int so = 0; so < 2; ++so) A[so] = *reinterpret_cast<const f4*>(na.dz2t + (int64_t)(o0 + 16 * so + i) * B + r0 + 4 * kq);
-#pragma unroll
-    for (int si = 0; si < 2; ++si) Bv[si] = *reinterpret_cast<const f4*>(na.h1t + (int64_t)(i0 + 16 * si + i) * B + r0 + 4 * kq);
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int so = 0; so < 2; ++so)
-#pragma unroll
-        for (int si = 0; si < 2; ++si)
-          acc[so][si] = __builtin_amdgcn_mfma_f32_16x16x4f32(A[so][s], Bv[si][s], acc[so][si], 0, 0, 0);
-  }
+  int r0 = rbeg;
+  for (; r0 + 256 <= rbeg + rq; r0 += 256) fc2_chunk<16>(na.dz2t, na.h1t, B, r0, o0, i0, i, kq, acc);
+  for (; r0 < rbeg + rq; r0 += 64) fc2_chunk<4>(na.dz2t, na.h1t, B, r0, o0, i0, i, kq, acc);  // rq % 64 == 0
+  STAMP(a, 3, 1);
   // lane holds dW[o = 16 so + 4 kq + r][i = 16 si + (lane & 15)]
 #pragma unroll
   for (int so = 0; so < 2; ++so)
@@ -539,47 +671,62 @@ __device__ void fc2_tile(const SacArgs& a, int t, int ob, int ib, int tid, float
     for (int si = 0; si < 2; ++si)
 #pragma unroll
       for (int r = 0; r < 4; ++r) red[(w * 32 + 16 * so + 4 * kq + r) * 33 + 16 * si + i] = acc[so][si][r];
-  __syncthreads();
+  lds_sync();
+  STAMP(a, 3, 2);
   const int o = tid >> 3, ic = (tid & 7) * 4;
   const int64_t w2 = a.off[net_shape(t)].t[2];
-  float* w2t = a.P + a.w2t[t];
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
-    const int col = ic + c;
+    const int col = ic + c, n = o0 + o, k = i0 + col;
     const float g = ((red[(0 * 32 + o) * 33 + col] + red[(1 * 32 + o) * 33 + col]) + red[(2 * 32 + o) * 33 + col]) +
                     red[(3 * 32 + o) * 33 + col];
-    const int64_t idx = w2 + (int64_t)(o0 + o) * kH + i0 + col;
+    const int64_t idx = w2 + (int64_t)n * kH + k;
     update_elem(a, t, idx, g);
-    w2t[(int64_t)(i0 + col) * kH + o0 + o] = a.P[a.net[t] + idx];
+    const float p = a.P[a.net[t] + idx];
+    a.P[a.w2f[t] + swz(n, k)] = p;   // kernel copies: forward and backward fragment order
+    a.P[a.w2tf[t] + swz(k, n)] = p;
+    if (t == 3) a.P[a.w2f[4] + swz(n, k)] = a.P[a.net[4] + idx];  // the target's forward copy
   }
 }
 
-// fc1.weight / fc1.bias / fc2.bias / head weights of 32 features of net t
-// (and the head biases in block 0): batch reductions on the VALU
-__device__ void small_params(const SacArgs& a, int t, int ob, int tid, float* xs) {
+constexpr int kSmallF = 8;  // features per small-parameter workgroup (32 lanes each)
+
+// fc1.weight / fc1.bias / fc2.bias / head weights of 8 features of net t (and
+// the head biases in block 0): batch reductions on the VALU, lane p of a
+// feature summing rows 4p + 128q (+0..3); then one Adam item per lane
+__device__ void small_params(const SacArgs& a, int t, int fb, int tid, float* xs) {
   const NetAct& na = a.na[t];
   const int B = a.B, D = a.D, in = net_in(t, D);
   const NetOff& o = a.off[net_shape(t)];
-  const int f = 32 * ob + (tid >> 3), part = tid & 7;
+  const int f = kSmallF * fb + (tid >> 5), part = tid & 31;
   const float* g0 = rowf(a, t == 0 ? F_GMU : (t == 1 ? F_GC1 : (t == 2 ? F_GC2 : F_GV)));
   const float* g1 = t == 0 ? rowf(a, F_GSR) : nullptr;
   float sb2 = 0.f, sb1 = 0.f, sh0 = 0.f, sh1 = 0.f, sw[16];
 #pragma unroll
   for (int k = 0; k < 16; ++k) sw[k] = 0.f;
-  for (int c0 = 0; c0 < B; c0 += 256) {
-    __syncthreads();
-    {  // X rows c0 .. c0+255 of this net's input: state (+ the stored action for critics)
-      const int rr = tid;
-      for (int k = 0; k < 16; ++k) {
-        float v = 0.f;
-        if (k < D) v = a.s[(int64_t)(c0 + rr) * D + k];
-        else if (k == D && in > D) v = a.act[c0 + rr];
-        xs[rr * 17 + k] = v;
+  for (int c0 = 0; c0 < B; c0 += kXChunk) {
+    const int nr = B - c0 < kXChunk ? B - c0 : kXChunk;  // a multiple of 256
+    lds_sync();
+    {  // this net's input rows: state (+ the stored action); all loads in flight, then LDS
+      float v[kXChunk * 16 / kThreads];
+#pragma unroll
+      for (int m = 0; m < kXChunk * 16 / kThreads; ++m) {
+        const int e = tid + kThreads * m, rr = e >> 4, k = e & 15;
+        v[m] = 0.f;
+        if (rr < nr) {
+          if (k < D) v[m] = a.s[(int64_t)(c0 + rr) * D + k];
+          else if (k == D && in > D) v[m] = a.act[c0 + rr];
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < kXChunk * 16 / kThreads; ++m) {
+        const int e = tid + kThreads * m;
+        xs[(e >> 4) * 17 + (e & 15)] = v[m];
       }
     }
-    __syncthreads();
-#pragma unroll 1
-    for (int q = 0; q < 256; q += 32) {
+    lds_sync();
+#pragma unroll 4
+    for (int q = 0; q < nr; q += 128) {
       const int rl = q + 4 * part, r = c0 + rl;
       const f4 z2 = *reinterpret_cast<const f4*>(na.dz2t + (int64_t)f * B + r);
       const f4 z1 = *reinterpret_cast<const f4*>(na.dz1t + (int64_t)f * B + r);
@@ -599,42 +746,46 @@ __device__ void small_params(const SacArgs& a, int t, int ob, int tid, float* xs
     }
   }
 #pragma unroll
-  for (int s = 4; s > 0; s >>= 1) {
-    sb2 += __shfl_xor(sb2, s, 8);
-    sb1 += __shfl_xor(sb1, s, 8);
-    sh0 += __shfl_xor(sh0, s, 8);
-    sh1 += __shfl_xor(sh1, s, 8);
+  for (int m = 16; m > 0; m >>= 1) {
+    sb2 += __shfl_xor(sb2, m, 32);
+    sb1 += __shfl_xor(sb1, m, 32);
+    sh0 += __shfl_xor(sh0, m, 32);
+    sh1 += __shfl_xor(sh1, m, 32);
 #pragma unroll
-    for (int k = 0; k < 16; ++k) sw[k] += __shfl_xor(sw[k], s, 8);
+    for (int k = 0; k < 16; ++k) sw[k] += __shfl_xor(sw[k], m, 32);
   }
-  if (part == 0) {
-    update_elem(a, t, o.t[3] + f, sb2);
-    update_elem(a, t, o.t[1] + f, sb1);
-    update_elem(a, t, o.t[4] + f, sh0);
-    if (o.t[6] >= 0) update_elem(a, t, o.t[6] + f, sh1);
-    for (int k = 0; k < in; ++k) update_elem(a, t, o.t[0] + (int64_t)f * in + k, sw[k]);
-  }
-  if (ob == 0) {  // head biases: sums of the head-output gradients
-    __syncthreads();
+  STAMP(a, 3, 3);
+  // item part: 0..in-1 fc1.weight[f][k], then fc1.bias, fc2.bias, head-0 weight, head-1 weight
+  float g = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k)
+    if (k == part) g = sw[k];
+  int64_t idx = -1;
+  if (part < in) idx = o.t[0] + (int64_t)f * in + part;
+  else if (part == in) idx = o.t[1] + f, g = sb1;
+  else if (part == in + 1) idx = o.t[3] + f, g = sb2;
+  else if (part == in + 2) idx = o.t[4] + f, g = sh0;
+  else if (part == in + 3 && o.t[6] >= 0) idx = o.t[6] + f, g = sh1;
+  if (idx >= 0) update_elem(a, t, idx, g);
+  if (fb == 0) {  // head biases: sums of the head-output gradients
+    lds_sync();
     float s0 = 0.f, s1 = 0.f;
     for (int r = tid; r < B; r += kThreads) {
       s0 += g0[r];
       if (g1 != nullptr) s1 += g1[r];
     }
 #pragma unroll
-    for (int s = 32; s > 0; s >>= 1) {
-      s0 += __shfl_xor(s0, s, 64);
-      s1 += __shfl_xor(s1, s, 64);
+    for (int m = 32; m > 0; m >>= 1) {
+      s0 += __shfl_xor(s0, m, 64);
+      s1 += __shfl_xor(s1, m, 64);
     }
     if ((tid & 63) == 0) {
       xs[tid >> 6] = s0;
       xs[4 + (tid >> 6)] = s1;
     }
-    __syncthreads();
-    if (tid == 0) {
-      update_elem(a, t, o.t[5], ((xs[0] + xs[1]) + xs[2]) + xs[3]);
-      if (o.t[7] >= 0) update_elem(a, t, o.t[7], ((xs[4] + xs[5]) + xs[6]) + xs[7]);
-    }
+    lds_sync();
+    if (tid == 0) update_elem(a, t, o.t[5], ((xs[0] + xs[1]) + xs[2]) + xs[3]);
+    if (tid == 1 && o.t[7] >= 0) update_elem(a, t, o.t[7], ((xs[4] + xs[5]) + xs[6]) + xs[7]);
   }
 }
 
@@ -647,7 +798,7 @@ __device__ void reduce_losses(const SacArgs& a, int tid, float* xs) {
     for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
     if ((tid & 63) == 0) xs[4 * q + (tid >> 6)] = s;
   }
-  __syncthreads();
+  lds_sync();
   if (tid < 4 && a.losses != nullptr) {
     const float s = ((xs[4 * tid] + xs[4 * tid + 1]) + xs[4 * tid + 2]) + xs[4 * tid + 3];
     const float mean = s / (float)a.B;
@@ -660,44 +811,154 @@ constexpr int kFc2Tiles = 8 * 8;  // 32x32 tiles of a 256x256 layer
 __global__ void __launch_bounds__(kThreads) k_sac_update(SacArgs a) {
   __shared__ float sm[kUpdLds];
   const int tid = threadIdx.x, b = blockIdx.x;
+  STAMP(a, 3, 0);
   if (b < 4 * kFc2Tiles) {
-    const int t = b / kFc2Tiles, tile = b % kFc2Tiles;
-    fc2_tile(a, t, tile >> 3, tile & 7, tid, sm);
-  } else if (b < 4 * kFc2Tiles + 4 * 8) {
+#ifdef SACENV_SAC_DIAG_NO_FC2  // timing diagnostics only
+    if (tid >= 0) return;
+#endif
+    // workgroups go to the 8 XCDs round-robin (b % 8): XCD x gets the 2x4 block of
+    // 32x32 tiles (out rows 2(x>>1)..+1, in cols 4(x&1)..+3) of each net, so its L2
+    // fetches 2 dz2 and 4 h1 row panels instead of 8 + 8
+    const int t = b / kFc2Tiles, q = b % kFc2Tiles, x = q & 7, k = q >> 3;
+    fc2_tile(a, t, 2 * (x >> 1) + (k >> 2), 4 * (x & 1) + (k & 3), tid, sm);
+  } else if (b < 4 * kFc2Tiles + 4 * (kH / kSmallF)) {
     const int q = b - 4 * kFc2Tiles;
-    small_params(a, q >> 3, q & 7, tid, sm);
+#ifdef SACENV_SAC_DIAG_NO_SMALL  // timing diagnostics only
+    if (tid >= 0) return;
+#endif
+    small_params(a, q / (kH / kSmallF), q % (kH / kSmallF), tid, sm);
   } else {
     reduce_losses(a, tid, sm);
   }
+  STAMP(a, 3, 15);
 }
 
-// fc2.weight -> [in][out] transposes of nets 0..3
-__global__ void __launch_bounds__(kThreads) k_sac_transpose(SacArgs a) {
+// kernel copies of fc2.weight: fragment order for nets 0..4, transposed for 0..3
+__global__ void __launch_bounds__(kThreads) k_sac_sync(SacArgs a) {
   const int t = blockIdx.y;
   const float* w2 = a.P + a.net[t] + a.off[net_shape(t)].t[2];
-  float* w2t = a.P + a.w2t[t];
   for (int e = blockIdx.x * kThreads + threadIdx.x; e < kH * kH; e += gridDim.x * kThreads) {
-    const int o = e >> 8, i = e & (kH - 1);
-    w2t[i * kH + o] = w2[e];
+    const int n = e >> 8, k = e & (kH - 1);
+    const float v = w2[e];
+    a.P[a.w2f[t] + swz(n, k)] = v;
+    if (t < 4) a.P[a.w2tf[t] + swz(k, n)] = v;
   }
 }
 
-// choose_action for n rows: actor forward and the sample() draw
+// choose_action for n rows: actor forward and the sample() draw. 64 rows per
+// workgroup (four 16-row tiles against every weight fragment: 4x the MFMA
+// work per weight byte of the 16-row learn kernels); fc2's output never
+// leaves registers — the two heads are reduced from the accumulators.
+constexpr int kActRows = 64;
+
+struct ActLds {
+  float x[kActRows * kXP];
+  float h1[kActRows * kSP];
+  float head[4][kActRows][2];
+};
+
 __global__ void __launch_bounds__(kThreads) k_sac_act(SacArgs a, const float* __restrict__ obs, int n,
                                                         const float* __restrict__ eps, float* __restrict__ out,
                                                         float* __restrict__ logp) {
-  __shared__ RowLds l;
-  const int tid = threadIdx.x, row0 = blockIdx.x * kRows;
-  const int nrows = n - row0 < kRows ? n - row0 : kRows;
+  __shared__ ActLds l;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, i = lane & 15, kq = lane >> 4;
+  const int row0 = blockIdx.x * kActRows;
+  const int nrows = n - row0 < kActRows ? n - row0 : kActRows;
   const float* Pn = a.P + a.net[0];
   const NetOff& o = a.off[kActorShape];
-  load_x(l.x, obs, a.D, row0, nrows, nullptr, tid);
-  __syncthreads();
-  trunk(Pn, o, a.D, l, tid, nullptr, nullptr, 0, row0);
-  const float mu = row_dot(l.h2, Pn + o.t[4], 1, tid) + Pn[o.t[5]];
-  const float sr = row_dot(l.h2, Pn + o.t[6], 1, tid) + Pn[o.t[7]];
-  const int j = tid >> 4;
-  if ((tid & 15) == 0 && j < nrows) {
+  const int D = a.D;
+  for (int e = tid; e < kActRows * 16; e += kThreads) {
+    const int j = e >> 4, k = e & 15;
+    l.x[j * kXP + k] = (j < nrows && k < D) ? obs[(int64_t)(row0 + j) * D + k] : 0.f;
+  }
+  f4 acc[4][4];  // [feature tile t][row tile rt]
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt) acc[t][rt] = f4{0.f, 0.f, 0.f, 0.f};
+  {  // fc1 (K = obs_dim <= 16): one k-block
+    f4 av[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float* wp = Pn + o.t[0] + (64 * w + 16 * t + i) * D;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) av[t][s] = 4 * kq + s < D ? wp[4 * kq + s] : 0.f;
+    }
+    lds_sync();
+    f4 bx[4];
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt) bx[rt] = *reinterpret_cast<const f4*>(l.x + (16 * rt + i) * kXP + 4 * kq);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt)
+          acc[t][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t][s], bx[rt][s], acc[t][rt], 0, 0, 0);
+  }
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int n0 = 64 * w + 16 * t + 4 * kq;
+    const f4 bb = *reinterpret_cast<const f4*>(Pn + o.t[1] + n0);
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt) {
+      f4 y;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) y[r] = fmaxf(acc[t][rt][r] + bb[r], 0.f);
+      *reinterpret_cast<f4*>(l.h1 + (16 * rt + i) * kSP + n0) = y;
+      acc[t][rt] = f4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  lds_sync();
+  const float* W2f = a.P + a.w2f[0];
+#pragma unroll 4
+  for (int kb = 0; kb < kH / 16; ++kb) {
+    f4 av[4], bx[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) av[t] = *frag(W2f, w, t, kb, lane);
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt) bx[rt] = *reinterpret_cast<const f4*>(l.h1 + (16 * rt + i) * kSP + 16 * kb + 4 * kq);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt)
+          acc[t][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t][s], bx[rt][s], acc[t][rt], 0, 0, 0);
+  }
+  // heads from the accumulators: lane (i = row in tile, kq) holds features 64w + 16t + 4kq + r
+  float pm[4] = {0.f, 0.f, 0.f, 0.f}, ps[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int n0 = 64 * w + 16 * t + 4 * kq;
+    const f4 bb = *reinterpret_cast<const f4*>(Pn + o.t[3] + n0);
+    const f4 wm = *reinterpret_cast<const f4*>(Pn + o.t[4] + n0);
+    const f4 ws = *reinterpret_cast<const f4*>(Pn + o.t[6] + n0);
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float h = fmaxf(acc[t][rt][r] + bb[r], 0.f);
+        pm[rt] = fmaf(wm[r], h, pm[rt]);
+        ps[rt] = fmaf(ws[r], h, ps[rt]);
+      }
+  }
+#pragma unroll
+  for (int rt = 0; rt < 4; ++rt) {
+    pm[rt] += __shfl_xor(pm[rt], 16, 64);
+    pm[rt] += __shfl_xor(pm[rt], 32, 64);
+    ps[rt] += __shfl_xor(ps[rt], 16, 64);
+    ps[rt] += __shfl_xor(ps[rt], 32, 64);
+    if (kq == 0) {
+      l.head[w][16 * rt + i][0] = pm[rt];
+      l.head[w][16 * rt + i][1] = ps[rt];
+    }
+  }
+  lds_sync();
+  if (tid < nrows) {
+    const int j = tid;
+    const float mu = (((l.head[0][j][0] + l.head[1][j][0]) + l.head[2][j][0]) + l.head[3][j][0]) + Pn[o.t[5]];
+    const float sr = (((l.head[0][j][1] + l.head[1][j][1]) + l.head[2][j][1]) + l.head[3][j][1]) + Pn[o.t[7]];
     float tl, x, act, lp;
     const float sig = policy_sigma(sr, tl);
     policy_draw(mu, sig, eps[row0 + j], a.max_action, x, act, lp);
@@ -731,8 +992,12 @@ void make_layout(const SacenvSacParams* p, SacenvSacLayout* L) {
     L->adam_v[n] = q;
     q += sh[net_shape(n)].size;
   }
+  for (int n = 0; n < 5; ++n) {
+    L->w2f[n] = q;
+    q += (int64_t)kH * kH;
+  }
   for (int n = 0; n < 4; ++n) {
-    L->w2t[n] = q;
+    L->w2tf[n] = q;
     q += (int64_t)kH * kH;
   }
   L->total_floats = q;
@@ -741,6 +1006,9 @@ void make_layout(const SacenvSacParams* p, SacenvSacLayout* L) {
     for (int k = 0; k < 8; ++k) L->tensor[s][k] = sh[s].t[k];
   }
   L->scratch_bytes = (int64_t)sizeof(float) * p->batch * (16 * (int64_t)kH + F_COUNT);
+#ifdef SACENV_SAC_STAMPS
+  L->scratch_bytes += 4 * 1024 * 16 * 8;  // [phase][block][16] u64 after the row fields
+#endif
 }
 
 SacArgs make_args(const SacenvSacParams* p, float* weights) {
@@ -752,8 +1020,9 @@ SacArgs make_args(const SacenvSacParams* p, float* weights) {
   for (int n = 0; n < 4; ++n) {
     a.am[n] = L.adam_m[n];
     a.av[n] = L.adam_v[n];
-    a.w2t[n] = L.w2t[n];
+    a.w2tf[n] = L.w2tf[n];
   }
+  for (int n = 0; n < 5; ++n) a.w2f[n] = L.w2f[n];
   a.off[0] = net_off(p->obs_dim, 2);
   a.off[1] = net_off(p->obs_dim + 1, 1);
   a.off[2] = net_off(p->obs_dim, 1);
@@ -786,7 +1055,7 @@ extern "C" int sacenv_sac_sync(const SacenvSacParams* p, float* weights, void* s
   if (weights == nullptr) return SACENV_E_NULL;
   if (!aligned16(weights)) return SACENV_E_SIZE;
   const SacArgs a = make_args(p, weights);
-  hipLaunchKernelGGL(k_sac_transpose, dim3(64, 4), dim3(kThreads), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(k_sac_sync, dim3(64, 5), dim3(kThreads), 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }
 
@@ -801,7 +1070,7 @@ extern "C" int sacenv_sac_act(const SacenvSacParams* p, const float* weights, co
   SacenvSacParams q = *p;
   q.batch = 256;  // unused by the act kernel
   const SacArgs a = make_args(&q, const_cast<float*>(weights));
-  const int blocks = (n + kRows - 1) / kRows;
+  const int blocks = (n + kActRows - 1) / kActRows;
   hipLaunchKernelGGL(k_sac_act, dim3(blocks), dim3(kThreads), 0, (hipStream_t)stream, a, obs, (int)n, eps, action,
                      log_prob);
   return (int)hipGetLastError();
@@ -836,6 +1105,7 @@ extern "C" int sacenv_sac_learn(const SacenvSacParams* p, float* weights, void* 
     a.na[t].dz2t = scr + (4 * t + 3) * tile;
   }
   a.rows = scr + 16 * tile;
+  a.stamps = reinterpret_cast<unsigned long long*>(a.rows + (int64_t)F_COUNT * p->batch);
   // torch.optim.Adam (_multi_tensor_adam): Python-float scalars, cast to f32 in the kernels
   const double b1 = p->adam_beta1, b2 = p->adam_beta2;
   const double bc1 = 1.0 - pow(b1, (double)adam_step), bc2 = 1.0 - pow(b2, (double)adam_step);
@@ -848,9 +1118,9 @@ extern "C" int sacenv_sac_learn(const SacenvSacParams* p, float* weights, void* 
   a.nstep_critic = (float)((p->lr_critic / bc1) * -1.0);
   const int nrb = p->batch / kRows;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_sac_rows, dim3(5 * nrb), dim3(kThreads), 0, s, a, 0);
-  hipLaunchKernelGGL(k_sac_rows, dim3(4 * nrb), dim3(kThreads), 0, s, a, 1);
+  hipLaunchKernelGGL(k_sac_rows, dim3(4 * nrb), dim3(kThreads), 0, s, a, 0);
+  hipLaunchKernelGGL(k_sac_rows, dim3(6 * nrb), dim3(kThreads), 0, s, a, 1);
   hipLaunchKernelGGL(k_sac_rows, dim3(2 * nrb), dim3(kThreads), 0, s, a, 2);
-  hipLaunchKernelGGL(k_sac_update, dim3(4 * kFc2Tiles + 4 * 8 + 1), dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL(k_sac_update, dim3(4 * kFc2Tiles + 4 * (kH / kSmallF) + 1), dim3(kThreads), 0, s, a);
   return (int)hipGetLastError();
 }

@@ -114,7 +114,7 @@ class SacParams(C.Structure):
 
 class SacLayout(C.Structure):
     _fields_ = [("total_floats", _i64), ("net", _i64 * 5), ("adam_m", _i64 * 4), ("adam_v", _i64 * 4),
-                ("w2t", _i64 * 4), ("net_floats", _i64 * 3), ("tensor", (_i64 * 8) * 3),
+                ("w2f", _i64 * 5), ("w2tf", _i64 * 4), ("net_floats", _i64 * 3), ("tensor", (_i64 * 8) * 3),
                 ("scratch_bytes", _i64)]
 
 

@@ -431,7 +431,8 @@ def test_sac_layout(built_lib):
     regions = [(L.net[n], L.net[n] + L.net_floats[shapes[n]]) for n in range(5)]
     regions += [(L.adam_m[n], L.adam_m[n] + L.net_floats[shapes[n]]) for n in range(4)]
     regions += [(L.adam_v[n], L.adam_v[n] + L.net_floats[shapes[n]]) for n in range(4)]
-    regions += [(L.w2t[n], L.w2t[n] + H * H) for n in range(4)]
+    regions += [(L.w2f[n], L.w2f[n] + H * H) for n in range(5)]
+    regions += [(L.w2tf[n], L.w2tf[n] + H * H) for n in range(4)]
     regions.sort()
     for (a0, a1), (b0, b1) in zip(regions, regions[1:]):
         assert a1 <= b0 and a0 % 4 == 0
