@@ -10,7 +10,11 @@ main.py:70-114 for N envs at once, every tensor on the GPU:
   1 024-row batch sampled on the device (pinned to the reference by
   tests/test_agent_cpu.py).
 
-    python examples/train_vec_sac.py --envs 65536 --iters 200
+``--agent native`` (default) runs choose_action and learn on the fp32 MFMA
+kernels of sacenv_sac.hip (``NativeSAC``, checked against VecSAC by
+tests/test_sac_native_gpu.py); ``--agent torch`` on VecSAC.
+
+    python examples/train_vec_sac.py --envs 65536 --iters 200 [--agent torch]
 
 Prints one JSON line: env-steps/s of the whole loop (act + step + store +
 sample + update), and the env step's share of it.
@@ -34,13 +38,15 @@ def main(argv=None):
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--learn-every", type=int, default=1)
+    ap.add_argument("--agent", choices=("native", "torch"), default="native")
     args = ap.parse_args(argv)
     from sacenv import VecBoatEnv
     from sacenv.agent import VecSAC
+    from sacenv.sac_native import NativeSAC
     dev = torch.device("cuda")
     env = VecBoatEnv({"base_settings": {"experiment": 6, "test_mode": 0}}, args.envs, seed=0,
                      device=dev, max_episode_steps=500)
-    agent = VecSAC(dev, init_seed=0)
+    agent = (NativeSAC if args.agent == "native" else VecSAC)(dev, init_seed=0)
     obs = env.reset().clone()
     losses = None
 
@@ -70,7 +76,7 @@ def main(argv=None):
     torch.cuda.synchronize()
     el_env = time.perf_counter() - t1
     out = {"pipeline": "act + VecBoatEnv.step + replay store + sample(1024) + SAC update",
-           "envs": args.envs, "iters": args.iters,
+           "agent": args.agent, "envs": args.envs, "iters": args.iters,
            "env_steps_per_s": args.envs * args.iters / el, "ms_per_iter": el / args.iters * 1e3,
            "env_step_ms": el_env / args.iters * 1e3,
            "losses": None if losses is None else [float(x) for x in losses]}

@@ -104,7 +104,15 @@ enum RowField {
   F_COUNT
 };
 
-struct NetAct {   // feature-major [kH][B] activations of one optimised net
+// Activations that phase 3 reduces over the batch ([kH][B] per net) are kept in
+// the same fragment order with the batch row as k: (n, r) -> block (n / 16,
+// r / 16), lane (n % 16, (r % 16) / 4), component r % 4. A row block writes
+// exactly one column of blocks; phase 3 loads whole 1 KB fragments.
+__host__ __device__ inline int64_t act_off(int n, int r, int B) {
+  return ((int64_t)((n >> 4) * (B >> 4) + (r >> 4)) * 64 + ((r & 15) >> 2) * 16 + (n & 15)) * 4 + (r & 3);
+}
+
+struct NetAct {   // [kH][B] activations of one optimised net (act_off order)
   float* h1t;
   float* h2t;
   float* dz1t;
@@ -122,6 +130,7 @@ struct SacArgs {
   const float* eps1;
   const float* eps2;
   float* rows;         // row fields [F_COUNT][B]
+  float* xt;           // [16][B] fc1 inputs (act_off order): state, action, 1
   float* losses;
   NetAct na[4];        // actor, critic 1, critic 2, value
   int64_t net[5], am[4], av[4], w2f[5], w2tf[4];
@@ -181,7 +190,7 @@ __device__ __forceinline__ void load_tile_t(float* hl, const float* __restrict__
   const int j = tid & 15, fg = tid >> 4;
   float v[16];
 #pragma unroll
-  for (int q = 0; q < 16; ++q) v[q] = gT[(int64_t)(fg * 16 + q) * B + row0 + j];
+  for (int q = 0; q < 16; ++q) v[q] = gT[act_off(fg * 16 + q, row0 + j, B)];
 #pragma unroll
   for (int q = 0; q < 16; ++q) hl[j * kSP + fg * 16 + q] = v[q];
 }
@@ -191,7 +200,7 @@ __device__ __forceinline__ void store_tile_t(const float* hl, float* __restrict_
 #pragma unroll 4
   for (int q = 0; q < 16; ++q) {
     const int f = fg * 16 + q;
-    gT[(int64_t)f * B + row0 + j] = hl[j * kSP + f];
+    gT[act_off(f, row0 + j, B)] = hl[j * kSP + f];
   }
 }
 
@@ -297,7 +306,7 @@ __device__ __forceinline__ void epi_fwd(const f4 acc[4], const f4 bv[4], float* 
     *reinterpret_cast<f4*>(yl + j * kSP + n0) = y;
     if (gT != nullptr)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) gT[(int64_t)(n0 + r) * B + row0 + j] = y[r];
+      for (int r = 0; r < 4; ++r) gT[act_off(n0 + r, row0 + j, B)] = y[r];
   }
 }
 
@@ -315,7 +324,7 @@ __device__ __forceinline__ void epi_bwd(const f4 acc[4], const float* hl, float*
     if (zl != nullptr) *reinterpret_cast<f4*>(zl + j * kSP + n0) = z;
     if (gT != nullptr)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) gT[(int64_t)(n0 + r) * B + row0 + j] = z[r];
+      for (int r = 0; r < 4; ++r) gT[act_off(n0 + r, row0 + j, B)] = z[r];
   }
 }
 
@@ -459,6 +468,10 @@ __device__ float critic_fwd(const SacArgs& a, RowLds& l, int tid, int row0, int 
 __device__ void role_critic_stored(const SacArgs& a, RowLds& l, int tid, int row0, int c) {
   const float q = critic_fwd(a, l, tid, row0, c, a.act, true);
   if ((tid & 15) == 0) rowf(a, c == 1 ? F_QC1 : F_QC2)[row0 + (tid >> 4)] = q;
+  if (c == 1) {  // X^T of the fc1 inputs for phase 3: state, action at column D, 1 at column 15 (bias)
+    const int j = tid >> 4, k = tid & 15;
+    a.xt[act_off(k, row0 + j, a.B)] = k == 15 ? 1.f : l.x[j * kXP + k];
+  }
 }
 
 // critic c at the sample() actions: the value target's min q (:113-117)
@@ -619,26 +632,31 @@ __device__ __forceinline__ void update_elem(const SacArgs& a, int t, int64_t idx
   }
 }
 
-constexpr int kXChunk = 256;                // batch rows of X staged per pass (small_params)
-constexpr int kUpdLds = kXChunk * 17 > 4 * 32 * 33 ? kXChunk * 17 : 4 * 32 * 33;
+constexpr int kUpdLds = 4 * 32 * 33 + 128;  // fc2 tile partials + fc2.bias partials (small_params: 8 x 16 x 17)
 
 // C k-blocks of 16 rows: every load issued before the first MFMA (the update
-// launch runs one wave per SIMD: registers to spare, latency to hide)
+// launch runs one wave per SIMD: registers to spare, latency to hide); the
+// dz2 fragments are also summed per lane (fc2.bias gradient)
+__device__ __forceinline__ const f4* afrag(const float* __restrict__ gT, int nb, int rb, int B, int lane) {
+  return reinterpret_cast<const f4*>(gT + ((int64_t)nb * (B >> 4) + rb) * 256 + lane * 4);
+}
 template <int C>
 __device__ __forceinline__ void fc2_chunk(const float* __restrict__ dz2t, const float* __restrict__ h1t, int B,
-                                          int r0, int o0, int i0, int i, int kq, f4 acc[2][2]) {
+                                          int r0, int o0, int i0, int lane, f4 acc[2][2], float cs[2]) {
   f4 A[C][2], Bv[C][2];
 #pragma unroll
   for (int c = 0; c < C; ++c) {
-    const int r = r0 + 16 * c + 4 * kq;
+    const int rb = (r0 >> 4) + c;
 #pragma unroll
-    for (int so = 0; so < 2; ++so) A[c][so] = *reinterpret_cast<const f4*>(dz2t + (int64_t)(o0 + 16 * so + i) * B + r);
+    for (int so = 0; so < 2; ++so) A[c][so] = *afrag(dz2t, (o0 >> 4) + so, rb, B, lane);
 #pragma unroll
-    for (int si = 0; si < 2; ++si) Bv[c][si] = *reinterpret_cast<const f4*>(h1t + (int64_t)(i0 + 16 * si + i) * B + r);
+    for (int si = 0; si < 2; ++si) Bv[c][si] = *afrag(h1t, (i0 >> 4) + si, rb, B, lane);
   }
   __builtin_amdgcn_sched_barrier(0);  // all loads in flight before the first MFMA
 #pragma unroll
-  for (int c = 0; c < C; ++c)
+  for (int c = 0; c < C; ++c) {
+#pragma unroll
+    for (int so = 0; so < 2; ++so) cs[so] += ((A[c][so][0] + A[c][so][1]) + A[c][so][2]) + A[c][so][3];
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -646,23 +664,26 @@ __device__ __forceinline__ void fc2_chunk(const float* __restrict__ dz2t, const 
 #pragma unroll
         for (int si = 0; si < 2; ++si)
           acc[so][si] = __builtin_amdgcn_mfma_f32_16x16x4f32(A[c][so][s], Bv[c][si][s], acc[so][si], 0, 0, 0);
+  }
 }
 
 // fc2.weight gradient tile (32 out x 32 in) of net t: dW = dz2^T h1 over the
-// batch, each wave a quarter of the rows, then Adam and the transpose
+// batch, each wave a quarter of the rows, then Adam and the kernel copies;
+// tiles of the first in-column also take fc2.bias (sum of dz2 over the batch)
 __device__ void fc2_tile(const SacArgs& a, int t, int ob, int ib, int tid, float* red) {
-  const int lane = tid & 63, w = tid >> 6, i = lane & 15, kq = lane >> 4;
+  const int lane = tid & 63, w = tid >> 6, kq = lane >> 4;
   const NetAct& na = a.na[t];
   const int B = a.B, rq = B / 4, rbeg = w * rq;
   const int o0 = 32 * ob, i0 = 32 * ib;
   f4 acc[2][2];
+  float cs[2] = {0.f, 0.f};
 #pragma unroll
   for (int so = 0; so < 2; ++so)
 #pragma unroll
     for (int si = 0; si < 2; ++si) acc[so][si] = f4{0.f, 0.f, 0.f, 0.f};
   int r0 = rbeg;
-  for (; r0 + 256 <= rbeg + rq; r0 += 256) fc2_chunk<16>(na.dz2t, na.h1t, B, r0, o0, i0, i, kq, acc);
-  for (; r0 < rbeg + rq; r0 += 64) fc2_chunk<4>(na.dz2t, na.h1t, B, r0, o0, i0, i, kq, acc);  // rq % 64 == 0
+  for (; r0 + 256 <= rbeg + rq; r0 += 256) fc2_chunk<16>(na.dz2t, na.h1t, B, r0, o0, i0, lane, acc, cs);
+  for (; r0 < rbeg + rq; r0 += 64) fc2_chunk<4>(na.dz2t, na.h1t, B, r0, o0, i0, lane, acc, cs);  // rq % 64 == 0
   STAMP(a, 3, 1);
   // lane holds dW[o = 16 so + 4 kq + r][i = 16 si + (lane & 15)]
 #pragma unroll
@@ -670,7 +691,14 @@ __device__ void fc2_tile(const SacArgs& a, int t, int ob, int ib, int tid, float
 #pragma unroll
     for (int si = 0; si < 2; ++si)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) red[(w * 32 + 16 * so + 4 * kq + r) * 33 + 16 * si + i] = acc[so][si][r];
+      for (int r = 0; r < 4; ++r) red[(w * 32 + 16 * so + 4 * kq + r) * 33 + 16 * si + (lane & 15)] = acc[so][si][r];
+  float* bred = red + 4 * 32 * 33;  // [4 waves][32] fc2.bias partials
+#pragma unroll
+  for (int so = 0; so < 2; ++so) {
+    cs[so] += __shfl_xor(cs[so], 16, 64);
+    cs[so] += __shfl_xor(cs[so], 32, 64);
+    if (kq == 0) bred[w * 32 + 16 * so + (lane & 15)] = cs[so];
+  }
   lds_sync();
   STAMP(a, 3, 2);
   const int o = tid >> 3, ic = (tid & 7) * 4;
@@ -687,105 +715,94 @@ __device__ void fc2_tile(const SacArgs& a, int t, int ob, int ib, int tid, float
     a.P[a.w2tf[t] + swz(k, n)] = p;
     if (t == 3) a.P[a.w2f[4] + swz(n, k)] = a.P[a.net[4] + idx];  // the target's forward copy
   }
+  if (ib == 0 && tid < 32) {
+    const float g = ((bred[tid] + bred[32 + tid]) + bred[64 + tid]) + bred[96 + tid];
+    update_elem(a, t, a.off[net_shape(t)].t[3] + o0 + tid, g);
+  }
 }
 
-constexpr int kSmallF = 8;  // features per small-parameter workgroup (32 lanes each)
+constexpr int kSmallF = 16;  // features per small-parameter workgroup (one 16x16 tile)
 
-// fc1.weight / fc1.bias / fc2.bias / head weights of 8 features of net t (and
-// the head biases in block 0): batch reductions on the VALU, lane p of a
-// feature summing rows 4p + 128q (+0..3); then one Adam item per lane
-__device__ void small_params(const SacArgs& a, int t, int fb, int tid, float* xs) {
+template <int C>
+__device__ __forceinline__ void small_chunk(const NetAct& na, const float* __restrict__ xt, const float* __restrict__ g0,
+                                            const float* __restrict__ g1, int B, int nb, int rb0, int lane, f4& s1,
+                                            f4& s2) {
+  const int j = lane & 15, kq = lane >> 4;
+  f4 z1[C], x[C], h2[C], g[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const int rb = rb0 + c, r = 16 * rb + 4 * kq;
+    z1[c] = *afrag(na.dz1t, nb, rb, B, lane);
+    x[c] = *afrag(xt, 0, rb, B, lane);
+    h2[c] = *afrag(na.h2t, nb, rb, B, lane);
+    g[c] = f4{0.f, 0.f, 0.f, 0.f};
+    if (j == 0) g[c] = *reinterpret_cast<const f4*>(g0 + r);
+    if (j == 1 && g1 != nullptr) g[c] = *reinterpret_cast<const f4*>(g1 + r);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int c = 0; c < C; ++c)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      s1 = __builtin_amdgcn_mfma_f32_16x16x4f32(z1[c][s], x[c][s], s1, 0, 0, 0);
+      s2 = __builtin_amdgcn_mfma_f32_16x16x4f32(h2[c][s], g[c][s], s2, 0, 0, 0);
+    }
+}
+
+// fc1.weight and fc1.bias (dz1^T [X | 1]) and the head weights (h2^T G, G = the
+// head-output gradients) of 16 features of net t as two 16x16 MFMA tiles over
+// the batch (each wave a quarter of the rows); the head biases in block 0
+__device__ void small_params(const SacArgs& a, int t, int fb, int tid, float* red) {
+  const int lane = tid & 63, w = tid >> 6, kq = lane >> 4;
   const NetAct& na = a.na[t];
-  const int B = a.B, D = a.D, in = net_in(t, D);
+  const int B = a.B, in = net_in(t, a.D);
   const NetOff& o = a.off[net_shape(t)];
-  const int f = kSmallF * fb + (tid >> 5), part = tid & 31;
   const float* g0 = rowf(a, t == 0 ? F_GMU : (t == 1 ? F_GC1 : (t == 2 ? F_GC2 : F_GV)));
   const float* g1 = t == 0 ? rowf(a, F_GSR) : nullptr;
-  float sb2 = 0.f, sb1 = 0.f, sh0 = 0.f, sh1 = 0.f, sw[16];
+  f4 s1 = f4{0.f, 0.f, 0.f, 0.f}, s2 = f4{0.f, 0.f, 0.f, 0.f};
+  const int rbq = (B >> 4) / 4, rb0 = w * rbq;  // rbq % 4 == 0
+  int c0 = 0;
+  for (; c0 + 8 <= rbq; c0 += 8) small_chunk<8>(na, a.xt, g0, g1, B, fb, rb0 + c0, lane, s1, s2);
+  for (; c0 < rbq; c0 += 4) small_chunk<4>(na, a.xt, g0, g1, B, fb, rb0 + c0, lane, s1, s2);
+  // lane holds [f = 4 kq + r][col = lane & 15] of both tiles
 #pragma unroll
-  for (int k = 0; k < 16; ++k) sw[k] = 0.f;
-  for (int c0 = 0; c0 < B; c0 += kXChunk) {
-    const int nr = B - c0 < kXChunk ? B - c0 : kXChunk;  // a multiple of 256
-    lds_sync();
-    {  // this net's input rows: state (+ the stored action); all loads in flight, then LDS
-      float v[kXChunk * 16 / kThreads];
-#pragma unroll
-      for (int m = 0; m < kXChunk * 16 / kThreads; ++m) {
-        const int e = tid + kThreads * m, rr = e >> 4, k = e & 15;
-        v[m] = 0.f;
-        if (rr < nr) {
-          if (k < D) v[m] = a.s[(int64_t)(c0 + rr) * D + k];
-          else if (k == D && in > D) v[m] = a.act[c0 + rr];
-        }
-      }
-#pragma unroll
-      for (int m = 0; m < kXChunk * 16 / kThreads; ++m) {
-        const int e = tid + kThreads * m;
-        xs[(e >> 4) * 17 + (e & 15)] = v[m];
-      }
-    }
-    lds_sync();
-#pragma unroll 4
-    for (int q = 0; q < nr; q += 128) {
-      const int rl = q + 4 * part, r = c0 + rl;
-      const f4 z2 = *reinterpret_cast<const f4*>(na.dz2t + (int64_t)f * B + r);
-      const f4 z1 = *reinterpret_cast<const f4*>(na.dz1t + (int64_t)f * B + r);
-      const f4 h2 = *reinterpret_cast<const f4*>(na.h2t + (int64_t)f * B + r);
-      const f4 ga = *reinterpret_cast<const f4*>(g0 + r);
-      f4 gb = f4{0.f, 0.f, 0.f, 0.f};
-      if (g1 != nullptr) gb = *reinterpret_cast<const f4*>(g1 + r);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        sb2 += z2[e];
-        sb1 += z1[e];
-        sh0 = fmaf(ga[e], h2[e], sh0);
-        sh1 = fmaf(gb[e], h2[e], sh1);
-#pragma unroll
-        for (int k = 0; k < 16; ++k) sw[k] = fmaf(z1[e], xs[(rl + e) * 17 + k], sw[k]);
-      }
-    }
+  for (int r = 0; r < 4; ++r) {
+    red[((w * 2 + 0) * 16 + 4 * kq + r) * 17 + (lane & 15)] = s1[r];
+    red[((w * 2 + 1) * 16 + 4 * kq + r) * 17 + (lane & 15)] = s2[r];
   }
-#pragma unroll
-  for (int m = 16; m > 0; m >>= 1) {
-    sb2 += __shfl_xor(sb2, m, 32);
-    sb1 += __shfl_xor(sb1, m, 32);
-    sh0 += __shfl_xor(sh0, m, 32);
-    sh1 += __shfl_xor(sh1, m, 32);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) sw[k] += __shfl_xor(sw[k], m, 32);
-  }
+  lds_sync();
   STAMP(a, 3, 3);
-  // item part: 0..in-1 fc1.weight[f][k], then fc1.bias, fc2.bias, head-0 weight, head-1 weight
-  float g = 0.f;
-#pragma unroll
-  for (int k = 0; k < 16; ++k)
-    if (k == part) g = sw[k];
-  int64_t idx = -1;
-  if (part < in) idx = o.t[0] + (int64_t)f * in + part;
-  else if (part == in) idx = o.t[1] + f, g = sb1;
-  else if (part == in + 1) idx = o.t[3] + f, g = sb2;
-  else if (part == in + 2) idx = o.t[4] + f, g = sh0;
-  else if (part == in + 3 && o.t[6] >= 0) idx = o.t[6] + f, g = sh1;
-  if (idx >= 0) update_elem(a, t, idx, g);
+  {
+    const int f = tid >> 4, k = tid & 15, fg = kSmallF * fb + f;
+    auto sum4 = [&](int m) {
+      return ((red[((0 * 2 + m) * 16 + f) * 17 + k] + red[((1 * 2 + m) * 16 + f) * 17 + k]) +
+              red[((2 * 2 + m) * 16 + f) * 17 + k]) + red[((3 * 2 + m) * 16 + f) * 17 + k];
+    };
+    const float a1 = sum4(0), a2 = sum4(1);
+    if (k < in) update_elem(a, t, o.t[0] + (int64_t)fg * in + k, a1);  // fc1.weight
+    else if (k == 15) update_elem(a, t, o.t[1] + fg, a1);              // fc1.bias (the column of ones)
+    if (k == 0) update_elem(a, t, o.t[4] + fg, a2);                    // head-0 weight
+    else if (k == 1 && o.t[6] >= 0) update_elem(a, t, o.t[6] + fg, a2);  // head-1 weight
+  }
   if (fb == 0) {  // head biases: sums of the head-output gradients
     lds_sync();
-    float s0 = 0.f, s1 = 0.f;
+    float s0 = 0.f, sb = 0.f;
     for (int r = tid; r < B; r += kThreads) {
       s0 += g0[r];
-      if (g1 != nullptr) s1 += g1[r];
+      if (g1 != nullptr) sb += g1[r];
     }
 #pragma unroll
     for (int m = 32; m > 0; m >>= 1) {
       s0 += __shfl_xor(s0, m, 64);
-      s1 += __shfl_xor(s1, m, 64);
+      sb += __shfl_xor(sb, m, 64);
     }
     if ((tid & 63) == 0) {
-      xs[tid >> 6] = s0;
-      xs[4 + (tid >> 6)] = s1;
+      red[tid >> 6] = s0;
+      red[4 + (tid >> 6)] = sb;
     }
     lds_sync();
-    if (tid == 0) update_elem(a, t, o.t[5], ((xs[0] + xs[1]) + xs[2]) + xs[3]);
-    if (tid == 1 && o.t[7] >= 0) update_elem(a, t, o.t[7], ((xs[4] + xs[5]) + xs[6]) + xs[7]);
+    if (tid == 0) update_elem(a, t, o.t[5], ((red[0] + red[1]) + red[2]) + red[3]);
+    if (tid == 1 && o.t[7] >= 0) update_elem(a, t, o.t[7], ((red[4] + red[5]) + red[6]) + red[7]);
   }
 }
 
@@ -808,27 +825,33 @@ __device__ void reduce_losses(const SacArgs& a, int tid, float* xs) {
 
 constexpr int kFc2Tiles = 8 * 8;  // 32x32 tiles of a 256x256 layer
 
+// block order: the loss reduction and the 64 small-parameter blocks first (they
+// finish early and their CUs then take the last fc2 tiles), then 256 fc2 tiles
+constexpr int kSmallBlocks = 4 * (kH / kSmallF);
+
 __global__ void __launch_bounds__(kThreads) k_sac_update(SacArgs a) {
   __shared__ float sm[kUpdLds];
   const int tid = threadIdx.x, b = blockIdx.x;
   STAMP(a, 3, 0);
-  if (b < 4 * kFc2Tiles) {
+  if (b == 0) {
+    reduce_losses(a, tid, sm);
+  } else if (b <= kSmallBlocks) {
+    const int q = b - 1;
+#ifdef SACENV_SAC_DIAG_NO_SMALL  // timing diagnostics only
+    if (tid >= 0) return;
+#endif
+    small_params(a, q / (kH / kSmallF), q % (kH / kSmallF), tid, sm);
+  } else {
 #ifdef SACENV_SAC_DIAG_NO_FC2  // timing diagnostics only
     if (tid >= 0) return;
 #endif
     // workgroups go to the 8 XCDs round-robin (b % 8): XCD x gets the 2x4 block of
     // 32x32 tiles (out rows 2(x>>1)..+1, in cols 4(x&1)..+3) of each net, so its L2
     // fetches 2 dz2 and 4 h1 row panels instead of 8 + 8
-    const int t = b / kFc2Tiles, q = b % kFc2Tiles, x = q & 7, k = q >> 3;
-    fc2_tile(a, t, 2 * (x >> 1) + (k >> 2), 4 * (x & 1) + (k & 3), tid, sm);
-  } else if (b < 4 * kFc2Tiles + 4 * (kH / kSmallF)) {
-    const int q = b - 4 * kFc2Tiles;
-#ifdef SACENV_SAC_DIAG_NO_SMALL  // timing diagnostics only
-    if (tid >= 0) return;
-#endif
-    small_params(a, q / (kH / kSmallF), q % (kH / kSmallF), tid, sm);
-  } else {
-    reduce_losses(a, tid, sm);
+    const int u = b - 1 - kSmallBlocks;  // kSmallBlocks + 1 = 65: b % 8 == (u + 1) % 8
+    const int x = b & 7, k = u >> 3;
+    const int t = k >> 3, kk = k & 7;
+    fc2_tile(a, t, 2 * (x >> 1) + (kk >> 2), 4 * (x & 1) + (kk & 3), tid, sm);
   }
   STAMP(a, 3, 15);
 }
@@ -971,7 +994,7 @@ __global__ void __launch_bounds__(kThreads) k_sac_act(SacArgs a, const float* __
 
 int check(const SacenvSacParams* p) {
   if (p == nullptr) return SACENV_E_NULL;
-  if (p->hidden != kH || p->n_actions != 1 || p->obs_dim < 1 || p->obs_dim > 15) return SACENV_E_SIZE;
+  if (p->hidden != kH || p->n_actions != 1 || p->obs_dim < 1 || p->obs_dim > 14) return SACENV_E_SIZE;
   if (p->batch < 256 || p->batch % 256 != 0 || p->batch > (1 << 20)) return SACENV_E_SIZE;
   return SACENV_OK;
 }
@@ -1005,7 +1028,7 @@ void make_layout(const SacenvSacParams* p, SacenvSacLayout* L) {
     L->net_floats[s] = sh[s].size;
     for (int k = 0; k < 8; ++k) L->tensor[s][k] = sh[s].t[k];
   }
-  L->scratch_bytes = (int64_t)sizeof(float) * p->batch * (16 * (int64_t)kH + F_COUNT);
+  L->scratch_bytes = (int64_t)sizeof(float) * p->batch * (16 * (int64_t)kH + F_COUNT + 16);
 #ifdef SACENV_SAC_STAMPS
   L->scratch_bytes += 4 * 1024 * 16 * 8;  // [phase][block][16] u64 after the row fields
 #endif
@@ -1062,7 +1085,7 @@ extern "C" int sacenv_sac_sync(const SacenvSacParams* p, float* weights, void* s
 extern "C" int sacenv_sac_act(const SacenvSacParams* p, const float* weights, const float* obs, int32_t n,
                               const float* eps, float* action, float* log_prob, void* stream) {
   if (p == nullptr) return SACENV_E_NULL;
-  if (p->hidden != kH || p->n_actions != 1 || p->obs_dim < 1 || p->obs_dim > 15) return SACENV_E_SIZE;
+  if (p->hidden != kH || p->n_actions != 1 || p->obs_dim < 1 || p->obs_dim > 14) return SACENV_E_SIZE;
   if (n < 0) return SACENV_E_SIZE;
   if (n == 0) return SACENV_OK;
   if (weights == nullptr || obs == nullptr || eps == nullptr || action == nullptr) return SACENV_E_NULL;
@@ -1105,7 +1128,8 @@ extern "C" int sacenv_sac_learn(const SacenvSacParams* p, float* weights, void* 
     a.na[t].dz2t = scr + (4 * t + 3) * tile;
   }
   a.rows = scr + 16 * tile;
-  a.stamps = reinterpret_cast<unsigned long long*>(a.rows + (int64_t)F_COUNT * p->batch);
+  a.xt = a.rows + (int64_t)F_COUNT * p->batch;
+  a.stamps = reinterpret_cast<unsigned long long*>(a.xt + 16 * (int64_t)p->batch);
   // torch.optim.Adam (_multi_tensor_adam): Python-float scalars, cast to f32 in the kernels
   const double b1 = p->adam_beta1, b2 = p->adam_beta2;
   const double bc1 = 1.0 - pow(b1, (double)adam_step), bc2 = 1.0 - pow(b2, (double)adam_step);
@@ -1121,6 +1145,6 @@ extern "C" int sacenv_sac_learn(const SacenvSacParams* p, float* weights, void* 
   hipLaunchKernelGGL(k_sac_rows, dim3(4 * nrb), dim3(kThreads), 0, s, a, 0);
   hipLaunchKernelGGL(k_sac_rows, dim3(6 * nrb), dim3(kThreads), 0, s, a, 1);
   hipLaunchKernelGGL(k_sac_rows, dim3(2 * nrb), dim3(kThreads), 0, s, a, 2);
-  hipLaunchKernelGGL(k_sac_update, dim3(4 * kFc2Tiles + 4 * (kH / kSmallF) + 1), dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL(k_sac_update, dim3(1 + kSmallBlocks + 4 * kFc2Tiles), dim3(kThreads), 0, s, a);
   return (int)hipGetLastError();
 }

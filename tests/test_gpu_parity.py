@@ -735,8 +735,9 @@ def test_vec_recorder_reproduces_reference_episode_csv(tmp_path, gpu, built_lib)
     np.testing.assert_array_equal(w, table.T)
 
 
-def test_vec_sac_training_loop_runs_on_device(gpu, built_lib):
-    """§8(f) rank 2: batched act + step + replay + SAC update (examples/train_vec_sac.py)."""
+@pytest.mark.parametrize("agent", ["native", "torch"])
+def test_vec_sac_training_loop_runs_on_device(gpu, built_lib, agent):
+    """§8(f) ranks 2 and 4: batched act + step + replay + SAC update (examples/train_vec_sac.py)."""
     import importlib.util
     import os
     path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
@@ -744,7 +745,7 @@ def test_vec_sac_training_loop_runs_on_device(gpu, built_lib):
     spec = importlib.util.spec_from_file_location("train_vec_sac", path)
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
-    out = mod.main(["--envs", "2048", "--iters", "20"])
+    out = mod.main(["--envs", "2048", "--iters", "20", "--agent", agent])
     assert out["env_steps_per_s"] > 0 and out["losses"] is not None
     assert all(np.isfinite(out["losses"]))
 

@@ -437,7 +437,7 @@ def test_sac_layout(built_lib):
     for (a0, a1), (b0, b1) in zip(regions, regions[1:]):
         assert a1 <= b0 and a0 % 4 == 0
     assert regions[-1][1] == L.total_floats
-    assert L.scratch_bytes == 4 * 1024 * (16 * H + 28)
+    assert L.scratch_bytes == 4 * 1024 * (16 * H + 28 + 16)
 
 
 def test_sac_argument_errors_without_gpu(built_lib):
@@ -447,7 +447,7 @@ def test_sac_argument_errors_without_gpu(built_lib):
     assert built_lib.sacenv_sac_layout(ctypes.byref(_sac_params(batch=1000)), ctypes.byref(lay)) == -4
     assert built_lib.sacenv_sac_layout(ctypes.byref(_sac_params(hidden=128)), ctypes.byref(lay)) == -4
     assert built_lib.sacenv_sac_layout(ctypes.byref(_sac_params(n_actions=2)), ctypes.byref(lay)) == -4
-    assert built_lib.sacenv_sac_layout(ctypes.byref(_sac_params(obs_dim=16)), ctypes.byref(lay)) == -4
+    assert built_lib.sacenv_sac_layout(ctypes.byref(_sac_params(obs_dim=15)), ctypes.byref(lay)) == -4
     assert built_lib.sacenv_sac_layout(None, ctypes.byref(lay)) == -1
     p = _sac_params()
     args = [None] * 9

@@ -24,10 +24,10 @@ def main():
         nat.scratch.zero_()
         nat.learn((s, a, r, s, d), (e, e))
         torch.cuda.synchronize()
-        off = (16 * 256 * B + 28 * B)
+        off = (16 * 256 * B + 28 * B + 16 * B)
         st = nat.scratch[off: off + 4 * 1024 * 16 * 2].view(torch.int64).view(4, 1024, 16).cpu()
         res.append(st)
-    nblk = {0: 4 * 64, 1: 6 * 64, 2: 2 * 64, 3: 256 + 128 + 1}
+    nblk = {0: 4 * 64, 1: 6 * 64, 2: 2 * 64, 3: 256 + 64 + 1}
     roles = {0: ["actor", "value", "c1stored", "c2stored"], 1: ["c1rs", "c2rs", "c1loss", "c2loss", "c1s", "c2s"],
              2: ["actorbwd", "valuebwd"]}
     for ph in range(4):
@@ -43,7 +43,7 @@ def main():
                 print(f"phase {ph} {name:9s} start med {blk[:, 0].median():6.2f} max {blk[:, 0].max():6.2f}  "
                       f"end med {blk[:, 15].median():6.2f} max {blk[:, 15].max():6.2f} {inner}")
         else:
-            for name, sl in (("fc2", slice(0, 256)), ("small", slice(256, 384)), ("loss", slice(384, 385))):
+            for name, sl in (("fc2", slice(65, 321)), ("small", slice(1, 65)), ("loss", slice(0, 1))):
                 blk = med[sl]
                 print(f"phase 3 {name:9s} start med {blk[:, 0].median():6.2f} max {blk[:, 0].max():6.2f}  "
                       f"p1 {blk[:, 1].median():6.2f} p2 {blk[:, 2].median():6.2f} p3 {blk[:, 3].median():6.2f} "
