@@ -466,6 +466,13 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
                      "timing": kern_src,
                      "traffic_source": None if traffic is None else traffic["source"]},
         "cpu_baseline": None,
+        # N>1: what the pooled transitions cost -- every rank receives (world - 1) rows per step
+        "pooling": None if pool is None else {
+            "row_bytes_per_rank_step": wl.row_bytes(),
+            "received_bytes_per_rank": (world - 1) * wl.row_bytes() * steps,
+            "received_GBps_per_rank": (world - 1) * wl.row_bytes() * steps / el_max / 1e9,
+            "note": "the timed region ends when the last segment's all_gather has landed; with "
+                    "xGMI links of ~64 GB/s per direction the pooled bytes, not k_step, bound N>1"},
     }
 
 
