@@ -445,8 +445,10 @@ int sacenv_sac_act(const SacenvSacParams *p, const float *weights, const float *
  * action f32 [batch], reward f64 [batch] as sample_buffer returns it, done u8
  * [batch]) with the policy draws of its sample() (eps1) and rsample() (eps2),
  * f32 [batch]. adam_step = the optimizers' step count after this call (1 on
- * the first). losses (device f32 [4], may be NULL) <- value, actor, critic 1,
- * critic 2 losses. */
+ * the first; a captured graph replays the step it was captured with, so
+ * capture one graph per step value or call eagerly). losses (device f32 [4],
+ * may be NULL) <- value, actor, critic 1, critic 2 losses. Calls on one
+ * weights/scratch pair must be ordered on one stream. */
 int sacenv_sac_learn(const SacenvSacParams *p, float *weights, void *scratch, const float *state,
                      const float *action, const double *reward, const float *new_state,
                      const uint8_t *done, const float *eps1, const float *eps2, int32_t adam_step,
