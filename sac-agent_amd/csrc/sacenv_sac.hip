@@ -19,8 +19,9 @@
 //     critic c's own loss backward (target forward for value_, done-masked;
 //     q_hat = scale * reward + gamma * value_); critic c at the sample()
 //     actions (value target).
-//   phase 2 (x 2): actor backward (min of the critics, tanh-squashed Normal
-//     log-prob), value backward (value_target = min q - log_prob).
+//   phase 2 (x 4): actor backward (min of the critics, tanh-squashed Normal
+//     log-prob), value backward (value_target = min q - log_prob), each layer
+//     split over two workgroups by output features.
 //   phase 3: weight gradients as batch reductions (dW = dZ^T H on MFMA), Adam
 //     (torch.optim.Adam, foreach form) on the four optimised nets, the target
 //     soft update (:63-77), the transposes, and the four losses.
@@ -397,6 +398,54 @@ __device__ __forceinline__ void head_backward(const float* __restrict__ Pn, cons
   lds_sync();
 }
 
+// Half of a backward layer: output features [128 h, 128 h + 128), wave w
+// owning two 16x16 tiles (blocks 8h + 2w + t). Phase 2 splits each role's one
+// layer over two workgroups this way (twice the workgroups, half the MFMAs
+// each); every A fragment of the half is loaded before the first MFMA.
+struct HalfPre {
+  f4 v[kH / 16][2];
+};
+__device__ __forceinline__ void half_prefetch(const float* __restrict__ Wf, int lane, int nb0, HalfPre& p) {
+#pragma unroll
+  for (int kb = 0; kb < kH / 16; ++kb)
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+      p.v[kb][t] = *reinterpret_cast<const f4*>(Wf + ((int64_t)((nb0 + t) * 16 + kb) * 64 + lane) * 4);
+}
+
+__device__ __forceinline__ void head_backward_half(const float* __restrict__ Pn, const NetOff& o, const HalfPre& pre,
+                                                   RowLds& l, int tid, float* dz2t, float* dz1t, int B, int row0,
+                                                   int h) {
+  const int lane = tid & 63, w = tid >> 6, i = lane & 15, kq = lane >> 4;
+  const float* wh0 = Pn + o.t[4];
+  const float* wh1 = o.t[6] >= 0 ? Pn + o.t[6] : nullptr;
+  for (int e = tid; e < kRows * kH; e += kThreads) {
+    const int j = e >> 8, f = e & (kH - 1);
+    float g = wh0[f] * l.g0[j];
+    if (wh1 != nullptr) g = g + wh1[f] * l.g1[j];
+    l.z[j * kSP + f] = l.h2[j * kSP + f] > 0.f ? g : 0.f;
+  }
+  lds_sync();
+  const int nb0 = 8 * h + 2 * w;
+  f4 acc[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int kb = 0; kb < kH / 16; ++kb) {
+    const f4 b = *reinterpret_cast<const f4*>(l.z + i * kSP + 16 * kb + 4 * kq);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(pre.v[kb][t][s], b[s], acc[t], 0, 0, 0);
+  }
+  if (h == 0 && dz2t != nullptr) store_tile_t(l.z, dz2t, B, row0, tid);
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {  // relu backward on h1, dz1 -> global (act_off order)
+    const int n0 = 16 * (nb0 + t) + 4 * kq;
+    const f4 hv = *reinterpret_cast<const f4*>(l.h1 + i * kSP + n0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dz1t[act_off(n0 + r, row0 + i, B)] = hv[r] > 0.f ? acc[t][r] : 0.f;
+  }
+}
+
 // tanh-squashed Normal draw (networks.py:47-70): x = mean + eps * std,
 // action = tanh(x) * max_action, log_prob with the tanh correction
 __device__ __forceinline__ float policy_sigma(float sr, float& tl) {
@@ -530,10 +579,10 @@ __device__ void role_critic_loss(const SacArgs& a, RowLds& l, int tid, int row0,
 }
 
 // actor loss backward: mean(log_prob - min(q1, q2)) at the rsample() draw (:127-135)
-__device__ void role_actor_bwd(const SacArgs& a, RowLds& l, int tid, int row0) {
+__device__ void role_actor_bwd(const SacArgs& a, RowLds& l, int tid, int row0, int h) {
   const NetAct& na = a.na[0];
-  WPre pre;
-  w_prefetch(a.P + a.w2tf[0], tid & 63, tid >> 6, pre);
+  HalfPre pre;
+  half_prefetch(a.P + a.w2tf[0], tid & 63, 8 * h + 2 * (tid >> 6), pre);
   load_tile_t(l.h1, na.h1t, a.B, row0, tid);
   load_tile_t(l.h2, na.h2t, a.B, row0, tid);
   if (tid < kRows) {
@@ -558,19 +607,21 @@ __device__ void role_actor_bwd(const SacArgs& a, RowLds& l, int tid, int row0) {
     const float dsr = dsig * sig * 3.5f * (1.f - tl * tl);
     l.g0[tid] = dmu;
     l.g1[tid] = dsr;
-    rowf(a, F_GMU)[r] = dmu;
-    rowf(a, F_GSR)[r] = dsr;
-    rowf(a, F_LA)[r] = rowf(a, F_LP2)[r] - fminf(q1, q2);
+    if (h == 0) {
+      rowf(a, F_GMU)[r] = dmu;
+      rowf(a, F_GSR)[r] = dsr;
+      rowf(a, F_LA)[r] = rowf(a, F_LP2)[r] - fminf(q1, q2);
+    }
   }
   lds_sync();
-  head_backward(a.P + a.net[0], a.off[kActorShape], a.P + a.w2tf[0], pre, l, tid, na.dz2t, na.dz1t, a.B, row0, false);
+  head_backward_half(a.P + a.net[0], a.off[kActorShape], pre, l, tid, na.dz2t, na.dz1t, a.B, row0, h);
 }
 
 // value loss backward: 0.5 mse(value, min q(sample()) - log_prob) (:113-124)
-__device__ void role_value_bwd(const SacArgs& a, RowLds& l, int tid, int row0) {
+__device__ void role_value_bwd(const SacArgs& a, RowLds& l, int tid, int row0, int h) {
   const NetAct& na = a.na[3];
-  WPre pre;
-  w_prefetch(a.P + a.w2tf[3], tid & 63, tid >> 6, pre);
+  HalfPre pre;
+  half_prefetch(a.P + a.w2tf[3], tid & 63, 8 * h + 2 * (tid >> 6), pre);
   load_tile_t(l.h1, na.h1t, a.B, row0, tid);
   load_tile_t(l.h2, na.h2t, a.B, row0, tid);
   if (tid < kRows) {
@@ -579,11 +630,13 @@ __device__ void role_value_bwd(const SacArgs& a, RowLds& l, int tid, int row0) {
     const float d = rowf(a, F_V)[r] - target;
     const float g = d * a.inv_b;
     l.g0[tid] = g;
-    rowf(a, F_GV)[r] = g;
-    rowf(a, F_LV)[r] = d * d;
+    if (h == 0) {
+      rowf(a, F_GV)[r] = g;
+      rowf(a, F_LV)[r] = d * d;
+    }
   }
   lds_sync();
-  head_backward(a.P + a.net[3], a.off[kValueShape], a.P + a.w2tf[3], pre, l, tid, na.dz2t, na.dz1t, a.B, row0, false);
+  head_backward_half(a.P + a.net[3], a.off[kValueShape], pre, l, tid, na.dz2t, na.dz1t, a.B, row0, h);
 }
 
 // one or two workgroups per CU: registers for kPrefetch k-blocks of weights in flight
@@ -602,8 +655,8 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1
     else if (role < 4) role_critic_loss(a, l, tid, row0, role - 1);
     else role_critic_sample(a, l, tid, row0, role - 3);
   } else {
-    if (role == 0) role_actor_bwd(a, l, tid, row0);
-    else role_value_bwd(a, l, tid, row0);
+    if (role < 2) role_actor_bwd(a, l, tid, row0, role);  // two halves of each backward layer
+    else role_value_bwd(a, l, tid, row0, role - 2);
   }
   STAMP(a, phase, 15);
 }
@@ -1144,7 +1197,7 @@ extern "C" int sacenv_sac_learn(const SacenvSacParams* p, float* weights, void* 
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(k_sac_rows, dim3(4 * nrb), dim3(kThreads), 0, s, a, 0);
   hipLaunchKernelGGL(k_sac_rows, dim3(6 * nrb), dim3(kThreads), 0, s, a, 1);
-  hipLaunchKernelGGL(k_sac_rows, dim3(2 * nrb), dim3(kThreads), 0, s, a, 2);
+  hipLaunchKernelGGL(k_sac_rows, dim3(4 * nrb), dim3(kThreads), 0, s, a, 2);
   hipLaunchKernelGGL(k_sac_update, dim3(1 + kSmallBlocks + 4 * kFc2Tiles), dim3(kThreads), 0, s, a);
   return (int)hipGetLastError();
 }

@@ -27,9 +27,9 @@ def main():
         off = (16 * 256 * B + 28 * B + 16 * B)
         st = nat.scratch[off: off + 4 * 1024 * 16 * 2].view(torch.int64).view(4, 1024, 16).cpu()
         res.append(st)
-    nblk = {0: 4 * 64, 1: 6 * 64, 2: 2 * 64, 3: 256 + 64 + 1}
+    nblk = {0: 4 * 64, 1: 6 * 64, 2: 4 * 64, 3: 256 + 64 + 1}
     roles = {0: ["actor", "value", "c1stored", "c2stored"], 1: ["c1rs", "c2rs", "c1loss", "c2loss", "c1s", "c2s"],
-             2: ["actorbwd", "valuebwd"]}
+             2: ["actorbwd0", "actorbwd1", "valuebwd0", "valuebwd1"]}
     for ph in range(4):
         rows = []
         for st in res[5:]:
