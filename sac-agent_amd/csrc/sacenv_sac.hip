@@ -735,7 +735,13 @@ __device__ void fc2_tile(const SacArgs& a, int t, int ob, int ib, int tid, float
 #pragma unroll
     for (int si = 0; si < 2; ++si) acc[so][si] = f4{0.f, 0.f, 0.f, 0.f};
   int r0 = rbeg;
-  for (; r0 + 256 <= rbeg + rq; r0 += 256) fc2_chunk<16>(na.dz2t, na.h1t, B, r0, o0, i0, lane, acc, cs);
+#ifndef SACENV_SAC_FC2_CHUNK
+#define SACENV_SAC_FC2_CHUNK 12
+#endif
+  // chunks of 16 k-blocks hold 256 VGPRs of loads (one workgroup per CU); 12 + 4 stays
+  // under 256 so the small-parameter workgroups can share the CUs
+  for (; r0 + 16 * SACENV_SAC_FC2_CHUNK <= rbeg + rq; r0 += 16 * SACENV_SAC_FC2_CHUNK)
+    fc2_chunk<SACENV_SAC_FC2_CHUNK>(na.dz2t, na.h1t, B, r0, o0, i0, lane, acc, cs);
   for (; r0 < rbeg + rq; r0 += 64) fc2_chunk<4>(na.dz2t, na.h1t, B, r0, o0, i0, lane, acc, cs);  // rq % 64 == 0
   STAMP(a, 3, 1);
   // lane holds dW[o = 16 so + 4 kq + r][i = 16 si + (lane & 15)]
