@@ -456,3 +456,20 @@ def test_sac_argument_errors_without_gpu(built_lib):
     assert built_lib.sacenv_sac_learn(ctypes.byref(p), *([8] * 9), 1, None, None) == -4  # unaligned
     assert built_lib.sacenv_sac_act(ctypes.byref(p), None, None, 4, None, None, None, None) == -1
     assert built_lib.sacenv_sac_act(ctypes.byref(p), None, None, 0, None, None, None, None) == 0
+
+
+def test_native_sac_has_no_cpu_path(built_lib):
+    """NativeSAC runs on the SAC kernels only: a CPU device is refused, not emulated."""
+    from sacenv import _lib
+    from sacenv.sac_native import NativeSAC
+    with pytest.raises(_lib.SacenvError):
+        NativeSAC("cpu", init_seed=0, with_memory=False)
+
+
+def test_native_sac_views_follow_the_c_layout(built_lib):
+    """The torch parameter views NativeSAC builds sit at the C layout's tensor offsets."""
+    from sacenv import _lib
+    L = _lib.sac_layout(_sac_params())
+    # actor: w1 [256][11] at tensor[0][0]; critic w1 [256][12]; value heads follow fc2.bias
+    assert L.tensor[0][2] - L.tensor[0][0] == 256 * 11 + 256  # 2 816 floats of fc1.weight are 16-B aligned
+    assert L.tensor[1][1] == 256 * 12 and L.tensor[2][6] == -1 and L.tensor[0][6] > L.tensor[0][5]
