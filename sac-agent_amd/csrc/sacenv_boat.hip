@@ -1137,12 +1137,14 @@ __device__ void fit_group(const SacenvBoatParams& p, const Arena& A, const doubl
   }
 }
 
+// GS lanes per (env, curve): 8 for up to 8 knots, else 16; one instantiation
+// per width, so the 8-knot launch carries no 16-knot registers
+template <int GS>
 __global__ void __launch_bounds__(kWave) k_refill_fit(SacenvBoatParams p, Arena A, Tail T) {
   __shared__ double g[kMaxK * kMaxK];
   const int lane = threadIdx.x;
   const int nc = p.use_wind_table ? 0 : n_curves(p.experiment);
   const int nk = p.n_knots;
-  const int GS = nk > 8 ? 16 : 8;
   const int items = A.status()[2] * nc;  // (env, curve) groups
   if (items == 0 || (int)blockIdx.x * (kWave / GS) >= items) return;  // uniform
   for (int i = lane; i < nk * nk; i += kWave) g[i] = T.g[i];
@@ -1151,10 +1153,7 @@ __global__ void __launch_bounds__(kWave) k_refill_fit(SacenvBoatParams p, Arena 
   for (int base = blockIdx.x * per; base < items; base += gridDim.x * per) {
     const int item = base + lane / GS;
     if (item >= items) break;
-    if (GS == 8)
-      fit_group<8>(p, A, g, item, lane & 7, nc);
-    else
-      fit_group<16>(p, A, g, item, lane & 15, nc);
+    fit_group<GS>(p, A, g, item, lane & (GS - 1), nc);
   }
 }
 
@@ -2118,8 +2117,12 @@ int sacenv_boat_refill(const SacenvBoatParams* p, void* arena, void* stream) {
   // (episode, curve) items), grid-stride beyond it; blocks past the count exit
   // at once. Measured 0.12 us/step better than one block per owner wave.
   const int fit_blocks = SACENV_FIT_BLOCKS;
-  hipLaunchKernelGGL(k_refill_fit, dim3(fit_blocks), dim3(kWave), 0, (hipStream_t)stream, *p, A,
-                     make_tail(*p, arena));
+  if (p->n_knots > 8)
+    hipLaunchKernelGGL(k_refill_fit<16>, dim3(fit_blocks), dim3(kWave), 0, (hipStream_t)stream, *p, A,
+                       make_tail(*p, arena));
+  else
+    hipLaunchKernelGGL(k_refill_fit<8>, dim3(fit_blocks), dim3(kWave), 0, (hipStream_t)stream, *p, A,
+                       make_tail(*p, arena));
   return launch_status();
 }
 
