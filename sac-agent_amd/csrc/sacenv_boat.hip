@@ -456,8 +456,8 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 // Cache policy of the step's output stores. Default SACENV_ST_SC1:
 // write-through (sc1: the line leaves the XCD L2, so the launch ends with no
 // dirty lines to write back; measured 0.21 us/step faster than plain stores);
-// the obs rows (16-B stores, no sc1 atomic form) go nontemporal. A/B builds:
-// SACENV_ST_PLAIN, SACENV_ST_NT, SACENV_OBS_PLAIN.
+// the 16-B pairs and obs rows (no 16-B sc1 atomic form) as write-through buffer
+// stores (aux bit 4). A/B builds: SACENV_ST_PLAIN, SACENV_ST_NT, SACENV_OBS_NT.
 #if !defined(SACENV_ST_PLAIN) && !defined(SACENV_ST_NT) && !defined(SACENV_ST_SC1)
 #define SACENV_ST_SC1 1
 #endif
