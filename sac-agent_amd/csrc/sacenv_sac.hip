@@ -97,7 +97,7 @@ __host__ __device__ inline int64_t swz(int n, int k) {
 // per-row fields of the scratch, f32 [B] each
 enum RowField {
   F_MU, F_SR, F_SIG, F_TL, F_A1, F_LP1, F_A2, F_X2, F_LP2,   // actor forward + draws
-  F_V, F_VN_UNUSED,                                          // value; (value_ stays in the critic-loss role)
+  F_V,                                                       // value (value_ stays in the critic-loss role)
   F_QC1, F_QC2,                                              // critics at the stored actions
   F_Q1A1, F_Q2A1, F_Q1A2, F_Q2A2, F_DA1, F_DA2,              // critics at the draws, dq/da at a2
   F_GMU, F_GSR, F_GC1, F_GC2, F_GV,                          // head-output gradients

@@ -24,7 +24,7 @@ def main():
         nat.scratch.zero_()
         nat.learn((s, a, r, s, d), (e, e))
         torch.cuda.synchronize()
-        off = (16 * 256 * B + 28 * B + 16 * B)
+        off = (16 * 256 * B + 27 * B + 16 * B)
         st = nat.scratch[off: off + 4 * 1024 * 16 * 2].view(torch.int64).view(4, 1024, 16).cpu()
         res.append(st)
     nblk = {0: 4 * 64, 1: 6 * 64, 2: 4 * 64, 3: 256 + 64 + 1}
