@@ -52,7 +52,8 @@ HBM_PEAK = 8.0e12             # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 EPISODE_STEPS = 500
 SEG = 128              # step launches per refill (sacenv _lib.REFILL_PERIOD); one graph per segment
 ACTION_STEPS = 512     # the pre-generated action table cycles every 512 steps (4 segments)
-TRANS_ROW = "58-B/env transition row (s' f32x11, reward, action, obs3_next, done, term)"
+TRANS_ROW = ("45-B/env transition row (s' entries 0..8 f32, reward, action, term; rudder, fuel and "
+             "done rebuilt by the receiver)")
 
 
 def metric_name(args) -> str:
@@ -264,7 +265,7 @@ def make_workload(args, rank: int, dev) -> Workload:
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
     actions = torch.rand((ACTION_STEPS, N), generator=g, device=dev, dtype=torch.float32) * 2 - 1
-    lay = TransitionLayout(N, env.n_pad)
+    lay = TransitionLayout(N, env.n_pad, args.experiment)
     toy_bytes = [t.record.numel() + t.final_obs_bytes.numel() for t in toys]
     row_bytes = lay.nbytes + sum(toy_bytes)
 

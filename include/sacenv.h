@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SACENV_ABI_VERSION 12
+#define SACENV_ABI_VERSION 13
 #define SACENV_OBS_DIM 11      /* Boat.return_state, boat_env.py:308-323 */
 #define SACENV_MT_N 624        /* MT19937 words per env (numpy legacy RNG) */
 #define SACENV_MAX_KNOTS 16    /* wind.fixed_points upper bound */
@@ -43,7 +43,9 @@ extern "C" {
 #define SACENV_SLOTS 129       /* episode slots per env in autoreset mode (active + 128 ahead) */
 #define SACENV_REFILL_PERIOD 128 /* autoreset: at most this many step launches between refills */
 #define SACENV_RECORD_BYTES 50 /* packed per-env step record (see layout.record) */
-#define SACENV_TRANS_BYTES 58  /* per-env transition row of sacenv_boat_step_pooled */
+#define SACENV_TRANS_OBS 9      /* s' entries in the transition row (obs 0..8) */
+#define SACENV_TRANS_BYTES 45   /* per-env transition row of sacenv_boat_step_pooled */
+#define SACENV_TRANS_BYTES_EXP2 49 /* the same in experiment 2 (+ obs3_next) */
 #define SACENV_PAIR_STRIDE 16  /* bytes between envs in the paired f64 state fields */
 
 /* termination codes; 1..5 follow the info-dict key order boat_env.py:24-32,
@@ -212,21 +214,23 @@ int sacenv_boat_step(const SacenvBoatParams *p, void *arena, const float *action
 
 /* sacenv_boat_step that also writes the step's transitions for a pooled
  * replay buffer (main.py:81-88 -> agent/buffer.py:13-22) to
- * the device row `trans` (SACENV_TRANS_BYTES x n_pad bytes, 16-B aligned):
- *   s'       f32 [n_pad][11]  obs after the step, BEFORE any auto-reset (the
- *                             terminal obs of envs that ended)
+ * the device row `trans` (SACENV_TRANS_BYTES x n_pad bytes, experiment 2:
+ * SACENV_TRANS_BYTES_EXP2; 16-B aligned):
+ *   s'       f32 [n_pad][9]   obs entries 0..8 after the step, BEFORE any
+ *                             auto-reset (the terminal obs of envs that ended)
  *   reward   f32 [n_pad]
  *   action   f32 [n_pad]      the step's action
- *   obs3_next f32 [n_pad]     envs that auto-reset: obs[3] (normalised s_y)
- *                             of the new episode's first obs (its other
- *                             entries are fixed by the config: the first obs
- *                             of a fresh Boat, boat_env.py:152-198)
- *   done     u8  [n_pad]
- *   term     u8  [n_pad]
- * The previous step's transition row gives each env's s: s' of that row, or
- * for envs that ended there the fresh-Boat obs with obs3_next. 58 B per env
- * instead of the record + action + terminal obs (98 B), written by the step
- * launch itself (no copy launches). */
+ *   term     u8  [n_pad]      termination code; done = term != 0
+ *   obs3_next f32 [n_pad]     experiment 2 only: envs that auto-reset, obs[3]
+ *                             (normalised start s_y) of the new episode's
+ *                             first obs (its other entries are fixed by the
+ *                             config: a fresh Boat, boat_env.py:152-198)
+ * The receiver rebuilds the rest exactly: s'[9] (rudder) from its f64 rudder
+ * (0 at an episode start, += f64(action) / 10 per step with test_mode 0) as
+ * (rudder + pi/3) * (1 / (2 pi / 3)), s'[10] (fuel) as (fuel0 - steps) / fuel0;
+ * each env's s is the previous row's s', or the fresh-Boat obs for envs that
+ * ended there (sacenv/dist.py TransitionStream). 45 B per env instead of the
+ * record + action + terminal obs (98 B), written by the step launch itself. */
 int sacenv_boat_step_pooled(const SacenvBoatParams *p, void *arena, const float *action, void *trans,
                             void *stream);
 

@@ -1366,6 +1366,7 @@ __host__ __device__ inline bool t_from_index(double dt) {
   } while (0)
 
 // 64 obs rows (2816 B) from LDS to a 16-B aligned row block: 3 float4 stores
+template <int ROW = SACENV_OBS_DIM>  // floats per env row (11: obs; 9: the pooled row's s')
 __device__ __forceinline__ void store_obs_block(const float* lds_rows, float* dst_rows, int lane) {
   const f4v* src = reinterpret_cast<const f4v*>(lds_rows);
 #ifndef SACENV_OBS_NT  // write-through 16-B buffer stores (sc1, aux bit 4): 0.13 us/step
@@ -1373,9 +1374,9 @@ __device__ __forceinline__ void store_obs_block(const float* lds_rows, float* ds
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(dst_rows, 0, 0x7fffffff, 0x00020000);
 #endif
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {
+  for (int i = 0; i < (ROW * 16 + kWave - 1) / kWave; ++i) {
     const uint32_t q = (uint32_t)lane + kWave * i;
-    if (q < kWave * SACENV_OBS_DIM / 4) {
+    if (q < kWave * ROW / 4) {
 #ifndef SACENV_OBS_NT
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, src[q]), r, q * 16u, 0, 16);
 #else
@@ -1754,23 +1755,25 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
   if (!kRoll && trans != nullptr) {  // the pooled transition row (sacenv_boat_step_pooled)
-    // s' = the pre-reset obs: only restarting lanes' LDS rows differ from it
+    // s' entries 0..8 = the pre-reset obs (entries 9 and 10, rudder and fuel, follow
+    // on the receivers from the actions and the episode starts), reward, action,
+    // term (done = term != 0) and, in experiment 2, the new episode's obs[3]
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (restart) {
 #pragma unroll
-      for (int k = 0; k < SACENV_OBS_DIM; ++k) l.obs[lane * SACENV_OBS_DIM + k] = o.v[k];
-    }
+    for (int k = 0; k < SACENV_TRANS_OBS; ++k) l.obs[lane * SACENV_TRANS_OBS + k] = o.v[k];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    store_obs_block(l.obs, reinterpret_cast<float*>(trans) + row0, lane);
-    st_rec(*reinterpret_cast<float*>(trans + 44 * A.np + eo4), (float)reward);
-    st_rec(*reinterpret_cast<float*>(trans + 48 * A.np + eo4), act);
-    st_rec(*reinterpret_cast<float*>(trans + 52 * A.np + eo4), restart ? fo.v[3] : 0.0f);
-    st_rec(*reinterpret_cast<uint8_t*>(trans + 56 * A.np + e), (uint8_t)(ended ? 1 : 0));
-    st_rec(*reinterpret_cast<uint8_t*>(trans + 57 * A.np + e), term);
+    store_obs_block<SACENV_TRANS_OBS>(l.obs, reinterpret_cast<float*>(trans) + (int64_t)ob * kWave * SACENV_TRANS_OBS,
+                                      lane);
+    constexpr int kOff = 4 * SACENV_TRANS_OBS;  // byte columns (x n_pad) after s'
+    st_rec(*reinterpret_cast<float*>(trans + kOff * A.np + eo4), (float)reward);
+    st_rec(*reinterpret_cast<float*>(trans + (kOff + 4) * A.np + eo4), act);
+    st_rec(*reinterpret_cast<uint8_t*>(trans + (kOff + 8) * A.np + e), term);
+    if (pin.experiment == 2)
+      st_rec(*reinterpret_cast<float*>(trans + (kOff + 9) * A.np + eo4), restart ? fo.v[3] : 0.0f);
   }
   }  // steps
   if (kRoll) {  // the carried state, once

@@ -11,7 +11,7 @@ import os
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # .../sac-agent_amd
 LIB_PATH = os.environ.get("SACENV_LIB", os.path.join(PKG_ROOT, "build", "libsacenv.so"))
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 OBS_DIM = 11
 MT_N = 624
 MAX_KNOTS = 16
@@ -20,7 +20,14 @@ SLOTS = 129
 REFILL_PERIOD = 128  # autoreset: step launches allowed between sacenv_boat_refill calls
 STATUS_SLOT_UNDERFLOW = 1
 RECORD_BYTES = 50
-TRANS_BYTES = 58  # sacenv_boat_step_pooled's per-env transition row
+TRANS_OBS = 9           # s' entries in the pooled row (obs 0..8; 9 and 10 rebuilt by the receiver)
+TRANS_BYTES = 45        # sacenv_boat_step_pooled's per-env transition row
+TRANS_BYTES_EXP2 = 49   # experiment 2 (+ obs3_next)
+
+
+def trans_bytes(experiment: int) -> int:
+    """Bytes per env of the pooled transition row for this experiment."""
+    return TRANS_BYTES_EXP2 if int(experiment) == 2 else TRANS_BYTES
 
 TERM_NONE, TERM_REACHED_GOAL, TERM_OUT_OF_BOUNDS, TERM_OUT_OF_FUEL, \
     TERM_RUDDER_BROKEN, TERM_TIMEOUT, TERM_TRUNCATED = range(7)

@@ -16,10 +16,12 @@ The shared replay buffer consumes whole transitions (s, a, r, s', terminal)
 (main.py:83-88, agent/buffer.py:13-22). The record alone cannot form them:
 for an env that ended (and auto-reset) its obs is already the NEXT episode's
 first obs. The pooled row of a step is the transition row the step kernel
-writes itself (``sacenv_boat_step_pooled``, ``TransitionLayout``: s' before
-the reset, reward, action, done, term and the one obs entry a fresh Boat does
-not fix, 58 B per env); ``TransitionStream`` turns consecutive pooled rows
-back into (s, a, r, s', code).
+writes itself (``sacenv_boat_step_pooled``, ``TransitionLayout``: s' entries
+0..8 before the reset, reward, action, term, and in experiment 2 the one obs
+entry a fresh Boat does not fix; 45 B per env, 49 in experiment 2);
+``TransitionStream`` turns consecutive pooled rows back into (s, a, r, s',
+code), rebuilding s'[9] (rudder) and s'[10] (fuel) exactly from the actions
+and episode starts.
 """
 from __future__ import annotations
 
@@ -27,7 +29,9 @@ from dataclasses import dataclass
 
 import torch
 
-from ._lib import TRANS_BYTES
+import math
+
+from ._lib import TRANS_OBS, trans_bytes
 from .vec_env import RECORD_BYTES
 
 
@@ -73,42 +77,62 @@ class RecordLayout:
 @dataclass(frozen=True)
 class TransitionLayout:
     """One rank's pooled row for one step, as ``sacenv_boat_step_pooled`` writes it
-    (SACENV_TRANS_BYTES = 58 per env, per-field arrays of n_pad entries):
+    (per-field arrays of n_pad entries; ``_lib.trans_bytes(experiment)`` per env):
 
-        [ s' f32 [n_pad][11] | reward f32 | action f32 | obs3_next f32 | done u8 | term u8 ]
+        [ s' f32 [n_pad][9] | reward f32 | action f32 | term u8 | obs3_next f32 (exp 2) ]
 
-    s' is the obs BEFORE any auto-reset (the terminal obs of envs that ended);
-    the next transition's s of such an env is the fresh-Boat obs
-    (``first_obs_template``) with entry 3 = obs3_next.
+    s' holds obs entries 0..8 BEFORE any auto-reset (the terminal obs of envs
+    that ended); entries 9 (rudder) and 10 (fuel) and done (= term != 0) are
+    rebuilt by ``TransitionStream``. In experiment 2 the next transition's s of
+    an env that ended is the fresh-Boat obs (``first_obs_template``) with entry
+    3 = obs3_next; elsewhere the template itself.
     """
-    n: int       # envs per rank
-    n_pad: int   # the arena's padded row count (n rounded up to 64)
+    n: int            # envs per rank
+    n_pad: int        # the arena's padded row count (n rounded up to 64)
+    experiment: int = 6
+
+    @property
+    def per_env(self) -> int:
+        return trans_bytes(self.experiment)
 
     @property
     def nbytes(self) -> int:
-        return TRANS_BYTES * self.n_pad
+        return self.per_env * self.n_pad
 
     def views(self, row: torch.Tensor):
-        """(s' [n,11], reward [n], action [n], obs3_next [n], done [n], term [n])."""
-        n, NP = self.n, self.n_pad
+        """(s' entries 0..8 [n,9], reward [n], action [n], term [n], obs3_next [n] or None)."""
+        n, NP, K = self.n, self.n_pad, TRANS_OBS
         if row.dtype != torch.uint8 or row.numel() != self.nbytes:
             raise ValueError("row must be uint8 of TransitionLayout.nbytes")
         f = lambda a, b: row[a * NP: b * NP].view(torch.float32)[:n]  # noqa: E731
-        s_next = row[: 44 * NP].view(torch.float32).view(NP, 11)[:n]
-        return (s_next, f(44, 48), f(48, 52), f(52, 56), row[56 * NP: 57 * NP][:n],
-                row[57 * NP: 58 * NP][:n])
+        s9 = row[: 4 * K * NP].view(torch.float32).view(NP, K)[:n]
+        o = 4 * K
+        obs3 = f(o + 9, o + 13) if self.experiment == 2 else None
+        return s9, f(o, o + 4), f(o + 4, o + 8), row[(o + 8) * NP: (o + 9) * NP][:n], obs3
 
-    def pack(self, s_next, reward, action, obs3_next, done, term) -> torch.Tensor:
-        """Host-side packing (tests, and hosts without the kernel's buffers)."""
+    def pack(self, s_next, reward, action, obs3_next, term) -> torch.Tensor:
+        """Host-side packing (tests, and hosts without the kernel's buffers); s_next is
+        the full [n, 11] obs (entries 9 and 10 are not carried)."""
         row = torch.zeros(self.nbytes, dtype=torch.uint8, device=s_next.device)
-        for dst, src in zip(self.views(row), (s_next, reward, action, obs3_next, done, term)):
-            dst.copy_(src.reshape(dst.shape).to(dst.dtype))
+        s9, r, a, t, o3 = self.views(row)
+        s9.copy_(s_next[:, :TRANS_OBS].to(torch.float32))
+        r.copy_(reward.reshape(r.shape).to(torch.float32))
+        a.copy_(action.reshape(a.shape).to(torch.float32))
+        t.copy_(term.reshape(t.shape).to(torch.uint8))
+        if o3 is not None:
+            o3.copy_(obs3_next.reshape(o3.shape).to(torch.float32))
         return row
 
     def unpack_gathered(self, gathered: torch.Tensor, world: int):
-        """Global (s', reward, action, obs3_next, done, term) in global env-id order."""
+        """Global (s'[:, :9], reward, action, term, obs3_next or None) in global env-id order."""
         parts = [self.views(gathered[r * self.nbytes:(r + 1) * self.nbytes]) for r in range(world)]
-        return tuple(torch.cat([p[i] for p in parts]) for i in range(6))
+        cat = lambda i: torch.cat([p[i] for p in parts])  # noqa: E731
+        return cat(0), cat(1), cat(2), cat(3), (cat(4) if self.experiment == 2 else None)
+
+
+# the kernel's normalisations of the two rebuilt entries (make_obs, boat_env.py:318-319)
+_RUD_LO = math.pi / 3
+_RUD_SCALE = 1.0 / (math.pi / 3 - (-math.pi / 3))
 
 
 class TransitionStream:
@@ -116,25 +140,43 @@ class TransitionStream:
 
     ``s`` is the obs the action was taken on: the previous step's s', or for an
     env that ended there the first obs of its new episode (``first_obs``, the
-    fresh-Boat template, with entry 3 = that row's obs3_next); the reset obs
-    for the first step. ``s'`` is the step's obs before any auto-reset.
+    fresh-Boat template, with entry 3 = that row's obs3_next in experiment 2);
+    the reset obs for the first step (the stream starts at a reset). ``s'`` is
+    the step's obs before any auto-reset: entries 0..8 from the row, entry 9
+    from the env's f64 rudder (0 at an episode start, += f64(action) / 10 per
+    step with test_mode 0, boat_env.py:72-73) and entry 10 from its step count
+    (fuel = fuel0 - steps, :70), in the kernel's arithmetic (bit-identical).
     ``code`` is the term code (the replay buffer derives terminal from it,
-    main.py:83-88)."""
+    main.py:83-88); done = code != 0."""
 
     def __init__(self, layout: TransitionLayout, world: int, reset_obs: torch.Tensor,
-                 first_obs: torch.Tensor):
+                 first_obs: torch.Tensor, fuel0: int = 15000, test_mode: int = 0):
         self.layout, self.world = layout, int(world)
         self.prev = reset_obs.to(torch.float32).clone()
-        self.first = first_obs.to(torch.float32).to(self.prev.device).reshape(1, -1)
+        dev = self.prev.device
+        self.first = first_obs.to(torch.float32).to(dev).reshape(1, -1)
+        n = self.prev.shape[0]
+        self.rudder = torch.zeros(n, dtype=torch.float64, device=dev)
+        self.fuel = torch.full((n,), int(fuel0), dtype=torch.int64, device=dev)
+        self.fuel0, self.test_mode = int(fuel0), int(test_mode)
 
     def push(self, gathered_row: torch.Tensor):
-        s_next, reward, action, obs3, done, term = self.layout.unpack_gathered(gathered_row, self.world)
+        s9, reward, action, term, obs3 = self.layout.unpack_gathered(gathered_row, self.world)
+        rud = self.rudder + action.to(torch.float64) / 10.0 if self.test_mode == 0 else self.rudder
+        fuel = self.fuel - 1
+        s_next = torch.empty_like(self.prev)
+        s_next[:, :TRANS_OBS] = s9
+        s_next[:, 9] = ((rud + _RUD_LO) * _RUD_SCALE).to(torch.float32)
+        s_next[:, 10] = (fuel.to(torch.float64) / float(self.fuel0)).to(torch.float32)
         s = self.prev
-        d = done.bool()[:, None]
+        done = term != 0
         fresh = self.first.expand_as(s_next).clone()
-        fresh[:, 3] = obs3
-        self.prev = torch.where(d, fresh, s_next)
-        return s, action.clone(), reward.clone(), s_next.clone(), term.clone()
+        if obs3 is not None:
+            fresh[:, 3] = obs3
+        self.prev = torch.where(done[:, None], fresh, s_next)
+        self.rudder = torch.where(done, torch.zeros_like(rud), rud)
+        self.fuel = torch.where(done, torch.full_like(fuel, self.fuel0), fuel)
+        return s, action.clone(), reward.clone(), s_next, term.clone()
 
 
 def gather_records(record: torch.Tensor, out: torch.Tensor | None = None, group=None) -> torch.Tensor:

@@ -193,8 +193,9 @@ class MixedBatch:
             if b is None:
                 raise ValueError("a transition row needs the boat env")
             if (trans_row.dtype != torch.uint8 or trans_row.device != b.device or not trans_row.is_contiguous()
-                    or trans_row.numel() != _lib.TRANS_BYTES * b.n_pad):
-                raise ValueError("trans_row must be a contiguous uint8 device tensor of TRANS_BYTES * n_pad bytes")
+                    or trans_row.numel() != _lib.trans_bytes(b.params.experiment) * b.n_pad):
+                raise ValueError("trans_row must be a contiguous uint8 device tensor of "
+                                 "trans_bytes(experiment) * n_pad bytes")
             _lib.check(self.lib.sacenv_mixed_step_pooled(
                 b._pp, b.arena.data_ptr(), a.data_ptr(), self._tp, self._ta, len(self.toys),
                 trans_row.data_ptr(), stream))

@@ -239,14 +239,16 @@ class VecBoatEnv:
         self._after_step()
 
     def step_pooled_async(self, actions: torch.Tensor, trans_row: torch.Tensor) -> None:
-        """``step_async`` that also writes the step's transition row (s', reward,
-        action, obs3_next, done, term; ``sacenv_boat_step_pooled``) into ``trans_row``,
-        a 16-B aligned uint8 device tensor of ``_lib.TRANS_BYTES * n_pad`` bytes
-        (e.g. a row of a pooling buffer: no copy launches)."""
+        """``step_async`` that also writes the step's transition row (s' entries 0..8,
+        reward, action, term, and obs3_next in experiment 2; ``sacenv_boat_step_pooled``,
+        ``sacenv.dist.TransitionLayout``) into ``trans_row``, a 16-B aligned uint8
+        device tensor of ``_lib.trans_bytes(experiment) * n_pad`` bytes (e.g. a row
+        of a pooling buffer: no copy launches)."""
         self.check_actions(actions)
+        nb = _lib.trans_bytes(self.params.experiment) * self.n_pad
         if (trans_row.dtype != torch.uint8 or trans_row.device != self.device
-                or trans_row.numel() != _lib.TRANS_BYTES * self.n_pad or not trans_row.is_contiguous()):
-            raise ValueError("trans_row must be a contiguous uint8 device tensor of TRANS_BYTES * n_pad bytes")
+                or trans_row.numel() != nb or not trans_row.is_contiguous()):
+            raise ValueError(f"trans_row must be a contiguous uint8 device tensor of {nb} bytes")
         _lib.check(self.lib.sacenv_boat_step_pooled(self._pp, self._ptr, actions.data_ptr(),
                                                     trans_row.data_ptr(), self.stream))
         self._after_step()

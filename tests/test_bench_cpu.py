@@ -133,9 +133,9 @@ def test_driver_command_world2_gloo_segment_pooling():
     assert out["value"] > 0
     assert "1 in the timed region" in out["config"]["collective"]
     assert "gloo" in out["config"]["collective"]
-    # the row is the step kernel's 58-B/env transition row
-    assert f"{58 * N_PAD} B per rank-step" in out["config"]["collective"]
-    assert out["pooling"]["received_bytes_per_rank"] == (world - 1) * 58 * N_PAD * out["steps"]
+    # the row is the step kernel's 45-B/env transition row
+    assert f"{45 * N_PAD} B per rank-step" in out["config"]["collective"]
+    assert out["pooling"]["received_bytes_per_rank"] == (world - 1) * 45 * N_PAD * out["steps"]
     assert out["pooling"]["received_GBps_per_rank"] > 0
     for _, _, steps, refills in res:
         assert steps % 128 == 0 and refills == steps // 128

@@ -60,4 +60,4 @@ def test_bench_two_ranks_gloo_on_one_device():
     assert d["n_gpus"] == 2 and d["steps"] == 128 and d["value"] > 0
     assert d["config"]["global_envs"] == 2 * 8192
     assert "gloo all_gather per 128-step segment (1 in the timed region)" in d["config"]["collective"]
-    assert "58-B/env transition row" in d["config"]["collective"]
+    assert "45-B/env transition row" in d["config"]["collective"]

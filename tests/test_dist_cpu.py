@@ -182,7 +182,7 @@ def _transition_worker(rank, world, port, seg, q):
             # what sacenv_boat_step_pooled writes: s' before the reset, and the new
             # episode's obs[3] where an env restarted
             row = lay.pack(t(r["obs"]), t(r["reward"]), t(acts[k, off:off + n]),
-                           t(r["reset_obs"][:, 3]), t(r["done"]), t(r["term"]))
+                           t(r["reset_obs"][:, 3]), t(r["term"]))
             pool.push([row])
             drain()
         pool.flush()
@@ -221,10 +221,15 @@ def test_pooled_transitions_equal_single_process(world, seg):
     for k in range(STEPS):
         r = ora.step(acts[k])
         ps, pa, pr, pn, pc = pooled[k]
-        np.testing.assert_array_equal(ps, s)
+        # entries 0..8 travel in the row (bit-exact); 9 (rudder) and 10 (fuel) are rebuilt
+        # in the kernel's arithmetic, the oracle divides: equal to an f32 ulp
+        np.testing.assert_array_equal(ps[:, :9], s[:, :9])
+        np.testing.assert_allclose(ps[:, 9:], s[:, 9:], rtol=2e-7, atol=0)
         np.testing.assert_array_equal(pa, acts[k])
         np.testing.assert_array_equal(pr, r["reward"].astype(np.float32))
-        np.testing.assert_array_equal(pn, r["obs"].astype(np.float32))   # terminal obs where done
+        want = r["obs"].astype(np.float32)  # terminal obs where done
+        np.testing.assert_array_equal(pn[:, :9], want[:, :9])
+        np.testing.assert_allclose(pn[:, 9:], want[:, 9:], rtol=2e-7, atol=0)
         np.testing.assert_array_equal(pc, r["term"])
         ended += int(r["done"].sum())
         s = r["reset_obs"].astype(np.float32)
