@@ -639,13 +639,10 @@ __device__ void role_value_bwd(const SacArgs& a, RowLds& l, int tid, int row0, i
   head_backward_half(a.P + a.net[3], a.off[kValueShape], pre, l, tid, na.dz2t, na.dz1t, a.B, row0, h);
 }
 
-// one or two workgroups per CU: registers for kPrefetch k-blocks of weights in flight
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 2))) k_sac_rows(SacArgs a, int phase) {
-  __shared__ RowLds l;
+__device__ __forceinline__ void rows_body(const SacArgs& a, RowLds& l, int phase, int vb) {
   const int tid = threadIdx.x;
   const int nrb = a.B / kRows;
-  const int role = blockIdx.x / nrb, row0 = (blockIdx.x - role * nrb) * kRows;
-  STAMP(a, phase, 0);
+  const int role = vb / nrb, row0 = (vb - role * nrb) * kRows;
   if (phase == 0) {
     if (role == 0) role_actor_fwd(a, l, tid, row0);
     else if (role == 1) role_value_fwd(a, l, tid, row0);
@@ -658,6 +655,14 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1
     if (role < 2) role_actor_bwd(a, l, tid, row0, role);  // two halves of each backward layer
     else role_value_bwd(a, l, tid, row0, role - 2);
   }
+}
+constexpr int kPhaseRoles[3] = {4, 6, 4};
+
+// one or two workgroups per CU: registers for kPrefetch k-blocks of weights in flight
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 2))) k_sac_rows(SacArgs a, int phase) {
+  __shared__ RowLds l;
+  STAMP(a, phase, 0);
+  rows_body(a, l, phase, blockIdx.x);
   STAMP(a, phase, 15);
 }
 
@@ -888,10 +893,8 @@ constexpr int kFc2Tiles = 8 * 8;  // 32x32 tiles of a 256x256 layer
 // finish early and their CUs then take the last fc2 tiles), then 256 fc2 tiles
 constexpr int kSmallBlocks = 4 * (kH / kSmallF);
 
-__global__ void __launch_bounds__(kThreads) k_sac_update(SacArgs a) {
-  __shared__ float sm[kUpdLds];
-  const int tid = threadIdx.x, b = blockIdx.x;
-  STAMP(a, 3, 0);
+__device__ __forceinline__ void update_body(const SacArgs& a, float* sm, int b) {
+  const int tid = threadIdx.x;
   if (b == 0) {
     reduce_losses(a, tid, sm);
   } else if (b <= kSmallBlocks) {
@@ -912,6 +915,13 @@ __global__ void __launch_bounds__(kThreads) k_sac_update(SacArgs a) {
     const int t = k >> 3, kk = k & 7;
     fc2_tile(a, t, 2 * (x >> 1) + (kk >> 2), 4 * (x & 1) + (kk & 3), tid, sm);
   }
+}
+constexpr int kUpdateBlocks = 1 + kSmallBlocks + 4 * kFc2Tiles;
+
+__global__ void __launch_bounds__(kThreads) k_sac_update(SacArgs a) {
+  __shared__ float sm[kUpdLds];
+  STAMP(a, 3, 0);
+  update_body(a, sm, blockIdx.x);
   STAMP(a, 3, 15);
 }
 
@@ -1204,6 +1214,6 @@ extern "C" int sacenv_sac_learn(const SacenvSacParams* p, float* weights, void* 
   hipLaunchKernelGGL(k_sac_rows, dim3(4 * nrb), dim3(kThreads), 0, s, a, 0);
   hipLaunchKernelGGL(k_sac_rows, dim3(6 * nrb), dim3(kThreads), 0, s, a, 1);
   hipLaunchKernelGGL(k_sac_rows, dim3(4 * nrb), dim3(kThreads), 0, s, a, 2);
-  hipLaunchKernelGGL(k_sac_update, dim3(1 + kSmallBlocks + 4 * kFc2Tiles), dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL(k_sac_update, dim3(kUpdateBlocks), dim3(kThreads), 0, s, a);
   return (int)hipGetLastError();
 }
