@@ -656,7 +656,6 @@ __device__ __forceinline__ void rows_body(const SacArgs& a, RowLds& l, int phase
     else role_value_bwd(a, l, tid, row0, role - 2);
   }
 }
-constexpr int kPhaseRoles[3] = {4, 6, 4};
 
 // one or two workgroups per CU: registers for kPrefetch k-blocks of weights in flight
 __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 2))) k_sac_rows(SacArgs a, int phase) {
