@@ -12,6 +12,9 @@ set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=$GRAFT_REPO_ROOT/gpurun_out
 mkdir -p "$OUT"
+# the calibration probe is a gitignored build product: build it if this tree lacks it
+[ -x tools/probes/fetch_calib ] || /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 \
+  -o tools/probes/fetch_calib tools/probes/fetch_calib.hip || exit 1
 BENCH="python3 bench.py --steps ${PMC_STEPS:-256} --warmup 128 --no-cpu-baseline --no-graph"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_trace" -o run --output-format csv \
   -- python3 bench.py --no-cpu-baseline > "$OUT/prof_trace_bench.json" 2> "$OUT/prof_trace.log" || exit 1
