@@ -29,6 +29,8 @@ def test_driver_bench_command():
     assert d["steps"] == 128 and d["warmup"] == 128 and d["n_gpus"] == 1
     assert d["value"] > 0 and d["unit"] == "env-steps/s"
     assert d["ms_per_step"] * d["steps"] * 1e-3 <= wall
+    # every captured graph (4 action-table segments) ran once before the warm-up
+    assert d["setup"]["graph_first_replays"] == 512
     rf = d["roofline"]
     assert rf["bound"] == "hbm" and 0 < rf["frac"] < 1 and rf["kernel_avg_us"] > 0
     # the timed step includes its refill: never faster than the kernel alone
