@@ -91,6 +91,9 @@ def parse(argv=None):
     ap.add_argument("--pooling", choices=("gather", "none"), default="gather",
                     help="N>1: all-gather the full transitions per 128-step segment (configs[3]), "
                          "or none (sharded per-GPU replay, SURVEY.md §8(e)'s alternative)")
+    ap.add_argument("--pool-every", type=int, default=SEG,
+                    help="N>1 gather pooling: steps per all-gather (1 = one all-gather per step, "
+                         "SURVEY.md §8(e); 128 = one per segment, overlapped with the next)")
     ap.add_argument("--episode-steps", type=int, default=EPISODE_STEPS,
                     help="truncation length (0 = none)")
     return ap.parse_args(argv)
@@ -120,6 +123,34 @@ def init_dist(n_gpus: int):
         else:
             dist.init_process_group(backend)
     return rank, world, torch.device("cuda", local)
+
+
+XGMI_LINK_GBPS = 153.0  # the task brief's MI355X xGMI figure: 7 links x ~153 GB/s per GPU
+
+
+def dist_info(world: int, dev) -> dict | None:
+    """N>1: what ran the collectives (backend, RCCL version, each rank's device)."""
+    if world <= 1:
+        return None
+    import torch.distributed as dist
+    me = {"rank": dist.get_rank(), "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+          "device": str(dev)}
+    if dev.type == "cuda":
+        pr = torch.cuda.get_device_properties(dev)
+        me["device_name"] = pr.name
+        me["pci_bus_id"] = getattr(pr, "pci_bus_id", None)
+    ranks = [None] * world
+    dist.all_gather_object(ranks, me)
+    backend = dist.get_backend()
+    ver = None
+    if backend == "nccl":
+        try:
+            v = torch.cuda.nccl.version()
+            ver = ".".join(map(str, v)) if isinstance(v, tuple) else str(v)
+        except Exception as exc:  # noqa: BLE001
+            ver = f"unavailable: {exc}"
+    return {"world_size": world, "backend": "RCCL (nccl)" if backend == "nccl" else backend,
+            "rccl_version": ver, "ranks": ranks}
 
 
 def barrier(world):
@@ -158,9 +189,10 @@ def cpu_baseline(args, n_envs: int) -> dict:
     the bench's experiment), plus the vectorised port on the bench's shape."""
     budget = max(2.0, float(args.cpu_seconds))
     exps = sorted({1, int(args.experiment)})
-    per_leg = budget * 0.8 / (2 * len(exps))
+    per_leg = budget * 0.8 / (3 * len(exps))
     cmd = [sys.executable, os.path.join(ROOT, "tools", "cpu_c1.py"), "--seconds", f"{per_leg:.2f}",
-           "--experiments", ",".join(map(str, exps)), "--max-procs", "16"]
+           "--experiments", ",".join(map(str, exps)), "--max-procs", "16", "--mode", "scalar",
+           "--numpy-one-core"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
     if r.returncode != 0:
         raise RuntimeError(f"cpu_c1 failed: {r.stderr[-2000:]}")
@@ -168,12 +200,14 @@ def cpu_baseline(args, n_envs: int) -> dict:
     leg = c1["experiments"][str(args.experiment)]
     out = {"value": leg["all_cores"]["env_steps_per_s"], "unit": "env-steps/s",
            "cores": leg["all_cores"]["procs"], "kind": "port",
-           "sample": (f"SURVEY.md §8(d) C1: oracle/boat_oracle.py (numpy f64 restatement of "
-                      f"BoatEnv.step, boat_env.py:67-115), exp {args.experiment}, ONE env per process "
-                      f"(as the reference runs), {leg['all_cores']['procs']} processes pinned one per "
-                      f"core, U(-1,1) actions, auto-reset on done or at 500 steps, "
+           "sample": (f"SURVEY.md §8(d) C1 in §7.2's scalar N=1 mode: oracle/boat_scalar.py (BoatEnv.step, "
+                      f"boat_env.py:67-115, restated with Python floats + math, f64; per-episode wind "
+                      f"tables materialised at reset as the reference does), exp {args.experiment}, ONE "
+                      f"env per process (as the reference runs), {leg['all_cores']['procs']} processes "
+                      f"pinned one per core, U(-1,1) actions, reset on done or at 500 steps, "
                       f"{per_leg:.1f} s per leg"),
            "one_core": leg["one_core"]["env_steps_per_s"],
+           "one_core_numpy_n1": leg.get("one_core_numpy_n1", {}).get("env_steps_per_s"),
            "c1": c1}
     if not args.mixed:
         out["vectorised_port"] = _vectorised_port(n_envs, budget * 0.2, args.experiment)
@@ -289,86 +323,145 @@ def make_workload(args, rank: int, dev) -> Workload:
     return Workload(envs, stepper, refill, actions, pooled_step, row_bytes, N * len(envs), bytes_launch)
 
 
-# ---------------------------------------------------------------- timing loop
-def run_bench(args, rank: int, world: int, dev, wl: Workload):
-    """Warm up, time whole segments, measure k_step; rank 0 returns the JSON dict."""
-    use_graph = dev.type == "cuda" and not args.no_graph
-    pool = None
-    if world > 1:
-        import torch.distributed as dist
-        if args.pooling == "gather":
-            from sacenv.dist import SegmentPool
-            # each step's full transitions are copied into row j of a [SEG][row]
-            # staging buffer (graph-captured with the steps); ONE all-gather per
-            # segment pools them on a side stream while the next segment steps
-            pool = SegmentPool(wl.row_bytes(), SEG, dev)
-    st = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
+# ---------------------------------------------------------------- segments
+class SegmentRunner:
+    """Runs whole segments of the workload: steps k0 .. k0+SEG-1 (actions row k %
+    ACTION_STEPS), then the slot refill, then (N>1) the pooling of the segment's
+    transition rows. With a GPU and no ``--no-graph`` the SEG step launches of a
+    segment are ONE hipGraph replay (one graph per segment of the action table and
+    staging buffer); else eager launches. ``prepare()`` warms up and replays every
+    captured graph once (its device upload), and runs the same steps eagerly in
+    eager mode, so a graph runner and an eager runner of the same workload execute
+    the same step sequence (tests/test_bench_path_gpu.py holds them bit-identical).
 
-    def capture(k0: int, buf: int, with_pool: bool):
+    ``pool_every`` P (N>1): the rows of P consecutive steps go out in one
+    all-gather: P = SEG stages a segment's rows inside its graph and gathers them
+    after it (``SegmentPool``, on a side stream); P < SEG (e.g. 1, SURVEY.md §8(e)'s
+    one all-gather per step) steps eagerly and gathers every P steps."""
+
+    def __init__(self, args, wl: Workload, dev, pool=None, pool_every: int = SEG):
+        if SEG % pool_every:
+            raise ValueError(f"--pool-every must divide {SEG}")
+        self.args, self.wl, self.dev, self.pool = args, wl, dev, pool
+        self.pool_every = int(pool_every)
+        self.use_graph = dev.type == "cuda" and not args.no_graph and (pool is None or pool_every == SEG)
+        self.st = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
+        self.graphs = None
+        self.first_replays = 0
+        self.seg_events: list = []
+
+    def _steps(self, k0: int, with_pool: bool, buf=None, on_step=None) -> None:
+        """The SEG step launches of one segment, enqueued (captured or eager)."""
+        wl, p = self.wl, self.pool if with_pool else None
+        for j, k in enumerate(range(k0, k0 + SEG)):
+            if p is None:
+                wl.stepper(wl.actions[k % ACTION_STEPS])
+            elif self.pool_every == SEG:
+                wl.pooled_step(k, p.row(j, buf))
+            else:  # P < SEG: eager, one all-gather per P steps
+                jj = j % self.pool_every
+                if jj == 0:
+                    p.begin()
+                wl.pooled_step(k, p.row(jj))
+                if jj == self.pool_every - 1:
+                    p.fill = self.pool_every
+                    p.flush()
+            if on_step is not None:
+                on_step(k)
+
+    def _capture(self, k0: int, buf: int, with_pool: bool):
         gr = torch.cuda.CUDAGraph()
         # thread_local: a collective library thread querying its events while this
         # thread captures must not invalidate the capture
         with torch.cuda.graph(gr, capture_error_mode="thread_local"):
-            for j, k in enumerate(range(k0, k0 + SEG)):
-                if with_pool:
-                    wl.pooled_step(k, pool.row(j, buf))
-                else:
-                    wl.stepper(wl.actions[k % ACTION_STEPS])
+            self._steps(k0, with_pool, buf)
         return gr
 
-    graphs = None
-    first_replays = 0
-    if use_graph:
-        s = torch.cuda.Stream(device=dev)
-        s.wait_stream(st)
-        with torch.cuda.stream(s):  # warm the launch path before capturing
+    def capture_all(self, with_pool: bool) -> None:
+        bufs = (0, 1) if with_pool and self.pool is not None else (0,)
+        self.graphs = [[self._capture(base, b, with_pool and self.pool is not None) for b in bufs]
+                       for base in range(0, ACTION_STEPS, SEG)]
+
+    def prepare(self, on_step=None) -> None:
+        """Warm the launch path (3 steps + a refill), capture, and run every captured
+        graph once (each followed by its refill) before the warm-up: a graph's first
+        replay carries its upload to the device, which the driver's short --steps 20
+        --warmup 5 would otherwise put into the timed region. Eager mode runs the
+        same steps."""
+        wl, dev = self.wl, self.dev
+        if dev.type != "cuda":
+            return
+        if self.use_graph:
+            s = torch.cuda.Stream(device=dev)
+            s.wait_stream(self.st)
+            with torch.cuda.stream(s):
+                for k in range(3):
+                    wl.stepper(wl.actions[k])
+            self.st.wait_stream(s)
+        else:
             for k in range(3):
                 wl.stepper(wl.actions[k])
-        st.wait_stream(s)
+                if on_step is not None:
+                    on_step(k)
         wl.refill()
         _sync(dev)
-        # one graph per (segment of the action table, staging buffer)
-        bufs = (0, 1) if pool is not None else (0,)
-        graphs = [[capture(base, b, pool is not None) for b in bufs]
-                  for base in range(0, ACTION_STEPS, SEG)]
-        # replay every captured graph once (each followed by its refill) before the
-        # warm-up: a graph's first replay carries its upload to the device, which the
-        # driver's short --steps 20 --warmup 5 would otherwise put into the timed region
-        for gset in graphs:
-            for gr in gset:
-                gr.replay()
-                wl.refill()
-                first_replays += SEG
+        if self.use_graph:
+            self.capture_all(with_pool=self.pool is not None)
+            for gset in self.graphs:
+                for gr in gset:
+                    gr.replay()
+                    wl.refill()
+                    self.first_replays += SEG
+        else:
+            nbuf = 2 if self.pool is not None and self.pool_every == SEG else 1
+            for base in range(0, ACTION_STEPS, SEG):
+                for b in range(nbuf):
+                    self._steps(base, False, on_step=on_step)  # the graph replays' steps
+                    wl.refill()
+                    self.first_replays += SEG
         _sync(dev)
 
-    seg_events = []
-
-    def segment(k0: int, timed: bool, with_pool: bool = True):
+    def segment(self, k0: int, timed: bool = False, with_pool: bool = True, on_step=None) -> int:
         """Steps k0 .. k0+SEG-1 (k0 % SEG == 0), then the refill, then the pooling."""
-        p = pool if with_pool else None
-        if p is not None:
+        p = self.pool if with_pool else None
+        if p is not None and self.pool_every == SEG:
             p.begin()
         if timed:
-            ea, eb = _Clock(dev), _Clock(dev)
-            ea.record(st)
-        if graphs is not None:
-            gset = graphs[(k0 % ACTION_STEPS) // SEG]
+            ea, eb = _Clock(self.dev), _Clock(self.dev)
+            ea.record(self.st)
+        if self.graphs is not None:
+            gset = self.graphs[(k0 % ACTION_STEPS) // SEG]
             gset[p.buf if p is not None else 0].replay()
         else:
-            for j, k in enumerate(range(k0, k0 + SEG)):
-                if p is not None:
-                    wl.pooled_step(k, p.row(j))
-                else:
-                    wl.stepper(wl.actions[k % ACTION_STEPS])
+            self._steps(k0, p is not None, on_step=on_step)
         if timed:
-            eb.record(st)
-            seg_events.append((ea, eb))
-        wl.refill()
-        if p is not None:
+            eb.record(self.st)
+            self.seg_events.append((ea, eb))
+        self.wl.refill()
+        if p is not None and self.pool_every == SEG:
             p.fill = SEG
             p.flush()
         return k0 + SEG
 
+
+# ---------------------------------------------------------------- timing loop
+def run_bench(args, rank: int, world: int, dev, wl: Workload):
+    """Warm up, time whole segments, measure k_step; rank 0 returns the JSON dict."""
+    pool = None
+    pool_every = int(getattr(args, "pool_every", SEG))
+    if world > 1:
+        if args.pooling == "gather":
+            from sacenv.dist import SegmentPool
+            # each step's full transitions are written into row j of a [P][row]
+            # staging buffer (graph-captured with the steps when P = SEG); ONE
+            # all-gather per P steps pools them on a side stream
+            pool = SegmentPool(wl.row_bytes(), pool_every, dev)
+    run = SegmentRunner(args, wl, dev, pool, pool_every)
+    use_graph = run.use_graph
+    run.prepare()
+    st = run.st
+    seg_events = run.seg_events
+    segment = run.segment
     n_warm, n_timed = segs(args.warmup), segs(args.steps)
     k = 0
     for _ in range(n_warm):
@@ -403,9 +496,10 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
     # around 128-launch graph segments (refills excluded). N=1: the segments of
     # the timed region itself. N>1 (the segments also stage the pooled rows) or
     # eager: k_step-only segments replayed after the timed region.
-    if pool is not None or graphs is None:
-        if use_graph:
-            graphs = [[capture(base, 0, False)] for base in range(0, ACTION_STEPS, SEG)]
+    if pool is not None or not use_graph:
+        if dev.type == "cuda" and not args.no_graph:
+            run.capture_all(with_pool=False)
+            use_graph = True
         seg_events.clear()
         k = segment(k, False, with_pool=False)
         for _ in range(segs(args.kernel_launches)):
@@ -420,6 +514,7 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
     kern_s = sum(a.ms_to(b) for a, b in seg_events) * 1e-3 / (SEG * len(seg_events))
     step_s = ev0.ms_to(ev1) * 1e-3 / steps
 
+    dinfo = dist_info(world, dev)
     if rank != 0:
         return None
     achieved = wl.bytes_per_launch / kern_s
@@ -438,7 +533,7 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
         "warmup": n_warm * SEG,
         "requested": {"steps": args.steps, "warmup": args.warmup,
                       "rule": f"rounded up to whole {SEG}-step segments (each ends with its refill)"},
-        "setup": {"graph_first_replays": first_replays,
+        "setup": {"graph_first_replays": run.first_replays,
                   "note": "step launches of each captured graph's first replay (its device upload), "
                           "run before the warm-up, untimed"},
         "ms_per_step": el_max / steps * 1e3,
@@ -456,8 +551,10 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
                    "episode_steps": args.episode_steps, "parallelism": f"env-dp{world}",
                    "collective": (f"all_gather of each step's full transitions (the {TRANS_ROW} written by the "
                                   f"step kernel, {wl.row_bytes()} B per rank-step): one "
-                                  f"{backend} all_gather per {SEG}-step segment ({gathers_timed} in the "
-                                  "timed region) on a side stream, overlapped with the next segment")
+                                  f"{backend} all_gather per {pool_every}-step "
+                                  + ("segment" if pool_every == SEG else "group") +
+                                  f" ({gathers_timed} in the timed region) on a side stream"
+                                  + (", overlapped with the next segment" if pool_every == SEG else ""))
                    if pool is not None else (
                        "none: sharded per-GPU replay (--pooling none)" if world > 1 else None),
                    "launch": (f"hipGraph segments of {SEG} k_step launches" +
@@ -480,12 +577,18 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
                      "traffic_source": None if traffic is None else traffic["source"]},
         "cpu_baseline": None,
         # N>1: what the pooled transitions cost -- every rank receives (world - 1) rows per step
+        "dist": dinfo,
         "pooling": None if pool is None else {
+            "pool_every": pool_every,
+            "gathers_timed": gathers_timed,
             "row_bytes_per_rank_step": wl.row_bytes(),
             "received_bytes_per_rank": (world - 1) * wl.row_bytes() * steps,
             "received_GBps_per_rank": (world - 1) * wl.row_bytes() * steps / el_max / 1e9,
-            "note": "the timed region ends when the last segment's all_gather has landed; with "
-                    "xGMI links of ~64 GB/s per direction the pooled bytes, not k_step, bound N>1"},
+            # xGMI accounting: each peer's rows arrive over its own point-to-point link
+            "xgmi": {"link_peak_GBps": XGMI_LINK_GBPS, "links_used": world - 1,
+                     "per_link_GBps": wl.row_bytes() * steps / el_max / 1e9,
+                     "per_link_frac": wl.row_bytes() * steps / el_max / 1e9 / XGMI_LINK_GBPS},
+            "note": "the timed region ends when the last all_gather has landed"},
     }
 
 

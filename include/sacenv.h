@@ -411,7 +411,8 @@ int sacenv_replay_sample(const SacenvReplayParams *p, void *arena, int32_t batch
 #define SACENV_SAC_HIDDEN 256   /* layer1_size = layer2_size (original_config.yaml:18-19) */
 
 typedef struct SacenvSacParams {
-  int32_t obs_dim;       /* input_dims[0] (11 for the boat), 1..15 */
+  int32_t obs_dim;       /* input_dims[0] (11 for the boat), 1..14: the critic's fc1 input
+                            is obs_dim + the action + a bias column of ones, in 16 columns */
   int32_t n_actions;     /* 1 (the boat's action_space.shape) */
   int32_t hidden;        /* SACENV_SAC_HIDDEN */
   int32_t batch;         /* learn batch (batch_size), a multiple of 256 */

@@ -240,10 +240,9 @@ struct DrawLds : RngLds {  // draw + wave fit (init / host resets)
 #endif
 };
 
-// diagnostic phase clocks (tools/stamps.py; -DSACENV_STAMPS builds only).
-// SACENV_STAMPS_LIGHT keeps only each wave's start and end clock (no waits
-// inserted: the end clock is when the wave's last instruction issued).
-#if defined(SACENV_STAMPS) && !defined(SACENV_STAMPS_LIGHT)
+// diagnostic phase clocks (tools/stamps.py; -DSACENV_STAMPS builds only, never
+// loaded by the product path)
+#if defined(SACENV_STAMPS)
 #define DRAW_STAMP(l, i)                                                   \
   do {                                                                     \
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");            \
@@ -331,13 +330,9 @@ __device__ __forceinline__ void wind_at(const SacenvBoatParams& p, const Arena& 
 // fma(), the compiler builds each 64-bit coefficient in the accumulator with
 // two v_mov_b32 and a v_fmac: three VALU per polynomial term instead of one.
 __device__ __forceinline__ double fma_sc(double a, double b, double c) {
-#ifndef SACENV_FMA_PLAIN
   double r;
   asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
   return r;
-#else
-  return fma(a, b, c);
-#endif
 }
 
 // sin(x) for |x| <= 1.25 with no argument reduction: x + x^3 P(x^2), P the
@@ -359,11 +354,6 @@ __device__ __forceinline__ double sin_reduced(double x) {
   q = fma_sc(q, z, 1.6666666666666666e-01);    // 1/3! (sign below)
   return fma(-(x * z), q, x);
 }
-#ifndef SACENV_SIN_OCML  // A/B builds: ocml's sin everywhere (measured 0.13 us/step slower)
-#define SACENV_SIN_SMALL(x) sin_reduced(x)
-#else
-#define SACENV_SIN_SMALL(x) sin(x)
-#endif
 
 // sin and cos of x for |x| <= 1e5: k = rint(x 2/pi), r = x - k pi/2 by fma in
 // three Cody-Waite terms (each fma rounds once: r within ~1 ulp), Taylor
@@ -400,11 +390,6 @@ __device__ __forceinline__ void sincos_cw(double x, double* sp, double* cp) {
   *sp = (q & 2) ? -a : a;
   *cp = ((q + 1) & 2) ? -b : b;
 }
-#ifndef SACENV_SINCOS_OCML
-#define SACENV_SINCOS(x, s, c) sincos_cw(x, s, c)
-#else
-#define SACENV_SINCOS(x, s, c) sincos(x, s, c)
-#endif
 
 
 // x / c for a per-launch constant c, from r = RN(1/c): Markstein's correction
@@ -453,53 +438,23 @@ __device__ __forceinline__ Obs make_obs(const SacenvBoatParams& p, const ObsCons
 
 typedef float f4v __attribute__((ext_vector_type(4)));
 
-// Cache policy of the step's output stores. Default SACENV_ST_SC1:
-// write-through (sc1: the line leaves the XCD L2, so the launch ends with no
-// dirty lines to write back; measured 0.21 us/step faster than plain stores);
-// the 16-B pairs and obs rows (no 16-B sc1 atomic form) as write-through buffer
-// stores (aux bit 4). A/B builds: SACENV_ST_PLAIN, SACENV_ST_NT, SACENV_OBS_NT.
-#if !defined(SACENV_ST_PLAIN) && !defined(SACENV_ST_NT) && !defined(SACENV_ST_SC1)
-#define SACENV_ST_SC1 1
-#endif
+// Cache policy of the step's output stores: write-through (sc1: the line
+// leaves the XCD L2 as it issues, so the launch ends with no dirty lines to
+// write back at its boundary; measured 0.21 us/step faster than plain stores,
+// DESIGN.md §4). Scalars as agent-scope relaxed atomic stores; the 16-B pairs
+// and obs rows (no 16-B sc1 atomic form) as write-through buffer stores (aux
+// bit 4).
 template <class T>
 __device__ __forceinline__ void st_out(T& ref, T v) {
-#if defined(SACENV_ST_SC1)
   __hip_atomic_store(&ref, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#elif defined(SACENV_ST_NT)
-  __builtin_nontemporal_store(v, &ref);
-#else
-  ref = v;
-#endif
-}
-template <class T>
-__device__ __forceinline__ void st_rec(T& ref, T v) {  // reward / done / term bytes
-#ifdef SACENV_REC_PLAIN
-  ref = v;
-#else
-  st_out(ref, v);
-#endif
-}
-[[maybe_unused]] __device__ __forceinline__ void st_out4(f4v* ptr, f4v v) {  // SACENV_OBS_NT A/B
-#if (defined(SACENV_ST_NT) || defined(SACENV_ST_SC1)) && !defined(SACENV_OBS_PLAIN)
-  __builtin_nontemporal_store(v, ptr);
-#else
-  *ptr = v;
-#endif
 }
 
-// a 16-B pair of the paired state (block unit u): with the default policy a
-// write-through buffer store (sc1, aux bit 4); there is no 16-B sc1 atomic form
+// a 16-B pair of the paired state (block unit u), write-through
 typedef unsigned int u4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void st_pair(char* base, int u, uint32_t np, uint32_t eo, double a, double b) {
   const uint32_t off = (uint32_t)u * np + 2u * eo;
-#if defined(SACENV_ST_SC1)
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, make_double2(a, b)), r, off, 0, 16);
-#elif defined(SACENV_ST_NT)
-  __builtin_nontemporal_store(make_double2(a, b), reinterpret_cast<double2*>(base + off));
-#else
-  *reinterpret_cast<double2*>(base + off) = make_double2(a, b);
-#endif
 }
 
 __device__ __forceinline__ void store_obs(float* dst, const Obs& o) {
@@ -1066,9 +1021,6 @@ __global__ void __launch_bounds__(1024) k_compact(const uint8_t* __restrict__ do
 __global__ void __launch_bounds__(kWave) k_refill(SacenvBoatParams p, Arena A) {
   __shared__ RngLds lds;
   const int lane = threadIdx.x;
-#ifdef SACENV_DIAG_NO_REFILL  // timing diagnostics only
-  if (lane >= 0) return;
-#endif
   const Ranking k = rank_masks(A, lane);
   if (blockIdx.x == 0 && lane == 0) {
     A.status()[0] += 1;
@@ -1369,20 +1321,14 @@ __host__ __device__ inline bool t_from_index(double dt) {
 template <int ROW = SACENV_OBS_DIM>  // floats per env row (11: obs; 9: the pooled row's s')
 __device__ __forceinline__ void store_obs_block(const float* lds_rows, float* dst_rows, int lane) {
   const f4v* src = reinterpret_cast<const f4v*>(lds_rows);
-#ifndef SACENV_OBS_NT  // write-through 16-B buffer stores (sc1, aux bit 4): 0.13 us/step
-  // faster than nontemporal ones, which leave the rows dirty in L2 for the boundary
+  // write-through 16-B buffer stores (sc1, aux bit 4): 0.13 us/step faster than
+  // nontemporal ones, which leave the rows dirty in L2 for the boundary
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(dst_rows, 0, 0x7fffffff, 0x00020000);
-#endif
 #pragma unroll
   for (int i = 0; i < (ROW * 16 + kWave - 1) / kWave; ++i) {
     const uint32_t q = (uint32_t)lane + kWave * i;
-    if (q < kWave * ROW / 4) {
-#ifndef SACENV_OBS_NT
+    if (q < kWave * ROW / 4)
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, src[q]), r, q * 16u, 0, 16);
-#else
-      st_out4(reinterpret_cast<f4v*>(reinterpret_cast<char*>(dst_rows) + q * 16u), src[q]);
-#endif
-    }
   }
 }
 
@@ -1403,17 +1349,11 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
 #ifdef SACENV_STAMPS
   const uint64_t st_real0 = __builtin_amdgcn_s_memrealtime();
   uint64_t st_loaded = 0, st_computed = 0;
-#ifndef SACENV_STAMPS_LIGHT
 #define OWNER_STAMP(v)                                          \
   do {                                                          \
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); \
     v = __builtin_amdgcn_s_memrealtime();                       \
   } while (0)
-#else
-#define OWNER_STAMP(v) \
-  do {                 \
-  } while (0)
-#endif
 #else
 #define OWNER_STAMP(v) \
   do {                 \
@@ -1506,9 +1446,6 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
     const int wn = index + 1 > p.wind_len - 1 ? p.wind_len - 1 : index + 1;
     jn = knot_coord(p, wn).j;
     refresh = index == 0 || jn != knot_coord(p, wi).j;
-#ifdef SACENV_DIAG_NO_REFRESH  // timing diagnostics only
-    refresh = false;
-#endif
     {  // the piece of the next step's interval for refreshing lanes, stored at
       // the end (own registers, read only there). Unconditional loads, the
       // other lanes reading one fixed line: with no branch around them the
@@ -1531,11 +1468,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   // refresh loads above; no select between two loaded registers either).
   double y0n[2];
   int32_t syn = 0;
-#ifndef SACENV_DIAG_NO_REFRESH
   const bool hdr_refresh = p.autoreset && index == 0;
-#else
-  const bool hdr_refresh = false;
-#endif
   {
     const int ns = (cons + 1) % kSlots;
 #pragma unroll
@@ -1563,13 +1496,13 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   const bool first = index == 0;  // integrator counter == 0 (control_blocks.py:21-22)
   const double wsign = (double)((wv > 0.0) - (wv < 0.0));
   double swa, cwa;
-  SACENV_SINCOS(wa, &swa, &cwa);
+  sincos_cw(wa, &swa, &cwa);
 
   // eom_longitudinal :213-239
   const double F_R = v_x * v_x * p.c_r_front * 0.5 * p.rho * p.boat_area_front;
   const double v_x_w = v_x * p.one_minus_wf;
   const double J = p.n_rpm != 0.0 ? div_c(v_x_w, p.n_times_d, r_nd) : 0.0;  // :222-224
-  const double F_T = SACENV_SIN_SMALL(J) * p.n_squared * p.rho * p.d_pow4 * p.one_minus_td;
+  const double F_T = sin_reduced(J) * p.n_squared * p.rho * p.d_pow4 * p.one_minus_td;
   const double F_C = v_y * p.m_plus_my * v_r;
   const double F_W = (wv * wv * wsign * p.c_r_front * 0.5 * p.rho * p.boat_area_front) * cwa;
   const double a_x = div_c(-F_R + F_T + F_C + F_W, p.m_plus_mx, r_mx);
@@ -1578,7 +1511,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   // eom_transverse :241-265 (new v_x)
   const double vys = (double)((v_y > 0.0) - (v_y < 0.0));
   const double F_R2 = v_y * v_y * p.c_r_side * 0.5 * p.rho * p.boat_area_side * vys;
-  const double sin_rud = SACENV_SIN_SMALL(rudder);
+  const double sin_rud = sin_reduced(rudder);
   const double F_RU = sin_rud * (v_x * v_x * p.c_r_front * 0.5 * p.rho * p.rudder_area);
   const double F_C2 = v_x * p.m_plus_mx * v_r;
   const double F_W2 = (wv * wv * wsign * p.c_r_side * 0.5 * p.rho * p.boat_area_side) * swa;
@@ -1595,16 +1528,6 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   EARLY_STORE2(U_VY, v_y, v_r);
 
   // get_kinematics :283-306
-#ifdef SACENV_KIN_ATAN2  // the reference's expressions (A/B builds)
-  const double v = sqrt(v_x * v_x + v_y * v_y);
-  const double drift = atan2(v_x, v_y);
-  s_r = v_r * p.dt + s_r;
-  const double dir = drift - s_r;
-  double sd, cd;
-  sincos(dir, &sd, &cd);
-  s_x = (sd * v) * p.dt + s_x;
-  s_y = (cd * v) * p.dt + s_y;
-#else
   // drift = atan2(v_x, v_y) has sin = v_x / v, cos = v_y / v, so
   // sin(drift - s_r) v = v_x cos s_r - v_y sin s_r and
   // cos(drift - s_r) v = v_y cos s_r + v_x sin s_r: no atan2, sqrt or division
@@ -1612,10 +1535,9 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   // differences: the increments agree to a few ulp of v dt.
   s_r = v_r * p.dt + s_r;
   double ssr, csr;
-  SACENV_SINCOS(s_r, &ssr, &csr);
+  sincos_cw(s_r, &ssr, &csr);
   s_x = (v_x * csr - v_y * ssr) * p.dt + s_x;
   s_y = (v_y * csr + v_x * ssr) * p.dt + s_y;
-#endif
   index = index + 1;
   EARLY_STORE2(U_SX, s_x, s_y);
   EARLY_STORE2(U_SR, s_r, v_x);
@@ -1734,9 +1656,9 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
     syc = syn;
     cons = cons_out;
   }
-  st_rec(*reinterpret_cast<float*>(R + 44 * A.np + eo4), (float)reward);
-  st_rec(*reinterpret_cast<uint8_t*>(R + 48 * A.np + e), (uint8_t)(ended ? 1 : 0));
-  st_rec(*reinterpret_cast<uint8_t*>(R + 49 * A.np + e), term);
+  st_out(*reinterpret_cast<float*>(R + 44 * A.np + eo4), (float)reward);
+  st_out(*reinterpret_cast<uint8_t*>(R + 48 * A.np + e), (uint8_t)(ended ? 1 : 0));
+  st_out(*reinterpret_cast<uint8_t*>(R + 49 * A.np + e), term);
   // obs rows through LDS, stored as float4 (64 rows x 44 B = 176 float4); a
   // restarting env's row is its new episode's first obs
 #pragma unroll
@@ -1769,11 +1691,11 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
     store_obs_block<SACENV_TRANS_OBS>(l.obs, reinterpret_cast<float*>(trans) + (int64_t)ob * kWave * SACENV_TRANS_OBS,
                                       lane);
     constexpr int kOff = 4 * SACENV_TRANS_OBS;  // byte columns (x n_pad) after s'
-    st_rec(*reinterpret_cast<float*>(trans + kOff * A.np + eo4), (float)reward);
-    st_rec(*reinterpret_cast<float*>(trans + (kOff + 4) * A.np + eo4), act);
-    st_rec(*reinterpret_cast<uint8_t*>(trans + (kOff + 8) * A.np + e), term);
+    st_out(*reinterpret_cast<float*>(trans + kOff * A.np + eo4), (float)reward);
+    st_out(*reinterpret_cast<float*>(trans + (kOff + 4) * A.np + eo4), act);
+    st_out(*reinterpret_cast<uint8_t*>(trans + (kOff + 8) * A.np + e), term);
     if (pin.experiment == 2)
-      st_rec(*reinterpret_cast<float*>(trans + (kOff + 9) * A.np + eo4), restart ? fo.v[3] : 0.0f);
+      st_out(*reinterpret_cast<float*>(trans + (kOff + 9) * A.np + eo4), restart ? fo.v[3] : 0.0f);
   }
   }  // steps
   if (kRoll) {  // the carried state, once
@@ -1796,9 +1718,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   }
 
 #ifdef SACENV_STAMPS
-#ifndef SACENV_STAMPS_LIGHT
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
   if (lane == 0) {
     double* d = A.accel() + (int64_t)ob * 4;
     d[0] = (double)st_real0;
@@ -1811,34 +1731,18 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
 
 // The step launch. Grid: nb_boat owner waves, then (kMixed) the waves of
 // each toy arena: heterogeneous workgroups of one launch, selected by
-// uniform block-index ranges.
-// kStepWaves waves per workgroup (A/B builds: SACENV_STEP_WAVES); with
-// SACENV_STEP_LDS the workgroup declares that many bytes of LDS so that at
-// most one workgroup fits a CU (one wave per SIMD). Measured: 2 waves 6.29 us,
-// 2 waves one-per-CU 6.04, 4 waves 6.09-6.12, against 5.33-5.35 for one.
-#ifndef SACENV_STEP_WAVES
-#define SACENV_STEP_WAVES 1
-#endif
-constexpr int kStepWaves = SACENV_STEP_WAVES;
-struct StepLds {
-  OwnerLds w[kStepWaves];
-#ifdef SACENV_STEP_LDS
-  char pad[SACENV_STEP_LDS - sizeof(OwnerLds) * kStepWaves];
-#endif
-};
+// uniform block-index ranges. One wave per workgroup (measured against 2 and
+// 4 waves, with or without LDS padding to one workgroup per CU: 6.04-6.29 us
+// against 5.33-5.35).
 template <bool kMixed, int kNc, bool kTIdx>
-__global__ void __launch_bounds__(kWave * kStepWaves) k_step(SacenvBoatParams p, Arena A, Tail T,
+__global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, Arena A, Tail T,
                                                 const float* __restrict__ action, int nb_boat,
                                                 MixedToys M, char* __restrict__ trans) {
-  __shared__ StepLds slds;
-  const int lane = threadIdx.x & (kWave - 1), wv = kStepWaves > 1 ? (int)(threadIdx.x >> 6) : 0;
-  int b = (int)blockIdx.x * kStepWaves + wv;
-#ifdef SACENV_STEP_LDS
-  if (threadIdx.x == 0xFFFF) slds.pad[lane] = 0;  // keeps the pad allocated
-#endif
+  __shared__ OwnerLds slds;
+  const int lane = threadIdx.x;
+  int b = (int)blockIdx.x;
   if (!kMixed || b < nb_boat) {
-    if (kStepWaves > 1 && b >= nb_boat) return;
-    owner_wave<false, kNc, kTIdx>(vreg_params(p), A, vreg_tail(T), action, slds.w[wv], b, lane, 1,
+    owner_wave<false, kNc, kTIdx>(vreg_params(p), A, vreg_tail(T), action, slds, b, lane, 1,
                                   nullptr, nullptr, trans);
     return;
   }
@@ -2066,9 +1970,8 @@ static int boat_step(const SacenvBoatParams* p, void* arena, const float* action
   if (rc) return rc;
   if (arena == nullptr || action == nullptr) return SACENV_E_NULL;
   const int nb_boat = (int)(pad64(p->n_envs) / kWave);
-  const int grid = (nb_boat + kStepWaves - 1) / kStepWaves;
 #define SACENV_LAUNCH(NC, TI)                                                                         \
-  hipLaunchKernelGGL((k_step<false, NC, TI>), dim3(grid), dim3(kWave * kStepWaves), 0, (hipStream_t)stream, *p, \
+  hipLaunchKernelGGL((k_step<false, NC, TI>), dim3(nb_boat), dim3(kWave), 0, (hipStream_t)stream, *p, \
                      make_arena(*p, arena), make_tail(*p, arena), action, nb_boat, MixedToys{}, trans)
   SACENV_OWNER_DISPATCH(*p, SACENV_LAUNCH)
 #undef SACENV_LAUNCH
@@ -2112,14 +2015,11 @@ int sacenv_boat_refill(const SacenvBoatParams* p, void* arena, void* stream) {
   if ((rc = launch_status())) return rc;
   hipLaunchKernelGGL(k_refill, dim3(p->n_helpers), dim3(kWave), 0, (hipStream_t)stream, *p, A);
   if ((rc = launch_status())) return rc;
-#ifndef SACENV_FIT_BLOCKS
-#define SACENV_FIT_BLOCKS 8192
-#endif
   // the fit's item count (episodes drawn x curves) is on the device: a grid
   // that covers a typical refill in one pass (8 groups per block: 65 536
   // (episode, curve) items), grid-stride beyond it; blocks past the count exit
   // at once. Measured 0.12 us/step better than one block per owner wave.
-  const int fit_blocks = SACENV_FIT_BLOCKS;
+  constexpr int fit_blocks = 8192;
   if (p->n_knots > 8)
     hipLaunchKernelGGL(k_refill_fit<16>, dim3(fit_blocks), dim3(kWave), 0, (hipStream_t)stream, *p, A,
                        make_tail(*p, arena));
@@ -2198,9 +2098,8 @@ static int mixed_step(const SacenvBoatParams* bp, void* boat_arena, const float*
     nb += nb_boat;
   }
   if (nb == 0) return SACENV_OK;
-  const int grid = (nb + kStepWaves - 1) / kStepWaves;
 #define SACENV_LAUNCH(NC, TI) \
-  hipLaunchKernelGGL((k_step<true, NC, TI>), dim3(grid), dim3(kWave * kStepWaves), 0, (hipStream_t)stream, p, A, T, boat_action, nb_boat, M, trans)
+  hipLaunchKernelGGL((k_step<true, NC, TI>), dim3(nb), dim3(kWave), 0, (hipStream_t)stream, p, A, T, boat_action, nb_boat, M, trans)
   SACENV_OWNER_DISPATCH(p, SACENV_LAUNCH)
 #undef SACENV_LAUNCH
   return launch_status();

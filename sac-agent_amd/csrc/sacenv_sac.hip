@@ -211,10 +211,7 @@ __device__ __forceinline__ void store_tile_t(const float* hl, float* __restrict_
 // [kH][kin] (kin <= 16, scalar loads); else [kH][kH] (float4 loads, issued
 // kPrefetch k-blocks ahead: one block is 16 MFMAs = ~0.25 us, an L2 round
 // trip ~1 us, and hipcc on its own pipelines one block ahead)
-#ifndef SACENV_SAC_PREFETCH
-#define SACENV_SAC_PREFETCH 8
-#endif
-constexpr int kPrefetch = SACENV_SAC_PREFETCH;
+constexpr int kPrefetch = 8;
 
 // the first kPrefetch k-blocks of a 256x256 layer's A fragments, issued early
 struct WPre {
@@ -739,13 +736,11 @@ __device__ void fc2_tile(const SacArgs& a, int t, int ob, int ib, int tid, float
 #pragma unroll
     for (int si = 0; si < 2; ++si) acc[so][si] = f4{0.f, 0.f, 0.f, 0.f};
   int r0 = rbeg;
-#ifndef SACENV_SAC_FC2_CHUNK
-#define SACENV_SAC_FC2_CHUNK 12
-#endif
   // chunks of 16 k-blocks hold 256 VGPRs of loads (one workgroup per CU); 12 + 4 stays
   // under 256 so the small-parameter workgroups can share the CUs
-  for (; r0 + 16 * SACENV_SAC_FC2_CHUNK <= rbeg + rq; r0 += 16 * SACENV_SAC_FC2_CHUNK)
-    fc2_chunk<SACENV_SAC_FC2_CHUNK>(na.dz2t, na.h1t, B, r0, o0, i0, lane, acc, cs);
+  constexpr int kChunk = 12;
+  for (; r0 + 16 * kChunk <= rbeg + rq; r0 += 16 * kChunk)
+    fc2_chunk<kChunk>(na.dz2t, na.h1t, B, r0, o0, i0, lane, acc, cs);
   for (; r0 < rbeg + rq; r0 += 64) fc2_chunk<4>(na.dz2t, na.h1t, B, r0, o0, i0, lane, acc, cs);  // rq % 64 == 0
   STAMP(a, 3, 1);
   // lane holds dW[o = 16 so + 4 kq + r][i = 16 si + (lane & 15)]
@@ -898,14 +893,8 @@ __device__ __forceinline__ void update_body(const SacArgs& a, float* sm, int b) 
     reduce_losses(a, tid, sm);
   } else if (b <= kSmallBlocks) {
     const int q = b - 1;
-#ifdef SACENV_SAC_DIAG_NO_SMALL  // timing diagnostics only
-    if (tid >= 0) return;
-#endif
     small_params(a, q / (kH / kSmallF), q % (kH / kSmallF), tid, sm);
   } else {
-#ifdef SACENV_SAC_DIAG_NO_FC2  // timing diagnostics only
-    if (tid >= 0) return;
-#endif
     // workgroups go to the 8 XCDs round-robin (b % 8): XCD x gets the 2x4 block of
     // 32x32 tiles (out rows 2(x>>1)..+1, in cols 4(x&1)..+3) of each net, so its L2
     // fetches 2 dz2 and 4 h1 row panels instead of 8 + 8

@@ -8,8 +8,11 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # .../sac-agent_amd
-LIB_PATH = os.environ.get("SACENV_LIB", os.path.join(PKG_ROOT, "build", "libsacenv.so"))
+from . import _build
+
+PKG_ROOT = _build.PKG_ROOT
+LIB_PATH = os.environ.get("SACENV_LIB", _build.LIB)
+LOADED_DIGEST = None  # source digest of the loaded library (the in-tree build)
 
 ABI_VERSION = 13
 OBS_DIM = 11
@@ -145,11 +148,22 @@ def load(path: str | None = None):
     global _LIB
     if _LIB is not None and path is None:
         return _LIB
+    global LOADED_DIGEST
     p = path or LIB_PATH
     if not os.path.exists(p):
         raise SacenvError(
             f"libsacenv.so not found at {p}: build it with `python __graft_entry__.py build` "
             "(hipcc --offload-arch=gfx950). The env has no CPU fallback.")
+    digest = None
+    if os.path.abspath(p) == os.path.abspath(_build.LIB):
+        # the in-tree library must be the one the sources in this tree compile to
+        digest = _build.source_digest()
+        stamp = p + ".sha256"
+        have = open(stamp).read().strip() if os.path.exists(stamp) else None
+        if have != digest:
+            raise SacenvError(
+                f"{p} was not built from the sources in this tree (stamp {have and have[:16]}, "
+                f"sources {digest[:16]}): rebuild with `python __graft_entry__.py build`")
     # torch first: it brings its own HIP runtime, and the library must bind to
     # that same one (loaded before torch, the library's HIP calls found no
     # device on the MI355X box)
@@ -197,6 +211,7 @@ def load(path: str | None = None):
         raise SacenvError(f"libsacenv ABI {v} != expected {ABI_VERSION}")
     if path is None:
         _LIB = lib
+        LOADED_DIGEST = digest
     return lib
 
 

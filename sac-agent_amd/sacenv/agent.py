@@ -216,5 +216,63 @@ class VecSAC:
     def state_dicts(self) -> dict:
         return {n: getattr(self, n).state_dict() for n in self.NETS}
 
+    def optimizer_state(self) -> dict:
+        return {n: o.state_dict() for n, o in zip(self.NETS[:4], (self.opt_actor, self.opt_c1,
+                                                                   self.opt_c2, self.opt_value))}
 
-__all__ = ["AgentConfig", "Actor", "Critic", "Value", "VecSAC"]
+    def load_optimizer_state(self, state: dict) -> None:
+        for n, o in zip(self.NETS[:4], (self.opt_actor, self.opt_c1, self.opt_c2, self.opt_value)):
+            o.load_state_dict(state[n])
+
+    def save_models(self, experiment_dir: str, optimizer: bool = False) -> None:
+        """ContinuousAgent.save_models (continuous_agent.py:79-84): see ``save_models``."""
+        save_models(self, experiment_dir, optimizer)
+
+    def load_models(self, experiment_dir: str, optimizer: bool = False) -> None:
+        """ContinuousAgent.load_models (continuous_agent.py:86-91): see ``load_models``."""
+        load_models(self, experiment_dir, optimizer)
+
+
+# checkpoint file of each net: the reference's network names (continuous_agent.py:19-52),
+# under <experiment_dir>/checkpoints/ (networks/base_network.py:10-11)
+CHECKPOINT_NAMES = {"actor": "actor_network", "critic_1": "critic_network_1",
+                    "critic_2": "critic_network_2", "value": "value_network",
+                    "target_value": "target_value_network"}
+OPTIMIZER_FILE = "sac_optimizer"  # not in the reference: the Adam states, for exact resumes
+
+
+def save_models(agent, experiment_dir: str, optimizer: bool = False) -> None:
+    """Each net's ``state_dict`` to ``<experiment_dir>/checkpoints/<name>`` with
+    ``torch.save``, as BaseNetwork.save_checkpoint (networks/base_network.py:13-14)
+    writes it: the reference's ``load_checkpoint`` reads these files unchanged.
+    Tensors are saved as CPU copies (a parameter that views a larger device buffer
+    would otherwise carry the whole buffer). ``optimizer`` also writes the Adam
+    states (``OPTIMIZER_FILE``; the reference keeps none), so a resumed agent
+    continues bit for bit."""
+    import os
+    d = os.path.join(experiment_dir, "checkpoints")
+    os.makedirs(d, exist_ok=True)
+    for n in agent.NETS:
+        sd = {k: v.detach().cpu().clone() for k, v in getattr(agent, n).state_dict().items()}
+        torch.save(sd, os.path.join(d, CHECKPOINT_NAMES[n]))
+    if optimizer:
+        torch.save(agent.optimizer_state(), os.path.join(d, OPTIMIZER_FILE))
+
+
+def load_models(agent, experiment_dir: str, optimizer: bool = False) -> None:
+    """BaseNetwork.load_checkpoint (networks/base_network.py:16-17) for every net;
+    ``weights_only`` loads (the files hold tensors only)."""
+    import os
+    d = os.path.join(experiment_dir, "checkpoints")
+    for n in agent.NETS:
+        sd = torch.load(os.path.join(d, CHECKPOINT_NAMES[n]), map_location="cpu", weights_only=True)
+        getattr(agent, n).load_state_dict(sd)
+    if optimizer:
+        agent.load_optimizer_state(torch.load(os.path.join(d, OPTIMIZER_FILE), map_location="cpu",
+                                              weights_only=True))
+    if hasattr(agent, "sync"):
+        agent.sync()
+
+
+__all__ = ["AgentConfig", "Actor", "Critic", "Value", "VecSAC", "save_models", "load_models",
+           "CHECKPOINT_NAMES"]

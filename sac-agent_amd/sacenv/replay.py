@@ -20,6 +20,7 @@ There is no CPU path: without libsacenv.so these classes raise.
 from __future__ import annotations
 
 import ctypes as C
+import weakref
 
 import numpy as np
 import torch
@@ -64,7 +65,9 @@ class DeviceReplayBuffer:
         self.mt_key = view(L.mt_key, torch.int32, _lib.MT_N)
         self.mt_pos = view(L.mt_pos, torch.int32, 1)
         self.mem_cntr = 0                        # host mirror (buffer.py:6)
-        self._last_term = {}                     # id(env) -> u8 [num_envs] info['termination'] codes
+        # env -> u8 [num_envs] info['termination'] codes; weak keys: an env that is
+        # garbage-collected takes its bytes with it (no id() reuse by a new env)
+        self._last_term = weakref.WeakKeyDictionary()
         _lib.check(self.lib.sacenv_replay_init(self._pp, self.arena.data_ptr(), int(seed) & 0xFFFFFFFF,
                                                self.stream))
 
@@ -118,10 +121,10 @@ class DeviceReplayBuffer:
         only on the step that reached the goal (the evident intent)."""
         last = None
         if reference_terminal:
-            last = self._last_term.get(id(env))
+            last = self._last_term.get(env)
             if last is None or last.numel() != env.num_envs:
                 last = torch.zeros(env.num_envs, dtype=torch.uint8, device=self.device)
-                self._last_term[id(env)] = last
+                self._last_term[env] = last
         self.store_batch(prev_obs, actions, env.reward, env.obs, env.term, final_state=env.final_obs,
                          last_term=last)
 

@@ -25,7 +25,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib
-from .agent import AgentConfig, VecSAC
+from .agent import AgentConfig, VecSAC, load_models, save_models
 
 # torch parameter names per net, in the C layout's tensor order (w1, b1, w2, b2, head 0, head 1)
 _TENSORS = {
@@ -125,6 +125,9 @@ class NativeSAC:
         tau = self.cfg.tau if tau is None else tau
         for tp, p in zip(self.target_value.parameters(), self.value.parameters()):
             tp.copy_(tau * p.clone() + (1 - tau) * tp.clone())
+        # the target's fc2.weight has a kernel copy in fragment order (role_critic_loss
+        # reads it): refresh it, or the next learn() would use the stale target
+        self.sync()
 
     def _f32(self, x, n=None):
         t = torch.as_tensor(x, device=self.device).to(torch.float32).contiguous()
@@ -166,15 +169,41 @@ class NativeSAC:
             e1, e2 = torch.randn(B, device=self.device), torch.randn(B, device=self.device)
         else:
             e1, e2 = self._f32(noise[0], B), self._f32(noise[1], B)
-        self.adam_step += 1
+        step = self.adam_step + 1  # committed only once the call is accepted
         _lib.check(_lib.load().sacenv_sac_learn(
             C.byref(self.params), self.weights.data_ptr(), self.scratch.data_ptr(), state.data_ptr(),
             action.data_ptr(), reward.data_ptr(), state_.data_ptr(), done.data_ptr(), e1.data_ptr(),
-            e2.data_ptr(), self.adam_step, self.losses.data_ptr(), self._stream()))
-        return tuple(self.losses[i] for i in range(4))
+            e2.data_ptr(), step, self.losses.data_ptr(), self._stream()))
+        self.adam_step = step
+        # independent tensors (as VecSAC.learn returns): the next learn() rewrites self.losses
+        return tuple(self.losses.clone().unbind(0))
 
     def state_dicts(self) -> dict:
         return {n: getattr(self, n).state_dict() for n in self.NETS}
+
+    def optimizer_state(self) -> dict:
+        """The Adam moments of the four optimised nets and the step count (CPU copies)."""
+        out = {"step": torch.tensor(self.adam_step, dtype=torch.int64)}
+        for n in self.NETS[:4]:
+            for which, views in self.adam_state(n).items():
+                out.update({f"{n}.{which}.{k}": v.detach().cpu().clone() for k, v in views.items()})
+        return out
+
+    def load_optimizer_state(self, state: dict) -> None:
+        for n in self.NETS[:4]:
+            for which, views in self.adam_state(n).items():
+                for k, v in views.items():
+                    v.copy_(state[f"{n}.{which}.{k}"].reshape(v.shape))
+        self.adam_step = int(state["step"])
+
+    def save_models(self, experiment_dir: str, optimizer: bool = False) -> None:
+        """ContinuousAgent.save_models (continuous_agent.py:79-84), the reference's files."""
+        save_models(self, experiment_dir, optimizer)
+
+    def load_models(self, experiment_dir: str, optimizer: bool = False) -> None:
+        """ContinuousAgent.load_models (continuous_agent.py:86-91): the parameters are views
+        of the weights buffer, so load_state_dict writes it in place; then sync()."""
+        load_models(self, experiment_dir, optimizer)
 
 
 __all__ = ["NativeSAC"]

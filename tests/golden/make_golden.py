@@ -335,8 +335,8 @@ def run_sac_learn(n_calls=2, batch=1024, seed=0):
             new_state=rng.uniform(0, 1, (batch, 11)),
             done=rng.random(batch) < 0.1))
     Normal = torch.distributions.Normal
-    orig = (Normal.sample, Normal.rsample, F.mse_loss)
-    eps_log, mse_log = [], []
+    orig = (Normal.sample, Normal.rsample, F.mse_loss, torch.Tensor.backward)
+    eps_log, mse_log, bwd_log = [], [], []
     gen = torch.Generator().manual_seed(seed + 99)
 
     def sample(self, sample_shape=torch.Size()):
@@ -355,7 +355,12 @@ def run_sac_learn(n_calls=2, batch=1024, seed=0):
         mse_log.append(float(out))
         return out
 
+    def backward(self, *args, **kw):  # the loss each backward() starts from
+        bwd_log.append(float(self.detach()))
+        return orig[3](self, *args, **kw)
+
     Normal.sample, Normal.rsample, F.mse_loss = sample, rsample, mse
+    torch.Tensor.backward = backward
     try:
         for b in batches:
             agent.memory.mem_cntr = agent.batch_size
@@ -363,9 +368,11 @@ def run_sac_learn(n_calls=2, batch=1024, seed=0):
                                                            b["new_state"], b["done"]))
             agent.learn()
     finally:
-        Normal.sample, Normal.rsample, F.mse_loss = orig
+        Normal.sample, Normal.rsample, F.mse_loss = orig[:3]
+        torch.Tensor.backward = orig[3]
+    # per call: value_loss, actor_loss, critic_loss (continuous_agent.py:123,138,150)
     out = {"n_calls": n_calls, "seed": seed, "eps": np.asarray(eps_log, np.float32),
-           "mse": np.asarray(mse_log, np.float64)}
+           "mse": np.asarray(mse_log, np.float64), "backward_losses": np.asarray(bwd_log, np.float64)}
     for i, b in enumerate(batches):
         for k, v in b.items():
             out[f"b{i}_{k}"] = v

@@ -33,6 +33,12 @@ def check(agent, losses, z, rtol_w, rtol_l, init=None):
     np.testing.assert_allclose(losses[:, 0], 0.5 * mse[:, 0], rtol=rtol_l)
     np.testing.assert_allclose(losses[:, 2], 0.5 * mse[:, 1], rtol=rtol_l)
     np.testing.assert_allclose(losses[:, 3], 0.5 * mse[:, 2], rtol=rtol_l)
+    # the losses the reference's three backward() calls start from (value, actor,
+    # critic_1 + critic_2; continuous_agent.py:123,138,150): the actor loss too
+    bwd = z["backward_losses"].reshape(-1, 3)
+    np.testing.assert_allclose(losses[:, 0], bwd[:, 0], rtol=rtol_l)
+    np.testing.assert_allclose(losses[:, 1], bwd[:, 1], rtol=rtol_l)
+    np.testing.assert_allclose(losses[:, 2] + losses[:, 3], bwd[:, 2], rtol=rtol_l)
     for name in NETS:
         for k, v in getattr(agent, name).state_dict().items():
             want = z[f"w_{name}.{k}"]
@@ -72,3 +78,45 @@ def test_vec_sac_learn_matches_reference_gpu(gpu, built_lib):
             for n, sd in VecSAC("cpu", init_seed=int(z["seed"]), with_memory=False).state_dicts().items()}
     agent, losses = run_learn(gpu, z)
     check(agent, losses, z, rtol_w=1e-2, rtol_l=1e-4, init=init)
+
+
+def _fixture_batches(z, device="cpu"):
+    eps = torch.from_numpy(z["eps"])
+    for i in range(int(z["n_calls"])):
+        b = tuple(torch.from_numpy(z[f"b{i}_{k}"]).to(device)
+                  for k in ("state", "action", "reward", "new_state", "done"))
+        yield b, (eps[2 * i].to(device), eps[2 * i + 1].to(device))
+
+
+def checkpoint_round_trip(make, device, tmp_path, optimizer):
+    """ContinuousAgent.save_models / load_models (continuous_agent.py:79-91,
+    networks/base_network.py:13-17): agent A learns, saves; a fresh agent B with
+    other initial weights loads; then both learn the same batch -> bit-identical
+    losses and weights. Without the optimizer file B's Adam starts fresh, so A is
+    saved before its first learn(); with it, after two."""
+    from sacenv.agent import CHECKPOINT_NAMES
+    z = golden("sac_learn.npz")
+    batches = list(_fixture_batches(z, device))
+    a, b = make(0), make(5)
+    if optimizer:
+        for bt, nz in batches:
+            a.learn(bt, noise=nz)
+    a.save_models(str(tmp_path), optimizer=optimizer)
+    # the reference's files: one plain state_dict per net, under its network name
+    for n, fname in CHECKPOINT_NAMES.items():
+        sd = torch.load(tmp_path / "checkpoints" / fname, weights_only=True)
+        assert list(sd) == list(getattr(a, n).state_dict()), n
+    b.load_models(str(tmp_path), optimizer=optimizer)
+    bt, nz = batches[1]
+    la, lb = a.learn(bt, noise=nz), b.learn(bt, noise=nz)
+    assert [float(x) for x in la] == [float(x) for x in lb]
+    for n in NETS:
+        for k, v in getattr(a, n).state_dict().items():
+            assert torch.equal(v, getattr(b, n).state_dict()[k]), (n, k)
+
+
+@pytest.mark.parametrize("optimizer", [False, True])
+def test_vec_sac_checkpoint_round_trip_cpu(tmp_path, optimizer):
+    from sacenv.agent import VecSAC
+    checkpoint_round_trip(lambda s: VecSAC("cpu", init_seed=s, with_memory=False), "cpu", tmp_path,
+                          optimizer)

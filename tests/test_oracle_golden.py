@@ -131,3 +131,42 @@ def test_oracle_main_loop_terminal_persistence():
     # on steps that are not goals
     assert (t == 1).sum() > 0 and ((t >= 2) & (t <= 5)).sum() > 0
     assert (z["terminal"] & (t != 1)).sum() > 0
+
+
+@pytest.mark.parametrize("name", seeded_fixtures())
+def test_scalar_oracle_matches_seeded_fixtures(name):
+    """oracle/boat_scalar.py (one env, Python floats + math: SURVEY §7.2's scalar N=1
+    mode, the C1 CPU baseline) against the reference's seeded runs, env by env."""
+    from boat_scalar import ScalarBoat
+    z = golden(name)
+    cfg = config_from_fixture(z)
+    E, S = z["reward"].shape
+    fields = [str(f) for f in z["state_fields"]]
+    for e in range(E):
+        b = ScalarBoat(cfg, int(z["seeds"][e]))
+        obs0 = b.reset()
+        assert b.start_y == int(z["init_start_y"][e])
+        np.testing.assert_allclose(obs0, z["init_obs"][e], rtol=0, atol=1e-15)
+        terms, states, obss, rews, eps, resets, sys_ = [], [], [], [], [], [], []
+        for k in range(S):
+            obs, rew, term = b.step(float(z["actions"][e, k]))
+            st = {"s_x": b.s_x, "s_y": b.s_y, "s_r": b.s_r, "v_x": b.v_x, "v_y": b.v_y, "v_r": b.v_r,
+                  "a_x": b.a_x, "a_y": b.a_y, "a_r": b.a_r, "rudder_angle": b.rudder, "t": b.t,
+                  "fuel": b.fuel, "index": b.index}
+            terms.append(term)
+            states.append([st[f] for f in fields])
+            obss.append(obs)
+            rews.append(rew)
+            if z["done"][e, k]:
+                eps.append((k, b.ep_reward))
+                resets.append((k, b.reset()))
+                sys_.append((k, b.start_y))
+        np.testing.assert_array_equal(terms, z["term"][e], err_msg=f"{name} env {e}")
+        np.testing.assert_allclose(states, z["state"][e], rtol=0, atol=STATE_TOL)
+        np.testing.assert_allclose(obss, z["obs"][e], rtol=0, atol=1e-12)
+        np.testing.assert_allclose(rews, z["reward"][e], rtol=0, atol=1e-10)
+        for (k, v), (_, ro), (_, sy) in zip(eps, resets, sys_):
+            assert abs(v - z["ep_reward"][e, k]) <= 1e-9
+            np.testing.assert_allclose(ro, z["reset_obs"][e, k], rtol=0, atol=1e-15)
+            assert sy == int(z["start_y"][e, k])
+        np.testing.assert_array_equal(b.counters, z["counters"][e])

@@ -172,3 +172,45 @@ def test_native_rejects_bad_shapes(gpu, built_lib):
     batch, noise = _batch(gpu, B=512)
     with pytest.raises(ValueError):
         nat.learn(batch, noise)
+
+
+@pytest.mark.parametrize("kind", ["native", "torch"])
+@pytest.mark.parametrize("optimizer", [False, True])
+def test_checkpoint_round_trip_gpu(gpu, built_lib, tmp_path, kind, optimizer):
+    """save_models -> load_models into a fresh agent -> learn() bit-identical to the
+    original continuing (test_agent_cpu.checkpoint_round_trip); NativeSAC's parameters
+    are views of its weights buffer, refreshed by load_models' sync()."""
+    from sacenv.agent import VecSAC
+    from sacenv.sac_native import NativeSAC
+    from test_agent_cpu import checkpoint_round_trip
+    cls = NativeSAC if kind == "native" else VecSAC
+    checkpoint_round_trip(lambda s: cls(gpu, init_seed=s, with_memory=False), gpu, tmp_path, optimizer)
+
+
+def test_native_update_network_parameters_refreshes_kernel_copy(gpu, built_lib):
+    """A hard target update (tau = 1, as the reference constructor does) after the value
+    net changed: the next learn() must see the new target fc2 weights, whose kernel copy
+    in fragment order only sync() refreshes."""
+    ref, nat = _pair(gpu, seed=6)
+    for agent in (ref, nat):
+        with torch.no_grad():
+            agent.value.fc2.weight.mul_(2.0)
+            agent.value.fc2.bias.add_(0.5)
+        if agent is nat:
+            nat.sync()
+        agent.update_network_parameters(tau=1.0)
+    batch, noise = _batch(gpu, seed=12)
+    lr, ln = ref.learn(batch, noise), nat.learn(batch, noise)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose([float(x) for x in ln], [float(x) for x in lr], rtol=1e-4)
+
+
+def test_native_learn_returns_independent_losses(gpu, built_lib):
+    _, nat = _pair(gpu, seed=8)
+    b1, n1 = _batch(gpu, seed=20)
+    b2, n2 = _batch(gpu, seed=21)
+    l1 = nat.learn(b1, n1)
+    keep = [float(x) for x in l1]
+    l2 = nat.learn(b2, n2)
+    torch.cuda.synchronize()
+    assert [float(x) for x in l1] == keep and [float(x) for x in l2] != keep

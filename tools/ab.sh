@@ -1,8 +1,8 @@
 #!/bin/bash
 # A/B timing on one GPU box: the bench line of this tree ("base") against
-# full trees under ab/<name>/ (other revisions, each with its own built
-# library) and against variant libraries sac-agent_amd/build/libsacenv_<v>.so
-# of this tree. Rounds alternate, so drift hits every arm alike.
+# full trees under ab/<name>/ (other revisions, e.g. `git worktree add ab/x`,
+# each with its own built library). Rounds alternate, so drift hits every arm
+# alike. The product sources carry no A/B switches: a variant is a revision.
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -12,9 +12,7 @@ for round in 1 2; do
     if [ -d "ab/$v" ]; then
       (cd "ab/$v" && timeout -k 10 120 python bench.py $ARGS) > gpurun_out/ab_$v.json 2>gpurun_out/ab_$v.log || exit 1
     else
-      if [ "$v" != "base" ]; then export SACENV_LIB=$PWD/sac-agent_amd/build/libsacenv_$v.so; else unset SACENV_LIB; fi
       timeout -k 10 120 python bench.py $ARGS > gpurun_out/ab_$v.json 2>gpurun_out/ab_$v.log || exit 1
-      unset SACENV_LIB
     fi
     python -c "import json;d=json.load(open('gpurun_out/ab_$v.json'));print('r$round $v', round(d['value']/1e9,3), 'G/s', round(d['ms_per_step']*1e3,3), 'us/step kernel', round(d['roofline']['kernel_avg_us'],3))"
   done

@@ -32,8 +32,6 @@ for f in ("driver", "default", "c2", "c2_rollout", "c5", "rollout_k128", "131k")
           f"frac {r['frac']:.3f} cpu {c and round(c['value'])}")
 PY
 timeout -k 10 300 python tools/stamps.py --rebuild > gpurun_out/stamps_full.txt 2>&1 || exit 1
-STAMP_DEFINES=-DSACENV_STAMPS_LIGHT STAMP_LIB=libsacenv_stampsl.so timeout -k 10 300 python tools/stamps.py --rebuild \
-  > gpurun_out/stamps_light.txt 2>&1 || exit 1
 bash tools/pmc.sh > gpurun_out/pmc.log 2>&1 || { tail -20 gpurun_out/pmc.log; exit 1; }
 python -c "import json;d=json.load(open('gpurun_out/pmc_k_step.json'));print('pmc', d['trace_avg_ns'], d['hbm_bytes_per_launch'])"
 echo final_check done

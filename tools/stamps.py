@@ -53,8 +53,7 @@ def main():
     print(f"N={N} owner waves={nw} test_mode={tm}")
     print(f"owner span (first owner start -> last owner end) us: median {np.median(owner_end):.2f} "
           f"p90 {np.percentile(owner_end, 90):.2f}")
-    light = "LIGHT" in os.environ.get("STAMP_DEFINES", "")
-    for a, b, nm in (() if light else ((0, 2, "state+wind loads"), (2, 3, "compute"), (3, 1, "stores/end"))):
+    for a, b, nm in ((0, 2, "state+wind loads"), (2, 3, "compute"), (3, 1, "stores/end")):
         d = (r[..., b] - r[..., a]) / 100.0
         print(f"    owner {nm:16s} us median {np.median(d):6.2f} p90 {np.percentile(d, 90):6.2f}")
     skew = (r[..., 0] - t0[:, None]) / 100.0
