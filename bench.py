@@ -47,6 +47,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "sac-agent_amd"))
 
 BYTES_PER_ENV_STEP = 222      # state r+w 152, action 4, wind 16, obs 44, reward 4, done+term 2
+SEG_MIN_BYTES = 70 + 152 / 128  # the same with the state in registers for a 128-step persistent launch
 TOY_BYTES = {"parachute": 86, "car": 102}
 HBM_PEAK = 8.0e12             # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 EPISODE_STEPS = 500
@@ -74,7 +75,11 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=512)
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--experiment", type=int, default=6)
-    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="eager per-step launches (--launch step)")
+    ap.add_argument("--launch", choices=("segment", "step"), default="segment",
+                    help="segment: one persistent sacenv_boat_segment launch per 128 steps (state in "
+                         "registers, actions behind per-wave flags); step: one k_step launch per step, "
+                         "128 of them per hipGraph replay")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="total CPU-baseline budget (4 C1 legs + the vectorised port)")
@@ -242,12 +247,13 @@ def _vectorised_port(n_envs: int, seconds: float, experiment: int) -> dict:
             "sample": f"oracle/boat_oracle.py vectorised over {n} envs x {steps} steps ({el:.1f} s), 1 thread"}
 
 
-def load_traffic(n_envs: int, experiment: int):
-    """Per-launch HBM bytes of k_step from the committed rocprofv3 PMC summary
-    (tools/pmc.sh -> profiles/<round>_pmc_k_step.json, newest round first) for
-    this workload shape, or None."""
+def load_traffic(n_envs: int, experiment: int, launch: str = "step"):
+    """Per-step HBM bytes of the timed kernel from the committed rocprofv3 PMC summary
+    (tools/pmc.sh -> profiles/<round>_pmc_k_step.json or _pmc_segment.json, newest
+    round first) for this workload shape, or None."""
     import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_k_step.json")), reverse=True):
+    pat = "*pmc_segment.json" if launch == "segment" else "*pmc_k_step.json"
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", pat)), reverse=True):
         try:
             d = json.load(open(path))
         except Exception:  # noqa: BLE001
@@ -267,10 +273,12 @@ class Workload:
     ``envs`` the env objects."""
 
     def __init__(self, envs, stepper, refill, actions, pooled_step, row_bytes, per_gpu_envs,
-                 bytes_per_launch):
+                 bytes_per_launch, segment_step=None):
         self.envs, self.stepper, self.refill, self.actions = envs, stepper, refill, actions
         self.pooled_step, self._row_bytes = pooled_step, int(row_bytes)
         self.per_gpu_envs, self.bytes_per_launch = per_gpu_envs, bytes_per_launch
+        # segment_step(k0, n, trans=None): steps k0 .. k0+n-1 in one persistent launch
+        self.segment_step = segment_step
 
     def row_bytes(self) -> int:
         return self._row_bytes
@@ -319,8 +327,20 @@ def make_workload(args, rank: int, dev) -> Workload:
         else:
             env.step_pooled_async(a, row[: lay.nbytes])
 
+    # the persistent launch's action hand-off: every row of the table is published
+    # (the open-loop case of sacenv_boat_segment's per-wave flags; each wave still
+    # reads its flag every step)
+    ready = torch.full((env.n_pad // 64,), 0x7FFFFFFF, dtype=torch.int32, device=dev)
+
+    def segment_step(k0: int, n: int, trans=None):
+        r0 = k0 % ACTION_STEPS
+        assert r0 + n <= ACTION_STEPS
+        env.segment_async(actions[r0:], n, act_ready=ready, trans=trans,
+                          trans_stride=0 if trans is None else row_bytes)
+
     bytes_launch = BYTES_PER_ENV_STEP * N + (sum(TOY_BYTES.values()) * N if args.mixed else 0)
-    return Workload(envs, stepper, refill, actions, pooled_step, row_bytes, N * len(envs), bytes_launch)
+    return Workload(envs, stepper, refill, actions, pooled_step, row_bytes, N * len(envs), bytes_launch,
+                    None if args.mixed else segment_step)
 
 
 # ---------------------------------------------------------------- segments
@@ -344,15 +364,37 @@ class SegmentRunner:
             raise ValueError(f"--pool-every must divide {SEG}")
         self.args, self.wl, self.dev, self.pool = args, wl, dev, pool
         self.pool_every = int(pool_every)
-        self.use_graph = dev.type == "cuda" and not args.no_graph and (pool is None or pool_every == SEG)
+        # launch mode: "segment" (one persistent launch per segment, or per P steps
+        # when pooling every P), "graph" (SEG k_step launches per hipGraph replay),
+        # "eager" (SEG k_step launches)
+        # (the mixed batch has no persistent launch: it steps per launch)
+        want_seg = (getattr(args, "launch", "step") == "segment" and not args.no_graph
+                    and wl.segment_step is not None)
+        self.mode = ("segment" if want_seg and dev.type == "cuda" else
+                     "graph" if dev.type == "cuda" and not args.no_graph and (pool is None or pool_every == SEG)
+                     else "eager")
+        self.use_graph = self.mode == "graph"
         self.st = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
         self.graphs = None
         self.first_replays = 0
         self.seg_events: list = []
 
     def _steps(self, k0: int, with_pool: bool, buf=None, on_step=None) -> None:
-        """The SEG step launches of one segment, enqueued (captured or eager)."""
+        """The SEG steps of one segment, enqueued (captured, eager or persistent)."""
         wl, p = self.wl, self.pool if with_pool else None
+        if self.mode == "segment":
+            if p is None:
+                wl.segment_step(k0, SEG)
+                return
+            P = self.pool_every
+            for j0 in range(0, SEG, P):  # one launch per all-gather group
+                if P < SEG:
+                    p.begin()
+                wl.segment_step(k0 + j0, P, trans=p.stage[p.buf if buf is None else buf][: P * p.rb])
+                if P < SEG:
+                    p.fill = P
+                    p.flush()
+            return
         for j, k in enumerate(range(k0, k0 + SEG)):
             if p is None:
                 wl.stepper(wl.actions[k % ACTION_STEPS])
@@ -391,6 +433,15 @@ class SegmentRunner:
         wl, dev = self.wl, self.dev
         if dev.type != "cuda":
             return
+        if self.mode == "segment":  # the same steps as the graph and eager modes
+            wl.segment_step(0, 3)
+            wl.refill()
+            for base in range(0, ACTION_STEPS, SEG):
+                wl.segment_step(base, SEG)
+                wl.refill()
+                self.first_replays += SEG
+            _sync(dev)
+            return
         if self.use_graph:
             s = torch.cuda.Stream(device=dev)
             s.wait_stream(self.st)
@@ -426,6 +477,10 @@ class SegmentRunner:
         p = self.pool if with_pool else None
         if p is not None and self.pool_every == SEG:
             p.begin()
+        if p is not None and self.mode == "segment" and self.pool_every == SEG:
+            buf = p.buf
+        else:
+            buf = None
         if timed:
             ea, eb = _Clock(self.dev), _Clock(self.dev)
             ea.record(self.st)
@@ -433,7 +488,7 @@ class SegmentRunner:
             gset = self.graphs[(k0 % ACTION_STEPS) // SEG]
             gset[p.buf if p is not None else 0].replay()
         else:
-            self._steps(k0, p is not None, on_step=on_step)
+            self._steps(k0, p is not None, buf=buf, on_step=on_step)
         if timed:
             eb.record(self.st)
             self.seg_events.append((ea, eb))
@@ -496,21 +551,23 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
     # around 128-launch graph segments (refills excluded). N=1: the segments of
     # the timed region itself. N>1 (the segments also stage the pooled rows) or
     # eager: k_step-only segments replayed after the timed region.
-    if pool is not None or not use_graph:
-        if dev.type == "cuda" and not args.no_graph:
+    what = ("persistent sacenv_boat_segment launches" if run.mode == "segment" else
+            f"graph-replayed {SEG}-launch k_step segments")
+    if pool is not None or run.mode == "eager":
+        if run.mode == "eager" and dev.type == "cuda" and not args.no_graph:
             run.capture_all(with_pool=False)
-            use_graph = True
+            run.mode, use_graph = "graph", True
+            what = f"graph-replayed {SEG}-launch k_step segments"
         seg_events.clear()
         k = segment(k, False, with_pool=False)
         for _ in range(segs(args.kernel_launches)):
             k = segment(k, True, with_pool=False)
         _sync(dev)
-        kern_src = (f"events around {len(seg_events)} {'graph-replayed' if use_graph else 'eager'} "
-                    f"{SEG}-launch k_step segments after the timed region (no staging copy, no "
-                    "collective; refills between segments excluded)")
+        kern_src = (f"events around {len(seg_events)} {what if dev.type == 'cuda' else 'eager'} after the "
+                    "timed region (no staging copy, no collective; refills between segments excluded)")
     else:
-        kern_src = (f"HIP events around the {len(seg_events)} graph-replayed {SEG}-launch k_step "
-                    "segments of the timed region (refills between segments excluded)")
+        kern_src = (f"HIP events around the {len(seg_events)} {what} of the timed region (refills "
+                    "between segments excluded)")
     kern_s = sum(a.ms_to(b) for a, b in seg_events) * 1e-3 / (SEG * len(seg_events))
     step_s = ev0.ms_to(ev1) * 1e-3 / steps
 
@@ -518,7 +575,9 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
     if rank != 0:
         return None
     achieved = wl.bytes_per_launch / kern_s
-    traffic = None if args.mixed else load_traffic(wl.envs[0].num_envs, args.experiment)
+    seg_mode = run.mode == "segment"
+    traffic = None if args.mixed else load_traffic(wl.envs[0].num_envs, args.experiment,
+                                                   "segment" if seg_mode else "step")
     backend = None
     if world > 1:
         import torch.distributed as dist
@@ -534,8 +593,8 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
         "requested": {"steps": args.steps, "warmup": args.warmup,
                       "rule": f"rounded up to whole {SEG}-step segments (each ends with its refill)"},
         "setup": {"graph_first_replays": run.first_replays,
-                  "note": "step launches of each captured graph's first replay (its device upload), "
-                          "run before the warm-up, untimed"},
+                  "note": "steps of the first pass over the action table (a captured graph's first "
+                          "replay carries its device upload), run before the warm-up, untimed"},
         "ms_per_step": el_max / steps * 1e3,
         "higher_is_better": True,
         "scaling": "weak",
@@ -557,24 +616,39 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
                                   + (", overlapped with the next segment" if pool_every == SEG else ""))
                    if pool is not None else (
                        "none: sharded per-GPU replay (--pooling none)" if world > 1 else None),
-                   "launch": (f"hipGraph segments of {SEG} k_step launches" +
-                              (" (sacenv_boat_step_pooled: the step writes its pooled row)"
-                               if pool is not None and not args.mixed else
-                               " (+ the pooled-row copies per step)" if pool is not None else "") +
-                              " + the 3 refill launches" if use_graph else "eager"),
+                   "launch": (f"one persistent sacenv_boat_segment launch per {SEG} steps (k_rollout: the "
+                              "carried state in registers; each owner wave reads its action-row flag "
+                              "every step, all rows published) + the 3 refill launches"
+                              + (f"; one launch per {pool_every} steps when pooling" if pool is not None
+                                 and pool_every < SEG else "")
+                              if seg_mode else
+                              (f"hipGraph segments of {SEG} k_step launches" +
+                               (" (sacenv_boat_step_pooled: the step writes its pooled row)"
+                                if pool is not None and not args.mixed else
+                                " (+ the pooled-row copies per step)" if pool is not None else "") +
+                               " + the 3 refill launches" if use_graph else "eager")),
                    "refill": (f"k_need_masks + k_refill + k_refill_fit after every {SEG}-step segment, "
                               "inside the timed region") if not args.no_autoreset else None},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK,
                      "traffic": None if traffic is None else traffic["hbm_bytes_per_launch"],
-                     "kernel": "k_step<true> (mixed)" if args.mixed else "k_step",
+                     "kernel": ("k_rollout (sacenv_boat_segment, 128 steps per launch; per step below)"
+                                if seg_mode else "k_step<true> (mixed)" if args.mixed else "k_step"),
                      "bytes_per_launch": wl.bytes_per_launch,
                      "bytes_per_env_step": (dict(boat=BYTES_PER_ENV_STEP, **TOY_BYTES)
                                             if args.mixed else BYTES_PER_ENV_STEP),
                      "kernel_avg_us": kern_s * 1e6,
                      "step_us_incl_refill": step_s * 1e6,
                      "timing": kern_src,
-                     "traffic_source": None if traffic is None else traffic["source"]},
+                     "traffic_source": None if traffic is None else traffic["source"],
+                     # the persistent launch keeps the carried state (152 of the 222 B) in
+                     # registers between its steps: the bytes it must move per env-step
+                     "resident_state": None if not seg_mode else {
+                         "bytes_per_env_step": SEG_MIN_BYTES,
+                         "achieved_GBps": SEG_MIN_BYTES * N / kern_s / 1e9,
+                         "frac": SEG_MIN_BYTES * N / kern_s / HBM_PEAK,
+                         "note": "action 4 + wind sample 16 + obs 44 + reward 4 + done/term 2 per step, "
+                                 "state r+w 152 once per 128 steps; frac above is SURVEY §8(d)'s 222 B"}},
         "cpu_baseline": None,
         # N>1: what the pooled transitions cost -- every rank receives (world - 1) rows per step
         "dist": dinfo,

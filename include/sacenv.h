@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SACENV_ABI_VERSION 13
+#define SACENV_ABI_VERSION 14
 #define SACENV_OBS_DIM 11      /* Boat.return_state, boat_env.py:308-323 */
 #define SACENV_MT_N 624        /* MT19937 words per env (numpy legacy RNG) */
 #define SACENV_MAX_KNOTS 16    /* wind.fixed_points upper bound */
@@ -159,8 +159,10 @@ typedef struct SacenvBoatLayout {
 
 /* status bits (layout.status[1]); sticky until the arena is re-initialised */
 enum {
-  SACENV_STATUS_SLOT_UNDERFLOW = 1 /* an env restarted past its pre-drawn episodes: more than
-                                      SACENV_REFILL_PERIOD step launches without a refill */
+  SACENV_STATUS_SLOT_UNDERFLOW = 1, /* an env restarted past its pre-drawn episodes: more than
+                                       SACENV_REFILL_PERIOD step launches without a refill */
+  SACENV_STATUS_HANDOFF_TIMEOUT = 2  /* sacenv_boat_segment: an action row's flag never came
+                                        (~seconds); the launch stopped stepping */
 };
 
 int sacenv_abi_version(void);
@@ -247,6 +249,33 @@ int sacenv_boat_step_pooled(const SacenvBoatParams *p, void *arena, const float 
  * with a refill at most SACENV_REFILL_PERIOD launches before the last step). */
 int sacenv_boat_rollout(const SacenvBoatParams *p, void *arena, const float *actions, int32_t n_steps,
                         void *records, float *final_obs, void *stream);
+
+/* n_steps BoatEnv.step calls (boat_env.py:67-115) in ONE persistent launch,
+ * closed-loop safe: the step loop of main.py:70-91 with the env kept on the
+ * device between steps. Step ks reads its action row actions + ks *
+ * action_stride (device f32, n_envs values per row) and writes the arena's
+ * record and final_obs exactly as sacenv_boat_step does; results equal n_steps
+ * sacenv_boat_step calls bit for bit (the carried state stays in registers).
+ *   Action hand-off, per owner wave w (envs 64w .. 64w+63): when act_ready is
+ *   not NULL (device u32 [n_pad/64]), the wave steps ks only once act_ready[w]
+ *   >= seq0 + ks + 1 -- a producer (a policy on another stream) writes the
+ *   wave's 64 actions of row ks, then releases that value; every row already
+ *   published (e.g. act_ready[w] = 0x7fffffff) is the open-loop case.
+ *   act_ready == NULL: every row is ready. When step_done is not NULL (device
+ *   u32 [n_pad/64]), the wave stores step_done[w] = seq0 + ks + 1 once step
+ *   ks's record is visible device-wide (release); the record is rewritten by
+ *   step ks+1, which cannot start before row ks+1 is published, so a consumer
+ *   that reads step ks's record before publishing row ks+1 sees it intact.
+ *   Flags are read device-coherently (sc0 sc1); sequence numbers stay below
+ *   2^31. A flag that never comes (~seconds of polling) sets
+ *   SACENV_STATUS_HANDOFF_TIMEOUT and ends the launch.
+ * trans (nullable, 16-B aligned, trans_stride a multiple of 16): step ks's
+ * pooled transition row (sacenv_boat_step_pooled's format) at trans + ks *
+ * trans_stride. Counts as n_steps step launches for the refill contract
+ * (autoreset: n_steps <= SACENV_REFILL_PERIOD). */
+int sacenv_boat_segment(const SacenvBoatParams *p, void *arena, const float *actions, int64_t action_stride,
+                        int32_t n_steps, const uint32_t *act_ready, uint32_t *step_done, uint32_t seq0,
+                        void *trans, int64_t trans_stride, void *stream);
 
 /* Autoreset mode: draw (RNG, Boat.__init__ boat_env.py:144-201 / Wind
  * wind.py:26-99) and spline-fit the replacement episodes of every env that
@@ -446,6 +475,16 @@ int sacenv_sac_sync(const SacenvSacParams *p, float *weights, void *stream);
  * reparameterize=False); log_prob [n] may be NULL. */
 int sacenv_sac_act(const SacenvSacParams *p, const float *weights, const float *obs, int32_t n,
                    const float *eps, float *action, float *log_prob, void *stream);
+/* sacenv_sac_act as the producer of a closed loop with sacenv_boat_segment
+ * (main.py:70-91: choose_action, then env.step, with no launch boundary on the
+ * env side): the 64 rows of workgroup b are owner wave b's envs; it reads its
+ * obs rows once obs_ready[b] >= obs_want (the segment's step_done flags) and,
+ * once its actions are visible device-wide, stores act_ready[b] = act_value
+ * (the segment's act_ready flags). Values below 2^31; a flag that never comes
+ * (~seconds) sets SACENV_STATUS_HANDOFF_TIMEOUT in *status (nullable). */
+int sacenv_sac_act_handoff(const SacenvSacParams *p, const float *weights, const float *obs, int32_t n,
+                           const float *eps, float *action, const uint32_t *obs_ready, uint32_t obs_want,
+                           uint32_t *act_ready, uint32_t act_value, int32_t *status, void *stream);
 /* one learn() on a sampled batch (state, new_state f32 [batch][obs_dim],
  * action f32 [batch], reward f64 [batch] as sample_buffer returns it, done u8
  * [batch]) with the policy draws of its sample() (eps1) and rsample() (eps2),

@@ -1332,10 +1332,57 @@ __device__ __forceinline__ void store_obs_block(const float* lds_rows, float* ds
   }
 }
 
+// Where a multi-step launch (kRoll: sacenv_boat_rollout, sacenv_boat_segment)
+// puts step ks's outputs, and how it receives step ks's action.
+struct RollArgs {
+  char* rec;              // the 50-B/env record of step ks at rec + ks * rec_stride
+  int64_t rec_stride;     // bytes; 0: every step into the same record (the arena's)
+  float* fin;             // terminal obs of restarting envs at fin + ks * fin_stride (or null)
+  int64_t fin_stride;     // floats
+  char* trans;            // pooled transition row of step ks at trans + ks * trans_stride (or null)
+  int64_t trans_stride;   // bytes
+  int64_t act_stride;     // floats between consecutive action rows
+  // Action hand-off (sacenv_boat_segment): owner wave w steps ks only once
+  // ready[w] >= seq0 + ks + 1, and publishes done[w] = seq0 + ks + 1 once step
+  // ks's outputs are visible device-wide. ready == null: every row is ready.
+  const uint32_t* ready;
+  uint32_t* done;
+  uint32_t seq0;
+  int32_t* status;        // SACENV_STATUS_HANDOFF_TIMEOUT on a hand-off that never came
+};
+
+// A hand-off flag, read device-coherently (sc0 sc1: past the XCD's
+// non-coherent L2) with a vector load; the value is uniform.
+__device__ __forceinline__ uint32_t flag_load(const uint32_t* f) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(f), 0, 4, 0x00020000);
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)__builtin_amdgcn_raw_buffer_load_b32(r, 0, 0, 17));
+}
+// an action value of an explicitly handed-off row: device-coherent like the flag
+__device__ __forceinline__ float act_load(const char* row, uint32_t off) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(row), 0, 0x7fffffff,
+                                                                     0x00020000);
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 17));
+}
+constexpr uint32_t kSpinLimit = 1u << 22;  // ~seconds of polling: then the launch gives up
+// Spin until the flag reaches `want` (sequence numbers stay below 2^31). Returns
+// the last value seen; on timeout flags the status and returns 0.
+__device__ uint32_t wait_flag(const uint32_t* f, uint32_t want, uint32_t seen, int32_t* status, int lane) {
+  for (uint32_t it = 0; seen < want; ++it) {
+    if (it >= kSpinLimit) {
+      if (lane == 0) atomicOr(status, SACENV_STATUS_HANDOFF_TIMEOUT);
+      return 0u;
+    }
+    __builtin_amdgcn_s_sleep(2);
+    seen = flag_load(f);
+  }
+  return seen;
+}
+
 // One owner wave: BoatEnv.step for 64 consecutive envs, one per lane.
-// kRoll: n_steps steps in one launch (sacenv_boat_rollout) with the state in
-// registers, step k's record to rec + k * 50 n_pad and its terminal obs to
-// fin + k * 11 n_pad; the state is loaded once and stored once.
+// kRoll: n_steps steps in one launch (sacenv_boat_rollout, sacenv_boat_segment)
+// with the state in registers, step ks's outputs where RollArgs says; the
+// state is loaded once and stored once.
 // kNc: spline curves of the wind (0: constants or the shared table; 1: exp
 // 4/5; 2: exp 6); kTIdx: t derived from the index (t_from_index). Both are
 // launch constants; as template arguments the step carries no code (and no
@@ -1344,8 +1391,8 @@ __device__ __forceinline__ void store_obs_block(const float* lds_rows, float* ds
 template <bool kRoll, int kNc, bool kTIdx>
 __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Arena& A, const Tail& Tin,
                                            const float* __restrict__ action, OwnerLds& l, int ob,
-                                           int lane, int n_steps = 1, char* roll_rec = nullptr,
-                                           float* roll_fin = nullptr, char* trans = nullptr) {
+                                           int lane, int n_steps = 1, const RollArgs* ra = nullptr,
+                                           char* trans1 = nullptr) {
 #ifdef SACENV_STAMPS
   const uint64_t st_real0 = __builtin_amdgcn_s_memrealtime();
   uint64_t st_loaded = 0, st_computed = 0;
@@ -1363,9 +1410,21 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   const uint32_t eo = (uint32_t)e * 8u, eo4 = (uint32_t)e * 4u;  // per-lane byte offsets
   const char* const wbase = A.wk_wave(ob * kWave);  // the wave's slot-ring block (uniform)
   const bool active = e < pin.n_envs;
-  // the (first) action, in flight with the state loads
+  // the (first) action, in flight with the state loads. A handed-off row
+  // (sacenv_boat_segment) is read only after its flag says it is ready.
   const char* const abase = reinterpret_cast<const char*>(action) + (active ? eo4 : 0u);
-  float act_cur = *reinterpret_cast<const float*>(abase);
+  const uint32_t* const rdy = kRoll ? (ra->ready != nullptr ? ra->ready + ob : nullptr) : nullptr;
+  const int64_t arow = kRoll ? ra->act_stride * 4 : 0;  // bytes between action rows
+  uint32_t seen = 0;        // the latest value of this wave's ready flag
+  bool failed = false;      // a hand-off timed out: the launch stops stepping
+  float act_cur;
+  if (rdy != nullptr) {
+    seen = wait_flag(rdy, ra->seq0 + 1u, flag_load(rdy), ra->status, lane);
+    failed = seen == 0u;
+    act_cur = act_load(abase, 0u);
+  } else {
+    act_cur = *reinterpret_cast<const float*>(abase);
+  }
   constexpr bool t_idx = kTIdx;
   constexpr int nc = kNc;  // spline curves of the wind
   // per-lane 8-B loads straight into registers, coalesced over the wave's
@@ -1419,10 +1478,24 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
       if (c < nc) y0c[c] = A.f64e(U_W0N + 8 * c, eo);
     if (p.experiment == 2) syc = A.i32e(U_SYN, eo4);
   }
-  for (int ks = 0; ks < (kRoll ? n_steps : 1); ++ks) {
+  for (int ks = 0; ks < (kRoll ? n_steps : 1) && !failed; ++ks) {
   const float act = act_cur;
-  if (kRoll && ks + 1 < n_steps)  // the next step's action, a step ahead
-    act_cur = *reinterpret_cast<const float*>(abase + (int64_t)(ks + 1) * p.n_envs * 4);
+  // the next step's action, a step ahead: open-loop rows at once; a handed-off
+  // row if its flag already said so, else after this step's outputs (below)
+  bool act_next = false;
+  uint32_t flag_now = 0u;
+  if (kRoll && ks + 1 < n_steps) {
+    if (rdy == nullptr) {
+      act_cur = *reinterpret_cast<const float*>(abase + (int64_t)(ks + 1) * arow);
+      act_next = true;
+    } else {
+      if (seen >= ra->seq0 + (uint32_t)ks + 2u) {
+        act_cur = act_load(abase, (uint32_t)((ks + 1) * arow));
+        act_next = true;
+      }
+      flag_now = flag_load(rdy);  // in flight during the step, read at its end
+    }
+  }
   const int wi = index > p.wind_len - 1 ? p.wind_len - 1 : index;
   double wv = 0.0, wa = 0.0;
   bool refresh = false;
@@ -1578,10 +1651,12 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   const bool ended = term != SACENV_TERM_NONE;
 
   OWNER_STAMP(st_computed);
-  // this step's outputs: the arena's record, or the rollout's step-ks record
-  char* const R = kRoll ? roll_rec + (int64_t)ks * 50 * A.np : A.b + A.ur() * A.np;
-  float* const fin = kRoll ? (roll_fin != nullptr ? roll_fin + (int64_t)ks * A.np * SACENV_OBS_DIM : nullptr)
+  // this step's outputs: the arena's record, or the multi-step launch's
+  char* const R = kRoll ? ra->rec + (int64_t)ks * ra->rec_stride : A.b + A.ur() * A.np;
+  float* const fin = kRoll ? (ra->fin != nullptr ? ra->fin + (int64_t)ks * ra->fin_stride : nullptr)
                            : A.final_obs();
+  char* const trans = kRoll ? (ra->trans != nullptr ? ra->trans + (int64_t)ks * ra->trans_stride : nullptr)
+                            : trans1;
   if (p.out_flags & SACENV_OUT_REWARD64) A.at_e<double>(A.ur() + 126, eo) = reward;
   if (p.out_flags & SACENV_OUT_ACCEL) {
     A.at_e<double>(A.ur() + 102, eo) = a_x;
@@ -1676,7 +1751,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
-  if (!kRoll && trans != nullptr) {  // the pooled transition row (sacenv_boat_step_pooled)
+  if (trans != nullptr) {  // the pooled transition row (sacenv_boat_step_pooled)
     // s' entries 0..8 = the pre-reset obs (entries 9 and 10, rudder and fuel, follow
     // on the receivers from the actions and the episode starts), reward, action,
     // term (done = term != 0) and, in experiment 2, the new episode's obs[3]
@@ -1696,6 +1771,26 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
     st_out(*reinterpret_cast<uint8_t*>(trans + (kOff + 8) * A.np + e), term);
     if (pin.experiment == 2)
       st_out(*reinterpret_cast<float*>(trans + (kOff + 9) * A.np + eo4), restart ? fo.v[3] : 0.0f);
+    if (kRoll) {  // l.obs is rewritten by the next step
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+  }
+  if (kRoll && ra->done != nullptr) {
+    // step ks's outputs visible device-wide (release: L2 write-back + wait for
+    // the stores), then its done flag, write-through
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    if (lane == 0)
+      __hip_atomic_store(ra->done + ob, ra->seq0 + (uint32_t)ks + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (kRoll && rdy != nullptr && ks + 1 < n_steps) {
+    seen = flag_now > seen ? flag_now : seen;
+    if (!act_next) {  // closed loop: the next action comes after these outputs
+      seen = wait_flag(rdy, ra->seq0 + (uint32_t)ks + 2u, seen, ra->status, lane);
+      failed = seen == 0u;
+      act_cur = act_load(abase, (uint32_t)((ks + 1) * arow));
+    }
   }
   }  // steps
   if (kRoll) {  // the carried state, once
@@ -1742,8 +1837,8 @@ __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, Arena A, Tai
   const int lane = threadIdx.x;
   int b = (int)blockIdx.x;
   if (!kMixed || b < nb_boat) {
-    owner_wave<false, kNc, kTIdx>(vreg_params(p), A, vreg_tail(T), action, slds, b, lane, 1,
-                                  nullptr, nullptr, trans);
+    owner_wave<false, kNc, kTIdx>(vreg_params(p), A, vreg_tail(T), action, slds, b, lane, 1, nullptr,
+                                  trans);
     return;
   }
   b -= nb_boat;
@@ -1756,15 +1851,15 @@ __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, Arena A, Tai
 
 
 
-// n_steps BoatEnv.step launches fused: open-loop actions
-// [n_steps][n_envs], state in registers between the steps
+// n_steps BoatEnv.step launches fused, the state in registers between the
+// steps: open-loop rollouts (records per step) and the segment
+// launch (the arena's record every step, actions behind per-wave flags)
 template <int kNc, bool kTIdx>
 __global__ void __launch_bounds__(kWave) k_rollout(SacenvBoatParams p, Arena A, Tail T,
-                                                   const float* __restrict__ action, int n_steps,
-                                                   char* __restrict__ rec, float* __restrict__ fin) {
+                                                   const float* __restrict__ action, int n_steps, RollArgs ra) {
   __shared__ OwnerLds slds;
   owner_wave<true, kNc, kTIdx>(vreg_params(p), A, vreg_tail(T), action, slds, blockIdx.x, threadIdx.x, n_steps,
-                               rec, fin);
+                               &ra);
 }
 
 __global__ void __launch_bounds__(kWave) k_toy_init(SacenvToyParams p, ToyArena T, const int32_t* __restrict__ ids,
@@ -1989,20 +2084,71 @@ int sacenv_boat_step_pooled(const SacenvBoatParams* p, void* arena, const float*
   return boat_step(p, arena, action, static_cast<char*>(trans), stream);
 }
 
+// k_rollout for the launch's wind kind and t rule
+static int launch_multi(const SacenvBoatParams& p, void* arena, const float* actions, int n_steps, const RollArgs& ra,
+                        void* stream) {
+  const int nb_boat = (int)(pad64(p.n_envs) / kWave);
+#define SACENV_LAUNCH(NC, TI)                                                                              \
+  hipLaunchKernelGGL((k_rollout<NC, TI>), dim3(nb_boat), dim3(kWave), 0, (hipStream_t)stream, p,           \
+                     make_arena(p, arena), make_tail(p, arena), actions, n_steps, ra)
+  SACENV_OWNER_DISPATCH(p, SACENV_LAUNCH)
+#undef SACENV_LAUNCH
+  return launch_status();
+}
+
+// byte offsets of the record and the status words in the arena
+static int64_t A_ur_bytes(const SacenvBoatParams& p) {
+  SacenvBoatLayout L;
+  compute_layout(p.n_envs, p.n_knots, p.wind_len, p.use_wind_table, &L);
+  return L.record;
+}
+static int64_t status_offset(const SacenvBoatParams& p) {
+  SacenvBoatLayout L;
+  compute_layout(p.n_envs, p.n_knots, p.wind_len, p.use_wind_table, &L);
+  return L.status;
+}
+
 int sacenv_boat_rollout(const SacenvBoatParams* p, void* arena, const float* actions, int32_t n_steps,
                         void* records, float* final_obs, void* stream) {
   int rc = check_params(p);
   if (rc) return rc;
   if (arena == nullptr || actions == nullptr || records == nullptr) return SACENV_E_NULL;
   if (n_steps < 1 || (p->autoreset && n_steps > SACENV_REFILL_PERIOD)) return SACENV_E_SIZE;
-  const int nb_boat = (int)(pad64(p->n_envs) / kWave);
-#define SACENV_LAUNCH(NC, TI)                                                                            \
-  hipLaunchKernelGGL((k_rollout<NC, TI>), dim3(nb_boat), dim3(kWave), 0, (hipStream_t)stream, *p,        \
-                     make_arena(*p, arena), make_tail(*p, arena), actions, n_steps, static_cast<char*>(records), \
-                     final_obs)
-  SACENV_OWNER_DISPATCH(*p, SACENV_LAUNCH)
-#undef SACENV_LAUNCH
-  return launch_status();
+  const int64_t np = pad64(p->n_envs);
+  RollArgs ra{};
+  ra.rec = static_cast<char*>(records);
+  ra.rec_stride = 50 * np;
+  ra.fin = final_obs;
+  ra.fin_stride = np * SACENV_OBS_DIM;
+  ra.act_stride = p->n_envs;
+  return launch_multi(*p, arena, actions, n_steps, ra, stream);
+}
+
+int sacenv_boat_segment(const SacenvBoatParams* p, void* arena, const float* actions, int64_t action_stride,
+                        int32_t n_steps, const uint32_t* act_ready, uint32_t* step_done, uint32_t seq0,
+                        void* trans, int64_t trans_stride, void* stream) {
+  int rc = check_params(p);
+  if (rc) return rc;
+  if (arena == nullptr || actions == nullptr) return SACENV_E_NULL;
+  if (n_steps < 1 || (p->autoreset && n_steps > SACENV_REFILL_PERIOD)) return SACENV_E_SIZE;
+  if (action_stride < p->n_envs || (act_ready != nullptr && seq0 + (uint32_t)n_steps >= 0x80000000u))
+    return SACENV_E_RANGE;
+  if (trans != nullptr && ((reinterpret_cast<uintptr_t>(trans) & 15u) != 0u || (trans_stride & 15) != 0))
+    return SACENV_E_RANGE;  // float4 row stores
+  const Arena A = make_arena(*p, arena);
+  RollArgs ra{};
+  ra.rec = static_cast<char*>(arena) + A_ur_bytes(*p);
+  ra.rec_stride = 0;
+  ra.fin = reinterpret_cast<float*>(static_cast<char*>(arena) + A_ur_bytes(*p) + 50 * A.np);
+  ra.fin_stride = 0;
+  ra.trans = static_cast<char*>(trans);
+  ra.trans_stride = trans_stride;
+  ra.act_stride = action_stride;
+  ra.ready = act_ready;
+  ra.done = step_done;
+  ra.seq0 = seq0;
+  ra.status = reinterpret_cast<int32_t*>(static_cast<char*>(arena) + status_offset(*p)) + 1;
+  return launch_multi(*p, arena, actions, n_steps, ra, stream);
 }
 
 int sacenv_boat_refill(const SacenvBoatParams* p, void* arena, void* stream) {

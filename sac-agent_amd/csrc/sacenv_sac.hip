@@ -937,12 +937,45 @@ struct ActLds {
   float head[4][kActRows][2];
 };
 
+// Closed-loop hand-off with sacenv_boat_segment (sacenv.h): workgroup b's 64
+// rows are owner wave b's envs. It reads its obs rows only once
+// obs_ready[b] >= obs_want (the env wave published the step), and publishes
+// act_ready[b] = act_value once its actions are visible device-wide.
+struct ActHandoff {
+  const uint32_t* obs_ready;  // null: no hand-off
+  uint32_t obs_want;
+  uint32_t* act_ready;
+  uint32_t act_value;
+  int32_t* status;            // SACENV_STATUS_HANDOFF_TIMEOUT bit (nullable)
+};
+
+__device__ __forceinline__ uint32_t flag_load(const uint32_t* f) {  // device-coherent (sc0 sc1)
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(f), 0, 4, 0x00020000);
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)__builtin_amdgcn_raw_buffer_load_b32(r, 0, 0, 17));
+}
+
 __global__ void __launch_bounds__(kThreads) k_sac_act(SacArgs a, const float* __restrict__ obs, int n,
                                                         const float* __restrict__ eps, float* __restrict__ out,
-                                                        float* __restrict__ logp) {
+                                                        float* __restrict__ logp, ActHandoff h) {
   __shared__ ActLds l;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, i = lane & 15, kq = lane >> 4;
   const int row0 = blockIdx.x * kActRows;
+  if (h.obs_ready != nullptr) {
+    if (tid < 64) {  // one wave polls (bounded: ~seconds), the workgroup waits at the barrier
+      const uint32_t* f = h.obs_ready + blockIdx.x;
+      uint32_t it = 0;
+      while (flag_load(f) < h.obs_want) {
+        if (++it >= (1u << 22)) {
+          if (tid == 0 && h.status != nullptr) atomicOr(h.status, SACENV_STATUS_HANDOFF_TIMEOUT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // no stale L2 lines of the obs rows
+  }
   const int nrows = n - row0 < kActRows ? n - row0 : kActRows;
   const float* Pn = a.P + a.net[0];
   const NetOff& o = a.off[kActorShape];
@@ -1045,6 +1078,12 @@ __global__ void __launch_bounds__(kThreads) k_sac_act(SacArgs a, const float* __
     out[row0 + j] = act;
     if (logp != nullptr) logp[row0 + j] = lp;
   }
+  if (h.act_ready != nullptr) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the actions, device-wide
+    __syncthreads();
+    if (tid == 0)
+      __hip_atomic_store(h.act_ready + blockIdx.x, h.act_value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // ---------------------------------------------------------------- host side
@@ -1139,8 +1178,8 @@ extern "C" int sacenv_sac_sync(const SacenvSacParams* p, float* weights, void* s
   return (int)hipGetLastError();
 }
 
-extern "C" int sacenv_sac_act(const SacenvSacParams* p, const float* weights, const float* obs, int32_t n,
-                              const float* eps, float* action, float* log_prob, void* stream) {
+static int sac_act(const SacenvSacParams* p, const float* weights, const float* obs, int32_t n, const float* eps,
+                   float* action, float* log_prob, const ActHandoff& h, void* stream) {
   if (p == nullptr) return SACENV_E_NULL;
   if (p->hidden != kH || p->n_actions != 1 || p->obs_dim < 1 || p->obs_dim > 14) return SACENV_E_SIZE;
   if (n < 0) return SACENV_E_SIZE;
@@ -1152,8 +1191,23 @@ extern "C" int sacenv_sac_act(const SacenvSacParams* p, const float* weights, co
   const SacArgs a = make_args(&q, const_cast<float*>(weights));
   const int blocks = (n + kActRows - 1) / kActRows;
   hipLaunchKernelGGL(k_sac_act, dim3(blocks), dim3(kThreads), 0, (hipStream_t)stream, a, obs, (int)n, eps, action,
-                     log_prob);
+                     log_prob, h);
   return (int)hipGetLastError();
+}
+
+extern "C" int sacenv_sac_act(const SacenvSacParams* p, const float* weights, const float* obs, int32_t n,
+                              const float* eps, float* action, float* log_prob, void* stream) {
+  return sac_act(p, weights, obs, n, eps, action, log_prob, ActHandoff{}, stream);
+}
+
+extern "C" int sacenv_sac_act_handoff(const SacenvSacParams* p, const float* weights, const float* obs,
+                                      int32_t n, const float* eps, float* action, const uint32_t* obs_ready,
+                                      uint32_t obs_want, uint32_t* act_ready, uint32_t act_value,
+                                      int32_t* status, void* stream) {
+  if (obs_ready == nullptr || act_ready == nullptr) return SACENV_E_NULL;
+  if (obs_want >= 0x80000000u || act_value >= 0x80000000u) return SACENV_E_RANGE;
+  return sac_act(p, weights, obs, n, eps, action, nullptr, ActHandoff{obs_ready, obs_want, act_ready, act_value, status},
+                 stream);
 }
 
 extern "C" int sacenv_sac_learn(const SacenvSacParams* p, float* weights, void* scratch, const float* state,

@@ -149,6 +149,24 @@ class NativeSAC:
         return out
 
     @torch.no_grad()
+    def choose_action_handoff(self, obs, eps, out, *, obs_ready, obs_want: int, act_ready, act_value: int,
+                              status=None) -> None:
+        """``choose_action`` as the producer of a closed loop with ``VecBoatEnv.segment_async``
+        (``sacenv_sac_act_handoff``): the 64 rows of block b (owner wave b's envs) are read once
+        ``obs_ready[b] >= obs_want`` and ``act_ready[b] = act_value`` is published once their
+        actions in ``out`` (f32 [N], device) are visible. Enqueued on the current stream."""
+        n = obs.shape[0]
+        if obs.dtype != torch.float32 or not obs.is_contiguous() or obs.shape[1] != self.params.obs_dim:
+            raise ValueError(f"obs must be a contiguous float32 [N, {self.params.obs_dim}] tensor")
+        for name, t, cnt in (("eps", eps, n), ("out", out, n)):
+            if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != cnt or t.device != self.device:
+                raise ValueError(f"{name} must be a contiguous float32 device tensor of {cnt} values")
+        _lib.check(_lib.load().sacenv_sac_act_handoff(
+            C.byref(self.params), self.weights.data_ptr(), obs.data_ptr(), n, eps.data_ptr(), out.data_ptr(),
+            obs_ready.data_ptr(), int(obs_want), act_ready.data_ptr(), int(act_value),
+            None if status is None else status.data_ptr(), self._stream()))
+
+    @torch.no_grad()
     def learn(self, batch=None, noise=None):
         """continuous_agent.py:96-154 as VecSAC.learn; returns the four losses (device scalars)."""
         B, D = self.cfg.batch_size, self.params.obs_dim

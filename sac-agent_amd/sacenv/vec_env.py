@@ -285,6 +285,48 @@ class VecBoatEnv:
             self._since_refill += K
         return records, final_obs
 
+    def segment_async(self, actions: torch.Tensor, n_steps: int | None = None, *, act_ready=None,
+                      step_done=None, seq0: int = 0, trans=None, trans_stride: int = 0) -> None:
+        """``n_steps`` BoatEnv.step calls in ONE persistent launch (``sacenv_boat_segment``):
+        the same results as ``n_steps`` ``step_async`` calls, bit for bit, with the
+        carried state in registers between the steps and each step's outputs in the
+        env's record / final_obs (as ``step``). ``actions`` is a [K >= n_steps, N] f32
+        device tensor whose rows may be strided (e.g. rows of a larger table).
+
+        Closed-loop hand-off per owner wave (64 envs): with ``act_ready`` (u32 device
+        [n_pad/64]) the wave steps ks only once ``act_ready[w] >= seq0 + ks + 1``;
+        with ``step_done`` it publishes ``seq0 + ks + 1`` there once step ks's outputs
+        are visible. ``trans`` (u8 device, 16-B aligned): step ks's pooled transition
+        row at ``trans[ks * trans_stride:]``."""
+        K = int(actions.shape[0]) if n_steps is None else int(n_steps)
+        if (not isinstance(actions, torch.Tensor) or actions.dtype != torch.float32
+                or actions.device != self.device or actions.dim() != 2
+                or actions.shape[1] != self.num_envs or actions.stride(1) != 1 or actions.shape[0] < K):
+            raise ValueError(f"actions must be a float32 [>= {K}, {self.num_envs}] device tensor with "
+                             "contiguous rows")
+        if self.autoreset and K > _lib.REFILL_PERIOD:
+            raise ValueError(f"a segment of more than {_lib.REFILL_PERIOD} steps in autoreset mode")
+        if self.autoreset and self.auto_refill and self._since_refill + K > _lib.REFILL_PERIOD:
+            self.refill()
+        nw = self.n_pad // 64
+        for name, f in (("act_ready", act_ready), ("step_done", step_done)):
+            if f is not None and (f.dtype not in (torch.int32, torch.uint32) or f.numel() < nw
+                                  or f.device != self.device or not f.is_contiguous()):
+                raise ValueError(f"{name} must be a contiguous 32-bit device tensor of n_pad/64 = {nw}")
+        if trans is not None:
+            nb = _lib.trans_bytes(self.params.experiment) * self.n_pad
+            if (trans.dtype != torch.uint8 or trans.device != self.device or not trans.is_contiguous()
+                    or trans.numel() < (K - 1) * int(trans_stride) + nb):
+                raise ValueError("trans must be a contiguous uint8 device tensor holding K rows")
+        _lib.check(self.lib.sacenv_boat_segment(
+            self._pp, self._ptr, actions.data_ptr(), int(actions.stride(0)), K,
+            None if act_ready is None else act_ready.data_ptr(),
+            None if step_done is None else step_done.data_ptr(), int(seq0) & 0xFFFFFFFF,
+            None if trans is None else trans.data_ptr(), int(trans_stride), self.stream))
+        self._keep_seg = (actions, act_ready, step_done, trans)
+        if self.autoreset:
+            self._since_refill += K
+
     def record_views(self, rec: torch.Tensor):
         """(obs [N, 11], reward [N], done [N], term [N]) views of one packed record."""
         NP, N = self.n_pad, self.num_envs

@@ -1,16 +1,18 @@
 """The bench's exact timed path under parity.
 
-``bench.py`` times graph-replayed 128-step segments of the BASELINE config
-(exp 6, 65 536 envs, 500-step episodes, in-kernel auto-reset, 8 192 refill
-helpers, ``auto_refill=False`` with the refill placed after every segment).
-This test builds that workload with bench's own ``make_workload`` and drives it
-with bench's own ``SegmentRunner`` -- ``prepare()`` (warm-up, capture, the
-first replay of every graph) and five timed-path segments -- next to an eager
-twin (``--no-graph``: the same runner issuing the same steps as separate
-launches), and checks:
+``bench.py`` times 128-step segments of the BASELINE config (exp 6, 65 536
+envs, 500-step episodes, in-kernel auto-reset, 8 192 refill helpers,
+``auto_refill=False`` with the refill placed after every segment), each one
+persistent ``sacenv_boat_segment`` launch (the default ``--launch segment``) or
+one hipGraph replay of 128 ``k_step`` launches (``--launch step``). This test
+builds that workload with bench's own ``make_workload`` and drives it with
+bench's own ``SegmentRunner`` -- ``prepare()`` (warm-up, capture, the first
+pass over the action table) and five timed-path segments -- in both modes,
+next to an eager twin (``--no-graph``: the same runner issuing the same steps
+as separate launches), and checks:
 
 (a) after ``prepare()`` and after every segment (each followed by its refill),
-    the two arenas -- carried state, slot rings, MT19937 states, counters, the
+    the three arenas -- carried state, slot rings, MT19937 states, counters, the
     last record and terminal obs -- are bit-identical;
 (b) every step of the eager twin against ``OracleVecBoat`` on a 256-env
     subsample: termination codes bit-exact, obs and terminal obs within
@@ -40,17 +42,19 @@ def _picked(t, pick_d):
     return t.index_select(0, pick_d).cpu().numpy()
 
 
-def test_bench_timed_path_graph_equals_eager_and_oracle(gpu, built_lib):
+def test_bench_timed_path_equals_eager_and_oracle(gpu, built_lib):
     import bench
-    args_g = bench.parse(["--no-cpu-baseline"])
+    args_s = bench.parse(["--no-cpu-baseline"])
+    args_g = bench.parse(["--no-cpu-baseline", "--launch", "step"])
     args_e = bench.parse(["--no-cpu-baseline", "--no-graph"])
-    assert (args_g.envs, args_g.experiment, args_g.episode_steps, args_g.helpers) == (65536, 6, 500, 8192)
-    wl_g, wl_e = bench.make_workload(args_g, 0, gpu), bench.make_workload(args_e, 0, gpu)
-    env_g, env_e = wl_g.envs[0], wl_e.envs[0]
+    assert args_s.launch == "segment"   # the default the driver times
+    assert (args_s.envs, args_s.experiment, args_s.episode_steps, args_s.helpers) == (65536, 6, 500, 8192)
+    wl_s, wl_g, wl_e = (bench.make_workload(a, 0, gpu) for a in (args_s, args_g, args_e))
+    env_s, env_g, env_e = wl_s.envs[0], wl_g.envs[0], wl_e.envs[0]
     assert not env_g.auto_refill and env_g.autoreset
     torch.cuda.synchronize()
-    assert torch.equal(wl_g.actions, wl_e.actions)
-    assert torch.equal(env_g.arena, env_e.arena)
+    assert torch.equal(wl_g.actions, wl_e.actions) and torch.equal(wl_s.actions, wl_e.actions)
+    assert torch.equal(env_g.arena, env_e.arena) and torch.equal(env_s.arena, env_e.arena)
 
     N = env_e.num_envs
     pick = np.sort(np.random.default_rng(7).choice(N, 256, replace=False))
@@ -85,30 +89,35 @@ def test_bench_timed_path_graph_equals_eager_and_oracle(gpu, built_lib):
         if seen["phase"] == "segments":
             seen["trunc_in_segments"] += n_tr
 
-    run_g, run_e = bench.SegmentRunner(args_g, wl_g, gpu), bench.SegmentRunner(args_e, wl_e, gpu)
-    assert run_g.use_graph and not run_e.use_graph
+    run_s, run_g, run_e = (bench.SegmentRunner(a, w, gpu) for a, w in
+                           ((args_s, wl_s), (args_g, wl_g), (args_e, wl_e)))
+    assert (run_s.mode, run_g.mode, run_e.mode) == ("segment", "graph", "eager")
+    run_s.prepare()
     run_g.prepare()
     run_e.prepare(on_step=on_step)
     torch.cuda.synchronize()
-    assert run_g.first_replays == run_e.first_replays == 512
-    assert torch.equal(env_g.arena, env_e.arena), "arenas differ after prepare()"
+    assert run_s.first_replays == run_g.first_replays == run_e.first_replays == 512
+    assert torch.equal(env_g.arena, env_e.arena), "graph arena differs after prepare()"
+    assert torch.equal(env_s.arena, env_e.arena), "segment arena differs after prepare()"
 
     seen["phase"] = "segments"
     refills0 = int(env_g.status[0].item())
     k = 0
     for s in range(N_SEGMENTS):
+        ks = run_s.segment(k)
         kg = run_g.segment(k)
         ke = run_e.segment(k, on_step=on_step)
-        assert kg == ke == k + bench.SEG
+        assert ks == kg == ke == k + bench.SEG
         k = kg
         torch.cuda.synchronize()
-        if not torch.equal(env_g.arena, env_e.arena):
-            diff = torch.nonzero(env_g.arena != env_e.arena)[:8, 0].tolist()
-            raise AssertionError(f"arenas differ after segment {s} at bytes {diff}")
-        for f in STATE:  # the graph-replayed env itself, at the segment boundary
-            assert np.abs(_picked(getattr(env_g, f), pick_d) - getattr(ora, f)).max() <= STATE_TOL, f
-    env_g.check_status()
-    env_e.check_status()
+        for name, env in (("graph", env_g), ("segment", env_s)):
+            if not torch.equal(env.arena, env_e.arena):
+                diff = torch.nonzero(env.arena != env_e.arena)[:8, 0].tolist()
+                raise AssertionError(f"{name} arena differs after segment {s} at bytes {diff}")
+            for f in STATE:  # the timed-path env itself, at the segment boundary
+                assert np.abs(_picked(getattr(env, f), pick_d) - getattr(ora, f)).max() <= STATE_TOL, f
+    for env in (env_s, env_g, env_e):
+        env.check_status()
     assert int(env_g.status[0].item()) - refills0 == N_SEGMENTS   # one refill per segment
     np.testing.assert_array_equal(_picked(env_g.counters.t().contiguous(), pick_d), ora.counters)
     assert seen["steps"] == 3 + 512 + N_SEGMENTS * bench.SEG

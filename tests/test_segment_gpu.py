@@ -1,0 +1,138 @@
+"""sacenv_boat_segment: n_steps BoatEnv.step calls in one persistent launch.
+
+Parity bar: bit-identical to the same number of ``sacenv_boat_step`` launches
+(records, terminal obs, the whole arena) -- the per-step kernel is pinned to
+the reference by tests/test_gpu_parity.py, so equality carries that parity
+over. Covered: open-loop rows, rows behind already-published flags (the
+bench's configuration), strided action rows, the pooled transition rows,
+every step-kernel instantiation (2/1/0 wind curves, t derived or carried),
+refills between segments; the closed loop with the SAC policy handing off per
+owner wave (``sacenv.closed_loop.ClosedLoop``) against the eager
+``choose_action`` + ``step`` loop (main.py:70-91); a hand-off that never comes.
+Reference: environment/boat_env.py:67-126.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair(gpu, exp, tmax, dt, N, **kw):
+    from sacenv import VecBoatEnv
+    cfg = {"base_settings": {"experiment": exp, "test_mode": 0, "t_max": tmax, "dt": dt},
+           "boat_env": {"track_width": 30}}
+    kw = dict(dict(seed=11, device=gpu, autoreset=True, max_episode_steps=23, n_helpers=64), **kw)
+    return VecBoatEnv(cfg, N, **kw), VecBoatEnv(cfg, N, **kw)
+
+
+@pytest.mark.parametrize("exp,tmax,dt", [(6, 2500.0, 0.25), (4, 20.0, 0.25), (2, 2500.0, 0.25),
+                                         (3, 2500.0, 0.25), (6, 20.0, 0.1)])
+@pytest.mark.parametrize("flags", ["none", "published"])
+def test_segment_equals_steps(exp, tmax, dt, flags, gpu, built_lib):
+    N = 777
+    a_env, b_env = _pair(gpu, exp, tmax, dt, N)
+    nw = a_env.n_pad // 64
+    g = torch.Generator(device=gpu)
+    g.manual_seed(exp)
+    table = torch.rand((300, N), generator=g, device=gpu) * 2 - 1
+    table[:, ::7] *= 12.0                      # some rudders break at once
+    ready = torch.full((nw,), 0x7FFFFFFF, dtype=torch.int32, device=gpu) if flags == "published" else None
+    done = torch.zeros(nw, dtype=torch.int32, device=gpu)
+    k = 0
+    for rep, K in enumerate((128, 40, 128, 1, 77)):   # crosses refills (period 128)
+        rows = table[k % 150: k % 150 + K]          # strided rows of a larger table
+        a_env.segment_async(rows, K, act_ready=ready, step_done=done, seq0=k)
+        for j in range(K):
+            b_env.step_async(rows[j].contiguous())
+        k += K
+        torch.cuda.synchronize()
+        assert torch.equal(a_env.arena, b_env.arena), (rep, K)
+        assert int(done.min()) == k and int(done.max()) == k
+    a_env.check_status()
+
+
+@pytest.mark.parametrize("exp", [2, 6])
+def test_segment_pooled_rows_equal_step_pooled(exp, gpu, built_lib):
+    from sacenv import _lib
+    N = 1000
+    a_env, b_env = _pair(gpu, exp, 2500.0, 0.25, N)
+    row = _lib.trans_bytes(exp) * a_env.n_pad
+    K = 50
+    acts = torch.rand((K, N), device=gpu) * 2 - 1
+    ta = torch.zeros(K * row, dtype=torch.uint8, device=gpu)
+    tb = torch.zeros(K * row, dtype=torch.uint8, device=gpu)
+    a_env.segment_async(acts, K, trans=ta, trans_stride=row)
+    for j in range(K):
+        b_env.step_pooled_async(acts[j].contiguous(), tb[j * row:(j + 1) * row])
+    torch.cuda.synchronize()
+    assert torch.equal(ta, tb)
+    assert torch.equal(a_env.arena, b_env.arena)
+
+
+def test_segment_at_bench_size_equals_steps(gpu, built_lib):
+    """65 536 envs, exp 6, 500-step episodes, the bench's refill helpers: two segments."""
+    from sacenv import VecBoatEnv
+    kw = dict(seed=0, device=gpu, max_episode_steps=500, auto_refill=False)
+    cfg = {"base_settings": {"experiment": 6, "test_mode": 0}}
+    a_env, b_env = VecBoatEnv(cfg, 65536, **kw), VecBoatEnv(cfg, 65536, **kw)
+    a_env.reset()
+    b_env.reset()
+    acts = torch.rand((256, 65536), device=gpu) * 2 - 1
+    ready = torch.full((1024,), 0x7FFFFFFF, dtype=torch.int32, device=gpu)
+    for s in range(2):
+        a_env.segment_async(acts[128 * s:], 128, act_ready=ready)
+        for j in range(128):
+            b_env.step_async(acts[128 * s + j])
+        a_env.refill()
+        b_env.refill()
+        torch.cuda.synchronize()
+        assert torch.equal(a_env.arena, b_env.arena), s
+
+
+@pytest.mark.parametrize("N,K,segs", [(8192, 128, 3), (777, 37, 4)])
+def test_closed_loop_equals_eager_loop(N, K, segs, gpu, built_lib):
+    """ClosedLoop (the env as segment launches, the SAC policy per step on a second
+    stream, handing off per owner wave) = the eager loop of main.py:70-91:
+    ``a = choose_action(obs, eps); env.step(a)``, bit for bit (arena and actions)."""
+    from sacenv import VecBoatEnv
+    from sacenv.closed_loop import ClosedLoop
+    from sacenv.sac_native import NativeSAC
+    cfg = {"base_settings": {"experiment": 6, "test_mode": 0}}
+    kw = dict(seed=5, device=gpu, max_episode_steps=60, n_helpers=256)
+    a_env, b_env = VecBoatEnv(cfg, N, **kw), VecBoatEnv(cfg, N, **kw)
+    a_env.reset()
+    b_env.reset()
+    agent = NativeSAC(gpu, init_seed=3, with_memory=False)
+    loop = ClosedLoop(a_env, agent, segment=K)
+    g = torch.Generator(device=gpu)
+    g.manual_seed(1)
+    eps = torch.randn((segs, K, N), generator=g, device=gpu)
+    acts_b = []
+    for s in range(segs):
+        loop.run(eps[s])
+        for k in range(K):
+            a = agent.choose_action(b_env.obs, eps=eps[s, k])
+            acts_b.append(a.reshape(-1))
+            b_env.step_async(a.reshape(-1).contiguous())
+        torch.cuda.synchronize()
+        assert torch.equal(loop.actions[:K], torch.stack(acts_b[-K:])), s
+        assert torch.equal(a_env.arena, b_env.arena), s
+    a_env.check_status()
+    assert int(a_env.status[1]) == 0
+    assert int(loop.step_done.min()) == segs * K and int(loop.act_ready.max()) == segs * K
+
+
+def test_segment_handoff_timeout_sets_status(gpu, built_lib):
+    """A row whose flag never comes: the launch gives up after ~seconds of polling,
+    flags SACENV_STATUS_HANDOFF_TIMEOUT and returns (no hang)."""
+    from sacenv import VecBoatEnv, _lib
+    env = VecBoatEnv({"base_settings": {"experiment": 1}}, 128, device=gpu, autoreset=False)
+    env.reset()
+    ready = torch.zeros(2, dtype=torch.int32, device=gpu)
+    ready[0] = 3                                     # wave 0: rows 0..2 published, wave 1: none
+    acts = torch.zeros((8, 128), device=gpu)
+    env.segment_async(acts, 8, act_ready=ready)
+    torch.cuda.synchronize()
+    assert int(env.status[1]) & _lib.STATUS_HANDOFF_TIMEOUT
+    assert int(env.index[0]) == 3 and int(env.index[64]) == 0
