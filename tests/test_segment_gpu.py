@@ -22,7 +22,9 @@ def _pair(gpu, exp, tmax, dt, N, **kw):
     from sacenv import VecBoatEnv
     cfg = {"base_settings": {"experiment": exp, "test_mode": 0, "t_max": tmax, "dt": dt},
            "boat_env": {"track_width": 30}}
-    kw = dict(dict(seed=11, device=gpu, autoreset=True, max_episode_steps=23, n_helpers=64), **kw)
+    # the refill is placed by the tests (after every segment), the same for both envs
+    kw = dict(dict(seed=11, device=gpu, autoreset=True, max_episode_steps=23, n_helpers=64,
+                   auto_refill=False), **kw)
     return VecBoatEnv(cfg, N, **kw), VecBoatEnv(cfg, N, **kw)
 
 
@@ -45,6 +47,8 @@ def test_segment_equals_steps(exp, tmax, dt, flags, gpu, built_lib):
         a_env.segment_async(rows, K, act_ready=ready, step_done=done, seq0=k)
         for j in range(K):
             b_env.step_async(rows[j].contiguous())
+        a_env.refill()
+        b_env.refill()
         k += K
         torch.cuda.synchronize()
         assert torch.equal(a_env.arena, b_env.arena), (rep, K)
@@ -99,7 +103,7 @@ def test_closed_loop_equals_eager_loop(N, K, segs, gpu, built_lib):
     from sacenv.closed_loop import ClosedLoop
     from sacenv.sac_native import NativeSAC
     cfg = {"base_settings": {"experiment": 6, "test_mode": 0}}
-    kw = dict(seed=5, device=gpu, max_episode_steps=60, n_helpers=256)
+    kw = dict(seed=5, device=gpu, max_episode_steps=60, n_helpers=256, auto_refill=False)
     a_env, b_env = VecBoatEnv(cfg, N, **kw), VecBoatEnv(cfg, N, **kw)
     a_env.reset()
     b_env.reset()
@@ -115,6 +119,8 @@ def test_closed_loop_equals_eager_loop(N, K, segs, gpu, built_lib):
             a = agent.choose_action(b_env.obs, eps=eps[s, k])
             acts_b.append(a.reshape(-1))
             b_env.step_async(a.reshape(-1).contiguous())
+        a_env.refill()
+        b_env.refill()
         torch.cuda.synchronize()
         assert torch.equal(loop.actions[:K], torch.stack(acts_b[-K:])), s
         assert torch.equal(a_env.arena, b_env.arena), s
