@@ -55,6 +55,10 @@ class ClosedLoop:
         if q0 + K >= 0x7FFFFFFF:
             raise OverflowError("sequence numbers exhausted: build a new ClosedLoop")
         ps = self.policy_stream
+        # the policy's first read (row q0: step_done >= q0 holds at once) must follow
+        # every earlier write of the obs on the env's stream (reset, the previous
+        # segment): the flags order the steps of a segment, the stream the rest
+        ps.wait_stream(torch.cuda.current_stream(env.device))
         with torch.cuda.stream(ps):
             for k in range(K):
                 self.agent.choose_action_handoff(
