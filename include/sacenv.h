@@ -414,6 +414,28 @@ int sacenv_replay_store_env(const SacenvReplayParams *p, void *arena, int64_t n,
 int sacenv_replay_sample(const SacenvReplayParams *p, void *arena, int32_t batch, int64_t stored,
                          int64_t *idx, float *state, float *action, double *reward,
                          float *new_state, uint8_t *terminal, void *stream);
+/* A replay buffer shared by W ranks without moving the transitions (the
+ * pooled buffer of main.py:81-88 / agent/buffer.py:3-35):
+ * every rank keeps a full-size ring but writes only its own rows. Per env
+ * step the pooled buffer appends `period` transitions in global env order;
+ * this rank's n of them start at `offset`. store_shard writes them at ring
+ * rows (mem_cntr + offset + i) % mem_size and advances mem_cntr by period
+ * (offset + n <= period, n <= mem_size). sample_shard draws the batch exactly
+ * as sacenv_replay_sample (every rank's sampling stream, seeded alike, draws
+ * the same indices) and gathers the rows THIS rank wrote -- row p holds the
+ * latest global sequence number s = p (mod mem_size), s < mem_cntr; it is this
+ * rank's iff s mod period lies in [offset, offset + n) -- with the other rows'
+ * bytes zero, so an integer SUM all-reduce of the gathered bits over the ranks
+ * is the pooled buffer's batch, bit for bit: B rows cross the links per
+ * learn() instead of every transition per step. */
+int sacenv_replay_store_shard(const SacenvReplayParams *p, void *arena, int64_t n, int64_t offset,
+                              int64_t period, const float *state, const float *action, const void *reward,
+                              const float *new_state, const float *final_state, const uint8_t *code,
+                              uint8_t *last_term, void *stream);
+int sacenv_replay_sample_shard(const SacenvReplayParams *p, void *arena, int32_t batch, int64_t stored,
+                               int64_t offset, int64_t n, int64_t period, int64_t *idx, float *state,
+                               float *action, double *reward, float *new_state, uint8_t *terminal,
+                               void *stream);
 
 /* ------------------------------------------------------------------------
  * SAC agent on the device: the batched

@@ -87,7 +87,7 @@ __global__ void __launch_bounds__(kWave) k_rb_init(RB r, uint32_t seed) {
 // advances in a second launch (k_rb_advance), after every workgroup has read
 // it: stream order instead of a grid-wide atomic (one word takes ~90
 // returning atomics/µs) or an agent-scope acq_rel fence per workgroup.
-__global__ void __launch_bounds__(256) k_rb_store(SacenvReplayParams p, RB r, int64_t n,
+__global__ void __launch_bounds__(256) k_rb_store(SacenvReplayParams p, RB r, int64_t n, int64_t offset,
                                                   const float* __restrict__ state,
                                                   const float* __restrict__ action,
                                                   const void* __restrict__ reward,
@@ -95,7 +95,7 @@ __global__ void __launch_bounds__(256) k_rb_store(SacenvReplayParams p, RB r, in
                                                   const float* __restrict__ final_state,
                                                   const uint8_t* __restrict__ code,
                                                   uint8_t* __restrict__ last_term) {
-  const int64_t M = p.mem_size, c0 = *r.cntr();
+  const int64_t M = p.mem_size, c0 = *r.cntr() + offset;
   const int64_t first = n > M ? n - M : 0;
   const uint32_t rows = (uint32_t)(n - first);
   const uint32_t base = (uint32_t)((c0 + first) % M);  // ring row of stored row 0
@@ -196,24 +196,41 @@ __global__ void __launch_bounds__(kWave) k_rb_draw(SacenvReplayParams p, RB r, i
   mt_finish(st, l, r.pos(), lane);
 }
 
+// Sharded rows (sacenv_replay_sample_shard): ring row p holds the transition
+// with the latest global sequence number s <= mem_cntr - 1, s = p (mod M); this
+// shard wrote it iff (s mod period) is in [lo, hi). Rows of other shards come
+// out as zero bits.
+struct Shard {
+  int64_t period, lo, hi;  // period 0: every row is this shard's
+};
+__device__ __forceinline__ bool owns(const Shard& sh, int64_t cnt, int64_t M, int64_t row) {
+  if (sh.period == 0) return true;
+  const int64_t s = row + M * ((cnt - 1 - row) / M);
+  const int64_t u = s % sh.period;
+  return u >= sh.lo && u < sh.hi;
+}
+
 __global__ void __launch_bounds__(256) k_rb_gather(SacenvReplayParams p, RB r, int batch,
                                                    const int64_t* __restrict__ idx, float* __restrict__ st,
                                                    float* __restrict__ ac, double* __restrict__ rw,
-                                                   float* __restrict__ ns, uint8_t* __restrict__ tm) {
+                                                   float* __restrict__ ns, uint8_t* __restrict__ tm, Shard sh) {
   const int D = p.obs_dim, A = p.act_dim;
   const int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int64_t nd = (int64_t)batch * D, na = (int64_t)batch * A;
+  const int64_t cnt = *r.cntr(), M = p.mem_size;
   if (q < nd) {
     const int64_t i = q / D, k = q - i * D, row = idx[i];
-    if (st) st[q] = r.state()[row * D + k];
-    if (ns) ns[q] = r.new_state()[row * D + k];
+    const bool own = owns(sh, cnt, M, row);
+    if (st) st[q] = own ? r.state()[row * D + k] : 0.f;
+    if (ns) ns[q] = own ? r.new_state()[row * D + k] : 0.f;
   } else if (q < nd + na) {
-    const int64_t qq = q - nd, i = qq / A, k = qq - i * A;
-    if (ac) ac[qq] = r.action()[idx[i] * A + k];
+    const int64_t qq = q - nd, i = qq / A, k = qq - i * A, row = idx[i];
+    if (ac) ac[qq] = owns(sh, cnt, M, row) ? r.action()[row * A + k] : 0.f;
   } else if (q < nd + na + batch) {
     const int64_t i = q - nd - na, row = idx[i];
-    if (rw) rw[i] = r.reward()[row];
-    if (tm) tm[i] = r.terminal()[row];
+    const bool own = owns(sh, cnt, M, row);
+    if (rw) rw[i] = own ? r.reward()[row] : 0.0;
+    if (tm) tm[i] = own ? r.terminal()[row] : (uint8_t)0;
   }
 }
 
@@ -256,14 +273,13 @@ int sacenv_replay_init(const SacenvReplayParams* p, void* arena, uint32_t seed, 
   return status();
 }
 
-int sacenv_replay_store_env(const SacenvReplayParams* p, void* arena, int64_t n, const float* state,
-                            const float* action, const void* reward, const float* new_state,
-                            const float* final_state, const uint8_t* code, uint8_t* last_term,
-                            void* stream) {
+static int store(const SacenvReplayParams* p, void* arena, int64_t n, int64_t offset, int64_t advance,
+                 const float* state, const float* action, const void* reward, const float* new_state,
+                 const float* final_state, const uint8_t* code, uint8_t* last_term, void* stream) {
   int rc = check_replay(p);
   if (rc) return rc;
   if (n < 0) return SACENV_E_SIZE;
-  if (n == 0) return SACENV_OK;
+  if (n == 0 && advance == n) return SACENV_OK;
   if (!arena || !state || !action || !reward || !new_state || !code) return SACENV_E_NULL;
   const int64_t rows = n > p->mem_size ? p->mem_size : n;
   const int64_t total = rows * ((int64_t)p->obs_dim + p->act_dim + 1) + (last_term ? n - rows : 0);
@@ -271,11 +287,28 @@ int sacenv_replay_store_env(const SacenvReplayParams* p, void* arena, int64_t n,
   int64_t blocks = (total + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   const RB r = make_rb(*p, arena);
-  hipLaunchKernelGGL(k_rb_store, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *p, r, n, state,
-                     action, reward, new_state, final_state, code, last_term);
-  if ((rc = status())) return rc;
-  hipLaunchKernelGGL(k_rb_advance, dim3(1), dim3(kWave), 0, (hipStream_t)stream, r, n);
+  if (n > 0) {
+    hipLaunchKernelGGL(k_rb_store, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *p, r, n, offset,
+                       state, action, reward, new_state, final_state, code, last_term);
+    if ((rc = status())) return rc;
+  }
+  hipLaunchKernelGGL(k_rb_advance, dim3(1), dim3(kWave), 0, (hipStream_t)stream, r, advance);
   return status();
+}
+
+int sacenv_replay_store_env(const SacenvReplayParams* p, void* arena, int64_t n, const float* state,
+                            const float* action, const void* reward, const float* new_state,
+                            const float* final_state, const uint8_t* code, uint8_t* last_term,
+                            void* stream) {
+  return store(p, arena, n, 0, n, state, action, reward, new_state, final_state, code, last_term, stream);
+}
+
+int sacenv_replay_store_shard(const SacenvReplayParams* p, void* arena, int64_t n, int64_t offset, int64_t period,
+                              const float* state, const float* action, const void* reward, const float* new_state,
+                              const float* final_state, const uint8_t* code, uint8_t* last_term, void* stream) {
+  if (p == nullptr) return SACENV_E_NULL;
+  if (offset < 0 || n < 0 || period <= 0 || offset + n > period || n > p->mem_size) return SACENV_E_RANGE;
+  return store(p, arena, n, offset, period, state, action, reward, new_state, final_state, code, last_term, stream);
 }
 
 int sacenv_replay_store(const SacenvReplayParams* p, void* arena, int64_t n, const float* state,
@@ -285,9 +318,9 @@ int sacenv_replay_store(const SacenvReplayParams* p, void* arena, int64_t n, con
                                  nullptr, stream);
 }
 
-int sacenv_replay_sample(const SacenvReplayParams* p, void* arena, int32_t batch, int64_t stored,
-                         int64_t* idx, float* state, float* action, double* reward, float* new_state,
-                         uint8_t* terminal, void* stream) {
+static int sample(const SacenvReplayParams* p, void* arena, int32_t batch, int64_t stored, int64_t* idx,
+                  float* state, float* action, double* reward, float* new_state, uint8_t* terminal,
+                  const Shard& sh, void* stream) {
   int rc = check_replay(p);
   if (rc) return rc;
   if (batch < 0) return SACENV_E_SIZE;
@@ -299,8 +332,23 @@ int sacenv_replay_sample(const SacenvReplayParams* p, void* arena, int32_t batch
   if ((rc = status())) return rc;
   const int64_t total = (int64_t)batch * (p->obs_dim + p->act_dim + 1);
   hipLaunchKernelGGL(k_rb_gather, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *p,
-                     r, batch, idx, state, action, reward, new_state, terminal);
+                     r, batch, idx, state, action, reward, new_state, terminal, sh);
   return status();
+}
+
+int sacenv_replay_sample(const SacenvReplayParams* p, void* arena, int32_t batch, int64_t stored,
+                         int64_t* idx, float* state, float* action, double* reward, float* new_state,
+                         uint8_t* terminal, void* stream) {
+  return sample(p, arena, batch, stored, idx, state, action, reward, new_state, terminal, Shard{0, 0, 0}, stream);
+}
+
+int sacenv_replay_sample_shard(const SacenvReplayParams* p, void* arena, int32_t batch, int64_t stored,
+                               int64_t offset, int64_t n, int64_t period, int64_t* idx, float* state,
+                               float* action, double* reward, float* new_state, uint8_t* terminal,
+                               void* stream) {
+  if (offset < 0 || n < 0 || period <= 0 || offset + n > period) return SACENV_E_RANGE;
+  return sample(p, arena, batch, stored, idx, state, action, reward, new_state, terminal,
+                Shard{period, offset, offset + n}, stream);
 }
 
 }  // extern "C"

@@ -133,7 +133,8 @@ EXPORTS = ("sacenv_abi_version", "sacenv_error_string", "sacenv_boat_layout",
            "sacenv_boat_init", "sacenv_boat_reset", "sacenv_boat_reset_explicit",
            "sacenv_boat_step", "sacenv_boat_step_pooled", "sacenv_boat_rollout", "sacenv_boat_segment", "sacenv_boat_refill", "sacenv_boat_wind_eval", "sacenv_toy_layout", "sacenv_toy_init",
            "sacenv_toy_reset", "sacenv_toy_step", "sacenv_mixed_step", "sacenv_mixed_step_pooled", "sacenv_replay_layout",
-           "sacenv_replay_init", "sacenv_replay_store", "sacenv_replay_store_env", "sacenv_replay_sample",
+           "sacenv_replay_init", "sacenv_replay_store", "sacenv_replay_store_env", "sacenv_replay_sample", "sacenv_replay_store_shard",
+           "sacenv_replay_sample_shard",
            "sacenv_compact_done", "sacenv_boat_reset_list", "sacenv_sac_layout", "sacenv_sac_sync",
            "sacenv_sac_act", "sacenv_sac_act_handoff", "sacenv_sac_learn")
 
@@ -199,6 +200,9 @@ def load(path: str | None = None):
         "sacenv_replay_store": (C.c_int, [RP, _p, _i64, _p, _p, _p, _p, _p, _p, _p]),
         "sacenv_replay_store_env": (C.c_int, [RP, _p, _i64, _p, _p, _p, _p, _p, _p, _p, _p]),
         "sacenv_replay_sample": (C.c_int, [RP, _p, _i32, _i64, _p, _p, _p, _p, _p, _p, _p]),
+        "sacenv_replay_store_shard": (C.c_int, [RP, _p, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p]),
+        "sacenv_replay_sample_shard": (C.c_int, [RP, _p, _i32, _i64, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p,
+                                                 _p]),
         "sacenv_sac_layout": (C.c_int, [C.POINTER(SacParams), C.POINTER(SacLayout)]),
         "sacenv_sac_sync": (C.c_int, [C.POINTER(SacParams), _p, _p]),
         "sacenv_sac_act": (C.c_int, [C.POINTER(SacParams), _p, _p, _i32, _p, _p, _p, _p]),

@@ -145,6 +145,75 @@ class DeviceReplayBuffer:
         return st, ac, rw, ns, tm.bool(), idx
 
 
+class ShardedReplayBuffer(DeviceReplayBuffer):
+    """The replay buffer pooled over ``world`` ranks (main.py:81-88 with every rank's
+    envs feeding one agent/buffer.py:3-35 ring) WITHOUT moving the
+    transitions: each rank writes only its own envs' rows, at the ring positions
+    the pooled buffer gives them (``sacenv_replay_store_shard``: per step the pooled
+    ring appends ``world * n`` rows in global env order, rank r's at offset r*n), and
+    ``sample`` draws the pooled buffer's indices on every rank (same seed, same
+    stream: ``np.random.choice(max_mem, batch)``) and assembles the batch with one
+    integer SUM all-reduce of the gathered bits (each row comes from the one rank
+    that wrote it, the others contribute zero bits): the batch equals the pooled
+    buffer's bit for bit, and B rows cross the links per ``learn()`` instead of
+    every transition of every step (tests/test_dist_cpu.py)."""
+
+    def __init__(self, max_size, input_shape, n_actions, *, rank: int, world: int, envs_per_rank: int,
+                 device=None, seed: int = 0, group=None, **kw):
+        super().__init__(max_size, input_shape, n_actions, device=device, seed=seed, **kw)
+        self.rank, self.world, self.n = int(rank), int(world), int(envs_per_rank)
+        self.period, self.offset = self.world * self.n, self.rank * self.n
+        if self.period > self.mem_size:
+            raise ValueError("one step's pooled rows must fit the ring (world * envs <= max_size)")
+        self.group = group
+
+    def store_batch(self, state, action, reward, new_state, code, final_state=None, last_term=None) -> None:
+        """This rank's n rows of one pooled step (rank-local inputs, as DeviceReplayBuffer)."""
+        s = self._dev(state, torch.float32)
+        n = s.shape[0]
+        if n != self.n:
+            raise ValueError(f"a step stores this rank's {self.n} rows")
+        a = self._dev(action, torch.float32).reshape(n, -1)
+        r = self._dev(reward, torch.float32 if self.params.reward_f32 else torch.float64).reshape(n)
+        ns = self._dev(new_state, torch.float32)
+        c = self._dev(code, torch.uint8).reshape(n)
+        fs = None if final_state is None else self._dev(final_state, torch.float32)
+        _lib.check(self.lib.sacenv_replay_store_shard(
+            self._pp, self.arena.data_ptr(), n, self.offset, self.period, s.data_ptr(), a.data_ptr(),
+            r.data_ptr(), ns.data_ptr(), None if fs is None else fs.data_ptr(), c.data_ptr(),
+            None if last_term is None else last_term.data_ptr(), self.stream))
+        self._keep = (s, a, r, ns, c, fs)
+        self.mem_cntr += self.period
+
+    def sample(self, batch_size: int):
+        """The pooled buffer's sample_buffer (buffer.py:24-35), identical on every rank."""
+        import torch.distributed as dist
+        B = int(batch_size)
+        if self.mem_cntr == 0 and B > 0:
+            raise ValueError("a must be greater than 0 unless no samples are taken")
+        D, A = int(np.prod(self.input_shape)), self.n_actions
+        # one buffer of 32-bit words: state, new_state, action (f32), reward (f64 = 2 words), terminal
+        words = torch.zeros(B * (2 * D + A + 3), dtype=torch.int32, device=self.device)
+        st = words[: B * D].view(torch.float32).view(B, *self.input_shape)
+        ns = words[B * D: 2 * B * D].view(torch.float32).view(B, *self.input_shape)
+        o = 2 * B * D
+        ac = words[o: o + B * A].view(torch.float32).view(B, A)
+        o += B * A
+        rw = words[o: o + 2 * B].view(torch.float64)
+        o += 2 * B
+        tm32 = words[o: o + B]
+        tm = torch.empty(B, dtype=torch.uint8, device=self.device)
+        idx = torch.empty(B, dtype=torch.int64, device=self.device)
+        _lib.check(self.lib.sacenv_replay_sample_shard(
+            self._pp, self.arena.data_ptr(), B, self.mem_cntr, self.offset, self.n, self.period,
+            idx.data_ptr(), st.data_ptr(), ac.data_ptr(), rw.data_ptr(), ns.data_ptr(), tm.data_ptr(),
+            self.stream))
+        tm32.copy_(tm.to(torch.int32))
+        if self.world > 1:
+            dist.all_reduce(words, op=dist.ReduceOp.SUM, group=self.group)
+        return st, ac, rw, ns, tm32.to(torch.bool), idx
+
+
 class ReplayBuffer:
     """Drop-in for agent.buffer.ReplayBuffer (buffer.py:3-35), GPU-backed, numpy I/O,
     sampling from numpy's global RNG stream like ``np.random.choice`` (buffer.py:27)."""
