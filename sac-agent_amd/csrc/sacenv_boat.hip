@@ -1412,7 +1412,10 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   const bool active = e < pin.n_envs;
   // the (first) action, in flight with the state loads. A handed-off row
   // (sacenv_boat_segment) is read only after its flag says it is ready.
-  const char* const abase = reinterpret_cast<const char*>(action) + (active ? eo4 : 0u);
+  // Padding lanes (e >= n_envs) read their wave's first env -- memory their own
+  // wave's hand-off flag covers -- and step with action 0, so padding state
+  // never depends on another wave's row.
+  const char* const abase = reinterpret_cast<const char*>(action) + (active ? eo4 : (uint32_t)ob * 256u);
   const uint32_t* const rdy = kRoll ? (ra->ready != nullptr ? ra->ready + ob : nullptr) : nullptr;
   const int64_t arow = kRoll ? ra->act_stride * 4 : 0;  // bytes between action rows
   uint32_t seen = 0;        // the latest value of this wave's ready flag
@@ -1479,7 +1482,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
     if (p.experiment == 2) syc = A.i32e(U_SYN, eo4);
   }
   for (int ks = 0; ks < (kRoll ? n_steps : 1) && !failed; ++ks) {
-  const float act = act_cur;
+  const float act = active ? act_cur : 0.0f;
   // the next step's action, a step ahead: open-loop rows at once; a handed-off
   // row if its flag already said so, else after this step's outputs (below)
   bool act_next = false;
