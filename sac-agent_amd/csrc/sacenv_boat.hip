@@ -1352,12 +1352,17 @@ struct RollArgs {
 };
 
 // A hand-off flag, read device-coherently (sc0 sc1: past the XCD's
-// non-coherent L2) with a vector load; the value is uniform.
-__device__ __forceinline__ uint32_t flag_load(const uint32_t* f) {
+// non-coherent L2) with a vector load. flag_issue returns the loaded VGPR
+// without waiting for it; flag_value makes it uniform (and waits).
+__device__ __forceinline__ uint32_t flag_issue(const uint32_t* f) {
   const __amdgpu_buffer_rsrc_t r =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(f), 0, 4, 0x00020000);
-  return (uint32_t)__builtin_amdgcn_readfirstlane((int)__builtin_amdgcn_raw_buffer_load_b32(r, 0, 0, 17));
+  return __builtin_amdgcn_raw_buffer_load_b32(r, 0, 0, 17);
 }
+__device__ __forceinline__ uint32_t flag_value(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+__device__ __forceinline__ uint32_t flag_load(const uint32_t* f) { return flag_value(flag_issue(f)); }
 // an action value of an explicitly handed-off row: device-coherent like the flag
 __device__ __forceinline__ float act_load(const char* row, uint32_t off) {
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(row), 0, 0x7fffffff,
@@ -1420,14 +1425,17 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   const int64_t arow = kRoll ? ra->act_stride * 4 : 0;  // bytes between action rows
   uint32_t seen = 0;        // the latest value of this wave's ready flag
   bool failed = false;      // a hand-off timed out: the launch stops stepping
-  float act_cur;
+  bool per_step = false;    // rows still to be published: flag checks step by step
   if (rdy != nullptr) {
     seen = wait_flag(rdy, ra->seq0 + 1u, flag_load(rdy), ra->status, lane);
     failed = seen == 0u;
-    act_cur = act_load(abase, 0u);
-  } else {
-    act_cur = *reinterpret_cast<const float*>(abase);
+    // the rows the flag covers were written before it (the producer's release):
+    // drop any stale copy of them from this XCD's L2 once, then read them plainly.
+    // Rows published only later are read device-coherently, step by step.
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    per_step = seen < ra->seq0 + (uint32_t)n_steps;
   }
+  float act_cur = *reinterpret_cast<const float*>(abase);
   constexpr bool t_idx = kTIdx;
   constexpr int nc = kNc;  // spline curves of the wind
   // per-lane 8-B loads straight into registers, coalesced over the wave's
@@ -1488,7 +1496,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   bool act_next = false;
   uint32_t flag_now = 0u;
   if (kRoll && ks + 1 < n_steps) {
-    if (rdy == nullptr) {
+    if (!per_step) {  // open loop, or every row of the launch already published
       act_cur = *reinterpret_cast<const float*>(abase + (int64_t)(ks + 1) * arow);
       act_next = true;
     } else {
@@ -1496,7 +1504,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
         act_cur = act_load(abase, (uint32_t)((ks + 1) * arow));
         act_next = true;
       }
-      flag_now = flag_load(rdy);  // in flight during the step, read at its end
+      flag_now = flag_issue(rdy);  // in flight during the step, read at its end
     }
   }
   const int wi = index > p.wind_len - 1 ? p.wind_len - 1 : index;
@@ -1787,8 +1795,9 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
     if (lane == 0)
       __hip_atomic_store(ra->done + ob, ra->seq0 + (uint32_t)ks + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (kRoll && rdy != nullptr && ks + 1 < n_steps) {
-    seen = flag_now > seen ? flag_now : seen;
+  if (kRoll && per_step && ks + 1 < n_steps) {
+    const uint32_t fv = flag_value(flag_now);
+    seen = fv > seen ? fv : seen;
     if (!act_next) {  // closed loop: the next action comes after these outputs
       seen = wait_flag(rdy, ra->seq0 + (uint32_t)ks + 2u, seen, ra->status, lane);
       failed = seen == 0u;
