@@ -1393,11 +1393,14 @@ __device__ uint32_t wait_flag(const uint32_t* f, uint32_t want, uint32_t seen, i
 // launch constants; as template arguments the step carries no code (and no
 // loads whose pending registers the waitcnt pass must respect) of the other
 // wind kinds.
-template <bool kRoll, int kNc, bool kTIdx>
+// kHand (kRoll only): rows published step by step and/or done flags (the
+// closed loop); without it the loop carries no flag code at all (the launch
+// checked that every row was already published).
+template <bool kRoll, int kNc, bool kTIdx, bool kHand = false>
 __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Arena& A, const Tail& Tin,
                                            const float* __restrict__ action, OwnerLds& l, int ob,
                                            int lane, int n_steps = 1, const RollArgs* ra = nullptr,
-                                           char* trans1 = nullptr) {
+                                           char* trans1 = nullptr, uint32_t seen0 = 0u) {
 #ifdef SACENV_STAMPS
   const uint64_t st_real0 = __builtin_amdgcn_s_memrealtime();
   uint64_t st_loaded = 0, st_computed = 0;
@@ -1421,20 +1424,12 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   // wave's hand-off flag covers -- and step with action 0, so padding state
   // never depends on another wave's row.
   const char* const abase = reinterpret_cast<const char*>(action) + (active ? eo4 : (uint32_t)ob * 256u);
-  const uint32_t* const rdy = kRoll ? (ra->ready != nullptr ? ra->ready + ob : nullptr) : nullptr;
+  const uint32_t* const rdy = kHand ? (ra->ready != nullptr ? ra->ready + ob : nullptr) : nullptr;
   const int64_t arow = kRoll ? ra->act_stride * 4 : 0;  // bytes between action rows
-  uint32_t seen = 0;        // the latest value of this wave's ready flag
+  // kHand: the latest value of this wave's ready flag (the launch waited for row 0)
+  uint32_t seen = seen0;
   bool failed = false;      // a hand-off timed out: the launch stops stepping
-  bool per_step = false;    // rows still to be published: flag checks step by step
-  if (rdy != nullptr) {
-    seen = wait_flag(rdy, ra->seq0 + 1u, flag_load(rdy), ra->status, lane);
-    failed = seen == 0u;
-    // the rows the flag covers were written before it (the producer's release):
-    // drop any stale copy of them from this XCD's L2 once, then read them plainly.
-    // Rows published only later are read device-coherently, step by step.
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    per_step = seen < ra->seq0 + (uint32_t)n_steps;
-  }
+  const bool per_step = kHand && rdy != nullptr && seen < ra->seq0 + (uint32_t)n_steps;
   float act_cur = *reinterpret_cast<const float*>(abase);
   constexpr bool t_idx = kTIdx;
   constexpr int nc = kNc;  // spline curves of the wind
@@ -1489,14 +1484,14 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
       if (c < nc) y0c[c] = A.f64e(U_W0N + 8 * c, eo);
     if (p.experiment == 2) syc = A.i32e(U_SYN, eo4);
   }
-  for (int ks = 0; ks < (kRoll ? n_steps : 1) && !failed; ++ks) {
+  for (int ks = 0; ks < (kRoll ? n_steps : 1) && (!kHand || !failed); ++ks) {
   const float act = active ? act_cur : 0.0f;
   // the next step's action, a step ahead: open-loop rows at once; a handed-off
   // row if its flag already said so, else after this step's outputs (below)
   bool act_next = false;
   uint32_t flag_now = 0u;
   if (kRoll && ks + 1 < n_steps) {
-    if (!per_step) {  // open loop, or every row of the launch already published
+    if (!kHand || !per_step) {  // open loop, or every row of the launch already published
       act_cur = *reinterpret_cast<const float*>(abase + (int64_t)(ks + 1) * arow);
       act_next = true;
     } else {
@@ -1788,14 +1783,14 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
   }
-  if (kRoll && ra->done != nullptr) {
+  if (kHand && ra->done != nullptr) {
     // step ks's outputs visible device-wide (release: L2 write-back + wait for
     // the stores), then its done flag, write-through
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     if (lane == 0)
       __hip_atomic_store(ra->done + ob, ra->seq0 + (uint32_t)ks + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (kRoll && per_step && ks + 1 < n_steps) {
+  if (kHand && per_step && ks + 1 < n_steps) {
     const uint32_t fv = flag_value(flag_now);
     seen = fv > seen ? fv : seen;
     if (!act_next) {  // closed loop: the next action comes after these outputs
@@ -1805,6 +1800,8 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
     }
   }
   }  // steps
+  if (kHand && failed && ra->done != nullptr && lane == 0)  // waiters on this wave must not hang
+    __hip_atomic_store(ra->done + ob, 0x7FFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (kRoll) {  // the carried state, once
     A.f64e(U_SX, eo) = s_x, A.f64e(U_SY, eo) = s_y, A.f64e(U_SR, eo) = s_r;
     A.f64e(U_VX, eo) = v_x, A.f64e(U_VY, eo) = v_y, A.f64e(U_VR, eo) = v_r;
@@ -1870,8 +1867,28 @@ template <int kNc, bool kTIdx>
 __global__ void __launch_bounds__(kWave) k_rollout(SacenvBoatParams p, Arena A, Tail T,
                                                    const float* __restrict__ action, int n_steps, RollArgs ra) {
   __shared__ OwnerLds slds;
-  owner_wave<true, kNc, kTIdx>(vreg_params(p), A, vreg_tail(T), action, slds, blockIdx.x, threadIdx.x, n_steps,
-                               &ra);
+  const int ob = blockIdx.x, lane = threadIdx.x;
+  uint32_t seen = 0u;
+  bool hand = ra.done != nullptr;
+  if (ra.ready != nullptr) {
+    const uint32_t* rdy = ra.ready + ob;
+    seen = wait_flag(rdy, ra.seq0 + 1u, flag_load(rdy), ra.status, lane);
+    if (seen == 0u) {  // row 0 never came: nothing steps
+      if (ra.done != nullptr && lane == 0)  // waiters on this wave must not hang either
+        __hip_atomic_store(ra.done + ob, 0x7FFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    // the rows the flag covers were written before it (the producer's release):
+    // drop any stale copy of them from this XCD's L2 once, then read them plainly;
+    // rows published only later are read device-coherently, step by step
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    hand = hand || seen < ra.seq0 + (uint32_t)n_steps;
+  }
+  if (hand)
+    owner_wave<true, kNc, kTIdx, true>(vreg_params(p), A, vreg_tail(T), action, slds, ob, lane, n_steps, &ra,
+                                       nullptr, seen);
+  else
+    owner_wave<true, kNc, kTIdx, false>(vreg_params(p), A, vreg_tail(T), action, slds, ob, lane, n_steps, &ra);
 }
 
 __global__ void __launch_bounds__(kWave) k_toy_init(SacenvToyParams p, ToyArena T, const int32_t* __restrict__ ids,
