@@ -1396,7 +1396,7 @@ __device__ uint32_t wait_flag(const uint32_t* f, uint32_t want, uint32_t seen, i
 // kHand (kRoll only): rows published step by step and/or done flags (the
 // closed loop); without it the loop carries no flag code at all (the launch
 // checked that every row was already published).
-template <bool kRoll, int kNc, bool kTIdx, bool kHand = false>
+template <bool kRoll, int kNc, bool kTIdx, bool kHand = false, bool kTrans = true>
 __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Arena& A, const Tail& Tin,
                                            const float* __restrict__ action, OwnerLds& l, int ob,
                                            int lane, int n_steps = 1, const RollArgs* ra = nullptr,
@@ -1661,8 +1661,10 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   char* const R = kRoll ? ra->rec + (int64_t)ks * ra->rec_stride : A.b + A.ur() * A.np;
   float* const fin = kRoll ? (ra->fin != nullptr ? ra->fin + (int64_t)ks * ra->fin_stride : nullptr)
                            : A.final_obs();
-  char* const trans = kRoll ? (ra->trans != nullptr ? ra->trans + (int64_t)ks * ra->trans_stride : nullptr)
-                            : trans1;
+  // (kRoll: kTrans compiles the pooled row in or out; the step launch decides at run time)
+  char* const trans = !kTrans ? nullptr
+                              : kRoll ? (ra->trans != nullptr ? ra->trans + (int64_t)ks * ra->trans_stride : nullptr)
+                                      : trans1;
   if (p.out_flags & SACENV_OUT_REWARD64) A.at_e<double>(A.ur() + 126, eo) = reward;
   if (p.out_flags & SACENV_OUT_ACCEL) {
     A.at_e<double>(A.ur() + 102, eo) = a_x;
@@ -1863,7 +1865,7 @@ __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, Arena A, Tai
 // n_steps BoatEnv.step launches fused, the state in registers between the
 // steps: open-loop rollouts (records per step) and the segment
 // launch (the arena's record every step, actions behind per-wave flags)
-template <int kNc, bool kTIdx>
+template <int kNc, bool kTIdx, bool kTrans>
 __global__ void __launch_bounds__(kWave) k_rollout(SacenvBoatParams p, Arena A, Tail T,
                                                    const float* __restrict__ action, int n_steps, RollArgs ra) {
   __shared__ OwnerLds slds;
@@ -1885,10 +1887,11 @@ __global__ void __launch_bounds__(kWave) k_rollout(SacenvBoatParams p, Arena A, 
     hand = hand || seen < ra.seq0 + (uint32_t)n_steps;
   }
   if (hand)
-    owner_wave<true, kNc, kTIdx, true>(vreg_params(p), A, vreg_tail(T), action, slds, ob, lane, n_steps, &ra,
-                                       nullptr, seen);
+    owner_wave<true, kNc, kTIdx, true, kTrans>(vreg_params(p), A, vreg_tail(T), action, slds, ob, lane, n_steps,
+                                               &ra, nullptr, seen);
   else
-    owner_wave<true, kNc, kTIdx, false>(vreg_params(p), A, vreg_tail(T), action, slds, ob, lane, n_steps, &ra);
+    owner_wave<true, kNc, kTIdx, false, kTrans>(vreg_params(p), A, vreg_tail(T), action, slds, ob, lane, n_steps,
+                                                &ra);
 }
 
 __global__ void __launch_bounds__(kWave) k_toy_init(SacenvToyParams p, ToyArena T, const int32_t* __restrict__ ids,
@@ -2118,8 +2121,12 @@ static int launch_multi(const SacenvBoatParams& p, void* arena, const float* act
                         void* stream) {
   const int nb_boat = (int)(pad64(p.n_envs) / kWave);
 #define SACENV_LAUNCH(NC, TI)                                                                              \
-  hipLaunchKernelGGL((k_rollout<NC, TI>), dim3(nb_boat), dim3(kWave), 0, (hipStream_t)stream, p,           \
-                     make_arena(p, arena), make_tail(p, arena), actions, n_steps, ra)
+  if (ra.trans != nullptr)                                                                                 \
+    hipLaunchKernelGGL((k_rollout<NC, TI, true>), dim3(nb_boat), dim3(kWave), 0, (hipStream_t)stream, p,   \
+                       make_arena(p, arena), make_tail(p, arena), actions, n_steps, ra);                   \
+  else                                                                                                     \
+    hipLaunchKernelGGL((k_rollout<NC, TI, false>), dim3(nb_boat), dim3(kWave), 0, (hipStream_t)stream, p,  \
+                       make_arena(p, arena), make_tail(p, arena), actions, n_steps, ra)
   SACENV_OWNER_DISPATCH(p, SACENV_LAUNCH)
 #undef SACENV_LAUNCH
   return launch_status();
