@@ -96,6 +96,9 @@ def parse(argv=None):
     ap.add_argument("--pooling", choices=("gather", "none"), default="gather",
                     help="N>1: all-gather the full transitions per 128-step segment (configs[3]), "
                          "or none (sharded per-GPU replay, SURVEY.md §8(e)'s alternative)")
+    ap.add_argument("--refill-overlap", type=int, default=1, choices=(0, 1),
+                    help="--launch segment: two 64-step launches per segment, each refill on a side "
+                         "stream concurrent with the next launch (1), or the refill between launches (0)")
     ap.add_argument("--pool-every", type=int, default=SEG,
                     help="N>1 gather pooling: steps per all-gather (1 = one all-gather per step, "
                          "SURVEY.md §8(e); 128 = one per segment, overlapped with the next)")
@@ -374,15 +377,56 @@ class SegmentRunner:
                      "graph" if dev.type == "cuda" and not args.no_graph and (pool is None or pool_every == SEG)
                      else "eager")
         self.use_graph = self.mode == "graph"
+        # segment mode, refill overlap: launches of HALF steps; the refill after
+        # launch h runs on a side stream concurrently with launch h+1 and must be
+        # done before launch h+2. Safe with the 129-slot ring: launch h+1 reads
+        # episodes <= cons_h + 64 < the fill of the refill before (cons + 129),
+        # and the refill draws from the cons snapshot k_need_masks took.
+        self.overlap = (self.mode == "segment" and bool(getattr(args, "refill_overlap", 0))
+                        and pool is None)
+        if self.overlap:
+            self.rs = torch.cuda.Stream(device=dev, priority=0)
+            self.refill_done = [None, None]   # events of the last two refills (h-1, h-2)
         self.st = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
         self.graphs = None
         self.first_replays = 0
         self.seg_events: list = []
 
-    def _steps(self, k0: int, with_pool: bool, buf=None, on_step=None) -> None:
+    def _launch_overlapped(self, k0: int, n: int, timed: bool = False) -> None:
+        """One persistent launch of n steps, its refill on the side stream."""
+        wl, st, rs = self.wl, self.st, self.rs
+        ev = self.refill_done[1]          # the refill after launch h-2
+        if ev is not None:
+            st.wait_event(ev)
+        if timed:  # the launch alone (not the wait before it)
+            ea, eb = _Clock(self.dev), _Clock(self.dev)
+            ea.record(st)
+        wl.segment_step(k0, n)
+        if timed:
+            eb.record(st)
+            self.seg_events.append((ea, eb, n))
+        rs.wait_stream(st)
+        with torch.cuda.stream(rs):
+            wl.refill()
+            done = torch.cuda.Event()
+            done.record(rs)
+        self.refill_done = [done, self.refill_done[0]]
+
+    def drain_refills(self) -> None:
+        """The stepping stream waits for every refill in flight (overlap mode)."""
+        if self.overlap:
+            for ev in self.refill_done:
+                if ev is not None:
+                    self.st.wait_event(ev)
+
+    def _steps(self, k0: int, with_pool: bool, buf=None, on_step=None, timed: bool = False) -> None:
         """The SEG steps of one segment, enqueued (captured, eager or persistent)."""
         wl, p = self.wl, self.pool if with_pool else None
         if self.mode == "segment":
+            if p is None and self.overlap:
+                for j0 in range(0, SEG, SEG // 2):
+                    self._launch_overlapped(k0 + j0, SEG // 2, timed)
+                return
             if p is None:
                 wl.segment_step(k0, SEG)
                 return
@@ -437,9 +481,13 @@ class SegmentRunner:
             wl.segment_step(0, 3)
             wl.refill()
             for base in range(0, ACTION_STEPS, SEG):
-                wl.segment_step(base, SEG)
-                wl.refill()
+                if self.overlap:
+                    self._steps(base, False)
+                else:
+                    wl.segment_step(base, SEG)
+                    wl.refill()
                 self.first_replays += SEG
+            self.drain_refills()
             _sync(dev)
             return
         if self.use_graph:
@@ -481,18 +529,20 @@ class SegmentRunner:
             buf = p.buf
         else:
             buf = None
-        if timed:
+        own = timed and not (self.overlap and p is None)  # overlap: events per launch
+        if own:
             ea, eb = _Clock(self.dev), _Clock(self.dev)
             ea.record(self.st)
         if self.graphs is not None:
             gset = self.graphs[(k0 % ACTION_STEPS) // SEG]
             gset[p.buf if p is not None else 0].replay()
         else:
-            self._steps(k0, p is not None, buf=buf, on_step=on_step)
-        if timed:
+            self._steps(k0, p is not None, buf=buf, on_step=on_step, timed=timed)
+        if own:
             eb.record(self.st)
-            self.seg_events.append((ea, eb))
-        self.wl.refill()
+            self.seg_events.append((ea, eb, SEG))
+        if not self.overlap:
+            self.wl.refill()
         if p is not None and self.pool_every == SEG:
             p.fill = SEG
             p.flush()
@@ -521,6 +571,7 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
     k = 0
     for _ in range(n_warm):
         k = segment(k, False)
+    run.drain_refills()
     if pool is not None:
         pool.wait()
     _sync(dev)
@@ -534,6 +585,7 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
         k = segment(k, True)
     if pool is not None:
         pool.wait()  # the last segment's transitions are pooled inside the timed region
+    run.drain_refills()  # the last refills are inside the timed region too
     ev1.record(st)
     gathers_timed = (pool.flushes if pool is not None else 0) - g0
     _sync(dev)
@@ -568,7 +620,7 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
     else:
         kern_src = (f"HIP events around the {len(seg_events)} {what} of the timed region (refills "
                     "between segments excluded)")
-    kern_s = sum(a.ms_to(b) for a, b in seg_events) * 1e-3 / (SEG * len(seg_events))
+    kern_s = sum(a.ms_to(b) for a, b, _ in seg_events) * 1e-3 / sum(n for _, _, n in seg_events)
     step_s = ev0.ms_to(ev1) * 1e-3 / steps
 
     dinfo = dist_info(world, dev)
@@ -616,9 +668,11 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
                                   + (", overlapped with the next segment" if pool_every == SEG else ""))
                    if pool is not None else (
                        "none: sharded per-GPU replay (--pooling none)" if world > 1 else None),
-                   "launch": (f"one persistent sacenv_boat_segment launch per {SEG} steps (k_rollout: the "
-                              "carried state in registers; each owner wave reads its action-row flag "
-                              "every step, all rows published) + the 3 refill launches"
+                   "launch": ((f"two persistent sacenv_boat_segment launches of {SEG // 2} steps per {SEG}-step "
+                               "segment" if run.overlap else
+                               f"one persistent sacenv_boat_segment launch per {SEG} steps") +
+                              " (k_rollout: the carried state in registers; each owner wave checks its "
+                              "action-row flag, all rows published) + the 3 refill launches after each"
                               + (f"; one launch per {pool_every} steps when pooling" if pool is not None
                                  and pool_every < SEG else "")
                               if seg_mode else
@@ -627,8 +681,12 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
                                 if pool is not None and not args.mixed else
                                 " (+ the pooled-row copies per step)" if pool is not None else "") +
                                " + the 3 refill launches" if use_graph else "eager")),
-                   "refill": (f"k_need_masks + k_refill + k_refill_fit after every {SEG}-step segment, "
-                              "inside the timed region") if not args.no_autoreset else None},
+                   "refill": None if args.no_autoreset else (
+                       f"k_need_masks + k_refill + k_refill_fit after every {SEG // 2}-step launch on a side "
+                       "stream, concurrent with the next launch and done before the one after, inside the "
+                       "timed region" if run.overlap else
+                       f"k_need_masks + k_refill + k_refill_fit after every {SEG}-step segment, inside the "
+                       "timed region")},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK,
                      "traffic": None if traffic is None else traffic["hbm_bytes_per_launch"],

@@ -56,7 +56,7 @@ constexpr int U_SX = 0, U_SY = 8, U_SR = 16, U_VX = 24, U_VY = 32, U_VR = 40, U_
               U_EP = 56, U_COEF = 64, U_W0N = 128, U_T = 144, U_IDX = 152,
               U_CONS = 156, U_FILL = 160, U_MTPOS = 164, U_SYN = 168, U_STARTY = 172,
               U_CNT = U_STARTY + 4 * kSlots,
-              U_LIST = U_CNT + 4 * SACENV_N_COUNTERS, U_WIND = U_LIST + 12;
+              U_LIST = U_CNT + 4 * SACENV_N_COUNTERS, U_CSNAP = U_LIST + 12, U_WIND = U_CSNAP + 4;
 constexpr int U_MT_BYTES = 4 * kMtN;
 // The f64 fields below U_PAIRED are stored as 16-B pairs per env, [n_pad][2]:
 // (s_x, s_y) (s_r, v_x) (v_y, v_r) (rudder, ep_reward), the spline piece as
@@ -150,6 +150,10 @@ struct Arena {
     return reinterpret_cast<unsigned long long*>(tail());
   }
 
+  // each env's episode counter as k_need_masks saw it: the refill tops the ring
+  // up from this snapshot, so a step launch that runs concurrently with the
+  // refill (and rewrites cons) cannot change what it draws
+  __device__ __forceinline__ int32_t* cons_snap() const { return i32(U_CSNAP); }
   // [0] refills done, [1] SACENV_STATUS_* bits, [2] envs ranked by the last refill
   __device__ __forceinline__ int32_t* status() const {
     return reinterpret_cast<int32_t*>(tail() + align256(8 * nwaves()));
@@ -195,7 +199,7 @@ struct Arena {
   __device__ __forceinline__ T& at_e(int64_t unit, uint32_t off) const {
     return *reinterpret_cast<T*>(b + unit * np + off);
   }
-  // the per-env fields below U_WIND: the whole byte offset in 32 bits (u < 720
+  // the per-env fields below U_WIND: the whole byte offset in 32 bits (u < 724
   // and n_pad <= 2^22 by check_params), so each access is one VALU add
   // on the lane offset and an SGPR-base load/store
   template <class T>
@@ -1028,7 +1032,7 @@ __global__ void __launch_bounds__(kWave) k_refill(SacenvBoatParams p, Arena A) {
   }
   for (int rr = blockIdx.x; rr < k.total; rr += gridDim.x) {
     const int e = ranked_env(A, k, rr, lane);
-    const int c = A.i32(U_CONS)[e];
+    const int c = A.cons_snap()[e];
     const int f0 = A.i32(U_FILL)[e];
     int pos = A.i32(U_MTPOS)[e];  // in flight with cons / fill
     if (c >= f0 && lane == 0) atomicOr(&A.status()[1], SACENV_STATUS_SLOT_UNDERFLOW);
@@ -1115,9 +1119,11 @@ __global__ void __launch_bounds__(kWave) k_refill_fit(SacenvBoatParams p, Arena 
 // flags of its own (measured: owner-side flag words cost 0.25-0.4 us/step).
 __global__ void __launch_bounds__(kWave) k_need_masks(SacenvBoatParams p, Arena A) {
   const int w = blockIdx.x, e = w * kWave + threadIdx.x;
-  const bool need = e < p.n_envs && A.i32(U_FILL)[e] < A.i32(U_CONS)[e] + kSlots;
+  const int c = e < p.n_envs ? A.i32(U_CONS)[e] : 0;
+  const bool need = e < p.n_envs && A.i32(U_FILL)[e] < c + kSlots;
   const unsigned long long m = __ballot(need);
   if (threadIdx.x == 0) A.refill_mask()[w] = m;
+  if (need) A.cons_snap()[e] = c;
 }
 
 // Uniform fp64 constants as VGPR copies: the step reads ~40 config doubles,
