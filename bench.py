@@ -96,7 +96,7 @@ def parse(argv=None):
     ap.add_argument("--pooling", choices=("gather", "none"), default="gather",
                     help="N>1: all-gather the full transitions per 128-step segment (configs[3]), "
                          "or none (sharded per-GPU replay, SURVEY.md §8(e)'s alternative)")
-    ap.add_argument("--refill-overlap", type=int, default=1, choices=(0, 1),
+    ap.add_argument("--refill-overlap", type=int, default=0, choices=(0, 1),
                     help="--launch segment: two 64-step launches per segment, each refill on a side "
                          "stream concurrent with the next launch (1), or the refill between launches (0)")
     ap.add_argument("--pool-every", type=int, default=SEG,
@@ -261,10 +261,10 @@ def load_traffic(n_envs: int, experiment: int, launch: str = "step"):
             d = json.load(open(path))
         except Exception:  # noqa: BLE001
             continue
-        if int(d.get("envs", -1)) == n_envs and int(d.get("experiment", 6)) == experiment \
-                and "hbm_bytes_per_launch" in d:
-            return {"hbm_bytes_per_launch": float(d["hbm_bytes_per_launch"]),
-                    "source": os.path.relpath(path, ROOT)}
+        key = "hbm_bytes_per_step" if launch == "segment" else "hbm_bytes_per_launch"
+        if int(d.get("envs", -1)) == n_envs and int(d.get("experiment", 6)) == experiment and key in d:
+            # per step of all envs (a k_step launch; 1/128 of a persistent launch)
+            return {"hbm_bytes_per_launch": float(d[key]), "source": os.path.relpath(path, ROOT)}
     return None
 
 

@@ -60,11 +60,11 @@ def _same(env, ref, bookkeeping: bool) -> bool:
 
 def test_bench_timed_path_equals_eager_and_oracle(gpu, built_lib):
     import bench
-    args_s = bench.parse(["--no-cpu-baseline"])
-    args_q = bench.parse(["--no-cpu-baseline", "--refill-overlap", "0"])
+    args_s = bench.parse(["--no-cpu-baseline", "--refill-overlap", "1"])
+    args_q = bench.parse(["--no-cpu-baseline"])
     args_g = bench.parse(["--no-cpu-baseline", "--launch", "step"])
     args_e = bench.parse(["--no-cpu-baseline", "--no-graph"])
-    assert args_s.launch == "segment" and args_s.refill_overlap == 1   # the default the driver times
+    assert args_q.launch == "segment" and args_q.refill_overlap == 0   # the default the driver times
     assert (args_s.envs, args_s.experiment, args_s.episode_steps, args_s.helpers) == (65536, 6, 500, 8192)
     wls = [bench.make_workload(a, 0, gpu) for a in (args_s, args_q, args_g, args_e)]
     wl_e = wls[-1]

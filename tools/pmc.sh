@@ -1,13 +1,15 @@
 #!/bin/bash
 # rocprofv3 evidence for the bench kernel (run on the GPU box from the repo root):
-#   1. kernel trace + stats of the default bench command (graph replay);
+#   PMC_KERNEL=segment (default: the persistent k_rollout of --launch segment) or
+#   step (k_step of --launch step);
+#   1. kernel trace + stats of the bench command;
 #   2. PMC passes, one per run, --pmc never combined with a trace domain (pool
 #      rule), each within the per-block limits (<= 4 TCC, <= 8 SQ counters):
 #      memory-side read requests split by size, WRITE_SIZE + L2 hit/miss,
 #      FETCH_SIZE (the guide's convention), and two SQ instruction passes;
 #   3. the same memory passes over tools/probes/fetch_calib (known bytes, the
 #      8-B/lane access pattern of k_step) to calibrate them.
-# tools/pmc_summary.py reduces everything to gpurun_out/pmc_k_step.json.
+# tools/pmc_summary.py reduces everything to gpurun_out/pmc_<kernel>.json.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=$GRAFT_REPO_ROOT/gpurun_out
@@ -15,9 +17,11 @@ mkdir -p "$OUT"
 # the calibration probe is a gitignored build product: build it if this tree lacks it
 [ -x tools/probes/fetch_calib ] || /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 \
   -o tools/probes/fetch_calib tools/probes/fetch_calib.hip || exit 1
-BENCH="python3 bench.py --steps ${PMC_STEPS:-256} --warmup 128 --no-cpu-baseline --no-graph"
+MODE=${PMC_KERNEL:-segment}
+if [ "$MODE" = step ]; then LAUNCH="--launch step"; PMCL="--launch step --no-graph"; else LAUNCH=""; PMCL=""; fi
+BENCH="python3 bench.py --steps ${PMC_STEPS:-256} --warmup 128 --no-cpu-baseline $PMCL"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_trace" -o run --output-format csv \
-  -- python3 bench.py --no-cpu-baseline > "$OUT/prof_trace_bench.json" 2> "$OUT/prof_trace.log" || exit 1
+  -- python3 bench.py --no-cpu-baseline $LAUNCH > "$OUT/prof_trace_bench.json" 2> "$OUT/prof_trace.log" || exit 1
 i=0
 while read -r c; do
   i=$((i+1))
@@ -32,4 +36,4 @@ FETCH_SIZE
 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64
 SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_INT32
 LIST
-python3 tools/pmc_summary.py "$OUT" || exit 1
+python3 tools/pmc_summary.py "$OUT" "$MODE" || exit 1

@@ -1,8 +1,10 @@
-"""Reduce tools/pmc.sh's rocprofv3 output to per-launch figures for k_step.
+"""Reduce tools/pmc.sh's rocprofv3 output to per-launch figures for the bench kernel.
 
-Writes gpurun_out/pmc_k_step.json:
-* the kernel trace's mean duration of k_step;
-* per-launch counter means for k_step and for the calibration kernels of
+Mode "step": k_step, gpurun_out/pmc_k_step.json. Mode "segment": the persistent
+k_rollout of sacenv_boat_segment (128 steps per launch), gpurun_out/pmc_segment.json,
+with the per-launch figures also divided into per-step ones. Either holds:
+* the kernel trace's mean duration;
+* per-launch counter means for the kernel and for the calibration kernels of
   tools/probes/fetch_calib (k_calib8: k_step's 8-B/lane access pattern with
   known bytes: 10 485 760 read, 7 864 320 written per launch);
 * HBM-side bytes per launch from the read requests split by size
@@ -17,6 +19,7 @@ import os
 import sys
 
 KERNEL = "k_step"
+STEPS_PER_LAUNCH = 1
 CALIB = {"k_calib8": (10485760.0, 7864320.0), "k_calib16": (10485760.0, 7864320.0)}
 
 
@@ -33,7 +36,7 @@ def means(prefix, out_dir, name):
     for d in sorted(glob.glob(os.path.join(out_dir, prefix + "*"))):
         for r in rows(os.path.join(d, "**", "*counter_collection.csv")):
             kn = r.get("Kernel_Name", "")
-            if name in kn and (name != KERNEL or "k_step<false" in kn or "k_stepILb0E" in kn):
+            if name in kn and (name != "k_step" or "k_step<false" in kn or "k_stepILb0E" in kn):
                 by.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in by.items()}
 
@@ -92,9 +95,17 @@ def main(out_dir):
         res["experiment"] = d["config"]["experiment"]
         res["bench_kernel_avg_us"] = d["roofline"]["kernel_avg_us"]
         res["algorithmic_bytes_per_launch"] = d["roofline"]["bytes_per_launch"]
-    json.dump(res, open(os.path.join(out_dir, "pmc_k_step.json"), "w"), indent=1)
+    if STEPS_PER_LAUNCH > 1 and "hbm_bytes_per_launch" in res:
+        res["steps_per_launch"] = STEPS_PER_LAUNCH
+        res["hbm_bytes_per_step"] = res["hbm_bytes_per_launch"] / STEPS_PER_LAUNCH
+        if "trace_avg_ns" in res:
+            res["trace_avg_ns_per_step"] = res["trace_avg_ns"] / STEPS_PER_LAUNCH
+    name = "pmc_k_step.json" if KERNEL == "k_step" else "pmc_segment.json"
+    json.dump(res, open(os.path.join(out_dir, name), "w"), indent=1)
     print(json.dumps(res, indent=1))
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 2 and sys.argv[2] == "segment":
+        KERNEL, STEPS_PER_LAUNCH = "k_rollout", 128
     main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out")
