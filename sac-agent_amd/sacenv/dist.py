@@ -286,3 +286,15 @@ class SegmentPool:
         """Step k's pooled record [world * record_bytes], rank order (a copy)."""
         g = gathered.view(self.world, n_steps, self.rb)
         return g[:, k].reshape(-1).clone()
+
+
+def shard_owner(rows, cntr: int, mem_size: int, period: int, n_per_rank: int):
+    """Which rank wrote ring row ``rows`` of a pooled replay buffer that appends
+    ``period = world * n_per_rank`` rows per step in global env order (rank r's at
+    offset r * n_per_rank): the row holds the latest global sequence number
+    s = row (mod mem_size) below ``cntr``; its writer is (s mod period) // n_per_rank.
+    The rule ``sacenv_replay_sample_shard`` applies on the device (ShardedReplayBuffer)."""
+    import numpy as np
+    rows = np.asarray(rows, dtype=np.int64)
+    s = rows + mem_size * ((cntr - 1 - rows) // mem_size)
+    return (s % period) // n_per_rank

@@ -234,3 +234,67 @@ def test_pooled_transitions_equal_single_process(world, seg):
         ended += int(r["done"].sum())
         s = r["reset_obs"].astype(np.float32)
     assert ended > STEPS // 2   # the ended-env rows were exercised
+
+
+def _sharded_worker(rank, world, port, n, M, steps, B, q):
+    """Rank-local ring rows (this rank's transitions only, at the pooled buffer's
+    positions), shared sampling stream, integer SUM all-reduce of the owned rows."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "sac-agent_amd"))
+    from sacenv.dist import shard_owner
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        W = world * n
+        ring = np.zeros((M, 3), np.int64)          # a row's payload: (step, global env, marker)
+        rs = np.random.RandomState(11)             # every rank: the same stream
+        cntr, out = 0, []
+        for t in range(steps):
+            rows = (cntr + rank * n + np.arange(n)) % M   # sacenv_replay_store_shard's positions
+            ring[rows] = np.stack([np.full(n, t), rank * n + np.arange(n), np.full(n, 7)], 1)
+            cntr += W
+            if t % 2 == 1:
+                idx = rs.choice(min(cntr, M), B)   # buffer.py:27
+                own = shard_owner(idx, cntr, M, W, n) == rank
+                mine = torch.from_numpy(np.where(own[:, None], ring[idx], 0))
+                dist.all_reduce(mine, op=dist.ReduceOp.SUM)
+                out.append((idx, mine.numpy()))
+        q.put((rank, out))
+    except Exception as exc:  # noqa: BLE001
+        q.put((rank, repr(exc)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n,M", [(2, 5, 23), (3, 4, 50), (2, 8, 16)])
+def test_sharded_replay_equals_pooled_buffer(world, n, M):
+    """SURVEY §8(e)'s lighter exchange, on gloo: each rank writes only its own rows
+    (at the pooled ring's positions), every rank draws the same indices, and one SUM
+    all-reduce of the owned rows gives the pooled buffer's batch -- including rows
+    that wrapped around the ring and changed writer (M not a multiple of world * n)."""
+    steps, B = 12, 9
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_sharded_worker, args=(r, world, port, n, M, steps, B, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert all(not isinstance(v, str) for v in res.values()), res
+    # the pooled buffer: one process stores every rank's rows in global env order
+    W = world * n
+    ring = np.zeros((M, 3), np.int64)
+    rs = np.random.RandomState(11)
+    cntr, k = 0, 0
+    for t in range(steps):
+        ring[(cntr + np.arange(W)) % M] = np.stack([np.full(W, t), np.arange(W), np.full(W, 7)], 1)
+        cntr += W
+        if t % 2 == 1:
+            idx = rs.choice(min(cntr, M), B)
+            for r in range(world):
+                got_idx, got = res[r][k]
+                np.testing.assert_array_equal(got_idx, idx)
+                np.testing.assert_array_equal(got, ring[idx])
+            k += 1
