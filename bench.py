@@ -335,11 +335,21 @@ def make_workload(args, rank: int, dev) -> Workload:
     # reads its flag every step)
     ready = torch.full((env.n_pad // 64,), 0x7FFFFFFF, dtype=torch.int32, device=dev)
 
+    import ctypes as C
+    seg_fn, a0, astride = env.lib.sacenv_boat_segment, actions.data_ptr(), actions.stride(0)
+    # the arguments are built right here (table [512, N] f32 contiguous, one flag per owner wave)
+    assert actions.is_contiguous() and ready.numel() == env.n_pad // 64
+
     def segment_step(k0: int, n: int, trans=None):
+        # sacenv_boat_segment (VecBoatEnv.segment_async without its per-call Python
+        # checks): the timed loop pays one ctypes call
         r0 = k0 % ACTION_STEPS
         assert r0 + n <= ACTION_STEPS
-        env.segment_async(actions[r0:], n, act_ready=ready, trans=trans,
-                          trans_stride=0 if trans is None else row_bytes)
+        if trans is not None and trans.numel() < (n - 1) * row_bytes + lay.nbytes:
+            raise ValueError("pooled rows buffer too small")
+        _lib.check(seg_fn(env._pp, env._ptr, C.c_void_p(a0 + 4 * r0 * astride), astride, n, ready.data_ptr(),
+                          None, 0, None if trans is None else trans.data_ptr(),
+                          0 if trans is None else row_bytes, torch.cuda.current_stream(dev).cuda_stream))
 
     bytes_launch = BYTES_PER_ENV_STEP * N + (sum(TOY_BYTES.values()) * N if args.mixed else 0)
     return Workload(envs, stepper, refill, actions, pooled_step, row_bytes, N * len(envs), bytes_launch,
@@ -391,6 +401,14 @@ class SegmentRunner:
         self.graphs = None
         self.first_replays = 0
         self.seg_events: list = []
+        self._clocks: list = []   # pre-created events for the timed segments (no creation inside)
+
+    def reserve_clocks(self, n: int) -> None:
+        """Create the timing events of n timed launches ahead of the timed region."""
+        self._clocks = [(_Clock(self.dev), _Clock(self.dev)) for _ in range(n)]
+
+    def _clock_pair(self):
+        return self._clocks.pop() if self._clocks else (_Clock(self.dev), _Clock(self.dev))
 
     def _launch_overlapped(self, k0: int, n: int, timed: bool = False) -> None:
         """One persistent launch of n steps, its refill on the side stream."""
@@ -399,7 +417,7 @@ class SegmentRunner:
         if ev is not None:
             st.wait_event(ev)
         if timed:  # the launch alone (not the wait before it)
-            ea, eb = _Clock(self.dev), _Clock(self.dev)
+            ea, eb = self._clock_pair()
             ea.record(st)
         wl.segment_step(k0, n)
         if timed:
@@ -531,7 +549,7 @@ class SegmentRunner:
             buf = None
         own = timed and not (self.overlap and p is None)  # overlap: events per launch
         if own:
-            ea, eb = _Clock(self.dev), _Clock(self.dev)
+            ea, eb = self._clock_pair()
             ea.record(self.st)
         if self.graphs is not None:
             gset = self.graphs[(k0 % ACTION_STEPS) // SEG]
@@ -578,6 +596,7 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
     barrier(world)
     _sync(dev)
     ev0, ev1 = _Clock(dev), _Clock(dev)
+    run.reserve_clocks(2 * n_timed)
     t0 = time.perf_counter()
     ev0.record(st)
     g0 = pool.flushes if pool is not None else 0
