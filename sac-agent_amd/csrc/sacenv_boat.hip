@@ -1017,6 +1017,22 @@ __global__ void __launch_bounds__(1024) k_compact(const uint8_t* __restrict__ do
   if (t == 0) *count = base_s;
 }
 
+// Non-serialising phase clocks of the refill (tools/refill_stamps.py; -DSACENV_STAMPS
+// builds only): a stamp is taken once the value(s) it names are in registers
+// (the empty asm consumes them), no other wait is added.
+#ifdef SACENV_STAMPS
+#define REFILL_STAMP(slot, ...)                                     \
+  do {                                                              \
+    asm volatile("" ::__VA_ARGS__);                                 \
+    (slot) = __builtin_amdgcn_s_memrealtime();                      \
+  } while (0)
+constexpr int kRefillStamps = 24;  // per refill wave: start, ranked, 4 x (5 per env), end, envs
+#else
+#define REFILL_STAMP(slot, ...) \
+  do {                          \
+  } while (0)
+#endif
+
 // sacenv_boat_refill, launch 1: every env flagged in the refill masks gets
 // its slot ring topped up to SLOTS episodes (fill = cons + SLOTS), drawn in
 // the env's order (start y and raw knots), one wave per env (rank h,
@@ -1025,25 +1041,40 @@ __global__ void __launch_bounds__(1024) k_compact(const uint8_t* __restrict__ do
 __global__ void __launch_bounds__(kWave) k_refill(SacenvBoatParams p, Arena A) {
   __shared__ RngLds lds;
   const int lane = threadIdx.x;
+#ifdef SACENV_STAMPS
+  uint64_t stm[kRefillStamps] = {};
+  int n_st = 0;
+#endif
+  REFILL_STAMP(stm[0], "s"(lane));
   const Ranking k = rank_masks(A, lane);
+  REFILL_STAMP(stm[1], "s"(k.total));
   if (blockIdx.x == 0 && lane == 0) {
     A.status()[0] += 1;
     A.status()[2] = k.total;
   }
   for (int rr = blockIdx.x; rr < k.total; rr += gridDim.x) {
+#ifdef SACENV_STAMPS
+    const int sb = 2 + 5 * (n_st < 4 ? n_st : 3);
+    ++n_st;
+#endif
+    REFILL_STAMP(stm[sb], "s"(rr));
     const int e = ranked_env(A, k, rr, lane);
+    REFILL_STAMP(stm[sb + 1], "s"(e));
     const int c = A.cons_snap()[e];
     const int f0 = A.i32(U_FILL)[e];
     int pos = A.i32(U_MTPOS)[e];  // in flight with cons / fill
+    REFILL_STAMP(stm[sb + 2], "v"(c), "v"(f0), "v"(pos));
     if (c >= f0 && lane == 0) atomicOr(&A.status()[1], SACENV_STATUS_SLOT_UNDERFLOW);
     int f = f0;
     for (; f < c + kSlots; ++f) {
       const int32_t start_y = draw_knots_wave(p, A, lds, e, lane, nullptr, nullptr, pos);
+      REFILL_STAMP(stm[sb + 3], "v"(start_y));
       pos = -1;
       __syncthreads();
       store_draw(p, A, lds, e, f % kSlots, start_y, lane, true);
       __syncthreads();
     }
+    REFILL_STAMP(stm[sb + 4], "v"(f));
     if (lane == 0) {
       A.i32(U_FILL)[e] = f;
       A.refill_list(0)[rr] = e;
@@ -1051,6 +1082,14 @@ __global__ void __launch_bounds__(kWave) k_refill(SacenvBoatParams p, Arena A) {
       A.refill_list(2)[rr] = f;
     }
   }
+#ifdef SACENV_STAMPS
+  stm[22] = __builtin_amdgcn_s_memrealtime();
+  stm[23] = (uint64_t)n_st;
+  if (lane == 0 && (int64_t)(blockIdx.x + 1) * kRefillStamps * 8 <= 24 * A.np) {
+    uint64_t* d = reinterpret_cast<uint64_t*>(A.accel()) + (int64_t)blockIdx.x * kRefillStamps;
+    for (int i = 0; i < kRefillStamps; ++i) d[i] = stm[i];
+  }
+#endif
 }
 
 // sacenv_boat_refill, launch 2: the spline fits of the episodes launch 1
@@ -1102,6 +1141,12 @@ __global__ void __launch_bounds__(kWave) k_refill_fit(SacenvBoatParams p, Arena 
   const int nc = p.use_wind_table ? 0 : n_curves(p.experiment);
   const int nk = p.n_knots;
   const int items = A.status()[2] * nc;  // (env, curve) groups
+#ifdef SACENV_STAMPS
+  const uint64_t st0 = __builtin_amdgcn_s_memrealtime();
+  uint64_t* const fst = reinterpret_cast<uint64_t*>(A.reward64()) + 2 * (int64_t)blockIdx.x;
+  const bool fst_ok = lane == 0 && (int64_t)(blockIdx.x + 1) * 16 <= 8 * A.np;
+  if (fst_ok) fst[0] = st0, fst[1] = 0;
+#endif
   if (items == 0 || (int)blockIdx.x * (kWave / GS) >= items) return;  // uniform
   for (int i = lane; i < nk * nk; i += kWave) g[i] = T.g[i];
   __syncthreads();
@@ -1111,6 +1156,10 @@ __global__ void __launch_bounds__(kWave) k_refill_fit(SacenvBoatParams p, Arena 
     if (item >= items) break;
     fit_group<GS>(p, A, g, item, lane & (GS - 1), nc);
   }
+#ifdef SACENV_STAMPS
+  __syncthreads();
+  if (fst_ok) fst[1] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 // sacenv_boat_refill, launch 0: which envs consumed pre-drawn episodes since

@@ -1,0 +1,110 @@
+"""Diagnostic: where k_refill's time goes, from non-serialising phase clocks.
+
+Builds sac-agent_amd/build/libsacenv_stamps.so with -DSACENV_STAMPS (never loaded by
+the product path), runs the bench workload (exp 6, 65 536 envs, 500-step episodes,
+persistent 128-step segments) and after each of a few refills reads the per-wave
+clocks k_refill writes into the (otherwise unused) accel region and k_refill_fit's
+per-block start/end in the reward64 region. A clock is taken once the values it
+names are in registers; no other wait is inserted (sacenv_boat.hip REFILL_STAMP).
+
+Per refill wave: start, after the mask ranking, then per env it draws (first four):
+iteration start, env found (ranked_env), counters loaded (cons snapshot, fill, MT
+position), draw done (window load, ballot, LDS exchange, knots), stores issued; end.
+Prints medians / percentiles in us (100 MHz s_memrealtime) and writes the summary
+as JSON to gpurun_out/refill_stamps.json.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "sac-agent_amd")
+LIB = os.path.join(PKG, "build", "libsacenv_stamps.so")
+
+
+def build():
+    sys.path.insert(0, ROOT)
+    import __graft_entry__ as g
+    cmd = [g._hipcc(), *g.HIPCC_FLAGS, "-DSACENV_STAMPS", "-I", os.path.join(ROOT, "include"),
+           *[os.path.join(PKG, "csrc", f) for f in g.SOURCES], "-o", LIB]
+    subprocess.run(cmd, check=True)
+
+
+def pct(x):
+    x = np.asarray(x, np.float64)
+    if x.size == 0:
+        return None
+    return {"median": float(np.median(x)), "p10": float(np.percentile(x, 10)),
+            "p90": float(np.percentile(x, 90)), "max": float(x.max()), "n": int(x.size)}
+
+
+def main():
+    if not os.path.exists(LIB) or "--rebuild" in sys.argv or "--build-only" in sys.argv:
+        build()
+    if "--build-only" in sys.argv:
+        return
+    os.environ["SACENV_LIB"] = LIB
+    sys.path.insert(0, PKG)
+    import torch
+    from sacenv import VecBoatEnv
+    N, H = 65536, 8192
+    env = VecBoatEnv({"base_settings": {"experiment": 6, "test_mode": 0}}, N, device="cuda",
+                     max_episode_steps=500, n_helpers=H, auto_refill=False)
+    env.reset()
+    acts = torch.rand(512, N, device="cuda") * 2 - 1
+    acc = env.arena[env.layout.accel: env.layout.accel + 24 * env.n_pad].view(torch.int64).view(-1, 24)
+    fit = env.arena[env.layout.reward64: env.layout.reward64 + 8 * env.n_pad].view(torch.int64).view(-1, 2)
+    samples = []
+    for s in range(12):
+        env.segment_async(acts[(128 * s) % 512:], 128)
+        torch.cuda.synchronize()
+        acc.zero_()
+        fit.zero_()
+        env.refill()
+        torch.cuda.synchronize()
+        if s >= 4:  # past the start-up transient
+            samples.append((acc[:H].cpu().numpy().copy(), fit[:H].cpu().numpy().copy(),
+                            int(env.status[2].item())))
+    tick = 0.01  # us per 100 MHz tick
+    out = {"envs": N, "helpers": H, "refills": []}
+    agg = {k: [] for k in ("rank", "find_env", "counters", "draw", "store", "per_env", "wave_span",
+                           "start_skew", "end_spread")}
+    for a, f, ranked in samples:
+        live = a[:, 0] > 0
+        a = a[live].astype(np.float64)
+        t0 = a[:, 0].min()
+        agg["start_skew"] += list((a[:, 0] - t0) * tick)
+        agg["end_spread"] += list((a[:, 22] - t0) * tick)
+        agg["wave_span"] += list((a[:, 22] - a[:, 0]) * tick)
+        agg["rank"] += list((a[:, 1] - a[:, 0]) * tick)
+        n_env = a[:, 23].astype(int)
+        for j in range(4):
+            b = 2 + 5 * j
+            m = n_env > j if j < 3 else n_env == 4  # slot 3 holds the last env of longer waves
+            if not m.any():
+                continue
+            r = a[m]
+            agg["find_env"] += list((r[:, b + 1] - r[:, b]) * tick)
+            agg["counters"] += list((r[:, b + 2] - r[:, b + 1]) * tick)
+            agg["draw"] += list((r[:, b + 3] - r[:, b + 2]) * tick)
+            agg["store"] += list((r[:, b + 4] - r[:, b + 3]) * tick)
+            agg["per_env"] += list((r[:, b + 4] - r[:, b]) * tick)
+        fl = f[f[:, 0] > 0].astype(np.float64)
+        fit_span = (fl[:, 1].max() - fl[:, 0].min()) * tick if (fl[:, 1] > 0).any() else None
+        out["refills"].append({"ranked_envs": ranked, "k_refill_span_us": float((a[:, 22].max() - t0) * tick),
+                               "envs_per_wave": pct(n_env), "k_refill_fit_span_us": fit_span})
+    out["phases_us"] = {k: pct(v) for k, v in agg.items()}
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "refill_stamps.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
+    for r in out["refills"]:
+        print("refill:", r)
+    for k, v in out["phases_us"].items():
+        print(f"{k:12s}", v and {kk: round(vv, 3) for kk, vv in v.items()})
+
+
+if __name__ == "__main__":
+    main()
