@@ -583,7 +583,7 @@ __device__ __forceinline__ void load_g(const SacenvBoatParams& p, const double* 
 // draws (replays) bypass the RNG. Returns start_y in all lanes.
 __device__ int32_t draw_knots_wave(const SacenvBoatParams& p, const Arena& A, RngLds& l, int e,
                                    int lane, const int32_t* ex_start_y, const double* ex_knots,
-                                   int pos0 = -1) {
+                                   int pos0 = -1, bool have_w0 = false, uint32_t w0_pre = 0u) {
   const int nk = p.n_knots;
   // draws follow the reference even when a recorded wind table overrides the
   // curves; only the spline fit is skipped then
@@ -612,7 +612,9 @@ __device__ int32_t draw_knots_wave(const SacenvBoatParams& p, const Arena& A, Rn
   mask |= mask >> 16;
   uint32_t val = 0;
   const int need = 2 * nk * ndraw;  // words of the knot values after the randint
-  const uint32_t w0 = mt_fetch(st, l, lane);
+  // the first window, or the caller's copy of it (raw words pos0 .. pos0+63 of the
+  // stored block, loaded ahead when the window does not cross the block end)
+  const uint32_t w0 = have_w0 ? mt_temper(w0_pre) : mt_fetch(st, l, lane);
   const unsigned long long acc0 = __ballot(((w0 & mask) <= rng) && lane < kWave - need);
   if (acc0) {
     // fast path: one 64-word window holds the randint draw and every knot
@@ -753,87 +755,6 @@ __device__ int32_t draw_episode_wave(const SacenvBoatParams& p, const Arena& A, 
   store_draw(p, A, l, e, slot, start_y, lane);
   fit_store_wave(p, A, l, e, slot, lane);
   return start_y;
-}
-
-// ---------------------------------------------------------------- refill ranking
-
-// Mask w flags the envs of owner wave w to refill. Every refill wave
-// ranks the flagged envs the same way (lane l owns the masks of waves l,
-// l+64, ...; envs ordered by lane, then mask, then bit) with DPP scans, so
-// rank rr maps to one env without atomics or cross-lane shuffles. The 8 KB
-// of masks stay in L2 (no LDS copy: more refill waves fit per CU).
-constexpr int kMaskRegs = 16;  // masks per lane held in registers (owner waves <= 1024)
-
-struct Ranking {
-  int incl, cnt, total, R;
-  unsigned long long mv[kMaskRegs];  // this lane's masks (waves lane, lane + 64, ...)
-};
-
-__device__ Ranking rank_masks(const Arena& A, int lane) {
-  const int nw = A.nwaves();
-  const unsigned long long* masks = A.refill_mask();
-  Ranking k;
-  k.R = (nw + kWave - 1) / kWave;  // masks per lane
-  int cnt = 0;
-  // fixed trip count and clamped (branch-free) addresses, so all loads are in
-  // flight at once before the first wait
-#pragma unroll
-  for (int i = 0; i < kMaskRegs; ++i) {
-    const int w = lane + kWave * i;
-    k.mv[i] = masks[w < nw ? w : nw - 1];
-  }
-#pragma unroll
-  for (int i = 0; i < kMaskRegs; ++i) {
-    if (lane + kWave * i >= nw) k.mv[i] = 0ull;
-    cnt += __popcll(k.mv[i]);
-  }
-  for (int i = kMaskRegs; i < k.R; ++i) {
-    const int w = lane + kWave * i;
-    cnt += w < nw ? __popcll(masks[w]) : 0;
-  }
-  k.cnt = cnt;
-  k.incl = wave_incl_scan(cnt);
-  k.total = __builtin_amdgcn_readlane(k.incl, kWave - 1);
-  return k;
-}
-
-// env of rank rr
-__device__ int ranked_env(const Arena& A, const Ranking& k, int rr, int lane) {
-  const int nw = A.nwaves();
-  const unsigned long long* masks = A.refill_mask();
-  const int L = __ffsll((long long)__ballot(k.incl > rr)) - 1;  // owning lane
-  int rem = rr - __builtin_amdgcn_readlane(k.incl - k.cnt, L);
-  int e = -1;
-  for (int i0 = 0; i0 < k.R && e < 0; i0 += kWave) {  // lane q takes L's mask i0 + q
-    const int w = L + kWave * (i0 + lane);
-    unsigned long long v = 0ull;
-    if (k.R <= kMaskRegs) {  // lane q <- mask q of lane L, from registers (no reload)
-#pragma unroll
-      for (int i = 0; i < kMaskRegs; ++i) {
-        const unsigned long long mi =
-            ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(k.mv[i] >> 32), L) << 32) |
-            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)k.mv[i], L);
-        if (lane == i) v = mi;
-      }
-    } else if (i0 + lane < k.R && w < nw) {
-      v = masks[w];
-    }
-    const int pc = __popcll(v);
-    const int ip = wave_incl_scan(pc);
-    const int chunk = __builtin_amdgcn_readlane(ip, kWave - 1);
-    if (rem < chunk) {
-      const int q = __ffsll((long long)__ballot(ip > rem)) - 1;
-      const int within = rem - __builtin_amdgcn_readlane(ip - pc, q);
-      const unsigned long long m =
-          ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), q) << 32) |
-          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, q);
-      // the within-th set bit of m: each lane tests its own bit, one ballot
-      const bool is_bit = ((m >> lane) & 1ull) && __popcll(m & ((1ull << lane) - 1ull)) == within;
-      e = (L + kWave * (i0 + q)) * kWave + (__ffsll((long long)__ballot(is_bit)) - 1);
-    }
-    rem -= chunk;
-  }
-  return e;
 }
 
 // scalar state of a fresh Boat (boat_env.py:152-198) and its observation;
@@ -1038,6 +959,7 @@ constexpr int kRefillStamps = 24;  // per refill wave: start, ranked, 4 x (5 per
 // the env's order (start y and raw knots), one wave per env (rank h,
 // h + grid, ...). Block 0 counts the refill and publishes the rank count for
 // launch 2.
+constexpr int kRefillAhead = 4;  // envs per refill wave whose inputs load together
 __global__ void __launch_bounds__(kWave) k_refill(SacenvBoatParams p, Arena A) {
   __shared__ RngLds lds;
   const int lane = threadIdx.x;
@@ -1046,40 +968,61 @@ __global__ void __launch_bounds__(kWave) k_refill(SacenvBoatParams p, Arena A) {
   int n_st = 0;
 #endif
   REFILL_STAMP(stm[0], "s"(lane));
-  const Ranking k = rank_masks(A, lane);
-  REFILL_STAMP(stm[1], "s"(k.total));
-  if (blockIdx.x == 0 && lane == 0) {
-    A.status()[0] += 1;
-    A.status()[2] = k.total;
-  }
-  for (int rr = blockIdx.x; rr < k.total; rr += gridDim.x) {
-#ifdef SACENV_STAMPS
-    const int sb = 2 + 5 * (n_st < 4 ? n_st : 3);
-    ++n_st;
-#endif
-    REFILL_STAMP(stm[sb], "s"(rr));
-    const int e = ranked_env(A, k, rr, lane);
-    REFILL_STAMP(stm[sb + 1], "s"(e));
-    const int c = A.cons_snap()[e];
-    const int f0 = A.i32(U_FILL)[e];
-    int pos = A.i32(U_MTPOS)[e];  // in flight with cons / fill
-    REFILL_STAMP(stm[sb + 2], "v"(c), "v"(f0), "v"(pos));
-    if (c >= f0 && lane == 0) atomicOr(&A.status()[1], SACENV_STATUS_SLOT_UNDERFLOW);
-    int f = f0;
-    for (; f < c + kSlots; ++f) {
-      const int32_t start_y = draw_knots_wave(p, A, lds, e, lane, nullptr, nullptr, pos);
-      REFILL_STAMP(stm[sb + 3], "v"(start_y));
-      pos = -1;
-      __syncthreads();
-      store_draw(p, A, lds, e, f % kSlots, start_y, lane, true);
-      __syncthreads();
+  const int total = __builtin_amdgcn_readfirstlane(A.status()[2]);  // ranked by k_need_masks
+  REFILL_STAMP(stm[1], "s"(total));
+  if (blockIdx.x == 0 && lane == 0) A.status()[0] += 1;
+  const int G = (int)gridDim.x;
+  for (int r0 = blockIdx.x; r0 < total; r0 += kRefillAhead * G) {
+    // the next kRefillAhead envs of this wave (ranks r0, r0 + G, ...): lane j loads env
+    // j's id, counters and (when it does not cross the MT block end) its first window
+    // in one go, so their latencies overlap instead of adding up env after env
+    const int rj = r0 + (lane & (kRefillAhead - 1)) * G;
+    const bool okj = lane < kRefillAhead && rj < total;
+    const int ej = okj ? A.refill_list(0)[rj] : 0;
+    const int cj = okj ? A.cons_snap()[ej] : 0;
+    const int fj = okj ? A.i32(U_FILL)[ej] : 0;
+    const int pj = okj ? A.i32(U_MTPOS)[ej] : kMtN;
+    uint32_t win[kRefillAhead];
+#pragma unroll
+    for (int j = 0; j < kRefillAhead; ++j) {
+      const int e = __builtin_amdgcn_readlane(ej, j), pos = __builtin_amdgcn_readlane(pj, j);
+      const bool fits = r0 + j * G < total && pos + kWave <= kMtN;
+      win[j] = A.mt_key()[(int64_t)e * kMtN + (fits ? pos + lane : lane)];
     }
-    REFILL_STAMP(stm[sb + 4], "v"(f));
-    if (lane == 0) {
-      A.i32(U_FILL)[e] = f;
-      A.refill_list(0)[rr] = e;
-      A.refill_list(1)[rr] = f0;
-      A.refill_list(2)[rr] = f;
+#pragma unroll
+    for (int j = 0; j < kRefillAhead; ++j) {
+      const int rr = r0 + j * G;
+      if (rr >= total) break;
+#ifdef SACENV_STAMPS
+      const int sb = 2 + 5 * (n_st < 4 ? n_st : 3);
+      ++n_st;
+#endif
+      REFILL_STAMP(stm[sb], "s"(rr));
+      const int e = __builtin_amdgcn_readlane(ej, j);
+      REFILL_STAMP(stm[sb + 1], "s"(e));
+      const int c = __builtin_amdgcn_readlane(cj, j);
+      const int f0 = __builtin_amdgcn_readlane(fj, j);
+      const int pos0 = __builtin_amdgcn_readlane(pj, j);
+      REFILL_STAMP(stm[sb + 2], "s"(c), "s"(f0), "s"(pos0));
+      if (c >= f0 && lane == 0) atomicOr(&A.status()[1], SACENV_STATUS_SLOT_UNDERFLOW);
+      int f = f0;
+      bool first = true;
+      for (; f < c + kSlots; ++f) {
+        const bool pre = first && pos0 + kWave <= kMtN;
+        const int32_t start_y = draw_knots_wave(p, A, lds, e, lane, nullptr, nullptr, first ? pos0 : -1, pre,
+                                                win[j]);
+        REFILL_STAMP(stm[sb + 3], "v"(start_y));
+        first = false;
+        __syncthreads();
+        store_draw(p, A, lds, e, f % kSlots, start_y, lane, true);
+        __syncthreads();
+      }
+      REFILL_STAMP(stm[sb + 4], "v"(f));
+      if (lane == 0) {
+        A.i32(U_FILL)[e] = f;
+        A.refill_list(1)[rr] = f0;
+        A.refill_list(2)[rr] = f;
+      }
     }
   }
 #ifdef SACENV_STAMPS
@@ -1166,13 +1109,55 @@ __global__ void __launch_bounds__(kWave) k_refill_fit(SacenvBoatParams p, Arena 
 // their ring was last topped up (fill < cons + SLOTS), one 64-bit mask per
 // owner wave. Derived from the episode counters, so the step launch keeps no
 // flags of its own (measured: owner-side flag words cost 0.25-0.4 us/step).
-__global__ void __launch_bounds__(kWave) k_need_masks(SacenvBoatParams p, Arena A) {
-  const int w = blockIdx.x, e = w * kWave + threadIdx.x;
-  const int c = e < p.n_envs ? A.i32(U_CONS)[e] : 0;
-  const bool need = e < p.n_envs && A.i32(U_FILL)[e] < c + kSlots;
-  const unsigned long long m = __ballot(need);
-  if (threadIdx.x == 0) A.refill_mask()[w] = m;
-  if (need) A.cons_snap()[e] = c;
+// 16 owner waves' envs per workgroup (one wave each). The LAST workgroup to
+// finish (a ticket in status[3]) ranks the flagged envs for launch 1: a block
+// scan of the mask popcounts, then every flagged env's id at its rank in
+// refill_list(0) and the count in status[2]. k_refill then finds its envs with
+// one load each instead of a wave-wide search per env.
+constexpr int kMaskThreads = 1024;
+__global__ void __launch_bounds__(kMaskThreads) k_need_masks(SacenvBoatParams p, Arena A) {
+  __shared__ int wsum[kMaskThreads / kWave];
+  __shared__ int last;
+  const int t = threadIdx.x, lane = t & (kWave - 1), wv = t >> 6;
+  const int nw = A.nwaves();
+  const int w = blockIdx.x * (kMaskThreads / kWave) + wv, e = w * kWave + lane;
+  if (w < nw) {
+    const int c = e < p.n_envs ? A.i32(U_CONS)[e] : 0;
+    const bool need = e < p.n_envs && A.i32(U_FILL)[e] < c + kSlots;
+    const unsigned long long m = __ballot(need);
+    if (lane == 0) A.refill_mask()[w] = m;
+    if (need) A.cons_snap()[e] = c;
+  }
+  // the masks of this workgroup, device-wide, before its ticket
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __syncthreads();
+  if (t == 0) last = atomicAdd(&A.status()[3], 1) == (int)gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every workgroup's masks
+  const unsigned long long* masks = A.refill_mask();
+  int base = 0;
+  for (int w0 = 0; w0 < nw; w0 += kMaskThreads) {  // one mask per thread and pass
+    const int mw = w0 + t;
+    const unsigned long long m = mw < nw ? masks[mw] : 0ull;
+    const int cnt = __popcll(m);
+    const int incl = wave_incl_scan(cnt);
+    if (lane == kWave - 1) wsum[wv] = incl;
+    __syncthreads();
+    int before = base;
+    for (int k = 0; k < wv; ++k) before += wsum[k];
+    int pos = before + incl - cnt;
+    for (unsigned long long b = m; b; b &= b - 1ull)
+      A.refill_list(0)[pos++] = mw * kWave + (__ffsll((long long)b) - 1);
+    int tot = 0;
+    for (int k = 0; k < kMaskThreads / kWave; ++k) tot += wsum[k];
+    base += tot;
+    __syncthreads();
+  }
+  if (t == 0) {
+    A.status()[2] = base;
+    A.status()[3] = 0;  // the next refill's tickets
+  }
 }
 
 // Uniform fp64 constants as VGPR copies: the step reads ~40 config doubles,
@@ -2248,7 +2233,8 @@ int sacenv_boat_refill(const SacenvBoatParams* p, void* arena, void* stream) {
   if (arena == nullptr) return SACENV_E_NULL;
   if (!p->autoreset) return SACENV_E_MODE;
   const Arena A = make_arena(*p, arena);
-  hipLaunchKernelGGL(k_need_masks, dim3((unsigned)(A.np / kWave)), dim3(kWave), 0, (hipStream_t)stream, *p, A);
+  const unsigned mask_blocks = (unsigned)((A.np / kWave + kMaskThreads / kWave - 1) / (kMaskThreads / kWave));
+  hipLaunchKernelGGL(k_need_masks, dim3(mask_blocks), dim3(kMaskThreads), 0, (hipStream_t)stream, *p, A);
   if ((rc = launch_status())) return rc;
   hipLaunchKernelGGL(k_refill, dim3(p->n_helpers), dim3(kWave), 0, (hipStream_t)stream, *p, A);
   if ((rc = launch_status())) return rc;
