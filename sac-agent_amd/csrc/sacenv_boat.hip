@@ -1130,10 +1130,14 @@ __global__ void __launch_bounds__(kMaskThreads) k_need_masks(SacenvBoatParams p,
     if (lane == 0) A.refill_mask()[w] = m;
     if (need) A.cons_snap()[e] = c;
   }
-  // the masks of this workgroup, device-wide, before its ticket
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  // the masks of this workgroup, device-wide, before its ticket: the barrier
+  // orders every wave's stores before thread 0's agent-scope release (one L2
+  // write-back per workgroup, not one per wave)
   __syncthreads();
-  if (t == 0) last = atomicAdd(&A.status()[3], 1) == (int)gridDim.x - 1;
+  if (t == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    last = atomicAdd(&A.status()[3], 1) == (int)gridDim.x - 1;
+  }
   __syncthreads();
   if (!last) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every workgroup's masks
