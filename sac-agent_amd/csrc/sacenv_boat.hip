@@ -1152,9 +1152,18 @@ __global__ void __launch_bounds__(kMaskThreads) k_need_masks(SacenvBoatParams p,
     __syncthreads();
     int before = base;
     for (int k = 0; k < wv; ++k) before += wsum[k];
-    int pos = before + incl - cnt;
-    for (unsigned long long b = m; b; b &= b - 1ull)
-      A.refill_list(0)[pos++] = mw * kWave + (__ffsll((long long)b) - 1);
+    const int pos = before + incl - cnt;  // rank of this thread's mask's first env
+    // the wave's 64 masks one at a time, lane l taking bit l: each mask's envs go
+    // out as one coalesced store (a lane per bit, not a scattered loop per lane)
+    for (int i = 0; i < kWave; ++i) {
+      const unsigned long long mi =
+          ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(m >> 32), i) << 32) |
+          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)m, i);
+      if (mi == 0ull) continue;  // uniform
+      const int pi = __builtin_amdgcn_readlane(pos, i);
+      if ((mi >> lane) & 1ull)
+        A.refill_list(0)[pi + __popcll(mi & ((1ull << lane) - 1ull))] = (w0 + wv * kWave + i) * kWave + lane;
+    }
     int tot = 0;
     for (int k = 0; k < kMaskThreads / kWave; ++k) tot += wsum[k];
     base += tot;
