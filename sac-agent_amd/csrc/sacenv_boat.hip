@@ -1125,17 +1125,28 @@ __global__ void __launch_bounds__(kMaskThreads) k_need_masks(SacenvBoatParams p,
   __shared__ int wsum[kMaskWaves];
   const int t = threadIdx.x, lane = t & (kWave - 1), wv = t >> 6;
   const int nw = A.nwaves();
-#pragma unroll 4
-  for (int w = wv; w < nw; w += kMaskWaves) {
-    const int e = w * kWave + lane;
-    const int c = e < p.n_envs ? A.i32(U_CONS)[e] : 0;
-    const bool need = e < p.n_envs && A.i32(U_FILL)[e] < c + kSlots;
-    const unsigned long long m = __ballot(need);
-    if (lane == 0) {
-      A.refill_mask()[w] = m;
-      if (w < kMaskLds) ml[w] = m;
+  constexpr int kBatch = 8;  // owner waves per wave whose counters are in flight together
+  for (int w0 = wv; w0 < nw; w0 += kBatch * kMaskWaves) {
+    int c[kBatch], f[kBatch];
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j) {
+      const int e = (w0 + j * kMaskWaves) * kWave + lane;
+      const bool in = w0 + j * kMaskWaves < nw && e < p.n_envs;
+      c[j] = in ? A.i32(U_CONS)[e] : 0;
+      f[j] = in ? A.i32(U_FILL)[e] : 0x7fffffff;
     }
-    if (need) A.cons_snap()[e] = c;
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j) {
+      const int w = w0 + j * kMaskWaves;
+      if (w >= nw) break;  // uniform
+      const bool need = f[j] < c[j] + kSlots;
+      const unsigned long long m = __ballot(need);
+      if (lane == 0) {
+        A.refill_mask()[w] = m;
+        if (w < kMaskLds) ml[w] = m;
+      }
+      if (need) A.cons_snap()[w * kWave + lane] = c[j];
+    }
   }
   __syncthreads();
   int base = 0;
