@@ -1111,48 +1111,41 @@ __global__ void __launch_bounds__(kWave) k_refill_fit(SacenvBoatParams p, Arena 
 // their ring was last topped up (fill < cons + SLOTS), one 64-bit mask per
 // owner wave. Derived from the episode counters, so the step launch keeps no
 // flags of its own (measured: owner-side flag words cost 0.25-0.4 us/step).
-// ONE workgroup of 1024 lanes: wave v takes owner waves v, v+16, ... (one env per
-// lane, coalesced), flags the envs whose ring is short (fill < cons + SLOTS),
-// keeps their cons snapshot and the masks (global and LDS), then ranks the
-// flagged envs for launch 1: a block scan of the mask popcounts, every flagged
-// env's id at its rank in refill_list(0) (one coalesced store per mask), the count
-// in status[2]. k_refill then finds its envs with one load each. One workgroup:
-// no grid-wide handshake (measured: a last-workgroup ticket cost 10 us more).
-constexpr int kMaskThreads = 1024, kMaskWaves = kMaskThreads / kWave;
-constexpr int kMaskLds = 1024;  // masks kept in LDS (owner waves <= 1024 at 65 536 envs)
+// 16 owner waves' envs per workgroup (one wave each). The LAST workgroup to
+// finish (a ticket in status[3]) ranks the flagged envs for launch 1: a block
+// scan of the mask popcounts, then every flagged env's id at its rank in
+// refill_list(0) and the count in status[2]. k_refill then finds its envs with
+// one load each instead of a wave-wide search per env.
+constexpr int kMaskThreads = 1024;
 __global__ void __launch_bounds__(kMaskThreads) k_need_masks(SacenvBoatParams p, Arena A) {
-  __shared__ unsigned long long ml[kMaskLds];
-  __shared__ int wsum[kMaskWaves];
+  __shared__ int wsum[kMaskThreads / kWave];
+  __shared__ int last;
   const int t = threadIdx.x, lane = t & (kWave - 1), wv = t >> 6;
   const int nw = A.nwaves();
-  constexpr int kBatch = 8;  // owner waves per wave whose counters are in flight together
-  for (int w0 = wv; w0 < nw; w0 += kBatch * kMaskWaves) {
-    int c[kBatch], f[kBatch];
-#pragma unroll
-    for (int j = 0; j < kBatch; ++j) {
-      const int e = (w0 + j * kMaskWaves) * kWave + lane;
-      const bool in = w0 + j * kMaskWaves < nw && e < p.n_envs;
-      c[j] = in ? A.i32(U_CONS)[e] : 0;
-      f[j] = in ? A.i32(U_FILL)[e] : 0x7fffffff;
-    }
-#pragma unroll
-    for (int j = 0; j < kBatch; ++j) {
-      const int w = w0 + j * kMaskWaves;
-      if (w >= nw) break;  // uniform
-      const bool need = f[j] < c[j] + kSlots;
-      const unsigned long long m = __ballot(need);
-      if (lane == 0) {
-        A.refill_mask()[w] = m;
-        if (w < kMaskLds) ml[w] = m;
-      }
-      if (need) A.cons_snap()[w * kWave + lane] = c[j];
-    }
+  const int w = blockIdx.x * (kMaskThreads / kWave) + wv, e = w * kWave + lane;
+  if (w < nw) {
+    const int c = e < p.n_envs ? A.i32(U_CONS)[e] : 0;
+    const bool need = e < p.n_envs && A.i32(U_FILL)[e] < c + kSlots;
+    const unsigned long long m = __ballot(need);
+    if (lane == 0) A.refill_mask()[w] = m;
+    if (need) A.cons_snap()[e] = c;
+  }
+  // the masks of this workgroup, device-wide, before its ticket: the barrier
+  // orders every wave's stores before thread 0's agent-scope release (one L2
+  // write-back per workgroup, not one per wave)
+  __syncthreads();
+  if (t == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    last = atomicAdd(&A.status()[3], 1) == (int)gridDim.x - 1;
   }
   __syncthreads();
+  if (!last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every workgroup's masks
+  const unsigned long long* masks = A.refill_mask();
   int base = 0;
   for (int w0 = 0; w0 < nw; w0 += kMaskThreads) {  // one mask per thread and pass
     const int mw = w0 + t;
-    const unsigned long long m = mw < nw ? (mw < kMaskLds ? ml[mw] : A.refill_mask()[mw]) : 0ull;
+    const unsigned long long m = mw < nw ? masks[mw] : 0ull;
     const int cnt = __popcll(m);
     const int incl = wave_incl_scan(cnt);
     if (lane == kWave - 1) wsum[wv] = incl;
@@ -1172,11 +1165,14 @@ __global__ void __launch_bounds__(kMaskThreads) k_need_masks(SacenvBoatParams p,
         A.refill_list(0)[pi + __popcll(mi & ((1ull << lane) - 1ull))] = (w0 + wv * kWave + i) * kWave + lane;
     }
     int tot = 0;
-    for (int k = 0; k < kMaskWaves; ++k) tot += wsum[k];
+    for (int k = 0; k < kMaskThreads / kWave; ++k) tot += wsum[k];
     base += tot;
     __syncthreads();
   }
-  if (t == 0) A.status()[2] = base;
+  if (t == 0) {
+    A.status()[2] = base;
+    A.status()[3] = 0;  // the next refill's tickets
+  }
 }
 
 // Uniform fp64 constants as VGPR copies: the step reads ~40 config doubles,
@@ -2253,7 +2249,8 @@ int sacenv_boat_refill(const SacenvBoatParams* p, void* arena, void* stream) {
   if (arena == nullptr) return SACENV_E_NULL;
   if (!p->autoreset) return SACENV_E_MODE;
   const Arena A = make_arena(*p, arena);
-  hipLaunchKernelGGL(k_need_masks, dim3(1), dim3(kMaskThreads), 0, (hipStream_t)stream, *p, A);
+  const unsigned mask_blocks = (unsigned)((A.np / kWave + kMaskThreads / kWave - 1) / (kMaskThreads / kWave));
+  hipLaunchKernelGGL(k_need_masks, dim3(mask_blocks), dim3(kMaskThreads), 0, (hipStream_t)stream, *p, A);
   if ((rc = launch_status())) return rc;
   hipLaunchKernelGGL(k_refill, dim3(p->n_helpers), dim3(kWave), 0, (hipStream_t)stream, *p, A);
   if ((rc = launch_status())) return rc;
