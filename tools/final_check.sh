@@ -2,36 +2,48 @@
 # Round-end evidence on one GPU box, each GPU step under its own time limit,
 # the first failure ends the script:
 #   parity tests (log kept), smoke(), the driver's bench command, the default
-#   bench line with cpu_baseline, the config lines (C2 per step and as K-step
-#   rollouts, C5 mixed, the K=128 rollout), phase stamps, then tools/pmc.sh
-#   (kernel trace + calibrated PMC passes).
+#   bench line (persistent segments) with cpu_baseline, the per-step-launch line,
+#   the config lines (C2, C5 mixed, 131 072 envs, the K=128 rollout), the N=2
+#   rehearsal over gloo on the one GPU (segment pooling and per-step pooling),
+#   the refill phase clocks, then tools/pmc.sh (kernel trace + calibrated PMC
+#   passes of the persistent segment kernel).
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread \
-  -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -4 gpurun_out/pytest_gpu.log
-[ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit 1
-tail -1 gpurun_out/smoke.log
+if [ -z "$SKIP_TESTS" ]; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread \
+    -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+  rc=$?; echo "pytest rc=$rc"; tail -4 gpurun_out/pytest_gpu.log
+  [ $rc -eq 0 ] || exit $rc
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit 1
+  tail -1 gpurun_out/smoke.log
+fi
 B="timeout -k 10 300 python bench.py"
 $B --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_driver.json 2> gpurun_out/bench_driver.log || exit 1
 $B > gpurun_out/bench_default.json 2> gpurun_out/bench_default.log || exit 1
+$B --launch step --no-cpu-baseline > gpurun_out/bench_step.json 2> gpurun_out/bench_step.log || exit 1
 $B --experiment 1 --envs 4096 --cpu-seconds 6 > gpurun_out/bench_c2.json 2> gpurun_out/bench_c2.log || exit 1
-$B --experiment 1 --envs 4096 --rollout 128 > gpurun_out/bench_c2_rollout.json 2> gpurun_out/bench_c2_rollout.log || exit 1
 $B --mixed --cpu-seconds 6 > gpurun_out/bench_c5.json 2> gpurun_out/bench_c5.log || exit 1
 $B --rollout 128 > gpurun_out/bench_rollout_k128.json 2> gpurun_out/bench_rollout_k128.log || exit 1
 $B --envs 131072 --no-cpu-baseline > gpurun_out/bench_131k.json 2> gpurun_out/bench_131k.log || exit 1
 python - <<'PY'
 import json
-for f in ("driver", "default", "c2", "c2_rollout", "c5", "rollout_k128", "131k"):
+for f in ("driver", "default", "step", "c2", "c5", "rollout_k128", "131k"):
     d = json.load(open(f"gpurun_out/bench_{f}.json"))
     r, c = d["roofline"], d.get("cpu_baseline")
     k = r.get("kernel_avg_us", r.get("kernel_avg_us_per_step"))
     print(f"{f:13s} {d['value']/1e9:7.3f} G/s {d['ms_per_step']*1e3:6.2f} us/step kernel {k:5.2f} us "
           f"frac {r['frac']:.3f} cpu {c and round(c['value'])}")
 PY
-timeout -k 10 300 python tools/stamps.py --rebuild > gpurun_out/stamps_full.txt 2>&1 || exit 1
+for pe in 128 1; do
+  port=$((29500 + pe))
+  SACENV_BENCH_BACKEND=gloo SACENV_BENCH_ONE_DEVICE=1 timeout -k 10 300 python -m torch.distributed.run \
+    --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port $port bench.py --gpus 2 \
+    --envs 65536 --pool-every $pe --steps 256 --warmup 128 > gpurun_out/rehearse_pe$pe.json \
+    2> gpurun_out/rehearse_pe$pe.log || { tail -20 gpurun_out/rehearse_pe$pe.log; exit 1; }
+  tail -1 gpurun_out/rehearse_pe$pe.json | python -c "import json,sys;d=json.loads(sys.stdin.read());print('rehearse pool_every', d['pooling']['pool_every'], round(d['value']/1e9,3), 'G/s', d['dist']['backend'], d['pooling']['received_GBps_per_rank'])"
+done
+timeout -k 10 300 python tools/refill_stamps.py --rebuild > gpurun_out/refill_stamps.txt 2>&1 || exit 1
 bash tools/pmc.sh > gpurun_out/pmc.log 2>&1 || { tail -20 gpurun_out/pmc.log; exit 1; }
-python -c "import json;d=json.load(open('gpurun_out/pmc_k_step.json'));print('pmc', d['trace_avg_ns'], d['hbm_bytes_per_launch'])"
+python -c "import json;d=json.load(open('gpurun_out/pmc_segment.json'));print('pmc', d['trace_avg_ns_per_step'], d['hbm_bytes_per_step'])"
 echo final_check done
