@@ -5,7 +5,7 @@
 #   bench line (persistent segments) with cpu_baseline, the per-step-launch line,
 #   the config lines (C2, C5 mixed, 131 072 envs, the K=128 rollout), the N=2
 #   rehearsal over gloo on the one GPU (segment pooling and per-step pooling),
-#   the refill phase clocks, then tools/pmc.sh (kernel trace + calibrated PMC
+#   then tools/pmc.sh (kernel trace + calibrated PMC
 #   passes of the persistent segment kernel).
 set -o pipefail
 export TMPDIR=/tmp
@@ -43,7 +43,6 @@ for pe in 128 1; do
     2> gpurun_out/rehearse_pe$pe.log || { tail -20 gpurun_out/rehearse_pe$pe.log; exit 1; }
   tail -1 gpurun_out/rehearse_pe$pe.json | python -c "import json,sys;d=json.loads(sys.stdin.read());print('rehearse pool_every', d['pooling']['pool_every'], round(d['value']/1e9,3), 'G/s', d['dist']['backend'], d['pooling']['received_GBps_per_rank'])"
 done
-timeout -k 10 300 python tools/refill_stamps.py --rebuild > gpurun_out/refill_stamps.txt 2>&1 || exit 1
 bash tools/pmc.sh > gpurun_out/pmc.log 2>&1 || { tail -20 gpurun_out/pmc.log; exit 1; }
 python -c "import json;d=json.load(open('gpurun_out/pmc_segment.json'));print('pmc', d['trace_avg_ns_per_step'], d['hbm_bytes_per_step'])"
 echo final_check done
