@@ -98,8 +98,15 @@ def main(out_dir):
     if STEPS_PER_LAUNCH > 1 and "hbm_bytes_per_launch" in res:
         res["steps_per_launch"] = STEPS_PER_LAUNCH
         res["hbm_bytes_per_step"] = res["hbm_bytes_per_launch"] / STEPS_PER_LAUNCH
-        if "trace_avg_ns" in res:
-            res["trace_avg_ns_per_step"] = res["trace_avg_ns"] / STEPS_PER_LAUNCH
+        # the per-step time from the full-length launches of the trace (the bench's
+        # warm-up launch runs 3 steps)
+        tr = [r for r in rows(os.path.join(out_dir, "prof_trace", "**", "*kernel_trace.csv"))
+              if KERNEL in r.get("Kernel_Name", "")]
+        d = sorted(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in tr)
+        if d:
+            full = [x for x in d if x >= 0.5 * d[len(d) // 2]]
+            res["trace_full_launches"] = len(full)
+            res["trace_avg_ns_per_step"] = sum(full) / len(full) / STEPS_PER_LAUNCH
     name = "pmc_k_step.json" if KERNEL == "k_step" else "pmc_segment.json"
     json.dump(res, open(os.path.join(out_dir, name), "w"), indent=1)
     print(json.dumps(res, indent=1))
