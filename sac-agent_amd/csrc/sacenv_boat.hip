@@ -329,65 +329,98 @@ __device__ __forceinline__ void wind_at(const SacenvBoatParams& p, const Arena& 
   }
 }
 
-// a * b + c with c a compile-time constant: one VOP3 v_fma_f64 reading c from
-// a scalar register pair (two SALU moves, off the VALU). Written as plain
-// fma(), the compiler builds each 64-bit coefficient in the accumulator with
-// two v_mov_b32 and a v_fmac: three VALU per polynomial term instead of one.
-__device__ __forceinline__ double fma_sc(double a, double b, double c) {
+// The polynomial coefficients below as loop-invariant VGPR copies (trig_k(),
+// once per launch). Written as plain fma() with literals, the compiler builds
+// each 64-bit coefficient with two v_mov_b32 and a v_fmac; read from SGPRs,
+// it rebuilt them with two s_mov_b32 per use inside the step loop (the SGPR
+// file is full with the loop's addresses): ~60 SALU issue slots per step.
+struct TrigK {
+  double s[10];  // sine series: 1/21!, -1/19!, 1/17!, ..., -1/3! (sincos_fast uses the last 8)
+  double c[7];   // cosine series: 1/16!, -1/14!, ..., 1/4!
+  double e[10];  // exp_v's polynomial (ocml's exp coefficients)
+};
+__device__ __forceinline__ double vconst(double x) {
   double r;
-  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+  asm volatile("v_mov_b64 %0, %1" : "=v"(r) : "s"(x));
+  return r;
+}
+__device__ __forceinline__ TrigK trig_k() {
+  constexpr double sn[10] = {1.9572941063391262e-20,  -8.22063524662432950e-18, 2.8114572543455206e-15,
+                             -7.647163731819816e-13,  1.6059043836821613e-10,   -2.505210838544172e-08,
+                             2.7557319223985893e-06,  -1.984126984126984e-04,   8.333333333333333e-03,
+                             -1.6666666666666666e-01};
+  constexpr double cs[7] = {4.779477332387385e-14, -1.1470745597729725e-11, 2.08767569878681e-09,
+                            -2.755731922398589e-07, 2.48015873015873e-05,   -1.388888888888889e-03,
+                            4.1666666666666664e-02};
+  TrigK k;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) k.s[i] = vconst(sn[i]);
+#pragma unroll
+  for (int i = 0; i < 7; ++i) k.c[i] = vconst(cs[i]);
+  constexpr double ex[10] = {2.5022322536502990e-08, 2.7630903490112654e-07, 2.755751454582531e-06,
+                             2.480149103909504e-05,  1.9841269589115522e-04, 1.3888888945916382e-03,
+                             8.333333333455043e-03,  4.1666666666519754e-02, 1.6666666666666477e-01,
+                             5.000000000000012e-01};
+#pragma unroll
+  for (int i = 0; i < 10; ++i) k.e[i] = vconst(ex[i]);
+  return k;
+}
+__device__ __forceinline__ double fma_v(double a, double b, double c) {
+  double r;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
   return r;
 }
 
-// sin(x) for |x| <= 1.25 with no argument reduction: x + x^3 P(x^2), P the
-// Taylor series through x^21 (truncation < 1e-20, below half an ulp), about
-// 12 FMAs against ocml's reduction + two polynomials + select. Waves with any
-// lane beyond the bound take ocml's sin (a uniform branch).
-__device__ __forceinline__ double sin_reduced(double x) {
-  constexpr double kBound = 1.25;
-  if (__ballot(!(fabs(x) <= kBound)) != 0ull) return sin(x);
-  const double z = x * x;
-  double q = fma_sc(z, -1.9572941063391262e-20, 8.22063524662432950e-18);  // -1/21!, 1/19!
-  q = fma_sc(q, z, -2.8114572543455206e-15);   // -1/17!
-  q = fma_sc(q, z, 7.6471637318198164e-13);    // 1/15!
-  q = fma_sc(q, z, -1.6059043836821613e-10);   // -1/13!
-  q = fma_sc(q, z, 2.5052108385441720e-08);    // 1/11!
-  q = fma_sc(q, z, -2.7557319223985893e-06);   // -1/9!
-  q = fma_sc(q, z, 1.9841269841269841e-04);    // 1/7!
-  q = fma_sc(q, z, -8.3333333333333333e-03);   // -1/5!
-  q = fma_sc(q, z, 1.6666666666666666e-01);    // 1/3! (sign below)
-  return fma(-(x * z), q, x);
+// exp(x): ocml's __ocml_exp_f64 restated operation for operation (the same
+// double for every x, NaN and the range ends included: within 1 ulp of glibc,
+// tools/ubench notes), its polynomial read from VGPRs. Inlined from the
+// library, the compiler kept the coefficients in VGPRs but fed them to
+// v_fmac, copying each one first: 9 v_mov_b64 a step.
+__device__ __forceinline__ double exp_v(double x, const TrigK& K) {
+  const double n = rint(x * 1.4426950408889634);
+  double r = fma(-0.69314718055994529, n, x);
+  r = fma(-2.3190468138462996e-17, n, r);
+  double q = fma_v(K.e[0], r, K.e[1]);
+#pragma unroll
+  for (int i = 2; i < 10; ++i) q = fma_v(r, q, K.e[i]);
+  q = fma(r, q, 1.0);
+  q = fma(r, q, 1.0);
+  double e = ldexp(q, (int)n);
+  e = 1024.0 < x ? __builtin_inf() : e;
+  return -1075.0 > x ? 0.0 : e;
 }
 
-// sin and cos of x for |x| <= 1e5: k = rint(x 2/pi), r = x - k pi/2 by fma in
-// three Cody-Waite terms (each fma rounds once: r within ~1 ulp), Taylor
+// sin(x) for |x| <= kSinBound with no argument reduction: x + x^3 P(x^2), P
+// the Taylor series through x^21 (truncation < 1e-20, below half an ulp),
+// about 12 FMAs against ocml's reduction + two polynomials + select.
+constexpr double kSinBound = 1.25;
+__device__ __forceinline__ double sin_taylor(double x, const TrigK& K) {
+  const double z = x * x;
+  double q = fma_v(z, K.s[0], K.s[1]);
+#pragma unroll
+  for (int i = 2; i < 10; ++i) q = fma_v(q, z, K.s[i]);
+  return fma(x * z, q, x);  // the negated series of before, bit for bit
+}
+
+// sin and cos of x for |x| <= kCwBound: k = rint(x 2/pi), r = x - k pi/2 by fma
+// in three Cody-Waite terms (each fma rounds once: r within ~1 ulp), Taylor
 // polynomials on |r| <= pi/4 (sin through r^17, cos through r^16: truncation
-// below 1e-17) and the quadrant swap. Waves with any lane beyond the bound
-// (or NaN) take ocml's sincos (a uniform branch).
-__device__ __forceinline__ void sincos_cw(double x, double* sp, double* cp) {
-  if (__ballot(!(fabs(x) <= 1.0e5)) != 0ull) {
-    sincos(x, sp, cp);
-    return;
-  }
+// below 1e-17) and the quadrant swap. Within 1 ulp of glibc's sin/cos up to
+// 1e13 (measured, 2e6 samples per decade); the bound keeps (int)k exact.
+constexpr double kCwBound = 1.0e5;
+__device__ __forceinline__ void sincos_fast(double x, double* sp, double* cp, const TrigK& K) {
   const double k = rint(x * 0.6366197723675814);
   double r = fma(-k, 1.5707963267948966, x);
   r = fma(-k, 6.123233995736766e-17, r);
   r = fma(-k, -1.4973849048591698e-33, r);
   const double z = r * r;
-  double ps = fma_sc(z, 2.8114572543455206e-15, -7.647163731819816e-13);  // 1/17!, -1/15!
-  ps = fma_sc(ps, z, 1.6059043836821613e-10);     // 1/13!
-  ps = fma_sc(ps, z, -2.505210838544172e-08);     // -1/11!
-  ps = fma_sc(ps, z, 2.7557319223985893e-06);     // 1/9!
-  ps = fma_sc(ps, z, -1.984126984126984e-04);     // -1/7!
-  ps = fma_sc(ps, z, 8.333333333333333e-03);      // 1/5!
-  ps = fma_sc(ps, z, -1.6666666666666666e-01);    // -1/3!
+  double ps = fma_v(z, K.s[2], K.s[3]);
+#pragma unroll
+  for (int i = 4; i < 10; ++i) ps = fma_v(ps, z, K.s[i]);
   const double sr = fma(r * z, ps, r);
-  double pc = fma_sc(z, 4.779477332387385e-14, -1.1470745597729725e-11);  // 1/16!, -1/14!
-  pc = fma_sc(pc, z, 2.08767569878681e-09);       // 1/12!
-  pc = fma_sc(pc, z, -2.755731922398589e-07);     // -1/10!
-  pc = fma_sc(pc, z, 2.48015873015873e-05);       // 1/8!
-  pc = fma_sc(pc, z, -1.388888888888889e-03);     // -1/6!
-  pc = fma_sc(pc, z, 4.1666666666666664e-02);     // 1/4!
+  double pc = fma_v(z, K.c[0], K.c[1]);
+#pragma unroll
+  for (int i = 2; i < 7; ++i) pc = fma_v(pc, z, K.c[i]);
   const double cr = 1.0 - fma(-(z * z), pc, 0.5 * z);
   const int q = (int)k;
   const double a = (q & 1) ? cr : sr, b = (q & 1) ? sr : cr;  // sin, cos of r + (q&1) pi/2
@@ -395,6 +428,50 @@ __device__ __forceinline__ void sincos_cw(double x, double* sp, double* cp) {
   *cp = ((q + 1) & 2) ? -b : b;
 }
 
+// The fast forms for every lane, then ocml's for the lanes outside their
+// range (NaN included) behind one wave-uniform branch that is almost never
+// taken: a lane's result depends on its own argument only. Each such branch
+// ends a scheduling region, so the step evaluates its early transcendentals
+// (wind angle, advance ratio, rudder: all known once the action is in) in
+// one region (trig3), where the three chains interleave, and keeps the one
+// late one (yaw) on its own.
+// (ocml's functions stay inline: called out of line, to keep their tables
+// and temporaries out of the step loop's registers, the step measured
+// 0.12 us slower -- the call's register save and restore conventions)
+struct SinCos {
+  double s, c;
+};
+__device__ __forceinline__ double sin_ocml(double x) { return sin(x); }
+__device__ __forceinline__ SinCos sincos_ocml(double x) {
+  SinCos r;
+  sincos(x, &r.s, &r.c);
+  return r;
+}
+
+__device__ __forceinline__ void sincos_cw(double x, double* sp, double* cp, const TrigK& K) {
+  sincos_fast(x, sp, cp, K);
+  const bool ok = fabs(x) <= kCwBound;
+  if (__ballot(!ok) != 0ull && !ok) {
+    const SinCos r = sincos_ocml(x);
+    *sp = r.s, *cp = r.c;
+  }
+}
+
+__device__ __forceinline__ void trig3(double j, double r, double w, double* sj, double* sr, double* sw,
+                                      double* cw, const TrigK& K) {
+  *sj = sin_taylor(j, K);
+  *sr = sin_taylor(r, K);
+  sincos_fast(w, sw, cw, K);
+  const bool okj = fabs(j) <= kSinBound, okr = fabs(r) <= kSinBound, okw = fabs(w) <= kCwBound;
+  if (__ballot(!(okj && okr && okw)) != 0ull) {
+    if (!okj) *sj = sin_ocml(j);
+    if (!okr) *sr = sin_ocml(r);
+    if (!okw) {
+      const SinCos q = sincos_ocml(w);
+      *sw = q.s, *cw = q.c;
+    }
+  }
+}
 
 // x / c for a per-launch constant c, from r = RN(1/c): Markstein's correction
 // step returns the correctly rounded quotient, i.e. the same double as IEEE
@@ -1523,6 +1600,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   // measured 0.09 us/step faster than doing it here, behind the burst)
   const SacenvBoatParams& p = pin;
   const Tail& T = Tin;
+  const TrigK K = trig_k();
   // Wind.get_wind(index) (wind.py:20-24, IndexError guard) of this step. Curves:
   // from the lane's copy of its spline piece (wind_coef, loaded with the
   // state). The copy is refreshed from the active slot at the end of a step
@@ -1539,7 +1617,25 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
       if (c < nc) y0c[c] = A.f64e(U_W0N + 8 * c, eo);
     if (p.experiment == 2) syc = A.i32e(U_SYN, eo4);
   }
+#ifdef SACENV_STAMPS
+  // per-phase shader-clock sums over a launch's steps (tools/phase_stamps.py):
+  // issue-progress clocks, no waits added; sched barriers pin the phase edges
+  uint64_t ph[4] = {0, 0, 0, 0}, ph_t = 0;
+#define PHASE(i)                                         \
+  do {                                                   \
+    __builtin_amdgcn_sched_barrier(0);                   \
+    const uint64_t ph_now = __builtin_amdgcn_s_memtime(); \
+    if ((i) > 0) ph[(i) - 1] += ph_now - ph_t;           \
+    ph_t = ph_now;                                       \
+    __builtin_amdgcn_sched_barrier(0);                   \
+  } while (0)
+#else
+#define PHASE(i) \
+  do {           \
+  } while (0)
+#endif
   for (int ks = 0; ks < (kRoll ? n_steps : 1) && (!kHand || !failed); ++ks) {
+  PHASE(0);
   const float act = active ? act_cur : 0.0f;
   // the next step's action, a step ahead: open-loop rows at once; a handed-off
   // row if its flag already said so, else after this step's outputs (below)
@@ -1629,14 +1725,15 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   if (!t_idx) EARLY_STORE(U_T, t);
   const bool first = index == 0;  // integrator counter == 0 (control_blocks.py:21-22)
   const double wsign = (double)((wv > 0.0) - (wv < 0.0));
-  double swa, cwa;
-  sincos_cw(wa, &swa, &cwa);
+  const double v_x_w = v_x * p.one_minus_wf;
+  const double J = p.n_rpm != 0.0 ? div_c(v_x_w, p.n_times_d, r_nd) : 0.0;  // :222-224
+  double sin_J, sin_rud, swa, cwa;
+  trig3(J, rudder, wa, &sin_J, &sin_rud, &swa, &cwa, K);
+  PHASE(1);
 
   // eom_longitudinal :213-239
   const double F_R = v_x * v_x * p.c_r_front * 0.5 * p.rho * p.boat_area_front;
-  const double v_x_w = v_x * p.one_minus_wf;
-  const double J = p.n_rpm != 0.0 ? div_c(v_x_w, p.n_times_d, r_nd) : 0.0;  // :222-224
-  const double F_T = sin_reduced(J) * p.n_squared * p.rho * p.d_pow4 * p.one_minus_td;
+  const double F_T = sin_J * p.n_squared * p.rho * p.d_pow4 * p.one_minus_td;
   const double F_C = v_y * p.m_plus_my * v_r;
   const double F_W = (wv * wv * wsign * p.c_r_front * 0.5 * p.rho * p.boat_area_front) * cwa;
   const double a_x = div_c(-F_R + F_T + F_C + F_W, p.m_plus_mx, r_mx);
@@ -1645,7 +1742,6 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   // eom_transverse :241-265 (new v_x)
   const double vys = (double)((v_y > 0.0) - (v_y < 0.0));
   const double F_R2 = v_y * v_y * p.c_r_side * 0.5 * p.rho * p.boat_area_side * vys;
-  const double sin_rud = sin_reduced(rudder);
   const double F_RU = sin_rud * (v_x * v_x * p.c_r_front * 0.5 * p.rho * p.rudder_area);
   const double F_C2 = v_x * p.m_plus_mx * v_r;
   const double F_W2 = (wv * wv * wsign * p.c_r_side * 0.5 * p.rho * p.boat_area_side) * swa;
@@ -1669,40 +1765,36 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   // differences: the increments agree to a few ulp of v dt.
   s_r = v_r * p.dt + s_r;
   double ssr, csr;
-  sincos_cw(s_r, &ssr, &csr);
+  sincos_cw(s_r, &ssr, &csr, K);
   s_x = (v_x * csr - v_y * ssr) * p.dt + s_x;
   s_y = (v_y * csr + v_x * ssr) * p.dt + s_y;
   index = index + 1;
   EARLY_STORE2(U_SX, s_x, s_y);
   EARLY_STORE2(U_SR, s_r, v_x);
   if (!kRoll) st_out(A.i32e(U_IDX, eo4), index);
+  PHASE(2);
 
   Obs o = make_obs(p, oc, s_x, v_x, a_x, s_y, v_y, a_y, s_r, v_r, a_r, rudder, (double)fuel);
 
   // exponential_reward (reward_functions.py:42-57), f_x = 0
   const double ay = fabs(s_y);
-  const double f_y = div_c(ay, p.track_width, r_w) / (1.0 + exp(p.reward_k * (ay - p.reward_center)));
+  const double f_y = div_c(ay, p.track_width, r_w) / (1.0 + exp_v(p.reward_k * (ay - p.reward_center), K));
   double reward = 0.0 - f_y;
 
-  // termination chain :84-105
-  uint8_t term = SACENV_TERM_NONE;
-  if (s_x >= p.goal_line) {
-    term = SACENV_TERM_REACHED_GOAL;
-    reward = reward + 1000.0;
-  } else if (fabs(s_y) > p.oob_limit || s_x < 0.0) {
-    term = SACENV_TERM_OUT_OF_BOUNDS;
-  } else if (fuel < 0) {
-    term = SACENV_TERM_OUT_OF_FUEL;
-  } else if (p.t_max <= t) {
-    term = SACENV_TERM_TIMEOUT;
-  } else if (rudder > kPi / 3 || rudder < -kPi / 3) {
-    term = SACENV_TERM_RUDDER_BROKEN;
-  }
+  // termination chain :84-105 (the first true condition wins), as selects: as an
+  // if/else-if chain it compiled to nested exec-mask branches (~25 SALU a step)
+  const bool goal = s_x >= p.goal_line;
+  int tm = (rudder > kPi / 3) | (rudder < -kPi / 3) ? SACENV_TERM_RUDDER_BROKEN : SACENV_TERM_NONE;
+  tm = p.t_max <= t ? SACENV_TERM_TIMEOUT : tm;
+  tm = fuel < 0 ? SACENV_TERM_OUT_OF_FUEL : tm;
+  tm = (fabs(s_y) > p.oob_limit) | (s_x < 0.0) ? SACENV_TERM_OUT_OF_BOUNDS : tm;
+  tm = goal ? SACENV_TERM_REACHED_GOAL : tm;
+  reward = goal ? reward + 1000.0 : reward;
   // penalties :107-111
-  if (rudder > kPi / 4 || rudder < -kPi / 4) reward = reward - fabs(rudder) * 100.0;
-  if (fabs(s_r) > kPi / 2) reward = reward - 1.0;
+  reward = (rudder > kPi / 4) | (rudder < -kPi / 4) ? reward - fabs(rudder) * 100.0 : reward;
+  reward = fabs(s_r) > kPi / 2 ? reward - 1.0 : reward;
   ep = ep + reward;
-  if (!active) term = SACENV_TERM_NONE;  // padding lanes never end
+  uint8_t term = active ? (uint8_t)tm : (uint8_t)SACENV_TERM_NONE;  // padding lanes never end
 
   if (term != SACENV_TERM_NONE)  // no-return atomic: nothing on the critical path waits
     __hip_atomic_fetch_add(&A.at_e<uint32_t>(U_CNT + 4 * (term - 1), eo4), 1u, __ATOMIC_RELAXED,
@@ -1710,6 +1802,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   if (term == SACENV_TERM_NONE && active && p.max_episode_steps > 0 && index >= p.max_episode_steps)
     term = SACENV_TERM_TRUNCATED;
   const bool ended = term != SACENV_TERM_NONE;
+  PHASE(3);
 
   OWNER_STAMP(st_computed);
   // this step's outputs: the arena's record, or the multi-step launch's
@@ -1856,6 +1949,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
       act_cur = act_load(abase, (uint32_t)((ks + 1) * arow));
     }
   }
+  PHASE(4);
   }  // steps
   if (kHand && failed && ra->done != nullptr && lane == 0)  // waiters on this wave must not hang
     __hip_atomic_store(ra->done + ob, 0x7FFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1880,7 +1974,11 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
 
 #ifdef SACENV_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (lane == 0) {
+  if (kRoll && lane == 0) {  // phase sums (shader clocks) of this launch
+    double* d = A.accel() + (int64_t)ob * 8;
+    for (int i = 0; i < 4; ++i) d[i] = (double)ph[i];
+    d[4] = (double)n_steps;
+  } else if (lane == 0) {
     double* d = A.accel() + (int64_t)ob * 4;
     d[0] = (double)st_real0;
     d[1] = (double)__builtin_amdgcn_s_memrealtime();
