@@ -492,10 +492,21 @@ struct Obs {
 
 struct ObsConst {  // per-launch reciprocals of the config-dependent spans
   double goal, two_w, fuel;
+  // the literal spans' reciprocals (k[7]: the rudder offset pi/3), as VGPR
+  // copies in the step loop (obs_const_v): as literals each use cost two s_mov
+  double k[8];
 };
 
 __device__ __forceinline__ ObsConst obs_const(const Tail& T) {
-  return ObsConst{T.r_goal, T.r_two_w, T.r_fuel};
+  return ObsConst{T.r_goal, T.r_two_w, T.r_fuel,
+                  {1.0 / 5.0, 1.0 / 0.025, 1.0 / 0.37, 1.0 / (2 * kPi), 1.0 / 8.5e-3, 1.0 / 1.4e-5,
+                   1.0 / (kPi / 3 - (-kPi / 3)), kPi / 3}};
+}
+__device__ __forceinline__ ObsConst obs_const_v(const Tail& T) {
+  ObsConst o = obs_const(T);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o.k[i] = vconst(o.k[i]);
+  return o;
 }
 
 __device__ __forceinline__ Obs make_obs(const SacenvBoatParams& p, const ObsConst& oc, double s_x,
@@ -504,15 +515,15 @@ __device__ __forceinline__ Obs make_obs(const SacenvBoatParams& p, const ObsCons
                                         double fuel) {
   Obs o;
   o.v[0] = (float)div_c(s_x, p.goal_line, oc.goal);
-  o.v[1] = (float)(v_x * (1.0 / 5.0));
-  o.v[2] = (float)(a_x * (1.0 / 0.025));
+  o.v[1] = (float)(v_x * oc.k[0]);
+  o.v[2] = (float)(a_x * oc.k[1]);
   o.v[3] = (float)div_c(s_y + p.track_width, p.track_width + p.track_width, oc.two_w);
   o.v[4] = (float)(v_y * (1.0 / 2.0));
-  o.v[5] = (float)(a_y * (1.0 / 0.37));
-  o.v[6] = (float)(s_r * (1.0 / (2 * kPi)));
-  o.v[7] = (float)(v_r * (1.0 / 8.5e-3));
-  o.v[8] = (float)(a_r * (1.0 / 1.4e-5));
-  o.v[9] = (float)((rudder + kPi / 3) * (1.0 / (kPi / 3 - (-kPi / 3))));
+  o.v[5] = (float)(a_y * oc.k[2]);
+  o.v[6] = (float)(s_r * oc.k[3]);
+  o.v[7] = (float)(v_r * oc.k[4]);
+  o.v[8] = (float)(a_r * oc.k[5]);
+  o.v[9] = (float)((rudder + oc.k[7]) * oc.k[6]);
   o.v[10] = (float)div_c(fuel, (double)p.fuel0, oc.fuel);
   return o;
 }
@@ -525,9 +536,17 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 // DESIGN.md §4). Scalars as agent-scope relaxed atomic stores; the 16-B pairs
 // and obs rows (no 16-B sc1 atomic form) as write-through buffer stores (aux
 // bit 4).
-template <class T>
+// kWT false: a plain (write-back) store, for the open-loop multi-step launch,
+// whose record rows are rewritten every step in place: they stay in the XCD's
+// L2 and are written back once, at the launch's end (measured: a write-through
+// record made every step wait for the previous step's stores to reach memory,
+// as the step's loads count behind them in vmcnt)
+template <bool kWT = true, class T>
 __device__ __forceinline__ void st_out(T& ref, T v) {
-  __hip_atomic_store(&ref, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (kWT)
+    __hip_atomic_store(&ref, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    ref = v;
 }
 
 // a 16-B pair of the paired state (block unit u), write-through
@@ -1449,8 +1468,23 @@ __host__ __device__ inline bool t_from_index(double dt) {
     if (!kRoll) st_pair(A.b, (u), (uint32_t)A.np, eo, (v0), (v1));  \
   } while (0)
 
+// one env's row of ROW floats (4-B aligned) from registers: dwordx4 stores,
+// then the 1..3-float tail as one store
+template <int ROW>
+__device__ __forceinline__ void store_row(float* row, const float* w) {
+  typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+  typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
+  typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
+#pragma unroll
+  for (int i = 0; i + 4 <= ROW; i += 4) *reinterpret_cast<f4u*>(row + i) = f4u{w[i], w[i + 1], w[i + 2], w[i + 3]};
+  constexpr int t = ROW & ~3;
+  if (ROW - t == 3) *reinterpret_cast<f3u*>(row + t) = f3u{w[t], w[t + 1], w[t + 2]};
+  if (ROW - t == 2) *reinterpret_cast<f2u*>(row + t) = f2u{w[t], w[t + 1]};
+  if (ROW - t == 1) row[t] = w[t];
+}
+
 // 64 obs rows (2816 B) from LDS to a 16-B aligned row block: 3 float4 stores
-template <int ROW = SACENV_OBS_DIM>  // floats per env row (11: obs; 9: the pooled row's s')
+template <int ROW = SACENV_OBS_DIM, bool kWT = true>  // floats per env row (11: obs; 9: the pooled row's s')
 __device__ __forceinline__ void store_obs_block(const float* lds_rows, float* dst_rows, int lane) {
   const f4v* src = reinterpret_cast<const f4v*>(lds_rows);
   // write-through 16-B buffer stores (sc1, aux bit 4): 0.13 us/step faster than
@@ -1460,7 +1494,7 @@ __device__ __forceinline__ void store_obs_block(const float* lds_rows, float* ds
   for (int i = 0; i < (ROW * 16 + kWave - 1) / kWave; ++i) {
     const uint32_t q = (uint32_t)lane + kWave * i;
     if (q < kWave * ROW / 4)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, src[q]), r, q * 16u, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, src[q]), r, q * 16u, 0, kWT ? 16 : 0);
   }
 }
 
@@ -1536,10 +1570,12 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
 #ifdef SACENV_STAMPS
   const uint64_t st_real0 = __builtin_amdgcn_s_memrealtime();
   uint64_t st_loaded = 0, st_computed = 0;
-#define OWNER_STAMP(v)                                          \
-  do {                                                          \
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); \
-    v = __builtin_amdgcn_s_memrealtime();                       \
+#define OWNER_STAMP(v)                                            \
+  do {                                                            \
+    if (!kRoll) { /* (multi-step launches: the PHASE clocks) */   \
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); \
+      v = __builtin_amdgcn_s_memrealtime();                       \
+    }                                                             \
   } while (0)
 #else
 #define OWNER_STAMP(v) \
@@ -1600,7 +1636,9 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   // measured 0.09 us/step faster than doing it here, behind the burst)
   const SacenvBoatParams& p = pin;
   const Tail& T = Tin;
+  constexpr bool kWT = !kRoll || kHand;  // write-through outputs (st_out)
   const TrigK K = trig_k();
+  const ObsConst oc = obs_const_v(T);
   // Wind.get_wind(index) (wind.py:20-24, IndexError guard) of this step. Curves:
   // from the lane's copy of its spline piece (wind_coef, loaded with the
   // state). The copy is refreshed from the active slot at the end of a step
@@ -1716,7 +1754,6 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   }
   OWNER_STAMP(st_loaded);
   const double r_mx = T.r_mx, r_my = T.r_my, r_iz = T.r_iz, r_nd = T.r_nd, r_w = T.r_w;
-  const ObsConst oc = obs_const(T);
 
   // BoatEnv.step :69-73
   t = t_idx ? (double)(index + 1) * p.dt : t + p.dt;  // boat_env.py:69
@@ -1887,47 +1924,62 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
     syc = syn;
     cons = cons_out;
   }
-  st_out(*reinterpret_cast<float*>(R + 44 * A.np + eo4), (float)reward);
-  st_out(*reinterpret_cast<uint8_t*>(R + 48 * A.np + e), (uint8_t)(ended ? 1 : 0));
-  st_out(*reinterpret_cast<uint8_t*>(R + 49 * A.np + e), term);
-  // obs rows through LDS, stored as float4 (64 rows x 44 B = 176 float4); a
-  // restarting env's row is its new episode's first obs
+  st_out<kWT>(*reinterpret_cast<float*>(R + 44 * A.np + eo4), (float)reward);
+  st_out<kWT>(*reinterpret_cast<uint8_t*>(R + 48 * A.np + e), (uint8_t)(ended ? 1 : 0));
+  st_out<kWT>(*reinterpret_cast<uint8_t*>(R + 49 * A.np + e), term);
+  // a restarting env's row is its new episode's first obs
+  if (!kWT) {
+    // write-back record (open-loop multi-step launch): each lane stores its own
+    // 44-B row as 16 + 16 + 12 B (4-B aligned vector stores): 0.08 us/step
+    // cheaper than the LDS-staged block below, whose LDS round trip and waits
+    // sit on the step's path
+    float w[SACENV_OBS_DIM];
 #pragma unroll
-  for (int k = 0; k < SACENV_OBS_DIM; ++k) l.obs[lane * SACENV_OBS_DIM + k] = restart ? fo.v[k] : o.v[k];
-  // the rows are this wave's own LDS: a wave's LDS accesses run in issue order,
-  // so only the compiler must keep the stores ahead of the loads (no workgroup
-  // barrier: a step workgroup may hold several owner waves, or toy waves)
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const int64_t row0 = (int64_t)ob * kWave * SACENV_OBS_DIM;
-  store_obs_block(l.obs, reinterpret_cast<float*>(R) + row0, lane);
-  if (kRoll) {  // l.obs is rewritten by the next step
+    for (int k = 0; k < SACENV_OBS_DIM; ++k) w[k] = restart ? fo.v[k] : o.v[k];
+    store_row<SACENV_OBS_DIM>(reinterpret_cast<float*>(R) + (int64_t)e * SACENV_OBS_DIM, w);
+  } else {
+    // obs rows through LDS, stored as write-through float4 (64 rows x 44 B = 176 float4)
+#pragma unroll
+    for (int k = 0; k < SACENV_OBS_DIM; ++k) l.obs[lane * SACENV_OBS_DIM + k] = restart ? fo.v[k] : o.v[k];
+    // the rows are this wave's own LDS: a wave's LDS accesses run in issue order,
+    // so only the compiler must keep the stores ahead of the loads (no workgroup
+    // barrier: a step workgroup may hold several owner waves, or toy waves)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int64_t row0 = (int64_t)ob * kWave * SACENV_OBS_DIM;
+    store_obs_block<SACENV_OBS_DIM, kWT>(l.obs, reinterpret_cast<float*>(R) + row0, lane);
+    if (kRoll) {  // l.obs is rewritten by the next step
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
   }
   if (trans != nullptr) {  // the pooled transition row (sacenv_boat_step_pooled)
     // s' entries 0..8 = the pre-reset obs (entries 9 and 10, rudder and fuel, follow
     // on the receivers from the actions and the episode starts), reward, action,
     // term (done = term != 0) and, in experiment 2, the new episode's obs[3]
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (!kWT) {  // per-lane rows, as the record's
+      store_row<SACENV_TRANS_OBS>(reinterpret_cast<float*>(trans) + (int64_t)e * SACENV_TRANS_OBS, o.v);
+    } else {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-    for (int k = 0; k < SACENV_TRANS_OBS; ++k) l.obs[lane * SACENV_TRANS_OBS + k] = o.v[k];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    store_obs_block<SACENV_TRANS_OBS>(l.obs, reinterpret_cast<float*>(trans) + (int64_t)ob * kWave * SACENV_TRANS_OBS,
-                                      lane);
+      for (int k = 0; k < SACENV_TRANS_OBS; ++k) l.obs[lane * SACENV_TRANS_OBS + k] = o.v[k];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      store_obs_block<SACENV_TRANS_OBS, kWT>(
+          l.obs, reinterpret_cast<float*>(trans) + (int64_t)ob * kWave * SACENV_TRANS_OBS, lane);
+    }
     constexpr int kOff = 4 * SACENV_TRANS_OBS;  // byte columns (x n_pad) after s'
-    st_out(*reinterpret_cast<float*>(trans + kOff * A.np + eo4), (float)reward);
-    st_out(*reinterpret_cast<float*>(trans + (kOff + 4) * A.np + eo4), act);
-    st_out(*reinterpret_cast<uint8_t*>(trans + (kOff + 8) * A.np + e), term);
+    st_out<kWT>(*reinterpret_cast<float*>(trans + kOff * A.np + eo4), (float)reward);
+    st_out<kWT>(*reinterpret_cast<float*>(trans + (kOff + 4) * A.np + eo4), act);
+    st_out<kWT>(*reinterpret_cast<uint8_t*>(trans + (kOff + 8) * A.np + e), term);
     if (pin.experiment == 2)
-      st_out(*reinterpret_cast<float*>(trans + (kOff + 9) * A.np + eo4), restart ? fo.v[3] : 0.0f);
-    if (kRoll) {  // l.obs is rewritten by the next step
+      st_out<kWT>(*reinterpret_cast<float*>(trans + (kOff + 9) * A.np + eo4), restart ? fo.v[3] : 0.0f);
+    if (kRoll && kWT) {  // l.obs is rewritten by the next step
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

@@ -33,6 +33,9 @@ def test_driver_bench_command():
     assert d["setup"]["graph_first_replays"] == 512
     rf = d["roofline"]
     assert rf["bound"] == "hbm" and 0 < rf["frac"] < 1 and rf["kernel_avg_us"] > 0
+    if rf["kernel"].startswith("k_rollout"):  # the persistent launch: resident-state bytes headline
+        assert abs(rf["bytes_per_env_step"] - (70 + 152 / 128)) < 1e-9
+        assert rf["survey_222B"]["bytes_per_env_step"] == 222
     # the timed step includes its refill: never faster than the kernel alone
     assert rf["step_us_incl_refill"] >= rf["kernel_avg_us"]
     cb = d["cpu_baseline"]

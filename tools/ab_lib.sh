@@ -4,7 +4,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 ARGS=${BENCH_ARGS:-"--no-cpu-baseline"}
-for round in 1 2; do
+for round in $(seq 1 ${ROUNDS:-2}); do
   for v in ${VARIANTS:-base}; do
     if [ "$v" = base ]; then unset SACENV_LIB; else export SACENV_LIB=$PWD/sac-agent_amd/build/libsacenv_$v.so; fi
     timeout -k 10 200 python bench.py $ARGS > gpurun_out/abl_$v.json 2> gpurun_out/abl_$v.log || { tail -5 gpurun_out/abl_$v.log; exit 1; }

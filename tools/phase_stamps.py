@@ -38,6 +38,9 @@ def build():
 
 
 def main():
+    # before anything imports sacenv (build() does, via __graft_entry__): _lib reads
+    # SACENV_LIB at import
+    os.environ["SACENV_LIB"] = LIB
     if not os.path.exists(LIB) or "--rebuild" in sys.argv or "--build-only" in sys.argv:
         build()
     if "--build-only" in sys.argv:
@@ -64,7 +67,10 @@ def main():
         eb.record()
         torch.cuda.synchronize()
         d = acc[: nw * 8].view(nw, 8).cpu().numpy()
-        assert (d[:, 4] == K).all(), "phase stamps missing (not a -DSACENV_STAMPS build?)"
+        if not (d[:, 4] == K).all():
+            raw = acc[: 64].cpu().numpy()
+            raise SystemExit(f"phase stamps missing: counts {np.unique(d[:, 4])[:8]}, first doubles {raw[:16]}, "
+                             f"lib {os.environ.get('SACENV_LIB')}")
         per_step = d[:, :4] / K
         med = np.median(per_step, axis=0)
         total = float(med.sum())

@@ -94,7 +94,7 @@ def main(out_dir):
         res["envs"] = d["config"]["envs_per_gpu"]
         res["experiment"] = d["config"]["experiment"]
         res["bench_kernel_avg_us"] = d["roofline"]["kernel_avg_us"]
-        res["algorithmic_bytes_per_launch"] = d["roofline"]["bytes_per_launch"]
+        res["algorithmic_bytes_per_step"] = d["roofline"].get("bytes_per_step", d["roofline"].get("bytes_per_launch"))
     if STEPS_PER_LAUNCH > 1 and "hbm_bytes_per_launch" in res:
         res["steps_per_launch"] = STEPS_PER_LAUNCH
         res["hbm_bytes_per_step"] = res["hbm_bytes_per_launch"] / STEPS_PER_LAUNCH

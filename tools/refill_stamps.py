@@ -42,6 +42,9 @@ def pct(x):
 
 
 def main():
+    # before anything imports sacenv (build() does, via __graft_entry__): _lib reads
+    # SACENV_LIB at import
+    os.environ["SACENV_LIB"] = LIB
     if not os.path.exists(LIB) or "--rebuild" in sys.argv or "--build-only" in sys.argv:
         build()
     if "--build-only" in sys.argv:
