@@ -180,6 +180,12 @@ struct Arena {
     const double2 a = *reinterpret_cast<const double2*>(base), b = *reinterpret_cast<const double2*>(base + 16);
     q[0] = a.x, q[1] = a.y, q[2] = b.x, q[3] = b.y;  // memory order: y0, m0, y1, m1
   }
+  // the 32 bytes at byte offset off of the wave's ring block (piece_if's load)
+  __device__ __forceinline__ void piece_at(const char* wbase, uint32_t off, double (&q)[4]) const {
+    const char* base = wbase + off;
+    const double2 a = *reinterpret_cast<const double2*>(base), b = *reinterpret_cast<const double2*>(base + 16);
+    q[0] = a.x, q[1] = a.y, q[2] = b.x, q[3] = b.y;
+  }
   // piece() for lane `lane` of the wave whose ring block starts at wbase, for
   // lanes with `use`; the others read the block's first line (a fixed address:
   // one cache line per wave), so the load needs no branch
@@ -227,6 +233,11 @@ struct Tail {
   const double* table;
   double r_mx, r_my, r_iz, r_nd, r_w;  // 1/(m+m_x), 1/(m+m_y), 1/(I+I_z), 1/(n D), 1/width
   double r_goal, r_two_w, r_fuel;      // observation spans: 1/goal, 1/(2 width), 1/fuel
+  // the force laws' constant factors, folded once per launch (make_tail): each
+  // law is then (velocity^2) x one constant instead of a left-to-right chain of
+  // four to six products (boat_env.py:213-281); ~30 fewer f64 multiplies a
+  // step, rounding within ~2 ulp of the reference's order (state tolerance 1e-5)
+  double k_front, k_thrust, k_side, k_rud_front, k_hull, k_rud_moment;
 };
 
 // ---------------------------------------------------------------- LDS of a drawing wave
@@ -1281,14 +1292,12 @@ __device__ __forceinline__ double vreg(double x) {
   return r;
 }
 __device__ __forceinline__ SacenvBoatParams vreg_params(SacenvBoatParams q) {
+  // (the force laws' factors are Tail's folded constants: not copied)
   q.dt = vreg(q.dt), q.t_max = vreg(q.t_max), q.goal_line = vreg(q.goal_line);
   q.oob_limit = vreg(q.oob_limit), q.track_width = vreg(q.track_width);
-  q.c_r_front = vreg(q.c_r_front), q.c_r_side = vreg(q.c_r_side), q.rho = vreg(q.rho);
-  q.boat_area_front = vreg(q.boat_area_front), q.boat_area_side = vreg(q.boat_area_side);
-  q.boat_l = vreg(q.boat_l), q.boat_b = vreg(q.boat_b), q.rudder_area = vreg(q.rudder_area);
   q.m_plus_mx = vreg(q.m_plus_mx), q.m_plus_my = vreg(q.m_plus_my), q.i_plus_iz = vreg(q.i_plus_iz);
-  q.one_minus_wf = vreg(q.one_minus_wf), q.one_minus_td = vreg(q.one_minus_td);
-  q.n_times_d = vreg(q.n_times_d), q.n_squared = vreg(q.n_squared), q.d_pow4 = vreg(q.d_pow4);
+  q.one_minus_wf = vreg(q.one_minus_wf);
+  q.n_times_d = vreg(q.n_times_d);
   q.reward_k = vreg(q.reward_k), q.reward_center = vreg(q.reward_center);
   q.knot_step = vreg(q.knot_step);
   return q;
@@ -1296,6 +1305,8 @@ __device__ __forceinline__ SacenvBoatParams vreg_params(SacenvBoatParams q) {
 __device__ __forceinline__ Tail vreg_tail(Tail t) {
   t.r_mx = vreg(t.r_mx), t.r_my = vreg(t.r_my), t.r_iz = vreg(t.r_iz), t.r_nd = vreg(t.r_nd);
   t.r_w = vreg(t.r_w), t.r_goal = vreg(t.r_goal), t.r_two_w = vreg(t.r_two_w), t.r_fuel = vreg(t.r_fuel);
+  t.k_front = vreg(t.k_front), t.k_thrust = vreg(t.k_thrust), t.k_side = vreg(t.k_side);
+  t.k_rud_front = vreg(t.k_rud_front), t.k_hull = vreg(t.k_hull), t.k_rud_moment = vreg(t.k_rud_moment);
   return t;
 }
 
@@ -1672,6 +1683,15 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   do {           \
   } while (0)
 #endif
+  // carried between the steps of a multi-step launch (updated at each step's
+  // end, not recomputed): the knot coordinate of this step's grid index, and
+  // the lane's ring byte offsets of its current and next episode slots
+  // (wko_l(slot, 0, 0, lane)): ~25 integer VALU a step less
+  Knot kcur = knot_coord(p, index > p.wind_len - 1 ? p.wind_len - 1 : index);
+  const uint32_t slot_bytes = 2u * 16u * (uint32_t)A.nk, lane_ring = A.wko_l(0, 0, 0, lane);
+  const int slot0 = cons % kSlots;
+  int nslot = slot0 + 1 == kSlots ? 0 : slot0 + 1;
+  uint32_t so = lane_ring + (uint32_t)slot0 * slot_bytes, sno = lane_ring + (uint32_t)nslot * slot_bytes;
   for (int ks = 0; ks < (kRoll ? n_steps : 1) && (!kHand || !failed); ++ks) {
   PHASE(0);
   const float act = active ? act_cur : 0.0f;
@@ -1692,6 +1712,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
     }
   }
   const int wi = index > p.wind_len - 1 ? p.wind_len - 1 : index;
+  Knot knext = kcur;
   double wv = 0.0, wa = 0.0;
   bool refresh = false;
   int jn = 0;
@@ -1699,7 +1720,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   if (nc == 0) {
     wind_at(p, A, T.table, 0, e, wi, wv, wa);  // constants or the shared table
   } else {
-    const double tt = knot_coord(p, wi).t;
+    const double tt = kcur.t;  // = knot_coord(p, wi).t
     const double c0 = spline_piece(cf[0], cf[2], cf[1], cf[3], tt);  // cf: y0 m0 y1 m1
     if (nc == 2) {  // exp 6 (the only two-curve experiment)
       wv = c0;
@@ -1712,19 +1733,19 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
       wa = ((c0 <= 0.5 / 2 ? 0.0 : 1.0) * kPi) + kPi / 2;
     }
     const int wn = index + 1 > p.wind_len - 1 ? p.wind_len - 1 : index + 1;
-    jn = knot_coord(p, wn).j;
-    refresh = index == 0 || jn != knot_coord(p, wi).j;
+    knext = knot_coord(p, wn);
+    jn = knext.j;
+    refresh = index == 0 || jn != kcur.j;
     {  // the piece of the next step's interval for refreshing lanes, stored at
       // the end (own registers, read only there). Unconditional loads, the
       // other lanes reading one fixed line: with no branch around them the
       // waitcnt pass can count the loads in flight (a load under a divergent
       // branch made the first use of every earlier load wait for all of them)
-      const int slot = cons % kSlots;
 #pragma unroll
       for (int c = 0; c < 2; ++c)
         if (c < nc) {
           double q[4];
-          A.piece_if(refresh, wbase, slot, c, jn, lane, q);
+          A.piece_at(wbase, refresh ? so + (uint32_t)(c * A.nk + jn) * 16u : 0u, q);
           rq[4 * c] = q[0], rq[4 * c + 1] = q[1], rq[4 * c + 2] = q[2], rq[4 * c + 3] = q[3];
         }
     }
@@ -1738,12 +1759,12 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   int32_t syn = 0;
   const bool hdr_refresh = p.autoreset && index == 0;
   {
-    const int ns = (cons + 1) % kSlots;
+    const int ns = nslot;  // (cons + 1) % kSlots
 #pragma unroll
     for (int c = 0; c < 2; ++c)
       if (c < nc) {
         // (rollout: the copy is in registers; other lanes read the ring's first line)
-        const double v = *(hdr_refresh ? A.wy0p(wbase, ns, c, lane)
+        const double v = *(hdr_refresh ? reinterpret_cast<const double*>(wbase + sno + (uint32_t)(c * A.nk) * 16u)
                                        : (kRoll ? A.wind_knots() : &A.f64e(U_W0N + 8 * c, eo)));
         y0n[c] = kRoll && !hdr_refresh ? y0c[c] : v;
       }
@@ -1769,27 +1790,29 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   PHASE(1);
 
   // eom_longitudinal :213-239
-  const double F_R = v_x * v_x * p.c_r_front * 0.5 * p.rho * p.boat_area_front;
-  const double F_T = sin_J * p.n_squared * p.rho * p.d_pow4 * p.one_minus_td;
+  const double F_R = (v_x * v_x) * T.k_front;
+  const double F_T = sin_J * T.k_thrust;
   const double F_C = v_y * p.m_plus_my * v_r;
-  const double F_W = (wv * wv * wsign * p.c_r_front * 0.5 * p.rho * p.boat_area_front) * cwa;
+  const double w2s = wv * wv * wsign;
+  const double F_W = (w2s * T.k_front) * cwa;
   const double a_x = div_c(-F_R + F_T + F_C + F_W, p.m_plus_mx, r_mx);
   v_x = first ? 3.0 : a_x * p.dt + v_x;
 
   // eom_transverse :241-265 (new v_x)
   const double vys = (double)((v_y > 0.0) - (v_y < 0.0));
-  const double F_R2 = v_y * v_y * p.c_r_side * 0.5 * p.rho * p.boat_area_side * vys;
-  const double F_RU = sin_rud * (v_x * v_x * p.c_r_front * 0.5 * p.rho * p.rudder_area);
+  const double F_R2 = (v_y * v_y) * T.k_side * vys;
+  const double vx2 = v_x * v_x;  // (the new v_x)
+  const double F_RU = sin_rud * (vx2 * T.k_rud_front);
   const double F_C2 = v_x * p.m_plus_mx * v_r;
-  const double F_W2 = (wv * wv * wsign * p.c_r_side * 0.5 * p.rho * p.boat_area_side) * swa;
+  const double F_W2 = (w2s * T.k_side) * swa;
   const double a_y = div_c(-F_R2 + F_RU + F_C2 + F_W2, p.m_plus_my, r_my);
   v_y = first ? 0.0 : a_y * p.dt + v_y;
 
   // eom_yawning :267-281
   const double vrs = (double)((v_r > 0.0) - (v_r < 0.0));
   const double vxs = (double)((v_x > 0.0) - (v_x < 0.0));
-  const double M_hull = v_r * v_r * p.c_r_side * 0.5 * p.rho * p.boat_area_side * p.boat_l * 5.0 * vrs;
-  const double M_rud = v_x * v_x * p.c_r_side * 0.5 * p.rho * p.rudder_area * sin_rud * (p.boat_b / 2) * vxs;
+  const double M_hull = (v_r * v_r) * T.k_hull * vrs;
+  const double M_rud = (vx2 * T.k_rud_moment) * sin_rud * vxs;
   const double a_r = div_c(-M_hull + M_rud, p.i_plus_iz, r_iz);
   v_r = first ? 0.0 : a_r * p.dt + v_r;
   EARLY_STORE2(U_VY, v_y, v_r);
@@ -1923,6 +1946,14 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
     for (int c = 0; c < 2; ++c) y0c[c] = y0n[c];
     syc = syn;
     cons = cons_out;
+    if (restart) {  // the next slot becomes current; grid index 0
+      so = sno;
+      nslot = nslot + 1 == kSlots ? 0 : nslot + 1;
+      sno = nslot == 0 ? lane_ring : sno + slot_bytes;
+      kcur = knot_coord(p, 0);
+    } else {
+      kcur = knext;
+    }
   }
   st_out<kWT>(*reinterpret_cast<float*>(R + 44 * A.np + eo4), (float)reward);
   st_out<kWT>(*reinterpret_cast<uint8_t*>(R + 48 * A.np + e), (uint8_t)(ended ? 1 : 0));
@@ -2166,6 +2197,12 @@ Tail make_tail(const SacenvBoatParams& p, void* arena) {
   T.r_goal = 1.0 / p.goal_line;
   T.r_two_w = 1.0 / (p.track_width + p.track_width);
   T.r_fuel = 1.0 / (double)p.fuel0;
+  T.k_front = p.c_r_front * 0.5 * p.rho * p.boat_area_front;                  // F_R, F_W
+  T.k_thrust = p.n_squared * p.rho * p.d_pow4 * p.one_minus_td;               // F_T / KT
+  T.k_side = p.c_r_side * 0.5 * p.rho * p.boat_area_side;                     // F_R (transverse), F_W
+  T.k_rud_front = p.c_r_front * 0.5 * p.rho * p.rudder_area;                  // F_RU
+  T.k_hull = p.c_r_side * 0.5 * p.rho * p.boat_area_side * p.boat_l * 5.0;    // M_hull
+  T.k_rud_moment = p.c_r_side * 0.5 * p.rho * p.rudder_area * (p.boat_b / 2);  // M_rudder
   return T;
 }
 

@@ -37,7 +37,8 @@ def main(argv):
             s = s.replace(a, b)
         open(p, "w").write(s)
         out = os.path.join(g.BUILD, f"libsacenv_{name}.so")
-        subprocess.run([g._hipcc(), *g.HIPCC_FLAGS, "-I", os.path.join(ROOT, "include"),
+        extra = os.environ.get("EXTRA_FLAGS", "").split()
+        subprocess.run([g._hipcc(), *g.HIPCC_FLAGS, *extra, "-I", os.path.join(ROOT, "include"),
                         *[os.path.join(d, f) for f in g.SOURCES], "-o", out], check=True)
     print("built", out)
 
