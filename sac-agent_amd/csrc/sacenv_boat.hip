@@ -1782,7 +1782,6 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   if (p.test_mode == 0) rudder = rudder + div_c((double)act, 10.0, 0.1);  // action / 10
   if (!t_idx) EARLY_STORE(U_T, t);
   const bool first = index == 0;  // integrator counter == 0 (control_blocks.py:21-22)
-  const double wsign = (double)((wv > 0.0) - (wv < 0.0));
   const double v_x_w = v_x * p.one_minus_wf;
   const double J = p.n_rpm != 0.0 ? div_c(v_x_w, p.n_times_d, r_nd) : 0.0;  // :222-224
   double sin_J, sin_rud, swa, cwa;
@@ -1793,14 +1792,16 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   const double F_R = (v_x * v_x) * T.k_front;
   const double F_T = sin_J * T.k_thrust;
   const double F_C = v_y * p.m_plus_my * v_r;
-  const double w2s = wv * wv * wsign;
+  // v^2 sign(v) as v |v| (|.| is a free operand modifier): one multiply instead
+  // of a square, two compares, a convert and a multiply; the same double for
+  // every v != 0 (multiplying by +-1 is exact, in any position)
+  const double w2s = wv * fabs(wv);
   const double F_W = (w2s * T.k_front) * cwa;
   const double a_x = div_c(-F_R + F_T + F_C + F_W, p.m_plus_mx, r_mx);
   v_x = first ? 3.0 : a_x * p.dt + v_x;
 
   // eom_transverse :241-265 (new v_x)
-  const double vys = (double)((v_y > 0.0) - (v_y < 0.0));
-  const double F_R2 = (v_y * v_y) * T.k_side * vys;
+  const double F_R2 = (v_y * fabs(v_y)) * T.k_side;
   const double vx2 = v_x * v_x;  // (the new v_x)
   const double F_RU = sin_rud * (vx2 * T.k_rud_front);
   const double F_C2 = v_x * p.m_plus_mx * v_r;
@@ -1809,10 +1810,8 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   v_y = first ? 0.0 : a_y * p.dt + v_y;
 
   // eom_yawning :267-281
-  const double vrs = (double)((v_r > 0.0) - (v_r < 0.0));
-  const double vxs = (double)((v_x > 0.0) - (v_x < 0.0));
-  const double M_hull = (v_r * v_r) * T.k_hull * vrs;
-  const double M_rud = (vx2 * T.k_rud_moment) * sin_rud * vxs;
+  const double M_hull = (v_r * fabs(v_r)) * T.k_hull;
+  const double M_rud = ((v_x * fabs(v_x)) * T.k_rud_moment) * sin_rud;
   const double a_r = div_c(-M_hull + M_rud, p.i_plus_iz, r_iz);
   v_r = first ? 0.0 : a_r * p.dt + v_r;
   EARLY_STORE2(U_VY, v_y, v_r);
