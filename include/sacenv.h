@@ -149,10 +149,10 @@ typedef struct SacenvBoatLayout {
   int64_t final_ep_reward;    /* f64 [n_pad] episode reward of envs that ended */
   int64_t accel;              /* f64 [3][n_pad] a_x, a_y, a_r */
   int64_t reward64;           /* f64 [n_pad] */
-  int64_t refill_mask;        /* u64 [n_pad/64] per owner wave: envs whose slot ring the last
-                                 sacenv_boat_refill topped up (fill < cons + SLOTS before it) */
+  int64_t refill_mask;        /* u64 [n_pad/64]: the refill's scratch (look-back words of its
+                                 listing launch: (epoch, envs listed) per 1 024 envs) */
   int64_t status;             /* i32 [64] (256 B): [0] refills done, [1] SACENV_STATUS_* bits,
-                                 [2] envs ranked by the last refill */
+                                 [2] envs listed by the last refill */
   int64_t spline_g;           /* f64 [n_knots][n_knots]: (m/6) = G @ knots (written by init) */
   int64_t wind_table;         /* f64 [2][wind_len] (velocity, angle), if use_wind_table */
 } SacenvBoatLayout;

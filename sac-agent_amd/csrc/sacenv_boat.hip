@@ -927,8 +927,14 @@ __global__ void k_spline_g(SacenvBoatParams p, double* __restrict__ g) {
     for (int j = 0; j < n; ++j) g[i * n + j] = r[i][j];
 }
 
+constexpr int kMaskThreads = 1024;
+constexpr uint32_t kSpinLimit = 1u << 22;  // ~seconds of polling: then a launch gives up
+
 __global__ void __launch_bounds__(kWave) k_seed(SacenvBoatParams p, Arena A, const uint32_t* __restrict__ seeds) {
   const int e = blockIdx.x * kWave + threadIdx.x;
+  // k_need_masks' look-back words (refill_mask): no stale epoch may match (the
+  // caller's arena need not be zeroed; k_need_masks' workgroups <= owner waves <= envs)
+  if (e < A.nwaves()) A.refill_mask()[e] = 0ull;
   if (e >= p.n_envs) return;
   // mt19937_seed (init_genrand), numpy RandomState._legacy_seeding(int)
   uint32_t x = seeds[e];
@@ -1077,9 +1083,9 @@ __global__ void __launch_bounds__(kWave) k_refill(SacenvBoatParams p, Arena A) {
   int n_st = 0;
 #endif
   REFILL_STAMP(stm[0], "s"(lane));
-  const int total = __builtin_amdgcn_readfirstlane(A.status()[2]);  // ranked by k_need_masks
+  const int total = __builtin_amdgcn_readfirstlane(A.status()[2]);  // listed by k_need_masks
   REFILL_STAMP(stm[1], "s"(total));
-  if (blockIdx.x == 0 && lane == 0) A.status()[0] += 1;
+  if (blockIdx.x == 0 && lane == 0) A.status()[0] += 1;  // (k_need_masks' epoch: read before, in stream order)
   const int G = (int)gridDim.x;
   for (int r0 = blockIdx.x; r0 < total; r0 += kRefillAhead * G) {
     // the next kRefillAhead envs of this wave (ranks r0, r0 + G, ...): lane j loads env
@@ -1215,71 +1221,72 @@ __global__ void __launch_bounds__(kWave) k_refill_fit(SacenvBoatParams p, Arena 
 }
 
 // sacenv_boat_refill, launch 0: which envs consumed pre-drawn episodes since
-// their ring was last topped up (fill < cons + SLOTS), one 64-bit mask per
-// owner wave. Derived from the episode counters, so the step launch keeps no
+// their ring was last topped up (fill < cons + SLOTS), listed for launch 1 in
+// env order. Derived from the episode counters, so the step launch keeps no
 // flags of its own (measured: owner-side flag words cost 0.25-0.4 us/step).
-// 16 owner waves' envs per workgroup (one wave each). The LAST workgroup to
-// finish (a ticket in status[3]) ranks the flagged envs for launch 1: a block
-// scan of the mask popcounts, then every flagged env's id at its rank in
-// refill_list(0) and the count in status[2]. k_refill then finds its envs with
-// one load each instead of a wave-wide search per env.
-constexpr int kMaskThreads = 1024;
+// 16 owner waves' envs per workgroup (one wave each). A workgroup counts its
+// flagged envs (ballots, a scan of the 16 popcounts), publishes the count as
+// its look-back word (refill_mask[b] = (epoch, count); epoch = refills done + 1,
+// so no word of an earlier refill matches and nothing is reset), sums the words
+// of workgroups 0..b-1 -- one vector load of up to 64 words per pass, polled
+// until every one carries this epoch -- and stores each flagged env's id at its
+// rank in refill_list(0), one coalesced store per wave; the last workgroup
+// stores the total in status[2]. k_refill then finds its envs with one load
+// each. The ranks are those of a serial scan over the envs (the lists, and so
+// the arenas, are the same at every run). Round 2's design had the last
+// workgroup to take a ticket rank all 1 024 masks: 14.7 us a refill.
+__device__ __forceinline__ unsigned long long lookback_load(const unsigned long long* w) {
+  return __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __global__ void __launch_bounds__(kMaskThreads) k_need_masks(SacenvBoatParams p, Arena A) {
-  __shared__ int wsum[kMaskThreads / kWave];
-  __shared__ int last;
+  __shared__ int wcnt[kMaskThreads / kWave];
   const int t = threadIdx.x, lane = t & (kWave - 1), wv = t >> 6;
-  const int nw = A.nwaves();
-  const int w = blockIdx.x * (kMaskThreads / kWave) + wv, e = w * kWave + lane;
+  const int nw = A.nwaves(), b = (int)blockIdx.x;
+  const int w = b * (kMaskThreads / kWave) + wv, e = w * kWave + lane;
+  const uint32_t epoch = (uint32_t)A.status()[0] + 1u;
+  bool need = false;
   if (w < nw) {
     const int c = e < p.n_envs ? A.i32(U_CONS)[e] : 0;
-    const bool need = e < p.n_envs && A.i32(U_FILL)[e] < c + kSlots;
-    const unsigned long long m = __ballot(need);
-    if (lane == 0) A.refill_mask()[w] = m;
+    need = e < p.n_envs && A.i32(U_FILL)[e] < c + kSlots;
     if (need) A.cons_snap()[e] = c;
   }
-  // the masks of this workgroup, device-wide, before its ticket: the barrier
-  // orders every wave's stores before thread 0's agent-scope release (one L2
-  // write-back per workgroup, not one per wave)
+  const unsigned long long m = __ballot(need);
+  if (lane == 0) wcnt[wv] = __popcll(m);
   __syncthreads();
-  if (t == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    last = atomicAdd(&A.status()[3], 1) == (int)gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every workgroup's masks
-  const unsigned long long* masks = A.refill_mask();
-  int base = 0;
-  for (int w0 = 0; w0 < nw; w0 += kMaskThreads) {  // one mask per thread and pass
-    const int mw = w0 + t;
-    const unsigned long long m = mw < nw ? masks[mw] : 0ull;
-    const int cnt = __popcll(m);
+  if (t < kWave) {  // wave 0: the workgroup's count, its look-back, each wave's base
+    unsigned long long* const look = A.refill_mask();
+    const int cnt = t < kMaskThreads / kWave ? wcnt[t] : 0;
     const int incl = wave_incl_scan(cnt);
-    if (lane == kWave - 1) wsum[wv] = incl;
-    __syncthreads();
-    int before = base;
-    for (int k = 0; k < wv; ++k) before += wsum[k];
-    const int pos = before + incl - cnt;  // rank of this thread's mask's first env
-    // the wave's 64 masks one at a time, lane l taking bit l: each mask's envs go
-    // out as one coalesced store (a lane per bit, not a scattered loop per lane)
-    for (int i = 0; i < kWave; ++i) {
-      const unsigned long long mi =
-          ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(m >> 32), i) << 32) |
-          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)m, i);
-      if (mi == 0ull) continue;  // uniform
-      const int pi = __builtin_amdgcn_readlane(pos, i);
-      if ((mi >> lane) & 1ull)
-        A.refill_list(0)[pi + __popcll(mi & ((1ull << lane) - 1ull))] = (w0 + wv * kWave + i) * kWave + lane;
+    const int total = __builtin_amdgcn_readlane(incl, kMaskThreads / kWave - 1);
+    if (t == 0)
+      __hip_atomic_store(look + b, ((unsigned long long)epoch << 32) | (uint32_t)total, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    int before = 0;
+    for (int q0 = 0; q0 < b; q0 += kWave) {
+      const int q = q0 + t;
+      unsigned long long x = q < b ? lookback_load(look + q) : ((unsigned long long)epoch << 32);
+      for (uint32_t it = 0; __ballot((uint32_t)(x >> 32) != epoch) != 0ull; ++it) {
+        if (it >= kSpinLimit) {  // a predecessor that never publishes: flag it, rank as if it listed none
+          if (t == 0) atomicOr(&A.status()[1], SACENV_STATUS_SLOT_UNDERFLOW);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        if ((uint32_t)(x >> 32) != epoch) x = lookback_load(look + q);
+      }
+      int v = (uint32_t)(x >> 32) == epoch ? (int)(uint32_t)x : 0;
+      v += __shfl_xor(v, 32);
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 8);
+      v += __shfl_xor(v, 4);
+      v += __shfl_xor(v, 2);
+      v += __shfl_xor(v, 1);
+      before += v;
     }
-    int tot = 0;
-    for (int k = 0; k < kMaskThreads / kWave; ++k) tot += wsum[k];
-    base += tot;
-    __syncthreads();
+    if (t < kMaskThreads / kWave) wcnt[t] = before + incl - cnt;
+    if (t == 0 && b == (int)gridDim.x - 1) A.status()[2] = before + total;
   }
-  if (t == 0) {
-    A.status()[2] = base;
-    A.status()[3] = 0;  // the next refill's tickets
-  }
+  __syncthreads();
+  if (need) A.refill_list(0)[wcnt[wv] + __popcll(m & ((1ull << lane) - 1ull))] = e;
 }
 
 // Uniform fp64 constants as VGPR copies: the step reads ~40 config doubles,
@@ -1546,7 +1553,6 @@ __device__ __forceinline__ float act_load(const char* row, uint32_t off) {
                                                                      0x00020000);
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 17));
 }
-constexpr uint32_t kSpinLimit = 1u << 22;  // ~seconds of polling: then the launch gives up
 // Spin until the flag reaches `want` (sequence numbers stay below 2^31). Returns
 // the last value seen; on timeout flags the status and returns 0.
 __device__ uint32_t wait_flag(const uint32_t* f, uint32_t want, uint32_t seen, int32_t* status, int lane) {
@@ -1850,7 +1856,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   tm = goal ? SACENV_TERM_REACHED_GOAL : tm;
   reward = goal ? reward + 1000.0 : reward;
   // penalties :107-111
-  reward = (rudder > kPi / 4) | (rudder < -kPi / 4) ? reward - fabs(rudder) * 100.0 : reward;
+  reward = ((rudder > kPi / 4) | (rudder < -kPi / 4)) ? reward - fabs(rudder) * 100.0 : reward;
   reward = fabs(s_r) > kPi / 2 ? reward - 1.0 : reward;
   ep = ep + reward;
   uint8_t term = active ? (uint8_t)tm : (uint8_t)SACENV_TERM_NONE;  // padding lanes never end
@@ -1885,23 +1891,37 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   // restarting wave with two extra barriers)
   if (restart && fin != nullptr) store_obs(fin + (int64_t)e * SACENV_OBS_DIM, o);
   int cons_out = cons;
-  Obs fo;  // first obs of the next episode (restarting lanes)
-  if (restart) {  // next episode from its pre-drawn slot: a fresh Boat (boat_env.py:152-198)
-    const double sy0 = p.experiment == 2 ? (double)syn : 0.0;  // :166-169
-    s_x = 0.0, s_y = sy0, s_r = 0.0, v_x = 0.0, v_y = 0.0, v_r = 0.0, rudder = 0.0;
-    t = 0.0, ep = 0.0;  // :122
-    index = 0;
-    if (p.experiment == 2 || p.fuel0 == 0) {
-      fo = make_obs(p, oc, 0.0, 0.0, 0.0, sy0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, (double)p.fuel0);
-    } else {  // make_obs of the zero state, folded: (0+W)/(2W) = 0.5 and fuel0/fuel0 = 1 exactly
-      constexpr float kRud0 = (float)((0.0 + kPi / 3) * (1.0 / (kPi / 3 - (-kPi / 3))));
+  // the record's obs row: this step's obs, or a restarting lane's first obs of
+  // its next episode. The restart's ~45 per-lane selects (state, row, slot ring)
+  // sit behind ONE wave-uniform branch: in most steps no lane of the wave ends
+  // its episode (an episode runs up to 500 steps), and the selects are skipped.
+  float row[SACENV_OBS_DIM];
 #pragma unroll
-      for (int k = 0; k < SACENV_OBS_DIM; ++k) fo.v[k] = 0.0f;
-      fo.v[3] = 0.5f;
-      fo.v[9] = kRud0;
-      fo.v[10] = 1.0f;
+  for (int k = 0; k < SACENV_OBS_DIM; ++k) row[k] = o.v[k];
+  float row3_new = 0.0f;  // (exp 2's pooled row: the new episode's obs[3])
+  const bool any_restart = __ballot(restart) != 0ull;
+  if (any_restart) {
+    if (restart) {  // next episode from its pre-drawn slot: a fresh Boat (boat_env.py:152-198)
+      const double sy0 = p.experiment == 2 ? (double)syn : 0.0;  // :166-169
+      s_x = 0.0, s_y = sy0, s_r = 0.0, v_x = 0.0, v_y = 0.0, v_r = 0.0, rudder = 0.0;
+      t = 0.0, ep = 0.0;  // :122
+      index = 0;
+      Obs fo;
+      if (p.experiment == 2 || p.fuel0 == 0) {
+        fo = make_obs(p, oc, 0.0, 0.0, 0.0, sy0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, (double)p.fuel0);
+      } else {  // make_obs of the zero state, folded: (0+W)/(2W) = 0.5 and fuel0/fuel0 = 1 exactly
+        constexpr float kRud0 = (float)((0.0 + kPi / 3) * (1.0 / (kPi / 3 - (-kPi / 3))));
+#pragma unroll
+        for (int k = 0; k < SACENV_OBS_DIM; ++k) fo.v[k] = 0.0f;
+        fo.v[3] = 0.5f;
+        fo.v[9] = kRud0;
+        fo.v[10] = 1.0f;
+      }
+#pragma unroll
+      for (int k = 0; k < SACENV_OBS_DIM; ++k) row[k] = fo.v[k];
+      row3_new = fo.v[3];
+      cons_out = cons + 1;
     }
-    cons_out = cons + 1;
   }
   // the dynamics' fields went out as they were computed; what is left: the
   // fresh state of restarting envs (same lane, same address: the later store
@@ -1932,12 +1952,8 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
         if (c < nc) st_out(A.f64e(U_W0N + 8 * c, eo), y0n[c]);
       if (p.experiment == 2) st_out(A.i32e(U_SYN, eo4), syn);
     }
-  } else {  // the same updates, in registers
-    if (restart) {
-#pragma unroll
-      for (int c = 0; c < 2; ++c)
-        if (c < nc) cf[4 * c] = y0n[c];
-    } else if (refresh) {
+  } else {  // the same updates, in registers (each behind a wave-uniform branch)
+    if (nc > 0 && __ballot(refresh && !restart) != 0ull && refresh && !restart) {
 #pragma unroll
       for (int k = 0; k < kCoef; ++k) cf[k] = rq[k];
     }
@@ -1945,13 +1961,15 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
     for (int c = 0; c < 2; ++c) y0c[c] = y0n[c];
     syc = syn;
     cons = cons_out;
-    if (restart) {  // the next slot becomes current; grid index 0
+    kcur = knext;
+    if (any_restart && restart) {  // the next slot becomes current; grid index 0
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+        if (c < nc) cf[4 * c] = y0n[c];
       so = sno;
       nslot = nslot + 1 == kSlots ? 0 : nslot + 1;
       sno = nslot == 0 ? lane_ring : sno + slot_bytes;
       kcur = knot_coord(p, 0);
-    } else {
-      kcur = knext;
     }
   }
   st_out<kWT>(*reinterpret_cast<float*>(R + 44 * A.np + eo4), (float)reward);
@@ -1963,14 +1981,11 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
     // 44-B row as 16 + 16 + 12 B (4-B aligned vector stores): 0.08 us/step
     // cheaper than the LDS-staged block below, whose LDS round trip and waits
     // sit on the step's path
-    float w[SACENV_OBS_DIM];
-#pragma unroll
-    for (int k = 0; k < SACENV_OBS_DIM; ++k) w[k] = restart ? fo.v[k] : o.v[k];
-    store_row<SACENV_OBS_DIM>(reinterpret_cast<float*>(R) + (int64_t)e * SACENV_OBS_DIM, w);
+    store_row<SACENV_OBS_DIM>(reinterpret_cast<float*>(R) + (int64_t)e * SACENV_OBS_DIM, row);
   } else {
     // obs rows through LDS, stored as write-through float4 (64 rows x 44 B = 176 float4)
 #pragma unroll
-    for (int k = 0; k < SACENV_OBS_DIM; ++k) l.obs[lane * SACENV_OBS_DIM + k] = restart ? fo.v[k] : o.v[k];
+    for (int k = 0; k < SACENV_OBS_DIM; ++k) l.obs[lane * SACENV_OBS_DIM + k] = row[k];
     // the rows are this wave's own LDS: a wave's LDS accesses run in issue order,
     // so only the compiler must keep the stores ahead of the loads (no workgroup
     // barrier: a step workgroup may hold several owner waves, or toy waves)
@@ -2008,7 +2023,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
     st_out<kWT>(*reinterpret_cast<float*>(trans + (kOff + 4) * A.np + eo4), act);
     st_out<kWT>(*reinterpret_cast<uint8_t*>(trans + (kOff + 8) * A.np + e), term);
     if (pin.experiment == 2)
-      st_out<kWT>(*reinterpret_cast<float*>(trans + (kOff + 9) * A.np + eo4), restart ? fo.v[3] : 0.0f);
+      st_out<kWT>(*reinterpret_cast<float*>(trans + (kOff + 9) * A.np + eo4), row3_new);
     if (kRoll && kWT) {  // l.obs is rewritten by the next step
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
