@@ -355,6 +355,7 @@ __device__ __forceinline__ double vconst(double x) {
   asm volatile("v_mov_b64 %0, %1" : "=v"(r) : "s"(x));
   return r;
 }
+template <bool kV = true>  // kV: VGPR copies (the multi-step loop); else plain constants
 __device__ __forceinline__ TrigK trig_k() {
   constexpr double sn[10] = {1.9572941063391262e-20,  -8.22063524662432950e-18, 2.8114572543455206e-15,
                              -7.647163731819816e-13,  1.6059043836821613e-10,   -2.505210838544172e-08,
@@ -365,15 +366,15 @@ __device__ __forceinline__ TrigK trig_k() {
                             4.1666666666666664e-02};
   TrigK k;
 #pragma unroll
-  for (int i = 0; i < 10; ++i) k.s[i] = vconst(sn[i]);
+  for (int i = 0; i < 10; ++i) k.s[i] = kV ? vconst(sn[i]) : sn[i];
 #pragma unroll
-  for (int i = 0; i < 7; ++i) k.c[i] = vconst(cs[i]);
+  for (int i = 0; i < 7; ++i) k.c[i] = kV ? vconst(cs[i]) : cs[i];
   constexpr double ex[10] = {2.5022322536502990e-08, 2.7630903490112654e-07, 2.755751454582531e-06,
                              2.480149103909504e-05,  1.9841269589115522e-04, 1.3888888945916382e-03,
                              8.333333333455043e-03,  4.1666666666519754e-02, 1.6666666666666477e-01,
                              5.000000000000012e-01};
 #pragma unroll
-  for (int i = 0; i < 10; ++i) k.e[i] = vconst(ex[i]);
+  for (int i = 0; i < 10; ++i) k.e[i] = kV ? vconst(ex[i]) : ex[i];
   return k;
 }
 __device__ __forceinline__ double fma_v(double a, double b, double c) {
@@ -1654,8 +1655,11 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   const SacenvBoatParams& p = pin;
   const Tail& T = Tin;
   constexpr bool kWT = !kRoll || kHand;  // write-through outputs (st_out)
-  const TrigK K = trig_k();
-  const ObsConst oc = obs_const_v(T);
+  // one-step launch: plain constants (the compiler places them; the VGPR copies
+  // cost their moves in every launch: k_step 5.02 -> 5.36 us measured), the
+  // multi-step loop: VGPR copies, moved once per launch
+  const TrigK K = trig_k<kRoll>();
+  const ObsConst oc = kRoll ? obs_const_v(T) : obs_const(T);
   // Wind.get_wind(index) (wind.py:20-24, IndexError guard) of this step. Curves:
   // from the lane's copy of its spline piece (wind_coef, loaded with the
   // state). The copy is refreshed from the active slot at the end of a step
@@ -2098,7 +2102,9 @@ __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, Arena A, Tai
   const int lane = threadIdx.x;
   int b = (int)blockIdx.x;
   if (!kMixed || b < nb_boat) {
-    owner_wave<false, kNc, kTIdx>(vreg_params(p), A, vreg_tail(T), action, slds, b, lane, 1, nullptr,
+    // (the parameters stay in SGPRs: VGPR copies ahead of the load burst delay it in
+    // every launch, measured k_step 5.79 -> 5.37 us without them)
+    owner_wave<false, kNc, kTIdx>(p, A, T, action, slds, b, lane, 1, nullptr,
                                   trans);
     return;
   }
