@@ -636,16 +636,38 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
     # eager: k_step-only segments replayed after the timed region.
     what = ("persistent sacenv_boat_segment launches" if run.mode == "segment" else
             f"graph-replayed {SEG}-launch k_step segments")
+    no_exchange = None
     if pool is not None or run.mode == "eager":
         if run.mode == "eager" and dev.type == "cuda" and not args.no_graph:
             run.capture_all(with_pool=False)
             run.mode, use_graph = "graph", True
             what = f"graph-replayed {SEG}-launch k_step segments"
         seg_events.clear()
+        run.timed_segments = 0  # (the event stride restarts: the first of these is timed)
         k = segment(k, False, with_pool=False)
-        for _ in range(segs(args.kernel_launches)):
+        # (N>1) the same segments and refills with no exchange, wall-timed like the
+        # timed region: the sharded-replay rate (--pooling none), reported beside
+        n_ne = segs(args.kernel_launches)
+        _sync(dev)
+        barrier(world)
+        _sync(dev)
+        t_ne = time.perf_counter()
+        for _ in range(n_ne):
             k = segment(k, True, with_pool=False)
         _sync(dev)
+        barrier(world)
+        el_ne = time.perf_counter() - t_ne
+        if world > 1:
+            import torch.distributed as dist
+            t = torch.tensor([el_ne], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el_ne = float(t.item())
+        no_exchange = {"value": world * wl.per_gpu_envs * n_ne * SEG / el_ne, "steps": n_ne * SEG,
+                       "ms_per_step": el_ne / (n_ne * SEG) * 1e3,
+                       "note": "the same persistent segments and refills after the timed region with no "
+                               "all_gather (each rank's transitions stay on its GPU: --pooling none, or "
+                               "ShardedReplayBuffer's B-row exchange per learn()), wall-timed between "
+                               "barriers, max over ranks"}
         kern_src = (f"events around {len(seg_events)} {what if dev.type == 'cuda' else 'eager'} after the "
                     "timed region (no staging copy, no collective; refills between segments excluded)")
     else:
@@ -761,7 +783,8 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
             "xgmi": {"link_peak_GBps": XGMI_LINK_GBPS, "links_used": world - 1,
                      "per_link_GBps": wl.row_bytes() * steps / el_max / 1e9,
                      "per_link_frac": wl.row_bytes() * steps / el_max / 1e9 / XGMI_LINK_GBPS},
-            "note": "the timed region ends when the last all_gather has landed"},
+            "note": "the timed region ends when the last all_gather has landed",
+            "no_exchange": no_exchange},
     }
 
 

@@ -137,5 +137,8 @@ def test_driver_command_world2_gloo_segment_pooling():
     assert f"{45 * N_PAD} B per rank-step" in out["config"]["collective"]
     assert out["pooling"]["received_bytes_per_rank"] == (world - 1) * 45 * N_PAD * out["steps"]
     assert out["pooling"]["received_GBps_per_rank"] > 0
+    # the no-exchange rate of the same segments, measured after the timed region
+    ne = out["pooling"]["no_exchange"]
+    assert ne["value"] > 0 and ne["steps"] % 128 == 0 and ne["ms_per_step"] > 0
     for _, _, steps, refills in res:
         assert steps % 128 == 0 and refills == steps // 128
