@@ -74,7 +74,7 @@ def main():
     tick = 0.01  # us per 100 MHz tick
     out = {"envs": N, "helpers": H, "refills": []}
     agg = {k: [] for k in ("rank", "find_env", "counters", "draw", "store", "per_env", "wave_span",
-                           "start_skew", "end_spread")}
+                           "start_skew", "end_spread", "fit_start", "fit_block", "fit_end", "fit_exit_start", "refill_to_fit_gap")}
     for a, f, ranked in samples:
         live = a[:, 0] > 0
         a = a[live].astype(np.float64)
@@ -97,6 +97,14 @@ def main():
             agg["per_env"] += list((r[:, b + 4] - r[:, b]) * tick)
         fl = f[f[:, 0] > 0].astype(np.float64)
         fit_span = (fl[:, 1].max() - fl[:, 0].min()) * tick if (fl[:, 1] > 0).any() else None
+        if fit_span is not None:  # blocks that fitted (end stamp): start skew, duration
+            fw = fl[fl[:, 1] > 0]
+            f0 = fl[:, 0].min()
+            agg["fit_start"] += list((fw[:, 0] - f0) * tick)
+            agg["fit_block"] += list((fw[:, 1] - fw[:, 0]) * tick)
+            agg["fit_end"] += list((fw[:, 1] - f0) * tick)
+            agg["fit_exit_start"] += list((fl[fl[:, 1] == 0][:, 0] - f0) * tick)
+            agg["refill_to_fit_gap"] += [float((f0 - a[:, 22].max()) * tick)]
         out["refills"].append({"ranked_envs": ranked, "k_refill_span_us": float((a[:, 22].max() - t0) * tick),
                                "envs_per_wave": pct(n_env), "k_refill_fit_span_us": fit_span})
     out["phases_us"] = {k: pct(v) for k, v in agg.items()}
