@@ -420,6 +420,8 @@ __device__ __forceinline__ double sin_taylor(double x, const TrigK& K) {
 // below 1e-17) and the quadrant swap. Within 1 ulp of glibc's sin/cos up to
 // 1e13 (measured, 2e6 samples per decade); the bound keeps (int)k exact.
 constexpr double kCwBound = 1.0e5;
+__device__ __forceinline__ void sincos_quadrant(double r, double z, double ps, double pc, double k, double* sp,
+                                                double* cp);
 __device__ __forceinline__ void sincos_fast(double x, double* sp, double* cp, const TrigK& K) {
   const double k = rint(x * 0.6366197723675814);
   double r = fma(-k, 1.5707963267948966, x);
@@ -429,10 +431,17 @@ __device__ __forceinline__ void sincos_fast(double x, double* sp, double* cp, co
   double ps = fma_v(z, K.s[2], K.s[3]);
 #pragma unroll
   for (int i = 4; i < 10; ++i) ps = fma_v(ps, z, K.s[i]);
-  const double sr = fma(r * z, ps, r);
   double pc = fma_v(z, K.c[0], K.c[1]);
 #pragma unroll
   for (int i = 2; i < 7; ++i) pc = fma_v(pc, z, K.c[i]);
+  sincos_quadrant(r, z, ps, pc, k, sp, cp);
+}
+
+// sincos_fast's tail: the series values from the two polynomials, then the
+// quadrant of k = rint(x 2/pi) (swap, and the signs as sign-bit xors)
+__device__ __forceinline__ void sincos_quadrant(double r, double z, double ps, double pc, double k, double* sp,
+                                                double* cp) {
+  const double sr = fma(r * z, ps, r);
   const double cr = 1.0 - fma(-(z * z), pc, 0.5 * z);
   const int q = (int)k;
   const double a = (q & 1) ? cr : sr, b = (q & 1) ? sr : cr;  // sin, cos of r + (q&1) pi/2
@@ -476,9 +485,32 @@ __device__ __forceinline__ void sincos_cw(double x, double* sp, double* cp, cons
 
 __device__ __forceinline__ void trig3(double j, double r, double w, double* sj, double* sr, double* sw,
                                       double* cw, const TrigK& K) {
-  *sj = sin_taylor(j, K);
-  *sr = sin_taylor(r, K);
-  sincos_fast(w, sw, cw, K);
+  // the four Horner chains (sin j, sin r, and the sin and cos polynomials of w's
+  // reduced argument) issued interleaved, their ends aligned: each FMA's
+  // dependent predecessor is three instructions back, so the chains hide each
+  // other's latency (written one after the other, the asm FMAs issued as two
+  // serial 10-deep chains with a hazard nop between dependent pairs). The same
+  // operations as sin_taylor / sincos_fast, so the same doubles.
+  const double kw = rint(w * 0.6366197723675814);
+  double rw = fma(-kw, 1.5707963267948966, w);
+  rw = fma(-kw, 6.123233995736766e-17, rw);
+  rw = fma(-kw, -1.4973849048591698e-33, rw);
+  const double zj = j * j, zr = r * r, zw = rw * rw;
+  double qj = fma_v(zj, K.s[0], K.s[1]);
+  double qr = fma_v(zr, K.s[0], K.s[1]);
+  double ps = 0.0, pc = 0.0;
+#pragma unroll
+  for (int i = 2; i < 10; ++i) {
+    qj = fma_v(qj, zj, K.s[i]);
+    qr = fma_v(qr, zr, K.s[i]);
+    if (i == 3) ps = fma_v(zw, K.s[2], K.s[3]);
+    if (i >= 4) ps = fma_v(ps, zw, K.s[i]);
+    if (i == 4) pc = fma_v(zw, K.c[0], K.c[1]);
+    if (i >= 5) pc = fma_v(pc, zw, K.c[i - 3]);
+  }
+  *sj = fma(j * zj, qj, j);
+  *sr = fma(r * zr, qr, r);
+  sincos_quadrant(rw, zw, ps, pc, kw, sw, cw);
   const bool okj = fabs(j) <= kSinBound, okr = fabs(r) <= kSinBound, okw = fabs(w) <= kCwBound;
   if (__ballot(!(okj && okr && okw)) != 0ull) {
     if (!okj) *sj = sin_ocml(j);
