@@ -1100,19 +1100,28 @@ __global__ void __launch_bounds__(1024) k_compact(const uint8_t* __restrict__ do
     asm volatile("" ::__VA_ARGS__);                                 \
     (slot) = __builtin_amdgcn_s_memrealtime();                      \
   } while (0)
-constexpr int kRefillStamps = 24;  // per refill wave: start, ranked, 4 x (5 per env), end, envs
+constexpr int kRefillStamps = 24;  // per refill wave: start, total read, fast path done, 19 wave draws, end, draws
 #else
 #define REFILL_STAMP(slot, ...) \
   do {                          \
   } while (0)
 #endif
 
-// sacenv_boat_refill, launch 1: every env flagged in the refill masks gets
-// its slot ring topped up to SLOTS episodes (fill = cons + SLOTS), drawn in
-// the env's order (start y and raw knots), one wave per env (rank h,
-// h + grid, ...). Block 0 counts the refill and publishes the rank count for
-// launch 2.
-constexpr int kRefillAhead = 4;  // envs per refill wave whose inputs load together
+// sacenv_boat_refill, launch 1: every listed env gets its slot ring topped up
+// to SLOTS episodes (fill = cons + SLOTS), drawn in the env's order (start y
+// and raw knots). A wave takes four consecutive ranks, one 16-lane group each.
+// Fast path, one episode per group: the group loads the 16 + 2*nk*curves words
+// at the env's MT position (when they lie inside the current 624-word block),
+// tempers them, takes the first accepted randint word among the first 16
+// (masked rejection, numpy legacy) and turns the following word pairs into the
+// knots (genrand_res53), lane = (curve, knot): one wave instruction serves four
+// envs, where the wave-per-env draw spent ~330 wave instructions on each (the
+// refill was VALU-bound). The rest -- windows that cross the block end (the
+// twist), a randint rejected 16 times, more than 8 knots, further episodes of
+// an env that consumed several -- goes through the wave-per-env draw
+// (draw_knots_wave), env by env. Block 0 counts the refill.
+constexpr int kGroupLanes = 16;
+constexpr int kGroups = kWave / kGroupLanes;
 __global__ void __launch_bounds__(kWave) k_refill(SacenvBoatParams p, Arena A) {
   __shared__ RngLds lds;
   const int lane = threadIdx.x;
@@ -1123,58 +1132,94 @@ __global__ void __launch_bounds__(kWave) k_refill(SacenvBoatParams p, Arena A) {
   REFILL_STAMP(stm[0], "s"(lane));
   const int total = __builtin_amdgcn_readfirstlane(A.status()[2]);  // listed by k_need_masks
   REFILL_STAMP(stm[1], "s"(total));
-  if (blockIdx.x == 0 && lane == 0) A.status()[0] += 1;  // (k_need_masks' epoch: read before, in stream order)
+  if (blockIdx.x == 0 && lane == 0) A.status()[0] += 1;
   const int G = (int)gridDim.x;
-  for (int r0 = blockIdx.x; r0 < total; r0 += kRefillAhead * G) {
-    // the next kRefillAhead envs of this wave (ranks r0, r0 + G, ...): lane j loads env
-    // j's id, counters and (when it does not cross the MT block end) its first window
-    // in one go, so their latencies overlap instead of adding up env after env
-    const int rj = r0 + (lane & (kRefillAhead - 1)) * G;
-    const bool okj = lane < kRefillAhead && rj < total;
-    const int ej = okj ? A.refill_list(0)[rj] : 0;
-    const int cj = okj ? A.cons_snap()[ej] : 0;
-    const int fj = okj ? A.i32(U_FILL)[ej] : 0;
-    const int pj = okj ? A.i32(U_MTPOS)[ej] : kMtN;
-    uint32_t win[kRefillAhead];
+  const int g = lane / kGroupLanes, gl = lane % kGroupLanes;
+  const int nk = p.n_knots;
+  const int ndraw = n_curves(p.experiment);  // draws follow the reference even with a wind table
+  const int ncurves = p.use_wind_table ? 0 : ndraw;
+  const int need = 2 * nk * ndraw;           // knot words after the randint word
+  const int nwords = kGroupLanes + need;     // <= 48 on the fast path
+  const bool grp_ok = nk <= 8;               // 16 lanes = 2 curves x 8 knots
+  const uint32_t rng = (uint32_t)(2 * p.start_y_half - 1);
+  uint32_t mask = rng;
+  mask |= mask >> 1;
+  mask |= mask >> 2;
+  mask |= mask >> 4;
+  mask |= mask >> 8;
+  mask |= mask >> 16;
+  for (int r0 = blockIdx.x * kGroups; r0 < total; r0 += kGroups * G) {
+    const int rr = r0 + g;
+    const bool ok = rr < total;
+    const int e = ok ? A.refill_list(0)[rr] : 0;
+    const int c = ok ? A.cons_snap()[e] : 0;
+    const int f0 = ok ? A.i32(U_FILL)[e] : 0;
+    const int pos = ok ? A.i32(U_MTPOS)[e] : kMtN;
+    if (ok && c >= f0 && gl == 0) atomicOr(&A.status()[1], SACENV_STATUS_SLOT_UNDERFLOW);
+    const int f_end = ok && f0 < c + kSlots ? c + kSlots : f0;
+    bool fast = ok && f0 < f_end && grp_ok && pos + nwords <= kMtN;
+    // the group's words pos .. pos + nwords - 1 (raw, key order), tempered
+    const uint32_t* key = A.mt_key() + (int64_t)e * kMtN + pos;
+    uint32_t w[3];
 #pragma unroll
-    for (int j = 0; j < kRefillAhead; ++j) {
-      const int e = __builtin_amdgcn_readlane(ej, j), pos = __builtin_amdgcn_readlane(pj, j);
-      const bool fits = r0 + j * G < total && pos + kWave <= kMtN;
-      win[j] = A.mt_key()[(int64_t)e * kMtN + (fits ? pos + lane : lane)];
+    for (int q = 0; q < 3; ++q)
+      w[q] = fast && gl + kGroupLanes * q < nwords ? mt_temper(key[gl + kGroupLanes * q]) : 0u;
+    uint32_t* const gw = lds.blk[0] + g * 3 * kGroupLanes;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) gw[gl + kGroupLanes * q] = w[q];
+    // np.random.randint (boat_env.py:147-150): the first accepted of the first 16 words
+    const unsigned long long acc = __ballot(fast && (w[0] & mask) <= rng);
+    const uint32_t gacc = (uint32_t)(acc >> (kGroupLanes * g)) & 0xFFFFu;
+    fast = fast && gacc != 0u;
+    const int k = fast ? __builtin_ctz(gacc) : 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the group's words, then reads
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    REFILL_STAMP(stm[2], "v"(k));
+    if (fast) {
+      const int slot = f0 % kSlots;
+      const int cc = gl / 8, jj = gl % 8;  // knot jj of curve cc (wind.py:78; velocity first)
+      if (cc < ncurves && jj < nk) {
+        const int src = k + 1 + cc * 2 * nk + 2 * jj;  // np.random.sample: res53 of two words
+        const double a = (double)(gw[src] >> 5), bb = (double)(gw[src + 1] >> 6);
+        A.knots_raw()[A.wix(slot, cc, jj, e)] = (a * 67108864.0 + bb) / 9007199254740992.0;
+      }
+      if (gl == 0) {
+        A.i32(U_STARTY)[(int64_t)slot * A.np + e] = -p.start_y_half + (int32_t)(gw[k] & mask);
+        A.i32(U_MTPOS)[e] = pos + k + 1 + need;
+      }
     }
-#pragma unroll
-    for (int j = 0; j < kRefillAhead; ++j) {
-      const int rr = r0 + j * G;
-      if (rr >= total) break;
-#ifdef SACENV_STAMPS
-      const int sb = 2 + 5 * (n_st < 4 ? n_st : 3);
-      ++n_st;
-#endif
-      REFILL_STAMP(stm[sb], "s"(rr));
-      const int e = __builtin_amdgcn_readlane(ej, j);
-      REFILL_STAMP(stm[sb + 1], "s"(e));
-      const int c = __builtin_amdgcn_readlane(cj, j);
-      const int f0 = __builtin_amdgcn_readlane(fj, j);
-      const int pos0 = __builtin_amdgcn_readlane(pj, j);
-      REFILL_STAMP(stm[sb + 2], "s"(c), "s"(f0), "s"(pos0));
-      if (c >= f0 && lane == 0) atomicOr(&A.status()[1], SACENV_STATUS_SLOT_UNDERFLOW);
-      int f = f0;
+    const int f_next = fast ? f0 + 1 : f0;          // the next episode to draw
+    const int pos_next = fast ? pos + k + 1 + need : pos;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // LDS free for the wave draws
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // the rest, env by env, by the whole wave
+#pragma unroll 1
+    for (int j = 0; j < kGroups; ++j) {
+      const int src = j * kGroupLanes;
+      if (__builtin_amdgcn_readlane((int)ok, src) == 0) break;  // uniform; later groups too
+      const int ej = __builtin_amdgcn_readlane(e, src);
+      const int fe = __builtin_amdgcn_readlane(f_end, src);
+      int f = __builtin_amdgcn_readlane(f_next, src);
+      const int pj = __builtin_amdgcn_readlane(pos_next, src);
       bool first = true;
-      for (; f < c + kSlots; ++f) {
-        const bool pre = first && pos0 + kWave <= kMtN;
-        const int32_t start_y = draw_knots_wave(p, A, lds, e, lane, nullptr, nullptr, first ? pos0 : -1, pre,
-                                                win[j]);
-        REFILL_STAMP(stm[sb + 3], "v"(start_y));
+      for (; f < fe; ++f) {
+        const int32_t start_y = draw_knots_wave(p, A, lds, ej, lane, nullptr, nullptr, first ? pj : -1);
+#ifdef SACENV_STAMPS
+        const int sb = 3 + (n_st < 18 ? n_st : 18);  // the end of each wave draw (first 19)
+        ++n_st;
+#endif
+        REFILL_STAMP(stm[sb], "v"(start_y));
         first = false;
         __syncthreads();
-        store_draw(p, A, lds, e, f % kSlots, start_y, lane, true);
+        store_draw(p, A, lds, ej, f % kSlots, start_y, lane, true);
         __syncthreads();
       }
-      REFILL_STAMP(stm[sb + 4], "v"(f));
       if (lane == 0) {
-        A.i32(U_FILL)[e] = f;
-        A.refill_list(1)[rr] = f0;
-        A.refill_list(2)[rr] = f;
+        A.i32(U_FILL)[ej] = fe;
+        A.refill_list(1)[r0 + j] = __builtin_amdgcn_readlane(f0, src);
+        A.refill_list(2)[r0 + j] = fe;
       }
     }
   }

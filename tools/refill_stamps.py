@@ -7,9 +7,8 @@ clocks k_refill writes into the (otherwise unused) accel region and k_refill_fit
 per-block start/end in the reward64 region. A clock is taken once the values it
 names are in registers; no other wait is inserted (sacenv_boat.hip REFILL_STAMP).
 
-Per refill wave: start, after the mask ranking, then per env it draws (first four):
-iteration start, env found (ranked_env), counters loaded (cons snapshot, fill, MT
-position), draw done (window load, ballot, LDS exchange, knots), stores issued; end.
+Per refill wave (round 3, grouped draw): start, status read, the four-env fast path
+done, the end of each wave-per-env draw that follows (the first 19), end, draw count.
 Prints medians / percentiles in us (100 MHz s_memrealtime) and writes the summary
 as JSON to gpurun_out/refill_stamps.json.
 """
@@ -73,8 +72,9 @@ def main():
                             int(env.status[2].item())))
     tick = 0.01  # us per 100 MHz tick
     out = {"envs": N, "helpers": H, "refills": []}
-    agg = {k: [] for k in ("rank", "find_env", "counters", "draw", "store", "per_env", "wave_span",
-                           "start_skew", "end_spread", "fit_start", "fit_block", "fit_end", "fit_exit_start", "refill_to_fit_gap")}
+    agg = {k: [] for k in ("read_total", "fast_path", "wave_draw", "slow_tail", "wave_span", "start_skew",
+                           "end_spread", "wave_draws", "fit_start", "fit_block", "fit_end", "fit_exit_start",
+                           "refill_to_fit_gap")}
     for a, f, ranked in samples:
         live = a[:, 0] > 0
         a = a[live].astype(np.float64)
@@ -82,19 +82,17 @@ def main():
         agg["start_skew"] += list((a[:, 0] - t0) * tick)
         agg["end_spread"] += list((a[:, 22] - t0) * tick)
         agg["wave_span"] += list((a[:, 22] - a[:, 0]) * tick)
-        agg["rank"] += list((a[:, 1] - a[:, 0]) * tick)
-        n_env = a[:, 23].astype(int)
-        for j in range(4):
-            b = 2 + 5 * j
-            m = n_env > j if j < 3 else n_env == 4  # slot 3 holds the last env of longer waves
-            if not m.any():
-                continue
-            r = a[m]
-            agg["find_env"] += list((r[:, b + 1] - r[:, b]) * tick)
-            agg["counters"] += list((r[:, b + 2] - r[:, b + 1]) * tick)
-            agg["draw"] += list((r[:, b + 3] - r[:, b + 2]) * tick)
-            agg["store"] += list((r[:, b + 4] - r[:, b + 3]) * tick)
-            agg["per_env"] += list((r[:, b + 4] - r[:, b]) * tick)
+        agg["read_total"] += list((a[:, 1] - a[:, 0]) * tick)
+        agg["fast_path"] += list((a[:, 2] - a[:, 1]) * tick)
+        n_dr = a[:, 23].astype(int)
+        agg["wave_draws"] += list(n_dr)
+        for r, n in zip(a, n_dr):
+            prev = r[2]
+            for j in range(min(n, 19)):
+                agg["wave_draw"].append((r[3 + j] - prev) * tick)
+                prev = r[3 + j]
+            if n:
+                agg["slow_tail"].append((r[22] - r[2]) * tick)
         fl = f[f[:, 0] > 0].astype(np.float64)
         fit_span = (fl[:, 1].max() - fl[:, 0].min()) * tick if (fl[:, 1] > 0).any() else None
         if fit_span is not None:  # blocks that fitted (end stamp): start skew, duration
@@ -105,8 +103,8 @@ def main():
             agg["fit_end"] += list((fw[:, 1] - f0) * tick)
             agg["fit_exit_start"] += list((fl[fl[:, 1] == 0][:, 0] - f0) * tick)
             agg["refill_to_fit_gap"] += [float((f0 - a[:, 22].max()) * tick)]
-        out["refills"].append({"ranked_envs": ranked, "k_refill_span_us": float((a[:, 22].max() - t0) * tick),
-                               "envs_per_wave": pct(n_env), "k_refill_fit_span_us": fit_span})
+        out["refills"].append({"listed_envs": ranked, "k_refill_span_us": float((a[:, 22].max() - t0) * tick),
+                               "waves_with_wave_draws": int((n_dr > 0).sum()), "k_refill_fit_span_us": fit_span})
     out["phases_us"] = {k: pct(v) for k, v in agg.items()}
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", "refill_stamps.json"), "w") as fh:
