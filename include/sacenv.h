@@ -135,7 +135,8 @@ typedef struct SacenvBoatLayout {
   int64_t start_y;            /* i32 [SLOTS][n_pad] Boat.s_y_start per slot */
   int64_t counters;           /* u32 [5][n_pad] cumulative termination counters */
   int64_t refill_list;        /* i32 [3][n_pad] by refill rank: env, first and end episode number drawn
-                                 (sacenv_boat_refill's draw launch -> its fit launch) */
+                                 (sacenv_boat_refill's listing launch writes env, fill, cons; its draw
+                                 launch the end episode; its fit launch reads them) */
   int64_t wind_knots;         /* f64 [n_pad][SLOTS][2][n_knots][2]: per episode slot and curve, each
                                  knot's folded value and 2nd derivative / 6 (episode-contiguous:
                                  the refill writes whole lines) */

@@ -150,9 +150,10 @@ struct Arena {
     return reinterpret_cast<unsigned long long*>(tail());
   }
 
-  // each env's episode counter as k_need_masks saw it: the refill tops the ring
-  // up from this snapshot, so a step launch that runs concurrently with the
-  // refill (and rewrites cons) cannot change what it draws
+  // per refill rank: the env's MT position as k_need_masks read it (its episode
+  // counter goes to refill_list(2)): the refill tops the ring up from these
+  // snapshots, so a step launch that runs concurrently with the refill (and
+  // rewrites cons) cannot change what it draws
   __device__ __forceinline__ int32_t* cons_snap() const { return i32(U_CSNAP); }
   // [0] refills done, [1] SACENV_STATUS_* bits, [2] envs ranked by the last refill
   __device__ __forceinline__ int32_t* status() const {
@@ -1148,13 +1149,23 @@ __global__ void __launch_bounds__(kWave) k_refill(SacenvBoatParams p, Arena A) {
   mask |= mask >> 4;
   mask |= mask >> 8;
   mask |= mask >> 16;
-  for (int r0 = blockIdx.x * kGroups; r0 < total; r0 += kGroups * G) {
+  // rank r's env, fill, cons snapshot and MT position (k_need_masks), loaded
+  // with the count and not behind it: list rows below n_pad are always memory
+  const int np_ = (int)A.np;
+  int r0 = blockIdx.x * kGroups;
+  int rq = r0 + g < np_ ? r0 + g : 0;
+  int e_n = A.refill_list(0)[rq], f_n = A.refill_list(1)[rq], c_n = A.refill_list(2)[rq], p_n = A.cons_snap()[rq];
+  for (; r0 < total; r0 += kGroups * G) {
     const int rr = r0 + g;
     const bool ok = rr < total;
-    const int e = ok ? A.refill_list(0)[rr] : 0;
-    const int c = ok ? A.cons_snap()[e] : 0;
-    const int f0 = ok ? A.i32(U_FILL)[e] : 0;
-    const int pos = ok ? A.i32(U_MTPOS)[e] : kMtN;
+    const int e = ok ? e_n : 0;
+    const int c = ok ? c_n : 0;
+    const int f0 = ok ? f_n : 0;
+    const int pos = ok ? p_n : kMtN;
+    if (r0 + kGroups * G < total) {  // the next iteration's rank, in flight with this one
+      rq = rr + kGroups * G < np_ ? rr + kGroups * G : 0;
+      e_n = A.refill_list(0)[rq], f_n = A.refill_list(1)[rq], c_n = A.refill_list(2)[rq], p_n = A.cons_snap()[rq];
+    }
     if (ok && c >= f0 && gl == 0) atomicOr(&A.status()[1], SACENV_STATUS_SLOT_UNDERFLOW);
     const int f_end = ok && f0 < c + kSlots ? c + kSlots : f0;
     bool fast = ok && f0 < f_end && grp_ok && pos + nwords <= kMtN;
@@ -1328,10 +1339,12 @@ __global__ void __launch_bounds__(kMaskThreads) k_need_masks(SacenvBoatParams p,
   const int w = b * (kMaskThreads / kWave) + wv, e = w * kWave + lane;
   const uint32_t epoch = (uint32_t)A.status()[0] + 1u;
   bool need = false;
-  if (w < nw) {
-    const int c = e < p.n_envs ? A.i32(U_CONS)[e] : 0;
-    need = e < p.n_envs && A.i32(U_FILL)[e] < c + kSlots;
-    if (need) A.cons_snap()[e] = c;
+  int c = 0, fl = 0, mp = 0;
+  if (w < nw && e < p.n_envs) {
+    c = A.i32(U_CONS)[e];
+    fl = A.i32(U_FILL)[e];
+    mp = A.i32(U_MTPOS)[e];
+    need = fl < c + kSlots;
   }
   const unsigned long long m = __ballot(need);
   if (lane == 0) wcnt[wv] = __popcll(m);
@@ -1369,7 +1382,13 @@ __global__ void __launch_bounds__(kMaskThreads) k_need_masks(SacenvBoatParams p,
     if (t == 0 && b == (int)gridDim.x - 1) A.status()[2] = before + total;
   }
   __syncthreads();
-  if (need) A.refill_list(0)[wcnt[wv] + __popcll(m & ((1ull << lane) - 1ull))] = e;
+  if (need) {  // rank r: the env and its counters as of now, one load each for k_refill
+    const int r = wcnt[wv] + __popcll(m & ((1ull << lane) - 1ull));
+    A.refill_list(0)[r] = e;
+    A.refill_list(1)[r] = fl;
+    A.refill_list(2)[r] = c;  // the cons snapshot (k_refill then stores the end episode here)
+    A.cons_snap()[r] = mp;
+  }
 }
 
 // Uniform fp64 constants as VGPR copies: the step reads ~40 config doubles,
