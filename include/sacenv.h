@@ -162,8 +162,10 @@ typedef struct SacenvBoatLayout {
 enum {
   SACENV_STATUS_SLOT_UNDERFLOW = 1, /* an env restarted past its pre-drawn episodes: more than
                                        SACENV_REFILL_PERIOD step launches without a refill */
-  SACENV_STATUS_HANDOFF_TIMEOUT = 2  /* sacenv_boat_segment: an action row's flag never came
+  SACENV_STATUS_HANDOFF_TIMEOUT = 2, /* sacenv_boat_segment: an action row's flag never came
                                         (~seconds); the launch stopped stepping */
+  SACENV_STATUS_LIST_TIMEOUT = 4      /* sacenv_boat_refill: a listing workgroup's look-back word
+                                        never came (~seconds); that refill's list is incomplete */
 };
 
 int sacenv_abi_version(void);

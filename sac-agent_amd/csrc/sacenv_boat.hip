@@ -1363,7 +1363,7 @@ __global__ void __launch_bounds__(kMaskThreads) k_need_masks(SacenvBoatParams p,
       unsigned long long x = q < b ? lookback_load(look + q) : ((unsigned long long)epoch << 32);
       for (uint32_t it = 0; __ballot((uint32_t)(x >> 32) != epoch) != 0ull; ++it) {
         if (it >= kSpinLimit) {  // a predecessor that never publishes: flag it, rank as if it listed none
-          if (t == 0) atomicOr(&A.status()[1], SACENV_STATUS_SLOT_UNDERFLOW);
+          if (t == 0) atomicOr(&A.status()[1], SACENV_STATUS_LIST_TIMEOUT);
           break;
         }
         __builtin_amdgcn_s_sleep(1);

@@ -23,6 +23,7 @@ SLOTS = 129
 REFILL_PERIOD = 128  # autoreset: step launches allowed between sacenv_boat_refill calls
 STATUS_SLOT_UNDERFLOW = 1
 STATUS_HANDOFF_TIMEOUT = 2
+STATUS_LIST_TIMEOUT = 4
 RECORD_BYTES = 50
 TRANS_OBS = 9           # s' entries in the pooled row (obs 0..8; 9 and 10 rebuilt by the receiver)
 TRANS_BYTES = 45        # sacenv_boat_step_pooled's per-env transition row

@@ -353,6 +353,8 @@ class VecBoatEnv:
         bits = int(self.status[1].item())
         if bits & _lib.STATUS_SLOT_UNDERFLOW:
             raise _lib.SacenvError("slot underflow: more than REFILL_PERIOD steps without refill()")
+        if bits & _lib.STATUS_LIST_TIMEOUT:
+            raise _lib.SacenvError("refill listing timed out: a listing workgroup never published")
 
     def step(self, actions):
         """BoatEnv.step for all envs (boat_env.py:67-115).
