@@ -114,9 +114,19 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
+MIN_TIMED_SEGS = 8   # the timed region holds at least 1 024 steps
+
+
 def segs(n_steps: int) -> int:
     """Whole segments covering n_steps (at least one)."""
     return max(1, -(-int(n_steps) // SEG))
+
+
+def timed_segs(n_steps: int) -> int:
+    """Timed segments for --steps n: whole segments, at least MIN_TIMED_SEGS. A single
+    128-step segment is a ~0.25-ms region in which the first launch's submission after an
+    idle stream and the closing synchronize (~44 us) were 13 % of the time."""
+    return max(MIN_TIMED_SEGS, segs(n_steps))
 
 
 # ---------------------------------------------------------------- distributed
@@ -597,7 +607,7 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
     st = run.st
     seg_events = run.seg_events
     segment = run.segment
-    n_warm, n_timed = segs(args.warmup), segs(args.steps)
+    n_warm, n_timed = segs(args.warmup), timed_segs(args.steps)
     k = 0
     for _ in range(n_warm):
         k = segment(k, False)
@@ -676,6 +686,9 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
     kern_s = sum(a.ms_to(b) for a, b, _ in seg_events) * 1e-3 / sum(n for _, _, n in seg_events)
     step_s = ev0.ms_to(ev1) * 1e-3 / steps
 
+    every = None
+    if world == 1 and run.mode == "segment" and not args.mixed and not args.no_autoreset:
+        every = every_output_rate(wl, dev, k0=k)
     dinfo = dist_info(world, dev)
     if rank != 0:
         return None
@@ -700,7 +713,8 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
         "steps": steps,
         "warmup": n_warm * SEG,
         "requested": {"steps": args.steps, "warmup": args.warmup,
-                      "rule": f"rounded up to whole {SEG}-step segments (each ends with its refill)"},
+                      "rule": f"rounded up to whole {SEG}-step segments (each ends with its refill); "
+                              f"at least {MIN_TIMED_SEGS * SEG} timed steps"},
         "setup": {"graph_first_replays": run.first_replays,
                   "note": "steps of the first pass over the action table (a captured graph's first "
                           "replay carries its device upload), run before the warm-up, untimed"},
@@ -770,6 +784,7 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
                          "note": "above 1: a step-per-launch design moving 222 B per env-step could not "
                                  "reach this rate at 8 TB/s; the persistent launch is bound by its "
                                  "instruction issue (one owner wave per SIMD), not by HBM"}},
+        "every_output": every,
         "cpu_baseline": None,
         # N>1: what the pooled transitions cost -- every rank receives (world - 1) rows per step
         "dist": dinfo,
@@ -786,6 +801,38 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
             "note": "the timed region ends when the last all_gather has landed",
             "no_exchange": no_exchange},
     }
+
+
+# ---------------------------------------------------------------- every-output rate
+def every_output_rate(wl: Workload, dev, n_segs: int = 8, k0: int = 0) -> dict | None:
+    """The same engine with EVERY step's outputs landing in HBM: K = 128-step
+    sacenv_boat_rollout launches writing each step's 50-B record (obs, reward, done,
+    term) and terminal obs to their own rows (the persistent segment rewrites one
+    record in place, so 127 of 128 steps' rows never leave L2), each followed by the
+    refill; wall-timed between synchronizes."""
+    if dev.type != "cuda":
+        return None
+    env, actions = wl.envs[0], wl.actions
+    recs = torch.empty((SEG, 50 * env.n_pad), dtype=torch.uint8, device=dev)
+    fin = torch.empty((SEG, env.n_pad, 11), dtype=torch.float32, device=dev)
+    k = k0
+    for _ in range(2):                       # warm (first launch of this instantiation)
+        env.rollout(actions[k % ACTION_STEPS: k % ACTION_STEPS + SEG], recs, fin)
+        env.refill()
+        k += SEG
+    _sync(dev)
+    t0 = time.perf_counter()
+    for _ in range(n_segs):
+        env.rollout(actions[k % ACTION_STEPS: k % ACTION_STEPS + SEG], recs, fin)
+        env.refill()
+        k += SEG
+    _sync(dev)
+    el = time.perf_counter() - t0
+    steps = n_segs * SEG
+    return {"value": env.num_envs * steps / el, "unit": "env-steps/s", "steps": steps,
+            "ms_per_step": el / steps * 1e3,
+            "note": "sacenv_boat_rollout, 128 steps per launch, every step's record and terminal obs "
+                    "written to its own rows, + the refill per launch; after the timed region, wall time"}
 
 
 # ---------------------------------------------------------------- rollout line

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SACENV_ABI_VERSION 14
+#define SACENV_ABI_VERSION 15
 #define SACENV_OBS_DIM 11      /* Boat.return_state, boat_env.py:308-323 */
 #define SACENV_MT_N 624        /* MT19937 words per env (numpy legacy RNG) */
 #define SACENV_MAX_KNOTS 16    /* wind.fixed_points upper bound */
@@ -167,6 +167,8 @@ enum {
   SACENV_STATUS_LIST_TIMEOUT = 4      /* sacenv_boat_refill: a listing workgroup's look-back word
                                         never came (~seconds); that refill's list is incomplete */
 };
+/* hand-off flag value of a wave / workgroup that gave up (sacenv_boat_segment) */
+#define SACENV_FLAG_ABORT 0xFFFFFFFFu
 
 int sacenv_abi_version(void);
 const char *sacenv_error_string(int code);
@@ -270,8 +272,13 @@ int sacenv_boat_rollout(const SacenvBoatParams *p, void *arena, const float *act
  *   step ks+1, which cannot start before row ks+1 is published, so a consumer
  *   that reads step ks's record before publishing row ks+1 sees it intact.
  *   Flags are read device-coherently (sc0 sc1); sequence numbers stay below
- *   2^31. A flag that never comes (~seconds of polling) sets
- *   SACENV_STATUS_HANDOFF_TIMEOUT and ends the launch.
+ *   2^31 (checked whenever act_ready or step_done is given). A flag that never
+ *   comes (~seconds of polling) sets SACENV_STATUS_HANDOFF_TIMEOUT and ends the
+ *   launch. Abort protocol: once that bit is set, every later hand-off launch
+ *   (this one, sacenv_sac_act_handoff) steps / computes nothing; a wave or
+ *   workgroup that gives up stores SACENV_FLAG_ABORT into the flag its peer
+ *   waits on, and a peer that reads SACENV_FLAG_ABORT gives up too (it never
+ *   reads the rows behind it). The host learns of it from the status bit.
  * trans (nullable, 16-B aligned, trans_stride a multiple of 16): step ks's
  * pooled transition row (sacenv_boat_step_pooled's format) at trans + ks *
  * trans_stride. Counts as n_steps step launches for the refill contract
@@ -279,6 +286,16 @@ int sacenv_boat_rollout(const SacenvBoatParams *p, void *arena, const float *act
 int sacenv_boat_segment(const SacenvBoatParams *p, void *arena, const float *actions, int64_t action_stride,
                         int32_t n_steps, const uint32_t *act_ready, uint32_t *step_done, uint32_t seq0,
                         void *trans, int64_t trans_stride, void *stream);
+
+/* Co-residency data for the closed loop (main.py:70-91 on the device): the
+ * workgroups per CU the segment launch's kernel can keep resident for these
+ * params (with or without pooled rows) and its grid (n_pad / 64 one-wave
+ * workgroups). The hand-off only makes progress when every owner wave and every
+ * policy workgroup it waits on can be resident at once; sacenv.ClosedLoop
+ * refuses a configuration that cannot. No reference counterpart (the reference
+ * steps one env on the host). */
+int sacenv_boat_segment_occupancy(const SacenvBoatParams *p, int32_t with_trans, int32_t *blocks_per_cu,
+                                  int32_t *grid);
 
 /* Autoreset mode: draw (RNG, Boat.__init__ boat_env.py:144-201 / Wind
  * wind.py:26-99) and spline-fit the replacement episodes of every env that
@@ -507,6 +524,10 @@ int sacenv_sac_act(const SacenvSacParams *p, const float *weights, const float *
  * once its actions are visible device-wide, stores act_ready[b] = act_value
  * (the segment's act_ready flags). Values below 2^31; a flag that never comes
  * (~seconds) sets SACENV_STATUS_HANDOFF_TIMEOUT in *status (nullable). */
+/* The act kernel's resident workgroups per CU and its grid for n rows (64 rows per
+ * 256-thread workgroup): the policy half of the closed loop's co-residency check. */
+int sacenv_sac_act_occupancy(int32_t n, int32_t *blocks_per_cu, int32_t *grid);
+
 int sacenv_sac_act_handoff(const SacenvSacParams *p, const float *weights, const float *obs, int32_t n,
                            const float *eps, float *action, const uint32_t *obs_ready, uint32_t obs_want,
                            uint32_t *act_ready, uint32_t act_value, int32_t *status, void *stream);

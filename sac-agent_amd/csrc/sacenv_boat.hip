@@ -2146,16 +2146,17 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   if (kHand && per_step && ks + 1 < n_steps) {
     const uint32_t fv = flag_value(flag_now);
     seen = fv > seen ? fv : seen;
-    if (!act_next) {  // closed loop: the next action comes after these outputs
+    failed = seen == SACENV_FLAG_ABORT;  // the producer gave up: so does this wave
+    if (!act_next && !failed) {  // closed loop: the next action comes after these outputs
       seen = wait_flag(rdy, ra->seq0 + (uint32_t)ks + 2u, seen, ra->status, lane);
-      failed = seen == 0u;
+      failed = seen == 0u || seen == SACENV_FLAG_ABORT;
       act_cur = act_load(abase, (uint32_t)((ks + 1) * arow));
     }
   }
   PHASE(4);
   }  // steps
   if (kHand && failed && ra->done != nullptr && lane == 0)  // waiters on this wave must not hang
-    __hip_atomic_store(ra->done + ob, 0x7FFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(ra->done + ob, SACENV_FLAG_ABORT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (kRoll) {  // the carried state, once
     A.f64e(U_SX, eo) = s_x, A.f64e(U_SY, eo) = s_y, A.f64e(U_SR, eo) = s_r;
     A.f64e(U_VX, eo) = v_x, A.f64e(U_VY, eo) = v_y, A.f64e(U_VR, eo) = v_r;
@@ -2230,14 +2231,24 @@ __global__ void __launch_bounds__(kWave) k_rollout(SacenvBoatParams p, Arena A, 
   const int ob = blockIdx.x, lane = threadIdx.x;
   uint32_t seen = 0u;
   bool hand = ra.done != nullptr;
-  if (ra.ready != nullptr) {
-    const uint32_t* rdy = ra.ready + ob;
-    seen = wait_flag(rdy, ra.seq0 + 1u, flag_load(rdy), ra.status, lane);
-    if (seen == 0u) {  // row 0 never came: nothing steps
+  if (ra.ready != nullptr || ra.done != nullptr) {
+    // abort protocol (sacenv.h): after a hand-off timeout anywhere, a hand-off
+    // launch steps nothing; a producer that gave up published SACENV_FLAG_ABORT
+    const uint32_t* rdy = ra.ready != nullptr ? ra.ready + ob : nullptr;
+    const uint32_t st = flag_issue(reinterpret_cast<const uint32_t*>(ra.status));
+    const uint32_t f0 = rdy != nullptr ? flag_issue(rdy) : 0u;
+    bool stop = (flag_value(st) & SACENV_STATUS_HANDOFF_TIMEOUT) != 0u;
+    if (!stop && rdy != nullptr) {
+      seen = wait_flag(rdy, ra.seq0 + 1u, flag_value(f0), ra.status, lane);
+      stop = seen == 0u || seen == SACENV_FLAG_ABORT;  // row 0 never came: nothing steps
+    }
+    if (stop) {
       if (ra.done != nullptr && lane == 0)  // waiters on this wave must not hang either
-        __hip_atomic_store(ra.done + ob, 0x7FFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ra.done + ob, SACENV_FLAG_ABORT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return;
     }
+  }
+  if (ra.ready != nullptr) {
     // the rows the flag covers were written before it (the producer's release):
     // drop any stale copy of them from this XCD's L2 once, then read them plainly;
     // rows published only later are read device-coherently, step by step
@@ -2532,7 +2543,8 @@ int sacenv_boat_segment(const SacenvBoatParams* p, void* arena, const float* act
   if (rc) return rc;
   if (arena == nullptr || actions == nullptr) return SACENV_E_NULL;
   if (n_steps < 1 || (p->autoreset && n_steps > SACENV_REFILL_PERIOD)) return SACENV_E_SIZE;
-  if (action_stride < p->n_envs || (act_ready != nullptr && seq0 + (uint32_t)n_steps >= 0x80000000u))
+  if (action_stride < p->n_envs ||
+      ((act_ready != nullptr || step_done != nullptr) && (uint64_t)seq0 + (uint64_t)n_steps >= 0x80000000ull))
     return SACENV_E_RANGE;
   if (trans != nullptr && ((reinterpret_cast<uintptr_t>(trans) & 15u) != 0u || (trans_stride & 15) != 0))
     return SACENV_E_RANGE;  // float4 row stores
@@ -2550,6 +2562,27 @@ int sacenv_boat_segment(const SacenvBoatParams* p, void* arena, const float* act
   ra.seq0 = seq0;
   ra.status = reinterpret_cast<int32_t*>(static_cast<char*>(arena) + status_offset(*p)) + 1;
   return launch_multi(*p, arena, actions, n_steps, ra, stream);
+}
+
+// Resident workgroups per CU of the segment launch's kernel for these params
+// (hipOccupancyMaxActiveBlocksPerMultiprocessor) and the launch's grid: the
+// closed loop checks that this grid and the policy's fit on the device together.
+int sacenv_boat_segment_occupancy(const SacenvBoatParams* p, int32_t with_trans, int32_t* blocks_per_cu,
+                                  int32_t* grid) {
+  int rc = check_params(p);
+  if (rc) return rc;
+  if (blocks_per_cu == nullptr || grid == nullptr) return SACENV_E_NULL;
+  int nb = 0;
+  hipError_t e = hipSuccess;
+#define SACENV_OCC(NC, TI)                                                                              \
+  e = with_trans ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_rollout<NC, TI, true>, kWave, 0)  \
+                 : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_rollout<NC, TI, false>, kWave, 0)
+  SACENV_OWNER_DISPATCH(*p, SACENV_OCC)
+#undef SACENV_OCC
+  if (e != hipSuccess) return (int)e;
+  *blocks_per_cu = nb;
+  *grid = (int32_t)(pad64(p->n_envs) / kWave);
+  return SACENV_OK;
 }
 
 int sacenv_boat_refill(const SacenvBoatParams* p, void* arena, void* stream) {

@@ -962,18 +962,32 @@ __global__ void __launch_bounds__(kThreads) k_sac_act(SacArgs a, const float* __
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, i = lane & 15, kq = lane >> 4;
   const int row0 = blockIdx.x * kActRows;
   if (h.obs_ready != nullptr) {
+    // Abort protocol (shared with sacenv_boat_segment): a hand-off that timed out
+    // anywhere leaves SACENV_STATUS_HANDOFF_TIMEOUT set, and every later hand-off
+    // launch refuses to compute; a wave that gives up publishes SACENV_FLAG_ABORT so
+    // its peer stops too instead of reading stale rows. No one waits forever.
+    bool abort = false;
     if (tid < 64) {  // one wave polls (bounded: ~seconds), the workgroup waits at the barrier
       const uint32_t* f = h.obs_ready + blockIdx.x;
-      uint32_t it = 0;
-      while (flag_load(f) < h.obs_want) {
+      abort = h.status != nullptr &&
+              (flag_load(reinterpret_cast<const uint32_t*>(h.status)) & SACENV_STATUS_HANDOFF_TIMEOUT) != 0;
+      uint32_t it = 0, v = abort ? 0u : flag_load(f);
+      while (!abort && v < h.obs_want) {
         if (++it >= (1u << 22)) {
           if (tid == 0 && h.status != nullptr) atomicOr(h.status, SACENV_STATUS_HANDOFF_TIMEOUT);
+          abort = true;
           break;
         }
         __builtin_amdgcn_s_sleep(2);
+        v = flag_load(f);
       }
+      abort = abort || v == SACENV_FLAG_ABORT;
     }
-    __syncthreads();
+    if (__syncthreads_or(abort ? 1 : 0)) {
+      if (tid == 0)  // the env wave waiting for this row must not hang: release it, as an abort
+        __hip_atomic_store(h.act_ready + blockIdx.x, SACENV_FLAG_ABORT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // no stale L2 lines of the obs rows
   }
   const int nrows = n - row0 < kActRows ? n - row0 : kActRows;
@@ -1198,6 +1212,19 @@ static int sac_act(const SacenvSacParams* p, const float* weights, const float* 
 extern "C" int sacenv_sac_act(const SacenvSacParams* p, const float* weights, const float* obs, int32_t n,
                               const float* eps, float* action, float* log_prob, void* stream) {
   return sac_act(p, weights, obs, n, eps, action, log_prob, ActHandoff{}, stream);
+}
+
+// Resident workgroups per CU of the act kernel and its grid for n rows (the
+// closed loop's co-residency check, sacenv.h).
+extern "C" int sacenv_sac_act_occupancy(int32_t n, int32_t* blocks_per_cu, int32_t* grid) {
+  if (blocks_per_cu == nullptr || grid == nullptr) return SACENV_E_NULL;
+  if (n < 0) return SACENV_E_SIZE;
+  int nb = 0;
+  const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sac_act, kThreads, 0);
+  if (e != hipSuccess) return (int)e;
+  *blocks_per_cu = nb;
+  *grid = (n + kActRows - 1) / kActRows;
+  return SACENV_OK;
 }
 
 extern "C" int sacenv_sac_act_handoff(const SacenvSacParams* p, const float* weights, const float* obs,

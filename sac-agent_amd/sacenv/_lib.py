@@ -14,7 +14,7 @@ PKG_ROOT = _build.PKG_ROOT
 LIB_PATH = os.environ.get("SACENV_LIB", _build.LIB)
 LOADED_DIGEST = None  # source digest of the loaded library (the in-tree build)
 
-ABI_VERSION = 14
+ABI_VERSION = 15
 OBS_DIM = 11
 MT_N = 624
 MAX_KNOTS = 16
@@ -24,6 +24,7 @@ REFILL_PERIOD = 128  # autoreset: step launches allowed between sacenv_boat_refi
 STATUS_SLOT_UNDERFLOW = 1
 STATUS_HANDOFF_TIMEOUT = 2
 STATUS_LIST_TIMEOUT = 4
+FLAG_ABORT = 0xFFFFFFFF  # hand-off flag of a wave / workgroup that gave up (sacenv.h)
 RECORD_BYTES = 50
 TRANS_OBS = 9           # s' entries in the pooled row (obs 0..8; 9 and 10 rebuilt by the receiver)
 TRANS_BYTES = 45        # sacenv_boat_step_pooled's per-env transition row
@@ -132,12 +133,13 @@ class SacLayout(C.Structure):
 
 EXPORTS = ("sacenv_abi_version", "sacenv_error_string", "sacenv_boat_layout",
            "sacenv_boat_init", "sacenv_boat_reset", "sacenv_boat_reset_explicit",
-           "sacenv_boat_step", "sacenv_boat_step_pooled", "sacenv_boat_rollout", "sacenv_boat_segment", "sacenv_boat_refill", "sacenv_boat_wind_eval", "sacenv_toy_layout", "sacenv_toy_init",
+           "sacenv_boat_step", "sacenv_boat_step_pooled", "sacenv_boat_rollout", "sacenv_boat_segment",
+           "sacenv_boat_segment_occupancy", "sacenv_boat_refill", "sacenv_boat_wind_eval", "sacenv_toy_layout", "sacenv_toy_init",
            "sacenv_toy_reset", "sacenv_toy_step", "sacenv_mixed_step", "sacenv_mixed_step_pooled", "sacenv_replay_layout",
            "sacenv_replay_init", "sacenv_replay_store", "sacenv_replay_store_env", "sacenv_replay_sample", "sacenv_replay_store_shard",
            "sacenv_replay_sample_shard",
            "sacenv_compact_done", "sacenv_boat_reset_list", "sacenv_sac_layout", "sacenv_sac_sync",
-           "sacenv_sac_act", "sacenv_sac_act_handoff", "sacenv_sac_learn")
+           "sacenv_sac_act", "sacenv_sac_act_handoff", "sacenv_sac_act_occupancy", "sacenv_sac_learn")
 
 _LIB = None
 
@@ -187,6 +189,7 @@ def load(path: str | None = None):
         "sacenv_boat_refill": (C.c_int, [P, _p, _p]),
         "sacenv_boat_rollout": (C.c_int, [P, _p, _p, _i32, _p, _p, _p]),
         "sacenv_boat_segment": (C.c_int, [P, _p, _p, _i64, _i32, _p, _p, C.c_uint32, _p, _i64, _p]),
+        "sacenv_boat_segment_occupancy": (C.c_int, [P, _i32, C.POINTER(_i32), C.POINTER(_i32)]),
         "sacenv_boat_wind_eval": (C.c_int, [P, _p, _p, _p, _i32, _p, _p, _p]),
         "sacenv_toy_layout": (C.c_int, [TP, C.POINTER(ToyLayout)]),
         "sacenv_toy_init": (C.c_int, [TP, _p, _p]),
@@ -209,6 +212,7 @@ def load(path: str | None = None):
         "sacenv_sac_act": (C.c_int, [C.POINTER(SacParams), _p, _p, _i32, _p, _p, _p, _p]),
         "sacenv_sac_act_handoff": (C.c_int, [C.POINTER(SacParams), _p, _p, _i32, _p, _p, _p, C.c_uint32, _p,
                                              C.c_uint32, _p, _p]),
+        "sacenv_sac_act_occupancy": (C.c_int, [_i32, C.POINTER(_i32), C.POINTER(_i32)]),
         "sacenv_sac_learn": (C.c_int, [C.POINTER(SacParams), _p, _p, _p, _p, _p, _p, _p, _p, _p, _i32,
                                        _p, _p]),
     }

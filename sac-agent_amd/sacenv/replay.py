@@ -187,31 +187,49 @@ class ShardedReplayBuffer(DeviceReplayBuffer):
 
     def sample(self, batch_size: int):
         """The pooled buffer's sample_buffer (buffer.py:24-35), identical on every rank."""
+        return self.sample_many(batch_size, 1)[0]
+
+    def sample_many(self, batch_size: int, n_batches: int):
+        """``n_batches`` consecutive sample_buffer calls (the batches of that many
+        ``learn()`` calls, e.g. one per step of a segment) assembled with ONE SUM
+        all-reduce: the same batches, in the same order, as ``n_batches`` ``sample``
+        calls (the index draws continue the buffer's one MT19937 stream), for one
+        collective's latency instead of ``n_batches``."""
         import torch.distributed as dist
-        B = int(batch_size)
+        B, n = int(batch_size), int(n_batches)
+        if n < 1:
+            raise ValueError("n_batches must be positive")
         if self.mem_cntr == 0 and B > 0:
             raise ValueError("a must be greater than 0 unless no samples are taken")
         D, A = int(np.prod(self.input_shape)), self.n_actions
-        # one buffer of 32-bit words: state, new_state, action (f32), reward (f64 = 2 words), terminal
-        words = torch.zeros(B * (2 * D + A + 3), dtype=torch.int32, device=self.device)
-        st = words[: B * D].view(torch.float32).view(B, *self.input_shape)
-        ns = words[B * D: 2 * B * D].view(torch.float32).view(B, *self.input_shape)
-        o = 2 * B * D
-        ac = words[o: o + B * A].view(torch.float32).view(B, A)
-        o += B * A
-        rw = words[o: o + 2 * B].view(torch.float64)
-        o += 2 * B
-        tm32 = words[o: o + B]
+        # per batch, 32-bit words: reward (f64 = 2 words, first: 8-B aligned), state,
+        # new_state, action (f32), terminal; each block padded to an even word count
+        per = B * (2 * D + A + 3)
+        per += per & 1
+        words = torch.zeros(n * per, dtype=torch.int32, device=self.device)
         tm = torch.empty(B, dtype=torch.uint8, device=self.device)
-        idx = torch.empty(B, dtype=torch.int64, device=self.device)
-        _lib.check(self.lib.sacenv_replay_sample_shard(
-            self._pp, self.arena.data_ptr(), B, self.mem_cntr, self.offset, self.n, self.period,
-            idx.data_ptr(), st.data_ptr(), ac.data_ptr(), rw.data_ptr(), ns.data_ptr(), tm.data_ptr(),
-            self.stream))
-        tm32.copy_(tm.to(torch.int32))
+        views = []
+        for i in range(n):
+            w = words[i * per: (i + 1) * per]
+            rw = w[: 2 * B].view(torch.float64)
+            o = 2 * B
+            st = w[o: o + B * D].view(torch.float32).view(B, *self.input_shape)
+            o += B * D
+            ns = w[o: o + B * D].view(torch.float32).view(B, *self.input_shape)
+            o += B * D
+            ac = w[o: o + B * A].view(torch.float32).view(B, A)
+            o += B * A
+            tm32 = w[o: o + B]
+            idx = torch.empty(B, dtype=torch.int64, device=self.device)
+            _lib.check(self.lib.sacenv_replay_sample_shard(
+                self._pp, self.arena.data_ptr(), B, self.mem_cntr, self.offset, self.n, self.period,
+                idx.data_ptr(), st.data_ptr(), ac.data_ptr(), rw.data_ptr(), ns.data_ptr(), tm.data_ptr(),
+                self.stream))
+            tm32.copy_(tm.to(torch.int32))
+            views.append((st, ac, rw, ns, tm32, idx))
         if self.world > 1:
             dist.all_reduce(words, op=dist.ReduceOp.SUM, group=self.group)
-        return st, ac, rw, ns, tm32.to(torch.bool), idx
+        return [(st, ac, rw, ns, tm32.to(torch.bool), idx) for st, ac, rw, ns, tm32, idx in views]
 
 
 class ReplayBuffer:

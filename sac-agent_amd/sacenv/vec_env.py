@@ -355,6 +355,9 @@ class VecBoatEnv:
             raise _lib.SacenvError("slot underflow: more than REFILL_PERIOD steps without refill()")
         if bits & _lib.STATUS_LIST_TIMEOUT:
             raise _lib.SacenvError("refill listing timed out: a listing workgroup never published")
+        if bits & _lib.STATUS_HANDOFF_TIMEOUT:
+            raise _lib.SacenvError("segment hand-off timed out: an action row's flag never came; "
+                                   "hand-off launches on this arena now step nothing")
 
     def step(self, actions):
         """BoatEnv.step for all envs (boat_env.py:67-115).

@@ -16,12 +16,19 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device)")
 
 
-def golden(name: str):
-    return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+def golden(name: str) -> dict:
+    """A fixture's arrays, decompressed once (an NpzFile re-reads its member per access)."""
+    with np.load(os.path.join(GOLDEN, name), allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
 
 
 def seeded_fixtures():
     return sorted(f for f in os.listdir(GOLDEN) if f.startswith("seeded_"))
+
+
+def long_fixtures():
+    """The 10 000-step scripted runs (make_golden.py run_long)."""
+    return sorted(f for f in os.listdir(GOLDEN) if f.startswith("long_"))
 
 
 @pytest.fixture(scope="session")

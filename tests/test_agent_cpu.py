@@ -17,7 +17,7 @@ NETS = ("actor", "critic_1", "critic_2", "value", "target_value")
 
 def run_learn(device, z):
     from sacenv.agent import VecSAC
-    cfg = {"agent": {k[4:]: z[k].item() for k in z.files if k.startswith("cfg_")}}
+    cfg = {"agent": {k[4:]: z[k].item() for k in z if k.startswith("cfg_")}}
     agent = VecSAC(device, cfg, init_seed=int(z["seed"]), with_memory=False)
     eps = torch.from_numpy(z["eps"])
     losses = []
@@ -65,7 +65,7 @@ def test_vec_sac_learn_matches_reference_cpu():
 def test_agent_config_from_reference_yaml():
     from sacenv.agent import AgentConfig
     z = golden("sac_learn.npz")
-    c = AgentConfig.from_any({"agent": {k[4:]: z[k].item() for k in z.files if k.startswith("cfg_")}})
+    c = AgentConfig.from_any({"agent": {k[4:]: z[k].item() for k in z if k.startswith("cfg_")}})
     assert c == AgentConfig()  # the defaults are configs/original_config.yaml:12-21
 
 

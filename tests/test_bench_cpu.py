@@ -65,9 +65,9 @@ def _run(rank, world, argv):
 
 def test_driver_command_world1_rounds_to_whole_segments():
     out, env = _run(0, 1, ["--gpus", "1", "--steps", "20", "--warmup", "5"])
-    assert out["steps"] == 128 and out["warmup"] == 128
+    assert out["steps"] == 8 * 128 and out["warmup"] == 128   # at least 8 timed segments
     assert out["requested"] == {"steps": 20, "warmup": 5, "rule": out["requested"]["rule"]}
-    # every segment ends with its refill; timed region = one whole segment (+1 k_step seg after)
+    # every segment ends with its refill; timed region = eight whole segments (+ k_step segs after)
     assert all(s % 128 == 0 for s in env.refill_at), env.refill_at
     assert env.refill_at[:2] == [128, 256]
     assert out["value"] > 0 and out["ms_per_step"] > 0
@@ -84,7 +84,7 @@ def test_metric_follows_the_config():
     assert "mixed batch" in bench.metric_name(m) and "32 768" in bench.metric_name(m)
 
 
-@pytest.mark.parametrize("steps,warmup,n_timed", [(20, 5, 1), (300, 0, 3)])
+@pytest.mark.parametrize("steps,warmup,n_timed", [(20, 5, 8), (300, 0, 8), (1100, 0, 9)])
 def test_segment_rounding(steps, warmup, n_timed):
     out, env = _run(0, 1, ["--steps", str(steps), "--warmup", str(warmup), "--kernel-launches", "1"])
     assert out["steps"] == n_timed * 128
@@ -129,9 +129,9 @@ def test_driver_command_world2_gloo_segment_pooling():
         assert p.exitcode == 0
     out = res[0][1]
     assert res[1][1] is None
-    assert out["steps"] == 128 and out["n_gpus"] == 2
+    assert out["steps"] == 8 * 128 and out["n_gpus"] == 2
     assert out["value"] > 0
-    assert "1 in the timed region" in out["config"]["collective"]
+    assert "8 in the timed region" in out["config"]["collective"]
     assert "gloo" in out["config"]["collective"]
     # the row is the step kernel's 45-B/env transition row
     assert f"{45 * N_PAD} B per rank-step" in out["config"]["collective"]

@@ -34,7 +34,7 @@ def declared_functions():
 def test_library_exports_header(built_lib):
     from sacenv import _lib
     names = declared_functions()
-    assert len(names) == 32
+    assert len(names) == 34
     assert set(names) == set(_lib.EXPORTS)
     for n in names:
         assert hasattr(built_lib, n), n
@@ -473,3 +473,23 @@ def test_native_sac_views_follow_the_c_layout(built_lib):
     # actor: w1 [256][11] at tensor[0][0]; critic w1 [256][12]; value heads follow fc2.bias
     assert L.tensor[0][2] - L.tensor[0][0] == 256 * 11 + 256  # 2 816 floats of fc1.weight are 16-B aligned
     assert L.tensor[1][1] == 256 * 12 and L.tensor[2][6] == -1 and L.tensor[0][6] > L.tensor[0][5]
+
+
+def test_closed_loop_co_residency_plan_arithmetic():
+    """sacenv.closed_loop's plan (no GPU): the segment grid's even share per CU plus one
+    policy launch's share must fit one CU; the policy is split into launches that do."""
+    from sacenv.closed_loop import make_plan, max_envs
+    p = make_plan(256, 8, 1024, 2, 1024, 65536)       # 4 owner waves/CU of 8: room for 1 act WG
+    assert p.seg_frac == 0.5 and p.chunk_waves == 256 and p.chunks == 4
+    p = make_plan(256, 16, 1024, 4, 1024, 65536)      # 4 of 16: 3 act WGs per CU
+    assert p.chunk_waves == 768 and p.chunks == 2
+    p = make_plan(256, 16, 100, 4, 100, 6400)         # small grids: one launch
+    assert p.chunk_waves == 100 and p.chunks == 1
+    with pytest.raises(ValueError):
+        make_plan(256, 8, 2048, 2, 2048, 131072)      # 8 of 8 per CU: no room
+    assert max_envs(256, 8, 2) == 65536
+    assert max_envs(256, 16, 4) == 64 * 256 * 12
+    n = max_envs(256, 10, 3)
+    make_plan(256, 10, n // 64, 3, n // 64, n)
+    with pytest.raises(ValueError):
+        make_plan(256, 10, n // 64 + 256, 3, n // 64 + 256, n + 64 * 256)

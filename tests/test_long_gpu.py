@@ -1,0 +1,249 @@
+"""The reference's long scripted runs (tests/golden/long_*.npz) on the MI355X.
+
+VERDICT r3 next 1: no earlier fixture reached the reference's turn-around branches
+(|s_r| > pi/2, boat_env.py:110-111; s_x < 0, :90; the default-t_max timeout, :98-101)
+or a heading far outside [-pi, pi] (the kernel's ``sincos_cw`` reduction). These
+fixtures do (``test_oracle_long.py`` asserts which branches each one reaches): 10 000
+steps of scripted rudder programs on default configs, the actions recorded.
+
+Three launch paths replay them, all through the C ABI:
+
+* ``sacenv_boat_step`` (``VecBoatEnv.step_async``), one launch per step, ended envs
+  reset by the host (``sacenv_boat_reset``) as the reference's main loop does;
+* ``sacenv_boat_segment`` (the timed kernel), driven by bench.py's own
+  ``SegmentRunner`` -- one persistent 128-step launch plus the slot refill per
+  segment, in-kernel auto-reset -- each step's pooled transition row (obs entries
+  0..8 before any reset, reward, term) written by the launch itself;
+* the same segments with ``VecBoatEnv.segment_async`` and per-wave hand-off flags
+  (the closed loop's launch form, every row published ahead).
+
+Bar (BASELINE north_star): term / done bit-exact at every step; carried state within
+STATE_TOL = 1e-5 at the kept steps (every 10th, every 128th, around each episode
+end); f64 reward within 1e-5 at every step (the step path), f32 reward and obs within
+f32 rounding (the segment paths).
+"""
+import numpy as np
+import pytest
+import torch
+
+from boat_oracle import config_from_fixture
+from conftest import golden, long_fixtures
+
+pytestmark = pytest.mark.gpu
+
+STATE_TOL = 1e-5
+OBS_TOL = 1e-6
+CARRIED = ("s_x", "s_y", "s_r", "v_x", "v_y", "v_r", "rudder_angle", "index")
+SEG = 128
+
+
+def _cfg_dict(z):
+    c = config_from_fixture(z)
+    return {"base_settings": {"experiment": c.experiment, "test_mode": c.test_mode,
+                              "dt": c.dt, "t_max": c.t_max},
+            "boat_env": {"track_width": c.track_width, "goal_line": c.goal_line,
+                         "boat_out_of_bounds_offset": c.oob_offset},
+            "boat": {"fuel": c.fuel}}
+
+
+def _dev_state(env):
+    """The fixture's 13 state fields of every env, as one f64 device tensor (no sync)."""
+    f = torch.float64
+    idx = env.index.to(f)
+    return torch.stack([env.s_x, env.s_y, env.s_r, env.v_x, env.v_y, env.v_r, env.accel[0],
+                        env.accel[1], env.accel[2], env.rudder, env.t.to(f),
+                        float(env.cfg.fuel) - idx, idx], 1)
+
+
+def _expected_state(z, j, k, reset: bool):
+    """The reference's state after step k (kept index j); after the host's reset of an
+    ended env when ``reset``."""
+    st = z["state"][:, j].copy()
+    if reset:
+        d = z["done"][:, k].astype(bool)
+        st[d] = z["reset_state"][:, j][d]
+    return st
+
+
+@pytest.mark.parametrize("name", long_fixtures())
+def test_long_fixture_step_launches(name, gpu, built_lib):
+    from sacenv import VecBoatEnv
+    z = golden(name)
+    E, S = z["reward"].shape
+    keep = {int(k): j for j, k in enumerate(z["keep"])}
+    env = VecBoatEnv(_cfg_dict(z), E, seeds=z["seeds"], device=gpu, autoreset=False,
+                     record_accel=True, record_reward64=True)
+    obs0 = env.reset().cpu().numpy()
+    np.testing.assert_allclose(obs0, z["init_obs"], rtol=0, atol=OBS_TOL)
+    acts = torch.from_numpy(np.ascontiguousarray(z["actions"].T)).to(gpu)     # [S, E]
+    K = len(keep)
+    term = torch.empty((S, E), dtype=torch.uint8, device=gpu)
+    done = torch.empty_like(term)
+    rew = torch.empty((S, E), dtype=torch.float64, device=gpu)
+    st = torch.empty((K, E, 13), dtype=torch.float64, device=gpu)
+    rst = torch.full((K, E, 13), float("nan"), dtype=torch.float64, device=gpu)
+    obs = torch.empty((K, E, 11), dtype=torch.float32, device=gpu)
+    robs = torch.full((K, E, 11), float("nan"), dtype=torch.float32, device=gpu)
+    for k in range(S):
+        env.step_async(acts[k])
+        term[k].copy_(env.term)
+        done[k].copy_(env.done)
+        rew[k].copy_(env.reward64)
+        j = keep.get(k)
+        if j is not None:
+            st[j].copy_(_dev_state(env))
+            obs[j].copy_(env.obs)
+        ended = np.flatnonzero(z["done"][:, k])
+        if ended.size:                      # main.py:72: reset when done
+            env.reset(ended)
+            rst[j].copy_(_dev_state(env))   # (episode ends are kept steps)
+            robs[j].copy_(env.obs)
+    torch.cuda.synchronize()
+    term, done, rew = term.cpu().numpy().T, done.cpu().numpy().T, rew.cpu().numpy().T
+    for e in range(E):
+        bad = np.flatnonzero(term[e] != z["term"][e])
+        assert bad.size == 0, f"{name} env {e}: term differs first at step {bad[:1]}"
+    np.testing.assert_array_equal(done, z["done"])
+    err_r = np.abs(rew - z["reward"]).max()
+    assert err_r <= STATE_TOL, f"reward off by {err_r}"
+    st, obs = st.cpu().numpy().transpose(1, 0, 2), obs.cpu().numpy().transpose(1, 0, 2)
+    err = np.abs(st - z["state"])
+    assert err.max() <= STATE_TOL, (f"state off by {err.max()} at kept step "
+                                    f"{z['keep'][np.unravel_index(err.argmax(), err.shape)[1]]}")
+    np.testing.assert_allclose(obs, z["obs"], rtol=OBS_TOL, atol=OBS_TOL)
+    rst, robs = rst.cpu().numpy().transpose(1, 0, 2), robs.cpu().numpy().transpose(1, 0, 2)
+    ends = ~np.isnan(z["reset_state"][..., 0])
+    assert ends.sum() == z["done"].sum() > 0
+    np.testing.assert_allclose(rst[ends], z["reset_state"][ends], rtol=0, atol=STATE_TOL)
+    np.testing.assert_allclose(robs[ends], z["reset_obs"][ends], rtol=0, atol=OBS_TOL)
+    np.testing.assert_array_equal(env.counters.cpu().numpy().T, z["counters"])
+    print(f"{name}: worst state err {err.max():.3e}, reward {err_r:.3e}")
+
+
+def _segment_env(z, gpu):
+    from sacenv import VecBoatEnv
+    E = z["reward"].shape[0]
+    env = VecBoatEnv(_cfg_dict(z), E, seeds=z["seeds"], device=gpu, autoreset=True,
+                     n_helpers=4, auto_refill=False)
+    env.reset()                       # main.py:72 (the constructor drew one Boat already)
+    return env
+
+
+def _check_segment_outputs(name, z, env, rows, seg_state):
+    """rows: [S_pad, row] pooled transition rows; seg_state: [n_seg, E, 8] carried state
+    after each segment."""
+    from sacenv.dist import TransitionLayout
+    E, S = z["reward"].shape
+    lay = TransitionLayout(E, env.n_pad, int(z["cfg_experiment"]))
+    rows = rows.cpu()
+    keep = {int(k): j for j, k in enumerate(z["keep"])}
+    term = np.empty((E, S), np.uint8)
+    rew = np.empty((E, S), np.float32)
+    s9 = {}
+    for k in range(S):
+        v = lay.views(rows[k])
+        term[:, k] = v[3].numpy()
+        rew[:, k] = v[1].numpy()
+        if k in keep:
+            s9[keep[k]] = v[0].numpy()
+    for e in range(E):
+        bad = np.flatnonzero(term[e] != z["term"][e])
+        assert bad.size == 0, f"{name} env {e}: term differs first at step {bad[:1]}"
+    np.testing.assert_allclose(rew, z["reward"], rtol=OBS_TOL, atol=1e-5)
+    for j, o in s9.items():
+        np.testing.assert_allclose(o, z["obs"][:, j, :9], rtol=OBS_TOL, atol=OBS_TOL,
+                                   err_msg=f"{name} step {z['keep'][j]}")
+    fields = [str(f) for f in z["state_fields"]]
+    cols = [fields.index(f) for f in CARRIED]
+    seg_state = seg_state.cpu().numpy()
+    worst = 0.0
+    for s in range(seg_state.shape[0]):
+        k = SEG * s + SEG - 1
+        if k >= S:
+            break
+        exp = _expected_state(z, keep[k], k, reset=True)[:, cols]
+        err = np.abs(seg_state[s] - exp).max()
+        worst = max(worst, err)
+        assert err <= STATE_TOL, f"{name}: carried state off by {err} after step {k}"
+    np.testing.assert_array_equal(env.counters.cpu().numpy().T, z["counters"])
+    env.check_status()
+    return worst
+
+
+def _carried(env):
+    f = torch.float64
+    return torch.stack([env.s_x, env.s_y, env.s_r, env.v_x, env.v_y, env.v_r, env.rudder,
+                        env.index.to(f)], 1)
+
+
+@pytest.mark.parametrize("name", long_fixtures())
+def test_long_fixture_bench_segment_runner(name, gpu, built_lib):
+    """bench.py's timed path: SegmentRunner in its default mode (one persistent
+    sacenv_boat_segment launch + the refill per 128 steps)."""
+    import ctypes as C
+
+    import bench
+    from sacenv import _lib
+    from sacenv.dist import TransitionLayout
+    z = golden(name)
+    E, S = z["reward"].shape
+    env = _segment_env(z, gpu)
+    n_seg = -(-S // SEG)
+    table = torch.zeros((n_seg * SEG, E), dtype=torch.float32, device=gpu)
+    table[:S] = torch.from_numpy(np.ascontiguousarray(z["actions"].T)).to(gpu)
+    rb = TransitionLayout(E, env.n_pad, int(z["cfg_experiment"])).nbytes
+    assert rb % 16 == 0
+    rows = torch.zeros((n_seg * SEG, rb), dtype=torch.uint8, device=gpu)
+    ready = torch.full((env.n_pad // 64,), 0x7FFFFFFF, dtype=torch.int32, device=gpu)
+
+    def segment_step(k0, n, trans=None):
+        # bench.make_workload's closure over this fixture's action table (rows k0..),
+        # each step's transition row written by the launch into rows[k]
+        _lib.check(env.lib.sacenv_boat_segment(
+            env._pp, env._ptr, C.c_void_p(table.data_ptr() + 4 * k0 * E), E, n, ready.data_ptr(),
+            None, 0, C.c_void_p(rows.data_ptr() + k0 * rb), rb,
+            torch.cuda.current_stream(gpu).cuda_stream))
+
+    wl = bench.Workload([env], env.step_async, env.refill, table, None, 0, E, 0, segment_step)
+    run = bench.SegmentRunner(bench.parse(["--no-cpu-baseline"]), wl, gpu)
+    assert run.mode == "segment" and not run.overlap
+    seg_state = torch.empty((n_seg, E, len(CARRIED)), dtype=torch.float64, device=gpu)
+    k = 0
+    for s in range(n_seg):
+        k = run.segment(k)
+        seg_state[s].copy_(_carried(env))
+    torch.cuda.synchronize()
+    assert int(env.status[0].item()) >= n_seg        # one refill per segment
+    worst = _check_segment_outputs(name, z, env, rows, seg_state)
+    print(f"{name}: segments, worst carried state err {worst:.3e}")
+
+
+@pytest.mark.parametrize("name", ["long_exp6.npz"])
+def test_long_fixture_segment_handoff_flags(name, gpu, built_lib):
+    """The same run through VecBoatEnv.segment_async with per-wave act_ready /
+    step_done flags (the closed loop's launch form), rows published one segment
+    ahead: the flag path gives the reference's results too."""
+    from sacenv import _lib
+    from sacenv.dist import TransitionLayout
+    z = golden(name)
+    E, S = z["reward"].shape
+    env = _segment_env(z, gpu)
+    n_seg = -(-S // SEG)
+    acts = torch.zeros((n_seg * SEG, E), dtype=torch.float32, device=gpu)
+    acts[:S] = torch.from_numpy(np.ascontiguousarray(z["actions"].T)).to(gpu)
+    rb = TransitionLayout(E, env.n_pad, int(z["cfg_experiment"])).nbytes
+    rows = torch.zeros((n_seg * SEG, rb), dtype=torch.uint8, device=gpu)
+    nw = env.n_pad // 64
+    act_ready = torch.zeros(nw, dtype=torch.int32, device=gpu)
+    step_done = torch.zeros(nw, dtype=torch.int32, device=gpu)
+    seg_state = torch.empty((n_seg, E, len(CARRIED)), dtype=torch.float64, device=gpu)
+    for s in range(n_seg):
+        act_ready.fill_(SEG * (s + 1))            # the segment's rows, published ahead
+        env.segment_async(acts[SEG * s: SEG * (s + 1)], SEG, act_ready=act_ready, step_done=step_done,
+                          seq0=SEG * s, trans=rows[SEG * s: SEG * (s + 1)].reshape(-1), trans_stride=rb)
+        env.refill()
+        seg_state[s].copy_(_carried(env))
+    torch.cuda.synchronize()
+    assert int(step_done[0].item()) == SEG * n_seg
+    assert int(env.status[1].item()) & _lib.STATUS_HANDOFF_TIMEOUT == 0
+    _check_segment_outputs(name, z, env, rows, seg_state)

@@ -116,7 +116,7 @@ def test_native_learn_matches_reference_fixture(gpu, built_lib):
     from sacenv.sac_native import NativeSAC
     from test_agent_cpu import check
     z = golden("sac_learn.npz")
-    cfg = {"agent": {k[4:]: z[k].item() for k in z.files if k.startswith("cfg_")}}
+    cfg = {"agent": {k[4:]: z[k].item() for k in z if k.startswith("cfg_")}}
     init = {n: {k: v.numpy().copy() for k, v in sd.items()}
             for n, sd in VecSAC("cpu", init_seed=int(z["seed"]), with_memory=False).state_dicts().items()}
     agent = NativeSAC(gpu, cfg, init_seed=int(z["seed"]), with_memory=False)

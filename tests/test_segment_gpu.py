@@ -142,3 +142,72 @@ def test_segment_handoff_timeout_sets_status(gpu, built_lib):
     torch.cuda.synchronize()
     assert int(env.status[1]) & _lib.STATUS_HANDOFF_TIMEOUT
     assert int(env.index[0]) == 3 and int(env.index[64]) == 0
+
+
+def test_closed_loop_after_a_timeout_refuses_and_steps_nothing(gpu, built_lib):
+    """after a hand-off timeout, later closed-loop launches must not step
+    on stale rows. The device's abort protocol makes them no-ops (no hang), check()
+    and check_status() raise, and run() refuses once check() has seen it."""
+    from sacenv import VecBoatEnv, _lib
+    from sacenv.closed_loop import ClosedLoop
+    from sacenv.sac_native import NativeSAC
+    env = VecBoatEnv({"base_settings": {"experiment": 1}}, 128, device=gpu, autoreset=False)
+    env.reset()
+    agent = NativeSAC(gpu, init_seed=3, with_memory=False)
+    loop = ClosedLoop(env, agent, segment=8)
+    ready = torch.zeros(2, dtype=torch.int32, device=gpu)
+    ready[0] = 3                                      # wave 1's rows never come: timeout
+    env.segment_async(torch.zeros((8, 128), device=gpu), 8, act_ready=ready)
+    torch.cuda.synchronize()
+    assert int(env.status[1]) & _lib.STATUS_HANDOFF_TIMEOUT
+    before = env.arena.clone()
+    loop.run(torch.randn((4, 128), device=gpu))      # enqueued: the device refuses it
+    torch.cuda.synchronize()
+    assert torch.equal(env.arena, before)            # nothing stepped, nothing written
+    assert int(loop.step_done.min()) == _lib.FLAG_ABORT - 2**32   # (int32 view of the abort flag)
+    with pytest.raises(_lib.SacenvError):
+        loop.check()
+    with pytest.raises(_lib.SacenvError):
+        loop.run(torch.randn((4, 128), device=gpu))
+    with pytest.raises(_lib.SacenvError):
+        env.check_status()
+
+
+def test_closed_loop_at_the_largest_co_resident_size(gpu, built_lib):
+    """the co-residency plan from both kernels' occupancy; at the
+    largest env count it accepts, the closed loop equals the eager loop bit for bit
+    (the policy split into launches that fit beside the segment grid); one owner wave
+    per CU more is refused."""
+    from sacenv import VecBoatEnv
+    from sacenv.closed_loop import ClosedLoop, make_plan, max_envs, occupancy
+    from sacenv.sac_native import NativeSAC
+    cfg = {"base_settings": {"experiment": 6, "test_mode": 0}}
+    kw = dict(seed=5, device=gpu, max_episode_steps=40, n_helpers=2048, auto_refill=False)
+    probe = VecBoatEnv(cfg, 64, **kw)
+    cus = torch.cuda.get_device_properties(gpu).multi_processor_count
+    bs, _, ba, _ = occupancy(probe.params, 64)
+    N = max_envs(cus, bs, ba)
+    print(f"segment {bs}/CU, act {ba}/CU, {cus} CUs: largest closed loop {N} envs")
+    assert N >= 65536                                 # the bench's size runs closed loop
+    with pytest.raises(ValueError):
+        nw = N // 64 + cus
+        make_plan(cus, bs, nw, ba, nw, N + 64 * cus)
+    a_env, b_env = VecBoatEnv(cfg, N, **kw), VecBoatEnv(cfg, N, **kw)
+    a_env.reset()
+    b_env.reset()
+    agent = NativeSAC(gpu, init_seed=3, with_memory=False)
+    K = 16
+    loop = ClosedLoop(a_env, agent, segment=K)
+    print(f"plan: {loop.plan}, {len(loop.chunks)} policy launches per step")
+    g = torch.Generator(device=gpu)
+    g.manual_seed(1)
+    for s in range(2):
+        eps = torch.randn((K, N), generator=g, device=gpu)
+        loop.run(eps)
+        for k in range(K):
+            b_env.step_async(agent.choose_action(b_env.obs, eps=eps[k]).reshape(-1).contiguous())
+        a_env.refill()
+        b_env.refill()
+        torch.cuda.synchronize()
+        assert torch.equal(a_env.arena, b_env.arena), s
+    loop.check()

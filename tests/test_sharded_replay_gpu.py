@@ -39,7 +39,7 @@ def _worker(rank, world, port, q):
         from sacenv import VecBoatEnv
         from sacenv.replay import DeviceReplayBuffer, ShardedReplayBuffer
         dev = torch.device("cuda", 0)
-        N, M, B, steps = 1000, 4999, 512, 12
+        N, M, B, steps = 1000 if world == 2 else 500, 4999, 511, 12   # B odd: f64 words stay aligned
         cfg = {"base_settings": {"experiment": 6, "test_mode": 0}, "boat_env": {"track_width": 30}}
         kw = dict(seed=3, device=dev, max_episode_steps=7)
         env = VecBoatEnv(cfg, N, env_id_offset=rank * N, **kw)
@@ -64,14 +64,17 @@ def _worker(rank, world, port, q):
                 ref.step(acts)
                 ref_rb.store_env_step(prev_r, acts, ref)
             if t % 3 == 2:
-                got = rb.sample(B)
+                # one batch, or (every 6th step) three learns' batches in ONE all-reduce
+                n_b = 3 if t % 6 == 5 else 1
+                gots = rb.sample_many(B, n_b) if n_b > 1 else [rb.sample(B)]
                 if ref_rb is not None:
-                    want = ref_rb.sample(B)
-                    torch.cuda.synchronize()
-                    assert torch.equal(got[5], want[5]), "indices"
-                    for i, (x, y) in enumerate(zip(got[:5], want[:5])):
-                        assert torch.equal(x.reshape(-1), y.reshape(-1).to(x.dtype)), (t, i)
-                    checked += 1
+                    for got in gots:
+                        want = ref_rb.sample(B)
+                        torch.cuda.synchronize()
+                        assert torch.equal(got[5], want[5]), "indices"
+                        for i, (x, y) in enumerate(zip(got[:5], want[:5])):
+                            assert torch.equal(x.reshape(-1), y.reshape(-1).to(x.dtype)), (t, i)
+                        checked += 1
         torch.cuda.synchronize()
         q.put((rank, checked))
     except Exception as exc:  # noqa: BLE001
@@ -81,8 +84,8 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_sharded_replay_equals_pooled_buffer_gpu(gpu, built_lib):
-    world = 2
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_replay_equals_pooled_buffer_gpu(world, gpu, built_lib):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -92,4 +95,4 @@ def test_sharded_replay_equals_pooled_buffer_gpu(gpu, built_lib):
     res = dict(q.get(timeout=240) for _ in ps)
     for p in ps:
         p.join(timeout=60)
-    assert res[0] == 4 and res[1] == 0, res
+    assert res[0] == 8 and all(res[r] == 0 for r in range(1, world)), res

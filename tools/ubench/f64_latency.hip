@@ -1,90 +1,116 @@
-// Microbenchmark: dependent vs independent v_fma_f64 issue on gfx950, one wave
-// per SIMD. Prints shader cycles (s_memtime) per FMA for 1, 2, 4 and 8
-// interleaved chains, and for a v_fma_f32 chain. Build: hipcc --offload-arch=gfx950 -O3.
+// Microbenchmark: FP64 VALU issue and dependent latency on gfx950.
+//
+// For each op (v_fma_f64, v_mul_f64, v_add_f64, v_fma_f32, an f64 FMA chain with an
+// independent integer chain beside it, v_rcp_f64) and each number of independent
+// chains per lane (1, 2, 4, 8), one kernel runs 64 x 64 x chains ops per lane at 1 and
+// 2 waves per SIMD (256 workgroups of 256 or 512 threads on 256 CUs). Reported:
+//   cyc/inst/wave  shader cycles (s_memtime) per instruction of one wave
+//   cyc/inst/SIMD  the same divided by the waves sharing the SIMD: the SIMD's issue
+//                  interval for this op (4.0 = one wave64 instruction every 4 cycles)
+//   TFLOP/s        chip-wide, from the wall time of the launch (FMA = 2 flops)
+// Build: hipcc --offload-arch=gfx950 -O3 -o f64_latency f64_latency.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
 
-template <int kChains, typename T>
-__global__ void chain(T* out, long long* cyc, T a, T b, int iters) {
-  T x[kChains];
-#pragma unroll
-  for (int c = 0; c < kChains; ++c) x[c] = (T)(threadIdx.x + c);
-  const long long t0 = __builtin_amdgcn_s_memtime();
-  for (int i = 0; i < iters; ++i) {
-#pragma unroll
-    for (int u = 0; u < 64; ++u)
-#pragma unroll
-      for (int c = 0; c < kChains; ++c) x[c] = __builtin_fma(x[c], a, b);
-  }
-  const long long t1 = __builtin_amdgcn_s_memtime();
-  T s = 0;
-#pragma unroll
-  for (int c = 0; c < kChains; ++c) s += x[c];
-  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
-  if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
-}
+enum Op { kFma64, kMul64, kAdd64, kFma32, kFma64Int, kRcp64 };
 
-// one dependent f64 chain with a wave-uniform guard branch every 16 FMAs
-__global__ void guarded(double* out, long long* cyc, double a, double b, int iters) {
-  double x = threadIdx.x;
+template <int kOp, int kChains>
+__global__ void __launch_bounds__(512) chain(double* out, long long* cyc, double a, double b, int iters) {
+  double x[kChains];
+  float xf[kChains];
+  int xi[kChains];
+#pragma unroll
+  for (int c = 0; c < kChains; ++c) {
+    x[c] = (double)(threadIdx.x + c) * 1e-3 + 1.0;
+    xf[c] = (float)x[c];
+    xi[c] = threadIdx.x + c;
+  }
+  const float af = (float)a, bf = (float)b;
   const long long t0 = __builtin_amdgcn_s_memtime();
   for (int i = 0; i < iters; ++i) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < 64; ++u) {
 #pragma unroll
-      for (int k = 0; k < 16; ++k) x = __builtin_fma(x, a, b);
-      if (__ballot(!(__builtin_fabs(x) <= 1e30)) != 0ull) x = sin(x);
+      for (int c = 0; c < kChains; ++c) {
+        if constexpr (kOp == kFma64) {
+          x[c] = __builtin_fma(x[c], a, b);
+        } else if constexpr (kOp == kMul64) {
+          x[c] = x[c] * a;
+        } else if constexpr (kOp == kAdd64) {
+          x[c] = x[c] + b;
+        } else if constexpr (kOp == kFma32) {
+          xf[c] = __builtin_fmaf(xf[c], af, bf);
+        } else if constexpr (kOp == kFma64Int) {
+          x[c] = __builtin_fma(x[c], a, b);
+          xi[c] = xi[c] * 3 + 7;
+        } else {
+          x[c] = __builtin_amdgcn_rcp(x[c]);
+        }
+      }
     }
+    asm volatile("" ::: "memory");
   }
   const long long t1 = __builtin_amdgcn_s_memtime();
-  out[blockIdx.x * blockDim.x + threadIdx.x] = x;
-  if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+  double s = 0;
+#pragma unroll
+  for (int c = 0; c < kChains; ++c) s += x[c] + (double)xf[c] + (double)xi[c];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+  if (threadIdx.x % 64 == 0) cyc[blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64] = t1 - t0;
 }
 
-template <int kChains, typename T>
-void run(const char* name, int blocks) {
-  T* out;
+static const char* kNames[] = {"v_fma_f64", "v_mul_f64", "v_add_f64", "v_fma_f32", "fma_f64+int", "v_rcp_f64"};
+
+template <int kOp, int kChains>
+void run(int waves_per_simd) {
+  const int blocks = 256, threads = 256 * waves_per_simd, iters = 64;
+  double* out;
   long long* cyc;
-  (void)hipMalloc(&out, sizeof(T) * blocks * 256);
-  (void)hipMalloc(&cyc, sizeof(long long) * blocks);
-  const int iters = 64;
-  chain<kChains, T><<<blocks, 256>>>(out, cyc, (T)0.999, (T)1e-3, iters);
-  (void)hipEvent_t e0, e1;
+  const int nw = blocks * threads / 64;
+  (void)hipMalloc(&out, sizeof(double) * blocks * threads);
+  (void)hipMalloc(&cyc, sizeof(long long) * nw);
+  hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
+  chain<kOp, kChains><<<blocks, threads>>>(out, cyc, 0.999, 1e-3, iters);
   (void)hipEventRecord(e0);
-  chain<kChains, T><<<blocks, 256>>>(out, cyc, (T)0.999, (T)1e-3, iters);
+  chain<kOp, kChains><<<blocks, threads>>>(out, cyc, 0.999, 1e-3, iters);
   (void)hipEventRecord(e1);
   (void)hipEventSynchronize(e1);
-  float ms;
+  float ms = 0;
   (void)hipEventElapsedTime(&ms, e0, e1);
-  long long h[4];
-  (void)hipMemcpy(h, cyc, sizeof(h), hipMemcpyDeviceToHost);
-  const double n = (double)iters * 64 * kChains;
-  printf("%-10s chains %d: %.2f cycles per fma per wave (wall %.3f ms, %.2f ns per fma)\n", name, kChains,
-         h[0] / n, ms, ms * 1e6 / n);
+  long long* h = new long long[nw];
+  (void)hipMemcpy(h, cyc, sizeof(long long) * nw, hipMemcpyDeviceToHost);
+  double mean = 0;
+  for (int i = 0; i < nw; ++i) mean += (double)h[i];
+  mean /= nw;
+  const double n = (double)iters * 64 * kChains;   // instructions of the measured op per wave
+  const double flops = (kOp == kFma64 || kOp == kFma32 || kOp == kFma64Int) ? 2.0 : 1.0;
+  printf("%-12s chains %d waves/SIMD %d: %6.2f cyc/inst/wave  %5.2f cyc/inst/SIMD  %6.1f TFLOP/s  (%.3f ms)\n",
+         kNames[kOp], kChains, waves_per_simd, mean / n, mean / n / waves_per_simd,
+         flops * n * 64.0 * nw / (ms * 1e-3) / 1e12, ms);
+  delete[] h;
   (void)hipFree(out);
   (void)hipFree(cyc);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+}
+
+template <int kOp>
+void sweep() {
+  for (int w = 1; w <= 2; ++w) {
+    run<kOp, 1>(w);
+    run<kOp, 2>(w);
+    run<kOp, 4>(w);
+    run<kOp, 8>(w);
+  }
 }
 
 int main() {
-  const int blocks = 256;  // 256 CUs x 4 waves: one wave per SIMD
-  run<1, double>("f64", blocks);
-  run<2, double>("f64", blocks);
-  run<4, double>("f64", blocks);
-  run<8, double>("f64", blocks);
-  {
-    double* out;
-    long long* cyc;
-    (void)hipMalloc(&out, sizeof(double) * blocks * 256);
-    (void)hipMalloc(&cyc, sizeof(long long) * blocks);
-    guarded<<<blocks, 256>>>(out, cyc, 0.999, 1e-3, 64);
-    guarded<<<blocks, 256>>>(out, cyc, 0.999, 1e-3, 64);
-    long long h;
-    (void)hipMemcpy(&h, cyc, sizeof(h), hipMemcpyDeviceToHost);
-    printf("f64 guarded chain: %.2f cycles per fma (16 fma + 1 guard)\n", h / (64.0 * 64));
-  }
-  run<1, float>("f32", blocks);
-  run<4, float>("f32", blocks);
+  sweep<kFma64>();
+  sweep<kMul64>();
+  sweep<kAdd64>();
+  sweep<kFma32>();
+  sweep<kFma64Int>();
+  sweep<kRcp64>();
   return 0;
 }
