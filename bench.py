@@ -52,6 +52,8 @@ sys.path.insert(0, os.path.join(ROOT, "sac-agent_amd"))
 BYTES_PER_ENV_STEP = 222      # state r+w 152, action 4, wind 16, obs 44, reward 4, done+term 2
 SEG_MIN_BYTES = 70 + 152 / 128  # the same with the state in registers for a 128-step persistent launch
 TOY_BYTES = {"parachute": 86, "car": 102}
+# the toys in the persistent mixed launch: obs 8 + reward 4 + done/term 2 per step, state r+w once
+TOY_SEG_BYTES = {"parachute": 14 + 72 / 128, "car": 14 + 88 / 128}
 HBM_PEAK = 8.0e12             # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 EPISODE_STEPS = 500
 SEG = 128              # step launches per refill (sacenv _lib.REFILL_PERIOD); one graph per segment
@@ -299,6 +301,7 @@ class Workload:
         self.per_gpu_envs, self.bytes_per_launch = per_gpu_envs, bytes_per_launch
         # segment_step(k0, n, trans=None): steps k0 .. k0+n-1 in one persistent launch
         self.segment_step = segment_step
+        self.segment_pools = True   # segment_step can write pooled transition rows
 
     def row_bytes(self) -> int:
         return self._row_bytes
@@ -368,9 +371,25 @@ def make_workload(args, rank: int, dev) -> Workload:
                           None, 0, None if trans is None else trans.data_ptr(),
                           0 if trans is None else row_bytes, torch.cuda.current_stream(dev).cuda_stream))
 
+    if args.mixed:
+        # the whole batch as ONE persistent launch per segment (sacenv_mixed_segment: the boat's
+        # open loop + each toy wave's loop, state in registers); pooled rows go through the
+        # per-step launches (graph mode) instead
+        mix_fn, tp, ta = env.lib.sacenv_mixed_segment, mixed._tp, mixed._ta
+
+        def segment_step(k0: int, n: int, trans=None):  # noqa: F811
+            if trans is not None:
+                raise ValueError("the persistent mixed launch writes no pooled rows")
+            r0 = k0 % ACTION_STEPS
+            assert r0 + n <= ACTION_STEPS
+            _lib.check(mix_fn(env._pp, env._ptr, C.c_void_p(a0 + 4 * r0 * astride), astride, n, tp, ta, len(toys),
+                              torch.cuda.current_stream(dev).cuda_stream))
+
     bytes_launch = BYTES_PER_ENV_STEP * N + (sum(TOY_BYTES.values()) * N if args.mixed else 0)
-    return Workload(envs, stepper, refill, actions, pooled_step, row_bytes, N * len(envs), bytes_launch,
-                    None if args.mixed else segment_step)
+    wl = Workload(envs, stepper, refill, actions, pooled_step, row_bytes, N * len(envs), bytes_launch,
+                  segment_step)
+    wl.segment_pools = not args.mixed
+    return wl
 
 
 # ---------------------------------------------------------------- segments
@@ -397,9 +416,9 @@ class SegmentRunner:
         # launch mode: "segment" (one persistent launch per segment, or per P steps
         # when pooling every P), "graph" (SEG k_step launches per hipGraph replay),
         # "eager" (SEG k_step launches)
-        # (the mixed batch has no persistent launch: it steps per launch)
+        # (the mixed batch: sacenv_mixed_segment; with pooled rows it steps per launch)
         want_seg = (getattr(args, "launch", "step") == "segment" and not args.no_graph
-                    and wl.segment_step is not None)
+                    and wl.segment_step is not None and (pool is None or wl.segment_pools))
         self.mode = ("segment" if want_seg and dev.type == "cuda" else
                      "graph" if dev.type == "cuda" and not args.no_graph and (pool is None or pool_every == SEG)
                      else "eager")
@@ -698,6 +717,8 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
     # with the state read and written once per 128-step launch
     N = wl.envs[0].num_envs
     algo_step = SEG_MIN_BYTES * N if seg_mode else wl.bytes_per_launch
+    if seg_mode and args.mixed:  # + the toys with their state resident: record 14 B per step
+        algo_step += sum(TOY_SEG_BYTES.values()) * N
     achieved = algo_step / kern_s
     traffic = None if args.mixed else load_traffic(wl.envs[0].num_envs, args.experiment,
                                                    "segment" if seg_mode else "step")
@@ -741,6 +762,8 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
                        "none: sharded per-GPU replay (--pooling none)" if world > 1 else None),
                    "launch": ((f"two persistent sacenv_boat_segment launches of {SEG // 2} steps per {SEG}-step "
                                "segment" if run.overlap else
+                               f"one persistent sacenv_mixed_segment launch per {SEG} steps (the boat's owner "
+                               "waves and every toy wave, state in registers)" if args.mixed else
                                f"one persistent sacenv_boat_segment launch per {SEG} steps") +
                               " (k_rollout: the carried state in registers; each owner wave checks its "
                               "action-row flag, all rows published) + the 3 refill launches after each"
@@ -761,10 +784,13 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK,
                      "traffic": None if traffic is None else traffic["hbm_bytes_per_launch"],
-                     "kernel": ("k_rollout (sacenv_boat_segment, 128 steps per launch; per step below)"
+                     "kernel": ("k_rollout_mixed (sacenv_mixed_segment, 128 steps per launch; per step below)"
+                                if seg_mode and args.mixed else
+                                "k_rollout (sacenv_boat_segment, 128 steps per launch; per step below)"
                                 if seg_mode else "k_step<true> (mixed)" if args.mixed else "k_step"),
                      "bytes_per_step": algo_step,
-                     "bytes_per_env_step": (SEG_MIN_BYTES if seg_mode else
+                     "bytes_per_env_step": (dict(boat=SEG_MIN_BYTES, **TOY_SEG_BYTES) if seg_mode and args.mixed
+                                            else SEG_MIN_BYTES if seg_mode else
                                             dict(boat=BYTES_PER_ENV_STEP, **TOY_BYTES)
                                             if args.mixed else BYTES_PER_ENV_STEP),
                      "kernel_avg_us": kern_s * 1e6,

@@ -375,6 +375,16 @@ int sacenv_mixed_step(const SacenvBoatParams *bp, void *boat_arena, const float 
 int sacenv_mixed_step_pooled(const SacenvBoatParams *bp, void *boat_arena, const float *boat_action,
                              const SacenvToyParams *toy_params, void *const *toy_arenas, int32_t n_toys,
                              void *trans, void *stream);
+/* The mixed batch as ONE persistent launch of n_steps steps (the boat as
+ * sacenv_boat_segment's open loop: action row ks at boat_actions + ks *
+ * action_stride, the carried state in registers; each toy wave runs n_steps
+ * iterations of toy_parachute.py:23-40 / toy_car.py:22-32 with its state in
+ * registers). Results equal n_steps sacenv_mixed_step calls bit for bit (the
+ * arenas, each step's record rewritten in place, the terminal obs of the last
+ * restart). Counts as n_steps step launches for the boat's refill contract. */
+int sacenv_mixed_segment(const SacenvBoatParams *bp, void *boat_arena, const float *boat_actions,
+                         int64_t action_stride, int32_t n_steps, const SacenvToyParams *toy_params,
+                         void *const *toy_arenas, int32_t n_toys, void *stream);
 
 /* ------------------------------------------------------------------------
  * Device replay buffer: agent/buffer.py:3-35 ReplayBuffer (SURVEY.md §8(f)

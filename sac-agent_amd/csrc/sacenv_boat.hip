@@ -389,7 +389,7 @@ __device__ __forceinline__ double fma_v(double a, double b, double c) {
 // tools/ubench notes), its polynomial read from VGPRs. Inlined from the
 // library, the compiler kept the coefficients in VGPRs but fed them to
 // v_fmac, copying each one first: 9 v_mov_b64 a step.
-__device__ __forceinline__ double exp_v(double x, const TrigK& K) {
+__device__ __forceinline__ double exp_ref(double x, const TrigK& K) {
   const double n = rint(x * 1.4426950408889634);
   double r = fma(-0.69314718055994529, n, x);
   r = fma(-2.3190468138462996e-17, n, r);
@@ -401,6 +401,41 @@ __device__ __forceinline__ double exp_v(double x, const TrigK& K) {
   double e = ldexp(q, (int)n);
   e = 1024.0 < x ? __builtin_inf() : e;
   return -1075.0 > x ? 0.0 : e;
+}
+
+// exp(x) on the step's path: the same reduction and polynomial, n by the
+// 1.5 * 2^52 shifter and 2^n as a constructed double; valid for |x| < 708
+// (normal results, where q * 2^n == ldexp(q, n) exactly; reward_ratio sends
+// the lanes outside to exp_ref). Saves v_rndne, v_cvt, v_ldexp and the two
+// range selects (8 cycles each at one wave per SIMD).
+__device__ __forceinline__ double exp_v(double x, const TrigK& K) {
+  const double t = fma(x, 1.4426950408889634, 6755399441055744.0);
+  const double n = t - 6755399441055744.0;
+  double r = fma(-0.69314718055994529, n, x);
+  r = fma(-2.3190468138462996e-17, n, r);
+  double q = fma_v(K.e[0], r, K.e[1]);
+#pragma unroll
+  for (int i = 2; i < 10; ++i) q = fma_v(r, q, K.e[i]);
+  q = fma(r, q, 1.0);
+  q = fma(r, q, 1.0);
+  return q * __hiloint2double((__double2loint(t) + 1023) << 20, 0);
+}
+
+// a / (1 + exp(x)) (reward_functions.py:53): the quotient from v_rcp_f64, two
+// Newton steps and Markstein's correction (within an ulp of the IEEE quotient,
+// ~half the instructions of the v_div_scale / fmas / fixup sequence); lanes
+// with |x| >= 708 (exp subnormal or infinite) take exp_ref and the IEEE
+// division behind one wave-uniform branch.
+__device__ __forceinline__ double reward_ratio(double a, double x, const TrigK& K) {
+  const double d = 1.0 + exp_v(x, K);
+  double r = __builtin_amdgcn_rcp(d);
+  r = fma(r, fma(-d, r, 1.0), r);
+  r = fma(r, fma(-d, r, 1.0), r);
+  const double q = a * r;
+  double f = fma(fma(-d, q, a), r, q);
+  const bool ok = fabs(x) < 708.0;
+  if (__ballot(!ok) != 0ull && !ok) f = a / (1.0 + exp_ref(x, K));
+  return f;
 }
 
 // sin(x) for |x| <= kSinBound with no argument reduction: x + x^3 P(x^2), P
@@ -421,10 +456,17 @@ __device__ __forceinline__ double sin_taylor(double x, const TrigK& K) {
 // below 1e-17) and the quadrant swap. Within 1 ulp of glibc's sin/cos up to
 // 1e13 (measured, 2e6 samples per decade); the bound keeps (int)k exact.
 constexpr double kCwBound = 1.0e5;
-__device__ __forceinline__ void sincos_quadrant(double r, double z, double ps, double pc, double k, double* sp,
+// Round-to-integer by the 1.5 * 2^52 shifter: t = fma(x, c, kShift) holds
+// rint(x c) (of the exact product) in its low word, and t - kShift is that
+// integer as a double -- one fma and one add instead of v_rndne_f64 and
+// v_cvt_i32_f64 (8 cycles each at one wave per SIMD, tools/ubench/valu_mix).
+// Valid for |x c| < 2^31.
+constexpr double kShift = 6755399441055744.0;
+__device__ __forceinline__ void sincos_quadrant(double r, double z, double ps, double pc, int q, double* sp,
                                                 double* cp);
 __device__ __forceinline__ void sincos_fast(double x, double* sp, double* cp, const TrigK& K) {
-  const double k = rint(x * 0.6366197723675814);
+  const double kt = fma(x, 0.6366197723675814, kShift);
+  const double k = kt - kShift;
   double r = fma(-k, 1.5707963267948966, x);
   r = fma(-k, 6.123233995736766e-17, r);
   r = fma(-k, -1.4973849048591698e-33, r);
@@ -435,16 +477,15 @@ __device__ __forceinline__ void sincos_fast(double x, double* sp, double* cp, co
   double pc = fma_v(z, K.c[0], K.c[1]);
 #pragma unroll
   for (int i = 2; i < 7; ++i) pc = fma_v(pc, z, K.c[i]);
-  sincos_quadrant(r, z, ps, pc, k, sp, cp);
+  sincos_quadrant(r, z, ps, pc, __double2loint(kt), sp, cp);
 }
 
 // sincos_fast's tail: the series values from the two polynomials, then the
-// quadrant of k = rint(x 2/pi) (swap, and the signs as sign-bit xors)
-__device__ __forceinline__ void sincos_quadrant(double r, double z, double ps, double pc, double k, double* sp,
+// quadrant q = rint(x 2/pi) (swap, and the signs as sign-bit xors)
+__device__ __forceinline__ void sincos_quadrant(double r, double z, double ps, double pc, int q, double* sp,
                                                 double* cp) {
   const double sr = fma(r * z, ps, r);
   const double cr = 1.0 - fma(-(z * z), pc, 0.5 * z);
-  const int q = (int)k;
   const double a = (q & 1) ? cr : sr, b = (q & 1) ? sr : cr;  // sin, cos of r + (q&1) pi/2
   // negate by the quadrant as a sign-bit xor on the high word (the same double as
   // -a, signed zeros and NaNs included): q & 2 for sin, (q + 1) & 2 for cos, moved
@@ -492,7 +533,8 @@ __device__ __forceinline__ void trig3(double j, double r, double w, double* sj, 
   // other's latency (written one after the other, the asm FMAs issued as two
   // serial 10-deep chains with a hazard nop between dependent pairs). The same
   // operations as sin_taylor / sincos_fast, so the same doubles.
-  const double kw = rint(w * 0.6366197723675814);
+  const double kwt = fma(w, 0.6366197723675814, kShift);
+  const double kw = kwt - kShift;
   double rw = fma(-kw, 1.5707963267948966, w);
   rw = fma(-kw, 6.123233995736766e-17, rw);
   rw = fma(-kw, -1.4973849048591698e-33, rw);
@@ -511,7 +553,7 @@ __device__ __forceinline__ void trig3(double j, double r, double w, double* sj, 
   }
   *sj = fma(j * zj, qj, j);
   *sr = fma(r * zr, qr, r);
-  sincos_quadrant(rw, zw, ps, pc, kw, sw, cw);
+  sincos_quadrant(rw, zw, ps, pc, __double2loint(kwt), sw, cw);
   const bool okj = fabs(j) <= kSinBound, okr = fabs(r) <= kSinBound, okw = fabs(w) <= kCwBound;
   if (__ballot(!(okj && okr && okw)) != 0ull) {
     if (!okj) *sj = sin_ocml(j);
@@ -925,6 +967,11 @@ __device__ __forceinline__ Obs fresh_state(const SacenvBoatParams& p, const Aren
   A.f64e(U_T, eo) = 0.0;
   A.f64e(U_EP, eo) = 0.0;  // :122
   A.i32(U_IDX)[e] = 0;
+  if (p.out_flags & SACENV_OUT_ACCEL) {  // a fresh Boat's a_x, a_y, a_r are 0 (:182-196)
+    A.at_e<double>(A.ur() + 102, eo) = 0.0;
+    A.at_e<double>(A.ur() + 110, eo) = 0.0;
+    A.at_e<double>(A.ur() + 118, eo) = 0.0;
+  }
   return make_obs(p, obs_const(T), 0.0, 0.0, 0.0, s_y, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, (double)p.fuel0);
 }
 
@@ -1546,6 +1593,43 @@ __device__ __forceinline__ void toy_wave(const SacenvToyParams& p, const ToyAren
   T.term()[e] = term;
 }
 
+// n_steps iterations of one toy wave in a persistent launch (sacenv_mixed_segment):
+// the state and the iteration count in registers, each step's record (obs,
+// reward, done, term) and a restarting lane's terminal obs stored as
+// toy_wave stores them, the counters added once at the end. Results equal
+// n_steps toy_wave launches bit for bit (the same toy_advance arithmetic).
+__device__ __forceinline__ void toy_roll_wave(const SacenvToyParams& p, const ToyArena& T, int ob, int lane,
+                                              int n_steps) {
+  const int e = ob * kWave + lane;
+  if (e >= p.n_envs) return;
+  double f[5];
+  for (int k = 0; k < 5; ++k) f[k] = T.f(k)[e];
+  int count = T.count()[e];
+  uint32_t ends[3] = {0u, 0u, 0u};
+  for (int ks = 0; ks < n_steps; ++ks) {
+    float obs[2];
+    uint8_t term = toy_advance(p, f, count, obs);
+    if (term == SACENV_TERM_NONE && p.max_episode_steps > 0 && count >= p.max_episode_steps)
+      term = SACENV_TERM_TRUNCATED;
+    if (term != SACENV_TERM_NONE) {
+      ++ends[term == SACENV_TOY_TERM_GROUND ? 0 : term == SACENV_TERM_TIMEOUT ? 1 : 2];
+      if (p.autoreset) {
+        reinterpret_cast<float2*>(T.final_obs())[e] = make_float2(obs[0], obs[1]);
+        toy_initial(p, f, obs);
+        count = 0;
+      }
+    }
+    reinterpret_cast<float2*>(T.obs())[e] = make_float2(obs[0], obs[1]);
+    T.reward()[e] = 0.0f;
+    T.done()[e] = term != SACENV_TERM_NONE ? 1 : 0;
+    T.term()[e] = term;
+  }
+  for (int k = 0; k < 5; ++k) T.f(k)[e] = f[k];
+  T.count()[e] = count;
+  for (int c = 0; c < 3; ++c)
+    if (ends[c] != 0u) T.ctr(c)[e] += ends[c];
+}
+
 // toy arenas stepped inside a mixed launch
 struct MixedToys {
   SacenvToyParams p[2];
@@ -1949,7 +2033,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
 
   // exponential_reward (reward_functions.py:42-57), f_x = 0
   const double ay = fabs(s_y);
-  const double f_y = div_c(ay, p.track_width, r_w) / (1.0 + exp_v(p.reward_k * (ay - p.reward_center), K));
+  const double f_y = reward_ratio(div_c(ay, p.track_width, r_w), p.reward_k * (ay - p.reward_center), K);
   double reward = 0.0 - f_y;
 
   // termination chain :84-105 (the first true condition wins), as selects: as an
@@ -2261,6 +2345,29 @@ __global__ void __launch_bounds__(kWave) k_rollout(SacenvBoatParams p, Arena A, 
   else
     owner_wave<true, kNc, kTIdx, false, kTrans>(vreg_params(p), A, vreg_tail(T), action, slds, ob, lane, n_steps,
                                                 &ra);
+}
+
+// sacenv_mixed_segment (BASELINE configs[4] as one persistent launch): the
+// boat's owner waves (k_rollout's open loop) and each toy arena's waves,
+// heterogeneous workgroups selected by uniform block-index ranges
+template <int kNc, bool kTIdx>
+__global__ void __launch_bounds__(kWave) k_rollout_mixed(SacenvBoatParams p, Arena A, Tail T,
+                                                         const float* __restrict__ action, int n_steps, RollArgs ra,
+                                                         int nb_boat, MixedToys M) {
+  __shared__ OwnerLds slds;
+  const int lane = threadIdx.x;
+  int b = (int)blockIdx.x;
+  if (b < nb_boat) {
+    owner_wave<true, kNc, kTIdx, false, false>(vreg_params(p), A, vreg_tail(T), action, slds, b, lane, n_steps,
+                                               &ra);
+    return;
+  }
+  b -= nb_boat;
+  if (b < M.nb[0]) {
+    toy_roll_wave(M.p[0], M.a[0], b, lane, n_steps);
+  } else if (M.n > 1) {
+    toy_roll_wave(M.p[1], M.a[1], b - M.nb[0], lane, n_steps);
+  }
 }
 
 __global__ void __launch_bounds__(kWave) k_toy_init(SacenvToyParams p, ToyArena T, const int32_t* __restrict__ ids,
@@ -2699,6 +2806,55 @@ int sacenv_mixed_step_pooled(const SacenvBoatParams* bp, void* boat_arena, const
   if ((reinterpret_cast<uintptr_t>(trans) & 15u) != 0u) return SACENV_E_RANGE;
   return mixed_step(bp, boat_arena, boat_action, toy_params, toy_arenas, n_toys, static_cast<char*>(trans),
                     stream);
+}
+
+int sacenv_mixed_segment(const SacenvBoatParams* bp, void* boat_arena, const float* boat_actions,
+                         int64_t action_stride, int32_t n_steps, const SacenvToyParams* toy_params,
+                         void* const* toy_arenas, int32_t n_toys, void* stream) {
+  int rc;
+  if (n_toys < 0 || n_toys > 2) return SACENV_E_SIZE;
+  if (n_toys > 0 && (toy_params == nullptr || toy_arenas == nullptr)) return SACENV_E_NULL;
+  if (n_steps < 1) return SACENV_E_SIZE;
+  MixedToys M{};
+  M.n = n_toys;
+  int nb = 0;
+  for (int t = 0; t < n_toys; ++t) {
+    if ((rc = check_toy(&toy_params[t]))) return rc;
+    if (toy_arenas[t] == nullptr) return SACENV_E_NULL;
+    M.p[t] = toy_params[t];
+    M.a[t] = make_toy_arena(toy_params[t], toy_arenas[t]);
+    M.nb[t] = blocks_for(toy_params[t].n_envs, kWave);
+    nb += M.nb[t];
+  }
+  SacenvBoatParams p{};
+  Arena A{};
+  Tail T{};
+  RollArgs ra{};
+  int nb_boat = 0;
+  if (bp != nullptr) {
+    if ((rc = check_params(bp))) return rc;
+    if (boat_arena == nullptr || boat_actions == nullptr) return SACENV_E_NULL;
+    if (bp->autoreset && n_steps > SACENV_REFILL_PERIOD) return SACENV_E_SIZE;
+    if (action_stride < bp->n_envs) return SACENV_E_RANGE;
+    p = *bp;
+    A = make_arena(p, boat_arena);
+    T = make_tail(p, boat_arena);
+    ra.rec = static_cast<char*>(boat_arena) + A_ur_bytes(p);
+    ra.rec_stride = 0;
+    ra.fin = reinterpret_cast<float*>(static_cast<char*>(boat_arena) + A_ur_bytes(p) + 50 * A.np);
+    ra.fin_stride = 0;
+    ra.act_stride = action_stride;
+    ra.status = reinterpret_cast<int32_t*>(static_cast<char*>(boat_arena) + status_offset(p)) + 1;
+    nb_boat = (int)(pad64(p.n_envs) / kWave);
+    nb += nb_boat;
+  }
+  if (nb == 0) return SACENV_OK;
+#define SACENV_LAUNCH(NC, TI)                                                                                  \
+  hipLaunchKernelGGL((k_rollout_mixed<NC, TI>), dim3(nb), dim3(kWave), 0, (hipStream_t)stream, p, A, T,        \
+                     boat_actions, n_steps, ra, nb_boat, M)
+  SACENV_OWNER_DISPATCH(p, SACENV_LAUNCH)
+#undef SACENV_LAUNCH
+  return launch_status();
 }
 
 int sacenv_boat_wind_eval(const SacenvBoatParams* p, const void* arena, const int32_t* env_ids,

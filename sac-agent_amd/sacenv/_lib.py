@@ -135,7 +135,8 @@ EXPORTS = ("sacenv_abi_version", "sacenv_error_string", "sacenv_boat_layout",
            "sacenv_boat_init", "sacenv_boat_reset", "sacenv_boat_reset_explicit",
            "sacenv_boat_step", "sacenv_boat_step_pooled", "sacenv_boat_rollout", "sacenv_boat_segment",
            "sacenv_boat_segment_occupancy", "sacenv_boat_refill", "sacenv_boat_wind_eval", "sacenv_toy_layout", "sacenv_toy_init",
-           "sacenv_toy_reset", "sacenv_toy_step", "sacenv_mixed_step", "sacenv_mixed_step_pooled", "sacenv_replay_layout",
+           "sacenv_toy_reset", "sacenv_toy_step", "sacenv_mixed_step", "sacenv_mixed_step_pooled",
+           "sacenv_mixed_segment", "sacenv_replay_layout",
            "sacenv_replay_init", "sacenv_replay_store", "sacenv_replay_store_env", "sacenv_replay_sample", "sacenv_replay_store_shard",
            "sacenv_replay_sample_shard",
            "sacenv_compact_done", "sacenv_boat_reset_list", "sacenv_sac_layout", "sacenv_sac_sync",
@@ -197,6 +198,7 @@ def load(path: str | None = None):
         "sacenv_toy_step": (C.c_int, [TP, _p, _p]),
         "sacenv_mixed_step": (C.c_int, [P, _p, _p, TP, C.POINTER(_p), _i32, _p]),
         "sacenv_mixed_step_pooled": (C.c_int, [P, _p, _p, TP, C.POINTER(_p), _i32, _p, _p]),
+        "sacenv_mixed_segment": (C.c_int, [P, _p, _p, _i64, _i32, TP, C.POINTER(_p), _i32, _p]),
         "sacenv_compact_done": (C.c_int, [_p, _i32, _p, _p, _p]),
         "sacenv_boat_reset_list": (C.c_int, [P, _p, _p, _p, _p]),
         "sacenv_replay_layout": (C.c_int, [RP, C.POINTER(ReplayLayout)]),

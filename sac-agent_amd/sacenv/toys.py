@@ -206,6 +206,35 @@ class MixedBatch:
         if b is not None:
             b._after_step()
 
+    def segment_async(self, boat_actions=None, n_steps: int | None = None) -> None:
+        """``n_steps`` steps of the whole batch in ONE persistent launch
+        (``sacenv_mixed_segment``): the same results as ``n_steps`` ``step_async``
+        calls, bit for bit. ``boat_actions``: a [K >= n_steps, N] f32 device tensor
+        with contiguous rows (row k drives step k; rows may be strided)."""
+        b = self.boat
+        stream = (b if b is not None else self.toys[0]).stream
+        a = None
+        if b is not None:
+            a = boat_actions
+            K = int(a.shape[0]) if n_steps is None else int(n_steps)
+            if (not isinstance(a, torch.Tensor) or a.dtype != torch.float32 or a.device != b.device
+                    or a.dim() != 2 or a.shape[1] != b.num_envs or a.stride(1) != 1 or a.shape[0] < K):
+                raise ValueError(f"boat_actions must be a float32 [>= {K}, {b.num_envs}] device tensor "
+                                 "with contiguous rows")
+            if b.autoreset and K > _lib.REFILL_PERIOD:
+                raise ValueError(f"a segment of more than {_lib.REFILL_PERIOD} steps in autoreset mode")
+            if b.autoreset and b.auto_refill and b._since_refill + K > _lib.REFILL_PERIOD:
+                b.refill()
+            self._keep = a
+        else:
+            K = int(n_steps)
+        _lib.check(self.lib.sacenv_mixed_segment(
+            b._pp if b is not None else None, b.arena.data_ptr() if b is not None else None,
+            a.data_ptr() if a is not None else None, int(a.stride(0)) if a is not None else 0, K,
+            self._tp, self._ta, len(self.toys), stream))
+        if b is not None and b.autoreset:
+            b._since_refill += K
+
 
 __all__ = ["ParachuteConfig", "CarConfig", "VecToyEnv", "ParachuteEnv", "CarEnv", "MixedBatch",
            "make_toy_params"]

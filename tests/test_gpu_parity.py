@@ -419,6 +419,83 @@ def test_mixed_launch_equals_separate_launches(gpu, built_lib):
         assert torch.equal(x.arena, y.arena)
 
 
+@pytest.mark.parametrize("K", [1, 37, 128])
+def test_mixed_segment_equals_mixed_steps(K, gpu, built_lib):
+    """sacenv_mixed_segment (the mixed batch as ONE persistent launch of K steps) =
+    K sacenv_mixed_step launches, bit for bit: boat and toy arenas (state, counters,
+    the last record, terminal obs), with restarts and truncations inside the
+    segments and refills between them (ragged sizes)."""
+    from sacenv import VecBoatEnv
+    from sacenv.toys import MixedBatch
+    cfg = {"base_settings": {"experiment": 6, "test_mode": 0}}
+    kw = dict(seed=5, device="cuda", max_episode_steps=23, n_helpers=16, auto_refill=False)
+    b1, b2 = VecBoatEnv(cfg, 3000, **kw), VecBoatEnv(cfg, 3000, **kw)
+    p1, p2 = _toy_env(1, 1000, max_episode_steps=29), _toy_env(1, 1000, max_episode_steps=29)
+    c1, c2 = _toy_env(2, 777, max_episode_steps=31), _toy_env(2, 777, max_episode_steps=31)
+    b1.reset()
+    b2.reset()
+    m1, m2 = MixedBatch(b1, [p1, c1]), MixedBatch(b2, [p2, c2])
+    g = torch.Generator(device="cuda")
+    g.manual_seed(3)
+    acts = torch.rand((3 * K, 3000), generator=g, device="cuda") * 2 - 1
+    for s in range(3):
+        m1.segment_async(acts[s * K: (s + 1) * K], K)
+        for k in range(s * K, (s + 1) * K):
+            m2.step_async(acts[k])
+        b1.refill()
+        b2.refill()
+        torch.cuda.synchronize()
+        for name, x, y in (("boat", b1, b2), ("parachute", p1, p2), ("car", c1, c2)):
+            assert torch.equal(x.arena, y.arena), (name, s)
+    b1.check_status()
+    if 3 * K > 31:   # the truncations (29 / 31 steps) fell inside the segments
+        assert int(p1.counters.sum()) > 0 and int(c1.counters.sum()) > 0
+
+
+def test_c5_mixed_segments_32768_each_vs_oracles(gpu, built_lib):
+    """BASELINE configs[4] on the persistent mixed launch (the bench's --mixed path):
+    128-step segments of boat exp 6 + parachute + car, 32 768 each; after every
+    segment all six carried boat fields of a subsample vs the boat oracle stepped
+    through the same 128 steps, every toy env's state and last obs vs the toy oracle."""
+    from sacenv import VecBoatEnv
+    from sacenv.toys import MixedBatch
+    from toy_oracle import OracleToy
+    N, SEGS, K = 32768, 3, 128
+    rng = np.random.default_rng(4)
+    seeds = np.arange(N, dtype=np.uint64) + 500
+    boat = VecBoatEnv({"base_settings": {"experiment": 6, "test_mode": 0}}, N, seeds=seeds, device=gpu,
+                      max_episode_steps=120, auto_refill=False)
+    par, car = _toy_env(1, N, max_episode_steps=110), _toy_env(2, N, max_episode_steps=130)
+    mix = MixedBatch(boat, [par, car])
+    boat.reset()
+    pick = np.sort(rng.choice(N, 192, replace=False))
+    ora = OracleVecBoat(OracleConfig(experiment=6), seeds[pick], max_episode_steps=120)
+    ora.reset()
+    toys = [OracleToy(1, N, max_episode_steps=110), OracleToy(2, N, max_episode_steps=130)]
+    ended = 0
+    for s in range(SEGS):
+        a = rng.uniform(-1, 1, (K, N)).astype(np.float32)
+        mix.segment_async(torch.from_numpy(a).to(gpu), K)
+        boat.refill()
+        for k in range(K):
+            ro = ora.step(a[k, pick])
+            ended += int(ro["done"].sum())
+            tr = [t.step() for t in toys]
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(boat.term.cpu().numpy()[pick], ro["term"], err_msg=f"segment {s}")
+        np.testing.assert_allclose(boat.obs.cpu().numpy()[pick], ro["reset_obs"], rtol=OBS_TOL, atol=OBS_TOL)
+        for f in ("s_x", "s_y", "s_r", "v_x", "v_y", "v_r"):
+            err = np.abs(getattr(boat, f).cpu().numpy()[pick] - getattr(ora, f)).max()
+            assert err <= STATE_TOL, (f, s, err)
+        for env, r in ((par, tr[0]), (car, tr[1])):
+            np.testing.assert_array_equal(env.term.cpu().numpy(), r["term"], err_msg=f"segment {s}")
+            np.testing.assert_allclose(env.obs.cpu().numpy(), r["obs"], rtol=1e-6, atol=1e-5)
+            np.testing.assert_allclose(env.state.cpu().numpy(), r["state"], rtol=0, atol=1e-5)
+    np.testing.assert_array_equal(boat.counters.cpu().numpy().T[pick], ora.counters)
+    boat.check_status()
+    assert ended > 0
+
+
 # ---------------------------------------------------------------- replay buffer (§8(f))
 
 @pytest.mark.parametrize("case", ["partial", "wrapped", "one_row", "small"])
@@ -834,7 +911,9 @@ def test_c5_mixed_32768_each_vs_oracles(gpu, built_lib):
         torch.cuda.synchronize()
         np.testing.assert_array_equal(boat.term.cpu().numpy()[pick], ro["term"], err_msg=f"step {k}")
         np.testing.assert_allclose(boat.obs.cpu().numpy()[pick], ro["reset_obs"], rtol=OBS_TOL, atol=OBS_TOL)
-        assert np.abs(boat.s_x.cpu().numpy()[pick] - ora.s_x).max() <= STATE_TOL
+        for f in ("s_x", "s_y", "s_r", "v_x", "v_y", "v_r"):   # every carried field
+            err = np.abs(getattr(boat, f).cpu().numpy()[pick] - getattr(ora, f)).max()
+            assert err <= STATE_TOL, (f, k, err)
         for env, r in ((par, tr[0]), (car, tr[1])):
             np.testing.assert_array_equal(env.term.cpu().numpy(), r["term"], err_msg=f"step {k}")
             np.testing.assert_allclose(env.obs.cpu().numpy(), r["obs"], rtol=1e-6, atol=1e-5)
