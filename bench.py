@@ -111,6 +111,9 @@ def parse(argv=None):
                     help="time every E-th timed segment's launch (the first always) with HIP events "
                          "for roofline.kernel_avg_us: each pair puts a stream marker on both sides of "
                          "the launch (measured: every segment 1.78 us/step, every 4th 1.74)")
+    ap.add_argument("--closed-loop", action="store_true",
+                    help="a separate line: the SAC actor choosing every step's actions on the device, handing "
+                         "off to the persistent env launch through per-wave flags (sacenv.closed_loop)")
     ap.add_argument("--episode-steps", type=int, default=EPISODE_STEPS,
                     help="truncation length (0 = none)")
     return ap.parse_args(argv)
@@ -284,6 +287,45 @@ def load_traffic(n_envs: int, experiment: int, launch: str = "step"):
         if int(d.get("envs", -1)) == n_envs and int(d.get("experiment", 6)) == experiment and key in d:
             # per step of all envs (a k_step launch; 1/128 of a persistent launch)
             return {"hbm_bytes_per_launch": float(d[key]), "source": os.path.relpath(path, ROOT)}
+    return None
+
+
+FP64_VECTOR_PEAK = 78.6e12   # MI355X datasheet FP64 vector: 256 CUs x 4 SIMDs x 16 FMA lanes x 2 x 2.4 GHz
+# measured ceilings (tools/ubench/f64_latency.hip, profiles/r04_ubench_*.txt): v_fma_f64 issue at one
+# wave per SIMD 5.1 shader cycles per wave instruction (dependent 5.8), at two waves 3.5 per SIMD;
+# 64-bit moves, conversions, rndne/ldexp/fract and AGPR reads ~8, v_readfirstlane ~24 (valu_mix.hip)
+UBENCH_F64_FMA_CYC_1WAVE = 5.1
+
+
+def load_compute(n_envs: int, experiment: int, kernel_s: float):
+    """The step's FP64 VALU roofline from the committed PMC passes (tools/pmc.sh ->
+    profiles/<round>_pmc_segment.json, newest first): VALU instructions and FP64
+    flops per wave-step, the achieved FP64 rate at this run's kernel time against
+    the datasheet peak, and the single-wave issue floor of that instruction count."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_segment.json")), reverse=True):
+        try:
+            d = json.load(open(path))
+        except Exception:  # noqa: BLE001
+            continue
+        if int(d.get("envs", -1)) != n_envs or int(d.get("experiment", 6)) != experiment:
+            continue
+        pw, K = d["per_wave"], float(d["steps_per_launch"])
+        valu = pw["INSTS_VALU"] / K
+        salu = pw["INSTS_SALU"] / K
+        flops = (2 * pw["INSTS_VALU_FMA_F64"] + pw["INSTS_VALU_MUL_F64"] + pw["INSTS_VALU_ADD_F64"]) / K
+        achieved = flops * n_envs / kernel_s
+        return {"unit": "TFLOP/s (FP64 vector)", "achieved": achieved / 1e12, "peak": FP64_VECTOR_PEAK / 1e12,
+                "frac": achieved / FP64_VECTOR_PEAK,
+                "fp64_flops_per_env_step": flops, "valu_per_wave_step": valu, "salu_per_wave_step": salu,
+                "f64_valu_per_wave_step": (pw["INSTS_VALU_FMA_F64"] + pw["INSTS_VALU_MUL_F64"]
+                                           + pw["INSTS_VALU_ADD_F64"]) / K,
+                "issue_floor_us_per_step": (valu + salu) * UBENCH_F64_FMA_CYC_1WAVE / 2.26e9 * 1e6,
+                "source": os.path.relpath(path, ROOT),
+                "note": "one owner wave per SIMD issues in order: ~5 shader cycles per f64 instruction at best "
+                        "(8 for 64-bit moves/conversions, ~7 for SALU between VALU), so the step is bound by "
+                        "instruction issue, not by HBM bytes (counter traffic is ~0.1 of the byte figure) nor "
+                        "by FP64 throughput; issue_floor = (VALU + SALU) x 5.1 cycles at 2.26 GHz"}
     return None
 
 
@@ -691,12 +733,16 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
             t = torch.tensor([el_ne], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el_ne = float(t.item())
+        sharded = None
+        if world > 1:
+            sharded = sharded_exchange(world, dev, el_ne / n_ne, wl.per_gpu_envs)
         no_exchange = {"value": world * wl.per_gpu_envs * n_ne * SEG / el_ne, "steps": n_ne * SEG,
                        "ms_per_step": el_ne / (n_ne * SEG) * 1e3,
                        "note": "the same persistent segments and refills after the timed region with no "
                                "all_gather (each rank's transitions stay on its GPU: --pooling none, or "
                                "ShardedReplayBuffer's B-row exchange per learn()), wall-timed between "
-                               "barriers, max over ranks"}
+                               "barriers, max over ranks",
+                       "sharded_exchange": sharded}
         kern_src = (f"events around {len(seg_events)} {what if dev.type == 'cuda' else 'eager'} after the "
                     "timed region (no staging copy, no collective; refills between segments excluded)")
     else:
@@ -782,6 +828,10 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
                        f"k_need_masks + k_refill + k_refill_fit after every {SEG}-step segment, inside the "
                        "timed region")},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
+                     "limiter": ("FP64 VALU instruction issue of one owner wave per SIMD (see compute)"
+                                 if seg_mode else "launch + latency chains (DESIGN.md §4.2)"),
+                     "compute": (load_compute(N, args.experiment, kern_s) if seg_mode and not args.mixed
+                                 else None),
                      "unit": "GB/s", "frac": achieved / HBM_PEAK,
                      "traffic": None if traffic is None else traffic["hbm_bytes_per_launch"],
                      "kernel": ("k_rollout_mixed (sacenv_mixed_segment, 128 steps per launch; per step below)"
@@ -861,6 +911,125 @@ def every_output_rate(wl: Workload, dev, n_segs: int = 8, k0: int = 0) -> dict |
                     "written to its own rows, + the refill per launch; after the timed region, wall time"}
 
 
+# ---------------------------------------------------------------- sharded replay exchange
+SHARD_BATCH = 1024      # agent.batch_size (configs/original_config.yaml)
+SHARD_WORDS = 2 * 11 + 1 + 2 + 1   # state, new_state (f32 x 11 each), action, reward (f64), terminal
+
+
+def sharded_exchange(world: int, dev, seg_s: float, n_envs: int) -> dict:
+    """The exact lighter exchange: ShardedReplayBuffer keeps each
+    rank's transitions on its GPU and assembles every sampled batch with one SUM all-reduce;
+    sample_many batches one segment's 128 learn() batches into ONE all-reduce of
+    128 x 1024 x 26 words (13.6 MB). Timed here on the run's own backend (RCCL on the node),
+    then charged in series to the measured no-exchange segment time."""
+    import torch.distributed as dist
+    n = SEG * SHARD_BATCH * SHARD_WORDS
+    words = torch.zeros(n + (n & 1), dtype=torch.int32, device=dev)
+    dist.all_reduce(words)                      # warm the communicator for this size
+    _sync(dev)
+    reps = 4
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        dist.all_reduce(words)
+    _sync(dev)
+    el = (time.perf_counter() - t0) / reps
+    t = torch.tensor([el], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    return {"value": world * n_envs * SEG / (seg_s + el), "unit": "env-steps/s",
+            "allreduce_ms_per_segment": el * 1e3, "bytes_per_segment": words.numel() * 4,
+            "segment_ms_no_exchange": seg_s * 1e3,
+            "note": "the no-exchange segment time + one SUM all-reduce of the segment's 128 learn() batches "
+                    "(ShardedReplayBuffer.sample_many: the pooled buffer's batches bit for bit, "
+                    "tests/test_sharded_replay_gpu.py), in series (not overlapped), max over ranks"}
+
+
+# ---------------------------------------------------------------- closed-loop line
+def bench_closed_loop(args, rank, world, dev):
+    """main.py:70-91's acting loop on the device: every step the
+    policy (NativeSAC choose_action: continuous_agent.py:57-61 on networks.py's actor,
+    hand-written MFMA) reads the env's obs and writes the actions the env step reads,
+    handing off per owner wave through device flags (sacenv.closed_loop.ClosedLoop): the
+    env as persistent sacenv_boat_segment launches, the policy as one launch per step
+    on a second stream, no host synchronisation between steps; the slot refill after
+    each 128-step segment. The policy's noise comes from two pre-drawn [128, N] normal
+    tables (the reference draws it inside choose_action)."""
+    from sacenv import VecBoatEnv
+    from sacenv.closed_loop import ClosedLoop
+    from sacenv.sac_native import NativeSAC
+    N = args.envs
+    env = VecBoatEnv({"base_settings": {"experiment": args.experiment, "test_mode": args.test_mode}}, N,
+                     seed=0, device=dev, max_episode_steps=args.episode_steps, env_id_offset=rank * N,
+                     n_helpers=args.helpers, auto_refill=False)
+    env.reset()
+    agent = NativeSAC(dev, init_seed=rank, with_memory=False)
+    loop = ClosedLoop(env, agent, segment=SEG)
+    g = torch.Generator(device=dev)
+    g.manual_seed(77 + rank)
+    eps = torch.randn((2, SEG, N), generator=g, device=dev)
+    state = {"i": 0}
+
+    def segment():
+        loop.run(eps[state["i"] % 2])
+        env.refill()
+        state["i"] += 1
+
+    for _ in range(segs(args.warmup)):
+        segment()
+    _sync(dev)
+    loop.check()
+    barrier(world)
+    n_timed = timed_segs(args.steps)
+    t0 = time.perf_counter()
+    for _ in range(n_timed):
+        segment()
+    _sync(dev)
+    barrier(world)
+    el = time.perf_counter() - t0
+    loop.check()
+    steps = n_timed * SEG
+    el_max = el
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el_max = float(t.item())
+    # the policy alone (sacenv_sac_act on the env's obs, one launch per step) for the split
+    ea, eb = _Clock(dev), _Clock(dev)
+    st = torch.cuda.current_stream(dev)
+    out = torch.empty(N, device=dev)
+    agent.choose_action(env.obs, eps=eps[0, 0])
+    ea.record(st)
+    for k in range(32):
+        agent.choose_action(env.obs, eps=eps[0, k])
+    eb.record(st)
+    _sync(dev)
+    act_us = ea.ms_to(eb) * 1e3 / 32
+    del out
+    if rank != 0:
+        return None
+    return {
+        "metric": f"env-steps/sec (whole node), boat_env exp-{args.experiment} closed loop (SAC actor + env "
+                  f"step per step, device hand-off), {N:,} envs/GPU".replace(",", " "),
+        "value": world * N * steps / el_max, "unit": "env-steps/s", "n_gpus": world, "steps": steps,
+        "warmup": segs(args.warmup) * SEG, "ms_per_step": el_max / steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64 env, f32 policy",
+        "data": "synthetic: random-init actor (torch.manual_seed), N(0,1) policy noise tables, per-env MT19937 "
+                "wind/start draws",
+        "config": {"workload": f"boat_env exp {args.experiment}, {N} envs/GPU, {args.episode_steps}-step "
+                               "episodes, in-kernel auto-reset; policy: NativeSAC choose_action (256-256 actor, "
+                               "tanh-squashed Normal) per step",
+                   "envs_per_gpu": N, "parallelism": f"env-dp{world}",
+                   "launch": "one persistent sacenv_boat_segment launch per 128 steps (act_ready / step_done "
+                             "flags per owner wave) + one sacenv_sac_act_handoff launch per step on a second "
+                             "stream + the 3 refill launches per segment",
+                   "co_residency": {k: getattr(loop.plan, k) for k in ("seg_vgprs", "act_vgprs", "act_lds",
+                                                                       "owner_waves_per_simd", "max_envs")}},
+        "policy_alone_us_per_step": act_us,
+        "cpu_baseline": None}
+
+
 # ---------------------------------------------------------------- rollout line
 def bench_rollout(args, wl: Workload, rank, world, dev):
     """SURVEY.md §7.6 K-step fused rollout: K steps of an open-loop action sequence per
@@ -931,11 +1100,20 @@ def bench_rollout(args, wl: Workload, rank, world, dev):
 def main(argv=None):
     args = parse(argv)
     cpu = None
-    if int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.no_cpu_baseline and not args.rollout:
+    if (int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.no_cpu_baseline and not args.rollout
+            and not args.closed_loop):
         # before anything touches the GPU: the C1 legs are child processes, and an
         # idle host keeps them from competing with the timed region's launches
         cpu = cpu_baseline(args, args.mixed_envs if args.mixed else args.envs)
     rank, world, dev = init_dist(args.gpus)
+    if args.closed_loop:
+        out = bench_closed_loop(args, rank, world, dev)
+        if out is not None:
+            print(json.dumps(out), flush=True)
+        if world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return
     wl = make_workload(args, rank, dev)
     if args.rollout:
         out = bench_rollout(args, wl, rank, world, dev)

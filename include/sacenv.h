@@ -289,13 +289,24 @@ int sacenv_boat_segment(const SacenvBoatParams *p, void *arena, const float *act
 
 /* Co-residency data for the closed loop (main.py:70-91 on the device): the
  * workgroups per CU the segment launch's kernel can keep resident for these
- * params (with or without pooled rows) and its grid (n_pad / 64 one-wave
- * workgroups). The hand-off only makes progress when every owner wave and every
- * policy workgroup it waits on can be resident at once; sacenv.ClosedLoop
- * refuses a configuration that cannot. No reference counterpart (the reference
- * steps one env on the host). */
+ * params (with or without pooled rows), its grid (n_pad / 64 one-wave
+ * workgroups), its VGPRs per lane as allocated and its LDS bytes per workgroup.
+ * The hand-off only makes progress when every owner wave and every policy
+ * workgroup it waits on can be resident at once; sacenv.ClosedLoop plans the
+ * policy launches by per-SIMD VGPR and per-CU LDS accounting and refuses a
+ * configuration that cannot. No reference counterpart (the reference steps one
+ * env on the host). */
+/* A HIP stream on a hardware queue of its own (hipExtStreamCreateWithCUMask over
+ * every CU; streams with a CU mask never share a queue). The closed loop's policy
+ * stream must run CONCURRENTLY with the env stream: ordinary streams are spread
+ * over GPU_MAX_HW_QUEUES shared hardware queues, and two that land on one queue
+ * serialise -- the persistent env launch queued behind a policy launch that waits
+ * for it is a deadlock until the hand-off timeout. */
+int sacenv_stream_create_exclusive(void **stream);
+int sacenv_stream_destroy(void *stream);
+
 int sacenv_boat_segment_occupancy(const SacenvBoatParams *p, int32_t with_trans, int32_t *blocks_per_cu,
-                                  int32_t *grid);
+                                  int32_t *grid, int32_t *vgprs, int32_t *lds_bytes);
 
 /* Autoreset mode: draw (RNG, Boat.__init__ boat_env.py:144-201 / Wind
  * wind.py:26-99) and spline-fit the replacement episodes of every env that
@@ -534,9 +545,11 @@ int sacenv_sac_act(const SacenvSacParams *p, const float *weights, const float *
  * once its actions are visible device-wide, stores act_ready[b] = act_value
  * (the segment's act_ready flags). Values below 2^31; a flag that never comes
  * (~seconds) sets SACENV_STATUS_HANDOFF_TIMEOUT in *status (nullable). */
-/* The act kernel's resident workgroups per CU and its grid for n rows (64 rows per
- * 256-thread workgroup): the policy half of the closed loop's co-residency check. */
-int sacenv_sac_act_occupancy(int32_t n, int32_t *blocks_per_cu, int32_t *grid);
+/* The hand-off act kernel's resident workgroups per CU, its grid for n rows (64
+ * rows per 256-thread workgroup), VGPRs per lane and LDS bytes per workgroup:
+ * the policy half of the closed loop's co-residency plan. */
+int sacenv_sac_act_occupancy(int32_t n, int32_t *blocks_per_cu, int32_t *grid, int32_t *vgprs,
+                             int32_t *lds_bytes);
 
 int sacenv_sac_act_handoff(const SacenvSacParams *p, const float *weights, const float *obs, int32_t n,
                            const float *eps, float *action, const uint32_t *obs_ready, uint32_t obs_want,

@@ -389,7 +389,7 @@ __device__ __forceinline__ double fma_v(double a, double b, double c) {
 // tools/ubench notes), its polynomial read from VGPRs. Inlined from the
 // library, the compiler kept the coefficients in VGPRs but fed them to
 // v_fmac, copying each one first: 9 v_mov_b64 a step.
-__device__ __forceinline__ double exp_ref(double x, const TrigK& K) {
+__device__ __forceinline__ double exp_v(double x, const TrigK& K) {
   const double n = rint(x * 1.4426950408889634);
   double r = fma(-0.69314718055994529, n, x);
   r = fma(-2.3190468138462996e-17, n, r);
@@ -401,41 +401,6 @@ __device__ __forceinline__ double exp_ref(double x, const TrigK& K) {
   double e = ldexp(q, (int)n);
   e = 1024.0 < x ? __builtin_inf() : e;
   return -1075.0 > x ? 0.0 : e;
-}
-
-// exp(x) on the step's path: the same reduction and polynomial, n by the
-// 1.5 * 2^52 shifter and 2^n as a constructed double; valid for |x| < 708
-// (normal results, where q * 2^n == ldexp(q, n) exactly; reward_ratio sends
-// the lanes outside to exp_ref). Saves v_rndne, v_cvt, v_ldexp and the two
-// range selects (8 cycles each at one wave per SIMD).
-__device__ __forceinline__ double exp_v(double x, const TrigK& K) {
-  const double t = fma(x, 1.4426950408889634, 6755399441055744.0);
-  const double n = t - 6755399441055744.0;
-  double r = fma(-0.69314718055994529, n, x);
-  r = fma(-2.3190468138462996e-17, n, r);
-  double q = fma_v(K.e[0], r, K.e[1]);
-#pragma unroll
-  for (int i = 2; i < 10; ++i) q = fma_v(r, q, K.e[i]);
-  q = fma(r, q, 1.0);
-  q = fma(r, q, 1.0);
-  return q * __hiloint2double((__double2loint(t) + 1023) << 20, 0);
-}
-
-// a / (1 + exp(x)) (reward_functions.py:53): the quotient from v_rcp_f64, two
-// Newton steps and Markstein's correction (within an ulp of the IEEE quotient,
-// ~half the instructions of the v_div_scale / fmas / fixup sequence); lanes
-// with |x| >= 708 (exp subnormal or infinite) take exp_ref and the IEEE
-// division behind one wave-uniform branch.
-__device__ __forceinline__ double reward_ratio(double a, double x, const TrigK& K) {
-  const double d = 1.0 + exp_v(x, K);
-  double r = __builtin_amdgcn_rcp(d);
-  r = fma(r, fma(-d, r, 1.0), r);
-  r = fma(r, fma(-d, r, 1.0), r);
-  const double q = a * r;
-  double f = fma(fma(-d, q, a), r, q);
-  const bool ok = fabs(x) < 708.0;
-  if (__ballot(!ok) != 0ull && !ok) f = a / (1.0 + exp_ref(x, K));
-  return f;
 }
 
 // sin(x) for |x| <= kSinBound with no argument reduction: x + x^3 P(x^2), P
@@ -456,17 +421,10 @@ __device__ __forceinline__ double sin_taylor(double x, const TrigK& K) {
 // below 1e-17) and the quadrant swap. Within 1 ulp of glibc's sin/cos up to
 // 1e13 (measured, 2e6 samples per decade); the bound keeps (int)k exact.
 constexpr double kCwBound = 1.0e5;
-// Round-to-integer by the 1.5 * 2^52 shifter: t = fma(x, c, kShift) holds
-// rint(x c) (of the exact product) in its low word, and t - kShift is that
-// integer as a double -- one fma and one add instead of v_rndne_f64 and
-// v_cvt_i32_f64 (8 cycles each at one wave per SIMD, tools/ubench/valu_mix).
-// Valid for |x c| < 2^31.
-constexpr double kShift = 6755399441055744.0;
-__device__ __forceinline__ void sincos_quadrant(double r, double z, double ps, double pc, int q, double* sp,
+__device__ __forceinline__ void sincos_quadrant(double r, double z, double ps, double pc, double k, double* sp,
                                                 double* cp);
 __device__ __forceinline__ void sincos_fast(double x, double* sp, double* cp, const TrigK& K) {
-  const double kt = fma(x, 0.6366197723675814, kShift);
-  const double k = kt - kShift;
+  const double k = rint(x * 0.6366197723675814);
   double r = fma(-k, 1.5707963267948966, x);
   r = fma(-k, 6.123233995736766e-17, r);
   r = fma(-k, -1.4973849048591698e-33, r);
@@ -477,15 +435,16 @@ __device__ __forceinline__ void sincos_fast(double x, double* sp, double* cp, co
   double pc = fma_v(z, K.c[0], K.c[1]);
 #pragma unroll
   for (int i = 2; i < 7; ++i) pc = fma_v(pc, z, K.c[i]);
-  sincos_quadrant(r, z, ps, pc, __double2loint(kt), sp, cp);
+  sincos_quadrant(r, z, ps, pc, k, sp, cp);
 }
 
 // sincos_fast's tail: the series values from the two polynomials, then the
-// quadrant q = rint(x 2/pi) (swap, and the signs as sign-bit xors)
-__device__ __forceinline__ void sincos_quadrant(double r, double z, double ps, double pc, int q, double* sp,
+// quadrant of k = rint(x 2/pi) (swap, and the signs as sign-bit xors)
+__device__ __forceinline__ void sincos_quadrant(double r, double z, double ps, double pc, double k, double* sp,
                                                 double* cp) {
   const double sr = fma(r * z, ps, r);
   const double cr = 1.0 - fma(-(z * z), pc, 0.5 * z);
+  const int q = (int)k;
   const double a = (q & 1) ? cr : sr, b = (q & 1) ? sr : cr;  // sin, cos of r + (q&1) pi/2
   // negate by the quadrant as a sign-bit xor on the high word (the same double as
   // -a, signed zeros and NaNs included): q & 2 for sin, (q + 1) & 2 for cos, moved
@@ -533,8 +492,7 @@ __device__ __forceinline__ void trig3(double j, double r, double w, double* sj, 
   // other's latency (written one after the other, the asm FMAs issued as two
   // serial 10-deep chains with a hazard nop between dependent pairs). The same
   // operations as sin_taylor / sincos_fast, so the same doubles.
-  const double kwt = fma(w, 0.6366197723675814, kShift);
-  const double kw = kwt - kShift;
+  const double kw = rint(w * 0.6366197723675814);
   double rw = fma(-kw, 1.5707963267948966, w);
   rw = fma(-kw, 6.123233995736766e-17, rw);
   rw = fma(-kw, -1.4973849048591698e-33, rw);
@@ -553,7 +511,7 @@ __device__ __forceinline__ void trig3(double j, double r, double w, double* sj, 
   }
   *sj = fma(j * zj, qj, j);
   *sr = fma(r * zr, qr, r);
-  sincos_quadrant(rw, zw, ps, pc, __double2loint(kwt), sw, cw);
+  sincos_quadrant(rw, zw, ps, pc, kw, sw, cw);
   const bool okj = fabs(j) <= kSinBound, okr = fabs(r) <= kSinBound, okw = fabs(w) <= kCwBound;
   if (__ballot(!(okj && okr && okw)) != 0ull) {
     if (!okj) *sj = sin_ocml(j);
@@ -708,14 +666,22 @@ __device__ __forceinline__ void interval_extrema(const SacenvBoatParams& p, int 
   mx = -INFINITY;
   const int L = p.wind_len;
   const double inv = p.knot_inv;
-  int lo = (int)ceil((double)j * inv) - 2;
+  // (inv = RN(1/knot_step) puts ceil(j inv) within one of the first grid index of
+  // interval j: start one below and step up, and symmetrically for the last)
+  int lo = (int)ceil((double)j * inv) - 1;
   if (lo < 0) lo = 0;
   while (lo < L && knot_coord(p, lo).j < j) ++lo;
-  int hi = (int)floor((double)(j + 1) * inv) + 2;
+  int hi = (int)floor((double)(j + 1) * inv) + 1;
   if (hi > L - 1) hi = L - 1;
   while (hi >= 0 && knot_coord(p, hi).j > j) --hi;
   if (lo > hi) return;
   const double qa = 3.0 * (b - a), qb = 6.0 * a, qc = y1 - y0 - 2.0 * a - b;
+  // the piece in the power basis, f(t) = y0 + c1 t + c2 t^2 + c3 t^3 (spline_piece
+  // expanded: c1 = y1 - y0 - 2 m0 - m1, c2 = 3 m0, c3 = m1 - m0): 3 FMAs per
+  // candidate instead of spline_piece's 11 operations. The extreme grid samples
+  // agree with spline_piece's evaluation of them to a few ulp (the renormalisation
+  // bar is the reference's interp1d samples, 1e-12: test_wind_tables_vs_reference)
+  const double c1 = qc, c2 = 3.0 * a, c3 = b - a;
   double r0 = -1.0, r1 = -1.0;  // roots of the derivative in [0,1]; -1 = none
   const double scale = fabs(qa) + fabs(qb) + fabs(qc);
   if (fabs(qa) <= 1e-14 * scale) {
@@ -730,26 +696,31 @@ __device__ __forceinline__ void interval_extrema(const SacenvBoatParams& p, int 
     }
   }
   const bool ok0 = r0 > -0.01 && r0 < 1.01, ok1 = r1 > -0.01 && r1 < 1.01;
-  const int i0 = ok0 ? (int)floor(((double)j + r0) * inv) : lo;
-  const int i1 = ok1 ? (int)floor(((double)j + r1) * inv) : lo;
+  // the candidates as doubles (exact small integers): every one lies in [lo, hi],
+  // i.e. in interval j, so its knot coordinate is t = i * knot_step - j, the same
+  // double knot_coord forms -- no integer conversions per candidate (v_cvt costs
+  // 8 cycles at one wave per SIMD, tools/ubench/valu_mix.hip)
+  const double jd = (double)j, lod = (double)lo, hid = (double)hi;
+  const double i0 = ok0 ? floor((jd + r0) * inv) : lod;
+  const double i1 = ok1 ? floor((jd + r1) * inv) : lod;
 #pragma unroll
   for (int t = 0; t < (10 + S - 1) / S; ++t) {
     const int q = s + S * t;  // candidate number 0..9
-    int i;
+    double i;
     if (q == 0) {
-      i = lo;
+      i = lod;
     } else if (q == 1) {
-      i = hi;
+      i = hid;
     } else {
       const bool first = q < 6;
-      const int d = (first ? q - 2 : q - 6) - 1;
+      const double d = (double)((first ? q - 2 : q - 6) - 1);
       const bool ok = first ? ok0 : ok1;
-      i = (first ? i0 : i1) + d;
-      i = i < lo ? lo : (i > hi ? hi : i);
-      i = ok ? i : lo;
+      i = fmin(fmax((first ? i0 : i1) + d, lod), hid);
+      i = ok ? i : lod;
     }
     if (q < 10) {
-      const double v = spline_piece(y0, y1, a, b, knot_coord(p, i).t);
+      const double t = i * p.knot_step - jd;
+      const double v = fma(fma(fma(c3, t, c2), t, c1), t, y0);
       mn = fmin(mn, v);
       mx = fmax(mx, v);
     }
@@ -1215,40 +1186,53 @@ __global__ void __launch_bounds__(kWave) k_refill(SacenvBoatParams p, Arena A) {
     }
     if (ok && c >= f0 && gl == 0) atomicOr(&A.status()[1], SACENV_STATUS_SLOT_UNDERFLOW);
     const int f_end = ok && f0 < c + kSlots ? c + kSlots : f0;
-    bool fast = ok && f0 < f_end && grp_ok && pos + nwords <= kMtN;
-    // the group's words pos .. pos + nwords - 1 (raw, key order), tempered
-    const uint32_t* key = A.mt_key() + (int64_t)e * kMtN + pos;
-    uint32_t w[3];
-#pragma unroll
-    for (int q = 0; q < 3; ++q)
-      w[q] = fast && gl + kGroupLanes * q < nwords ? mt_temper(key[gl + kGroupLanes * q]) : 0u;
+    // The group's episodes f0, f0+1, ... on the fast path, one per pass, while
+    // each next window lies inside the current MT block (round 4: an env that
+    // consumed several episodes drew only its first here, the rest wave by wave
+    // at ~4 us each -- about half of a refill's draws)
+    int f_next = f0, pos_next = pos;  // the next episode to draw and its MT position
+    bool live = ok && f0 < f_end && grp_ok;
     uint32_t* const gw = lds.blk[0] + g * 3 * kGroupLanes;
+#pragma unroll 1
+    while (__ballot(live) != 0ull) {  // uniform: until every group left the fast path
+      bool fast = live && pos_next + nwords <= kMtN;
+      // the group's words pos_next .. pos_next + nwords - 1 (raw, key order), tempered
+      const uint32_t* key = A.mt_key() + (int64_t)e * kMtN + pos_next;
+      uint32_t w[3];
 #pragma unroll
-    for (int q = 0; q < 3; ++q) gw[gl + kGroupLanes * q] = w[q];
-    // np.random.randint (boat_env.py:147-150): the first accepted of the first 16 words
-    const unsigned long long acc = __ballot(fast && (w[0] & mask) <= rng);
-    const uint32_t gacc = (uint32_t)(acc >> (kGroupLanes * g)) & 0xFFFFu;
-    fast = fast && gacc != 0u;
-    const int k = fast ? __builtin_ctz(gacc) : 0;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the group's words, then reads
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    REFILL_STAMP(stm[2], "v"(k));
-    if (fast) {
-      const int slot = f0 % kSlots;
-      const int cc = gl / 8, jj = gl % 8;  // knot jj of curve cc (wind.py:78; velocity first)
-      if (cc < ncurves && jj < nk) {
-        const int src = k + 1 + cc * 2 * nk + 2 * jj;  // np.random.sample: res53 of two words
-        const double a = (double)(gw[src] >> 5), bb = (double)(gw[src + 1] >> 6);
-        A.knots_raw()[A.wix(slot, cc, jj, e)] = (a * 67108864.0 + bb) / 9007199254740992.0;
+      for (int q = 0; q < 3; ++q)
+        w[q] = fast && gl + kGroupLanes * q < nwords ? mt_temper(key[gl + kGroupLanes * q]) : 0u;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the last pass's reads of gw are done
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int q = 0; q < 3; ++q) gw[gl + kGroupLanes * q] = w[q];
+      // np.random.randint (boat_env.py:147-150): the first accepted of the first 16 words
+      const unsigned long long acc = __ballot(fast && (w[0] & mask) <= rng);
+      const uint32_t gacc = (uint32_t)(acc >> (kGroupLanes * g)) & 0xFFFFu;
+      fast = fast && gacc != 0u;
+      const int k = fast ? __builtin_ctz(gacc) : 0;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the group's words, then reads
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      REFILL_STAMP(stm[2], "v"(k));
+      if (fast) {
+        const int slot = f_next % kSlots;
+        const int cc = gl / 8, jj = gl % 8;  // knot jj of curve cc (wind.py:78; velocity first)
+        if (cc < ncurves && jj < nk) {
+          const int src = k + 1 + cc * 2 * nk + 2 * jj;  // np.random.sample: res53 of two words
+          const double a = (double)(gw[src] >> 5), bb = (double)(gw[src + 1] >> 6);
+          A.knots_raw()[A.wix(slot, cc, jj, e)] = (a * 67108864.0 + bb) / 9007199254740992.0;
+        }
+        if (gl == 0) {
+          A.i32(U_STARTY)[(int64_t)slot * A.np + e] = -p.start_y_half + (int32_t)(gw[k] & mask);
+          A.i32(U_MTPOS)[e] = pos_next + k + 1 + need;
+        }
+        f_next = f_next + 1;
+        pos_next = pos_next + k + 1 + need;
       }
-      if (gl == 0) {
-        A.i32(U_STARTY)[(int64_t)slot * A.np + e] = -p.start_y_half + (int32_t)(gw[k] & mask);
-        A.i32(U_MTPOS)[e] = pos + k + 1 + need;
-      }
+      live = fast && f_next < f_end;
     }
-    const int f_next = fast ? f0 + 1 : f0;          // the next episode to draw
-    const int pos_next = fast ? pos + k + 1 + need : pos;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // LDS free for the wave draws
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -2033,7 +2017,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
 
   // exponential_reward (reward_functions.py:42-57), f_x = 0
   const double ay = fabs(s_y);
-  const double f_y = reward_ratio(div_c(ay, p.track_width, r_w), p.reward_k * (ay - p.reward_center), K);
+  const double f_y = div_c(ay, p.track_width, r_w) / (1.0 + exp_v(p.reward_k * (ay - p.reward_center), K));
   double reward = 0.0 - f_y;
 
   // termination chain :84-105 (the first true condition wins), as selects: as an
@@ -2470,6 +2454,30 @@ extern "C" {
 
 int sacenv_abi_version(void) { return SACENV_ABI_VERSION; }
 
+int sacenv_stream_create_exclusive(void** stream) {
+  if (stream == nullptr) return SACENV_E_NULL;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return (int)e;
+  hipDeviceProp_t prop;
+  e = hipGetDeviceProperties(&prop, dev);
+  if (e != hipSuccess) return (int)e;
+  uint32_t mask[64];
+  const int words = (prop.multiProcessorCount + 31) / 32;
+  if (words > 64) return SACENV_E_SIZE;
+  for (int i = 0; i < words; ++i) mask[i] = 0xFFFFFFFFu;  // every CU (extra bits are ignored)
+  hipStream_t s = nullptr;
+  e = hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask);
+  if (e != hipSuccess) return (int)e;
+  *stream = s;
+  return SACENV_OK;
+}
+
+int sacenv_stream_destroy(void* stream) {
+  if (stream == nullptr) return SACENV_E_NULL;
+  return (int)hipStreamDestroy((hipStream_t)stream);
+}
+
 const char* sacenv_error_string(int code) {
   switch (code) {
     case SACENV_OK: return "ok";
@@ -2671,24 +2679,33 @@ int sacenv_boat_segment(const SacenvBoatParams* p, void* arena, const float* act
   return launch_multi(*p, arena, actions, n_steps, ra, stream);
 }
 
-// Resident workgroups per CU of the segment launch's kernel for these params
-// (hipOccupancyMaxActiveBlocksPerMultiprocessor) and the launch's grid: the
-// closed loop checks that this grid and the policy's fit on the device together.
+// The segment launch's kernel resources for these params, for the closed
+// loop's co-residency plan (sacenv.h): resident one-wave workgroups per CU
+// (hipOccupancyMaxActiveBlocksPerMultiprocessor), the grid, VGPRs per lane as
+// allocated and LDS bytes per workgroup (hipFuncGetAttributes).
 int sacenv_boat_segment_occupancy(const SacenvBoatParams* p, int32_t with_trans, int32_t* blocks_per_cu,
-                                  int32_t* grid) {
+                                  int32_t* grid, int32_t* vgprs, int32_t* lds_bytes) {
   int rc = check_params(p);
   if (rc) return rc;
-  if (blocks_per_cu == nullptr || grid == nullptr) return SACENV_E_NULL;
+  if (blocks_per_cu == nullptr || grid == nullptr || vgprs == nullptr || lds_bytes == nullptr) return SACENV_E_NULL;
   int nb = 0;
   hipError_t e = hipSuccess;
-#define SACENV_OCC(NC, TI)                                                                              \
-  e = with_trans ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_rollout<NC, TI, true>, kWave, 0)  \
-                 : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_rollout<NC, TI, false>, kWave, 0)
+  hipFuncAttributes fa{};
+#define SACENV_OCC(NC, TI)                                                                                  \
+  if (with_trans) {                                                                                          \
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_rollout<NC, TI, true>, kWave, 0);                \
+    if (e == hipSuccess) e = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(k_rollout<NC, TI, true>)); \
+  } else {                                                                                                   \
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_rollout<NC, TI, false>, kWave, 0);               \
+    if (e == hipSuccess) e = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(k_rollout<NC, TI, false>)); \
+  }
   SACENV_OWNER_DISPATCH(*p, SACENV_OCC)
 #undef SACENV_OCC
   if (e != hipSuccess) return (int)e;
   *blocks_per_cu = nb;
   *grid = (int32_t)(pad64(p->n_envs) / kWave);
+  *vgprs = fa.numRegs;
+  *lds_bytes = (int32_t)fa.sharedSizeBytes;
   return SACENV_OK;
 }
 

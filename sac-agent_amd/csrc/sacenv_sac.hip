@@ -955,10 +955,12 @@ __device__ __forceinline__ uint32_t flag_load(const uint32_t* f) {  // device-co
   return (uint32_t)__builtin_amdgcn_readfirstlane((int)__builtin_amdgcn_raw_buffer_load_b32(r, 0, 0, 17));
 }
 
-__global__ void __launch_bounds__(kThreads) k_sac_act(SacArgs a, const float* __restrict__ obs, int n,
-                                                        const float* __restrict__ eps, float* __restrict__ out,
-                                                        float* __restrict__ logp, ActHandoff h) {
-  __shared__ ActLds l;
+constexpr int kHandoffLds = 84 * 1024;  // > 160 KB / 2: one hand-off workgroup per CU
+static_assert(sizeof(ActLds) <= (size_t)kHandoffLds, "ActLds above the hand-off LDS size");
+
+__device__ __forceinline__ void act_body(ActLds& l, const SacArgs& a, const float* __restrict__ obs, int n,
+                                         const float* __restrict__ eps, float* __restrict__ out,
+                                         float* __restrict__ logp, const ActHandoff& h) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, i = lane & 15, kq = lane >> 4;
   const int row0 = blockIdx.x * kActRows;
   if (h.obs_ready != nullptr) {
@@ -1192,6 +1194,27 @@ extern "C" int sacenv_sac_sync(const SacenvSacParams* p, float* weights, void* s
   return (int)hipGetLastError();
 }
 
+__global__ void __launch_bounds__(kThreads) k_sac_act(SacArgs a, const float* __restrict__ obs, int n,
+                                                        const float* __restrict__ eps, float* __restrict__ out,
+                                                        float* __restrict__ logp, ActHandoff h) {
+  __shared__ ActLds l;
+  act_body(l, a, obs, n, eps, out, logp, h);
+}
+
+// The closed loop's form (sacenv_sac_act_handoff): the same code held to 128
+// architectural VGPRs (~150 allocated, no spills) so that one policy wave fits
+// beside an owner wave of the segment launch (~320 VGPRs) on a SIMD's 512,
+// and launched with its LDS padded to kHandoffLds (> half of a CU's 160 KB):
+// a CU then holds at most ONE policy workgroup, which always leaves room for
+// the CU's owner waves -- no arrangement of dispatched policy workgroups can
+// keep an owner wave out (sacenv.closed_loop's co-residency plan).
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_num_vgpr(128)))
+k_sac_act_lean(SacArgs a, const float* __restrict__ obs, int n, const float* __restrict__ eps,
+               float* __restrict__ out, float* __restrict__ logp, ActHandoff h) {
+  __shared__ ActLds l;
+  act_body(l, a, obs, n, eps, out, logp, h);
+}
+
 static int sac_act(const SacenvSacParams* p, const float* weights, const float* obs, int32_t n, const float* eps,
                    float* action, float* log_prob, const ActHandoff& h, void* stream) {
   if (p == nullptr) return SACENV_E_NULL;
@@ -1204,8 +1227,12 @@ static int sac_act(const SacenvSacParams* p, const float* weights, const float* 
   q.batch = 256;  // unused by the act kernel
   const SacArgs a = make_args(&q, const_cast<float*>(weights));
   const int blocks = (n + kActRows - 1) / kActRows;
-  hipLaunchKernelGGL(k_sac_act, dim3(blocks), dim3(kThreads), 0, (hipStream_t)stream, a, obs, (int)n, eps, action,
-                     log_prob, h);
+  if (h.obs_ready != nullptr)  // LDS padded: at most one policy workgroup per CU (kHandoffLds)
+    hipLaunchKernelGGL(k_sac_act_lean, dim3(blocks), dim3(kThreads), kHandoffLds - sizeof(ActLds),
+                       (hipStream_t)stream, a, obs, (int)n, eps, action, log_prob, h);
+  else
+    hipLaunchKernelGGL(k_sac_act, dim3(blocks), dim3(kThreads), 0, (hipStream_t)stream, a, obs, (int)n, eps, action,
+                       log_prob, h);
   return (int)hipGetLastError();
 }
 
@@ -1214,16 +1241,24 @@ extern "C" int sacenv_sac_act(const SacenvSacParams* p, const float* weights, co
   return sac_act(p, weights, obs, n, eps, action, log_prob, ActHandoff{}, stream);
 }
 
-// Resident workgroups per CU of the act kernel and its grid for n rows (the
-// closed loop's co-residency check, sacenv.h).
-extern "C" int sacenv_sac_act_occupancy(int32_t n, int32_t* blocks_per_cu, int32_t* grid) {
-  if (blocks_per_cu == nullptr || grid == nullptr) return SACENV_E_NULL;
+// The hand-off act kernel's resources for the closed loop's co-residency plan
+// (sacenv.h): resident workgroups per CU alone, the grid for n rows, VGPRs per
+// lane (architectural + accumulation, as allocated) and LDS bytes per workgroup.
+extern "C" int sacenv_sac_act_occupancy(int32_t n, int32_t* blocks_per_cu, int32_t* grid, int32_t* vgprs,
+                                        int32_t* lds_bytes) {
+  if (blocks_per_cu == nullptr || grid == nullptr || vgprs == nullptr || lds_bytes == nullptr) return SACENV_E_NULL;
   if (n < 0) return SACENV_E_SIZE;
   int nb = 0;
-  const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sac_act, kThreads, 0);
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sac_act_lean, kThreads,
+                                                               kHandoffLds - sizeof(ActLds));
+  if (e != hipSuccess) return (int)e;
+  hipFuncAttributes fa{};
+  e = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(k_sac_act_lean));
   if (e != hipSuccess) return (int)e;
   *blocks_per_cu = nb;
   *grid = (n + kActRows - 1) / kActRows;
+  *vgprs = fa.numRegs;
+  *lds_bytes = kHandoffLds;  // static + the padding at launch
   return SACENV_OK;
 }
 

@@ -134,7 +134,8 @@ class SacLayout(C.Structure):
 EXPORTS = ("sacenv_abi_version", "sacenv_error_string", "sacenv_boat_layout",
            "sacenv_boat_init", "sacenv_boat_reset", "sacenv_boat_reset_explicit",
            "sacenv_boat_step", "sacenv_boat_step_pooled", "sacenv_boat_rollout", "sacenv_boat_segment",
-           "sacenv_boat_segment_occupancy", "sacenv_boat_refill", "sacenv_boat_wind_eval", "sacenv_toy_layout", "sacenv_toy_init",
+           "sacenv_boat_segment_occupancy", "sacenv_stream_create_exclusive", "sacenv_stream_destroy",
+           "sacenv_boat_refill", "sacenv_boat_wind_eval", "sacenv_toy_layout", "sacenv_toy_init",
            "sacenv_toy_reset", "sacenv_toy_step", "sacenv_mixed_step", "sacenv_mixed_step_pooled",
            "sacenv_mixed_segment", "sacenv_replay_layout",
            "sacenv_replay_init", "sacenv_replay_store", "sacenv_replay_store_env", "sacenv_replay_sample", "sacenv_replay_store_shard",
@@ -190,7 +191,9 @@ def load(path: str | None = None):
         "sacenv_boat_refill": (C.c_int, [P, _p, _p]),
         "sacenv_boat_rollout": (C.c_int, [P, _p, _p, _i32, _p, _p, _p]),
         "sacenv_boat_segment": (C.c_int, [P, _p, _p, _i64, _i32, _p, _p, C.c_uint32, _p, _i64, _p]),
-        "sacenv_boat_segment_occupancy": (C.c_int, [P, _i32, C.POINTER(_i32), C.POINTER(_i32)]),
+        "sacenv_boat_segment_occupancy": (C.c_int, [P, _i32] + [C.POINTER(_i32)] * 4),
+        "sacenv_stream_create_exclusive": (C.c_int, [C.POINTER(_p)]),
+        "sacenv_stream_destroy": (C.c_int, [_p]),
         "sacenv_boat_wind_eval": (C.c_int, [P, _p, _p, _p, _i32, _p, _p, _p]),
         "sacenv_toy_layout": (C.c_int, [TP, C.POINTER(ToyLayout)]),
         "sacenv_toy_init": (C.c_int, [TP, _p, _p]),
@@ -214,7 +217,7 @@ def load(path: str | None = None):
         "sacenv_sac_act": (C.c_int, [C.POINTER(SacParams), _p, _p, _i32, _p, _p, _p, _p]),
         "sacenv_sac_act_handoff": (C.c_int, [C.POINTER(SacParams), _p, _p, _i32, _p, _p, _p, C.c_uint32, _p,
                                              C.c_uint32, _p, _p]),
-        "sacenv_sac_act_occupancy": (C.c_int, [_i32, C.POINTER(_i32), C.POINTER(_i32)]),
+        "sacenv_sac_act_occupancy": (C.c_int, [_i32] + [C.POINTER(_i32)] * 4),
         "sacenv_sac_learn": (C.c_int, [C.POINTER(SacParams), _p, _p, _p, _p, _p, _p, _p, _p, _p, _i32,
                                        _p, _p]),
     }

@@ -22,17 +22,20 @@ bit (``test_closed_loop_equals_eager_loop`` in tests/test_segment_gpu.py).
 
 Co-residency. The hand-off makes progress only if every owner wave of the
 segment launch is resident while policy workgroups spin beside it: a policy
-workgroup waits for its own owner wave, and an owner wave that is not yet
-dispatched would wait for the slots the spinning workgroups hold. ``plan``
-(from ``hipOccupancyMaxActiveBlocksPerMultiprocessor`` of both kernels, through
-the C ABI) therefore requires the segment grid's even share per CU plus one
-policy launch's share per CU to fit in one CU's resources (as fractions of each
-kernel's own per-CU limit, which bounds every resource at once), and splits the
-policy's rows into launches of at most ``plan.chunk_waves`` owner waves (one
-launch per chunk per step, in order on the policy stream: a chunk's workgroups
-wait only for owner waves that are already resident). A configuration in which
-the segment grid alone does not leave room for one policy workgroup per CU is
-refused.
+workgroup waits for its own owner wave, owner waves never leave before the
+segment ends, and the policy's next launch starts only when the whole previous
+one is done. So the plan (``make_plan``, from both kernels' VGPRs and LDS as the
+library reports them through the C ABI) requires
+  * every owner wave to fit on the device at once with room left, on every
+    SIMD, for one policy wave (VGPRs: a SIMD holds 512 per lane, allocated in
+    granules of 8; wave slots: 8 per SIMD), and the CU's LDS to hold its owner
+    waves plus one policy workgroup;
+  * at most ONE policy workgroup per CU: the hand-off act kernel is launched with
+    its LDS padded past half a CU's 160 KB, so no arrangement of dispatched
+    policy workgroups can keep an owner wave out.
+Then all owner waves are resident, each policy workgroup's wait ends, and the
+policy launches drain. A configuration that fails is refused (65 536 envs fit:
+one owner wave of ~320 VGPRs per SIMD beside one ~152-VGPR policy wave).
 
 Timeouts. A flag that never comes (~seconds) sets SACENV_STATUS_HANDOFF_TIMEOUT;
 from then on every hand-off launch is a no-op on the device (sacenv.h's abort
@@ -42,7 +45,6 @@ protocol), ``check()`` raises, and ``run()`` refuses to enqueue more steps once
 from __future__ import annotations
 
 import ctypes as C
-import math
 from dataclasses import dataclass
 
 import torch
@@ -50,61 +52,67 @@ import torch
 from . import _lib
 
 
+SIMD_VGPRS = 512       # per lane: the unified architectural + accumulation file of a gfx950 SIMD
+VGPR_GRANULE = 8       # allocation granule (wave64)
+SIMDS_PER_CU = 4
+WAVE_SLOTS = 8         # waves per SIMD
+LDS_PER_CU = 160 * 1024
+
+
+def _alloc(v: int) -> int:
+    return -(-int(v) // VGPR_GRANULE) * VGPR_GRANULE
+
+
 @dataclass(frozen=True)
 class CoResidencyPlan:
-    cus: int                 # compute units of the device
-    seg_blocks_per_cu: int   # segment kernel: resident one-wave workgroups per CU
-    seg_grid: int            # owner waves (n_pad / 64)
-    act_blocks_per_cu: int   # act kernel: resident 256-thread workgroups per CU
-    act_grid: int            # policy workgroups for all rows (64 rows each)
-    chunk_waves: int         # owner waves per policy launch
-
-    @property
-    def seg_frac(self) -> float:
-        """The segment grid's even share of one CU, as a fraction of its per-CU limit."""
-        return math.ceil(self.seg_grid / self.cus) / self.seg_blocks_per_cu
-
-    @property
-    def chunks(self) -> int:
-        return -(-self.act_grid // self.chunk_waves)
+    cus: int            # compute units of the device
+    seg_grid: int       # owner waves (one-wave workgroups, n_pad / 64)
+    seg_vgprs: int      # per lane, allocated
+    seg_lds: int        # bytes per owner workgroup
+    act_grid: int       # policy workgroups (64 rows, 4 waves each)
+    act_vgprs: int
+    act_lds: int        # bytes per policy workgroup (padded: at most one per CU)
+    owner_waves_per_simd: int
+    max_envs: int       # the largest env count this pair of kernels admits
 
 
-def occupancy(params, num_envs: int) -> tuple[int, int, int, int]:
-    """(segment workgroups per CU, segment grid, act workgroups per CU, act grid) from the
-    library (hipOccupancyMaxActiveBlocksPerMultiprocessor of the launches' kernels)."""
+def occupancy(params, num_envs: int) -> dict:
+    """Both kernels' resources from the library (hipFuncGetAttributes, and
+    hipOccupancyMaxActiveBlocksPerMultiprocessor for each alone)."""
     lib = _lib.load()
-    bs, gs, ba, ga = C.c_int32(), C.c_int32(), C.c_int32(), C.c_int32()
-    _lib.check(lib.sacenv_boat_segment_occupancy(C.byref(params), 0, C.byref(bs), C.byref(gs)))
-    _lib.check(lib.sacenv_sac_act_occupancy(int(num_envs), C.byref(ba), C.byref(ga)))
-    return bs.value, gs.value, ba.value, ga.value
+    v = [C.c_int32() for _ in range(8)]
+    _lib.check(lib.sacenv_boat_segment_occupancy(C.byref(params), 0, *[C.byref(x) for x in v[:4]]))
+    _lib.check(lib.sacenv_sac_act_occupancy(int(num_envs), *[C.byref(x) for x in v[4:]]))
+    k = ("seg_per_cu", "seg_grid", "seg_vgprs", "seg_lds", "act_per_cu", "act_grid", "act_vgprs", "act_lds")
+    return {n: x.value for n, x in zip(k, v)}
 
 
-def make_plan(cus: int, seg_per_cu: int, seg_grid: int, act_per_cu: int, act_grid: int,
-              num_envs: int = 0) -> CoResidencyPlan:
-    """The largest policy chunk whose even share per CU fits beside the segment grid's."""
-    if seg_per_cu < 1 or act_per_cu < 1:
-        raise _lib.SacenvError(f"occupancy query returned {seg_per_cu} / {act_per_cu} workgroups per CU")
-    seg_frac = math.ceil(seg_grid / cus) / seg_per_cu
-    per_cu = math.floor((1.0 - seg_frac) * act_per_cu + 1e-9)   # policy workgroups per CU beside it
-    if per_cu < 1:
+def make_plan(cus: int, seg_grid: int, seg_vgprs: int, seg_lds: int, act_grid: int, act_vgprs: int,
+              act_lds: int, num_envs: int = 0) -> CoResidencyPlan:
+    """Per-SIMD VGPR / wave-slot and per-CU LDS accounting (module docstring)."""
+    if act_lds * 2 <= LDS_PER_CU:
+        raise _lib.SacenvError(f"hand-off policy workgroup LDS {act_lds} B does not exclude a second one per CU")
+    sv, av = _alloc(seg_vgprs), _alloc(act_vgprs)
+    # owner waves one SIMD can hold next to one policy wave, and the CU's LDS next to one policy workgroup
+    per_simd = min((SIMD_VGPRS - av) // sv if sv else WAVE_SLOTS, WAVE_SLOTS - 1)
+    if seg_lds:
+        per_simd = min(per_simd, (LDS_PER_CU - act_lds) // seg_lds // SIMDS_PER_CU)
+    cap = cus * SIMDS_PER_CU * max(per_simd, 0)
+    need = -(-seg_grid // (cus * SIMDS_PER_CU))
+    if per_simd < 1 or seg_grid > cap:
         raise ValueError(
-            f"closed loop cannot be co-resident: {num_envs} envs need {seg_grid} owner waves "
-            f"({math.ceil(seg_grid / cus)} per CU of {cus}, limit {seg_per_cu}), leaving no room for a "
-            f"policy workgroup (limit {act_per_cu} per CU); use fewer envs per GPU")
-    return CoResidencyPlan(cus, seg_per_cu, seg_grid, act_per_cu, act_grid, min(act_grid, per_cu * cus))
-
-
-def max_envs(cus: int, seg_per_cu: int, act_per_cu: int) -> int:
-    """The largest env count (a multiple of 64) ``make_plan`` accepts."""
-    waves_per_cu = math.floor(seg_per_cu * (1.0 - 1.0 / act_per_cu) + 1e-9)
-    return 64 * cus * waves_per_cu
+            f"closed loop cannot be co-resident: {num_envs} envs need {seg_grid} owner waves ({need} per SIMD of "
+            f"{cus * SIMDS_PER_CU}, {sv} VGPRs each); with one {av}-VGPR policy wave beside them a SIMD holds "
+            f"{max(per_simd, 0)}: use at most {64 * cap} envs per GPU")
+    return CoResidencyPlan(cus, seg_grid, sv, seg_lds, act_grid, av, act_lds, need, 64 * cap)
 
 
 def plan(env, n_cu: int | None = None) -> CoResidencyPlan:
     """The co-residency plan of a closed loop over ``env`` (raises if none exists)."""
     cus = int(n_cu) if n_cu is not None else torch.cuda.get_device_properties(env.device).multi_processor_count
-    bs, gs, ba, ga = occupancy(env.params, env.num_envs)
-    return make_plan(cus, bs, gs, ba, ga, env.num_envs)
+    o = occupancy(env.params, env.num_envs)
+    return make_plan(cus, o["seg_grid"], o["seg_vgprs"], o["seg_lds"], o["act_grid"], o["act_vgprs"], o["act_lds"],
+                     env.num_envs)
 
 
 class ClosedLoop:
@@ -121,14 +129,31 @@ class ClosedLoop:
         self.step_done = torch.zeros(nw, dtype=torch.int32, device=dev)
         self.actions = torch.zeros((self.K, env.num_envs), dtype=torch.float32, device=dev)
         self.status = env.status[1:2]
-        self.policy_stream = torch.cuda.Stream(device=dev)
+        # The two sides must run concurrently. The policy gets a hardware queue of its
+        # own (sacenv.h: two ordinary streams may share a queue and serialise, which
+        # deadlocks the hand-off); that stream is a BLOCKING one (hipExtStreamCreateWith-
+        # CUMask takes no flags), and the legacy null stream -- torch's default --
+        # implicitly waits for blocking streams, so the env's persistent launch goes on
+        # a non-blocking stream of its own, ordered after the caller's stream by events.
+        self.env_stream = torch.cuda.Stream(device=dev)
+        h = C.c_void_p()
+        with torch.cuda.device(dev):
+            _lib.check(_lib.load().sacenv_stream_create_exclusive(C.byref(h)))
+        self._policy_handle = h
+        self.policy_stream = torch.cuda.ExternalStream(h.value, device=dev)
         self.seq = 0
         self.failed = False
         self._keep = []
-        # the policy launches of one step: (row range, flag range) per chunk
-        cw, N = self.plan.chunk_waves, env.num_envs
-        self.chunks = [(64 * c0, min(N, 64 * (c0 + cw)), c0, min(nw, c0 + cw))
-                       for c0 in range(0, self.plan.act_grid, cw)]
+
+    def __del__(self):
+        h = getattr(self, "_policy_handle", None)
+        if h is not None and h.value:
+            try:
+                torch.cuda.synchronize(self.env.device)
+                _lib.load().sacenv_stream_destroy(h)
+            except Exception:  # noqa: BLE001  (interpreter shutdown)
+                pass
+            self._policy_handle = None
 
     def check(self) -> None:
         """Synchronise and raise if a hand-off timed out (then this loop stays refused)."""
@@ -151,20 +176,22 @@ class ClosedLoop:
         env, q0 = self.env, self.seq
         if q0 + K >= 0x7FFFFFFF:
             raise OverflowError("sequence numbers exhausted: build a new ClosedLoop")
-        ps = self.policy_stream
-        # the policy's first read (row q0: step_done >= q0 holds at once) must follow
-        # every earlier write of the obs on the env's stream (reset, the previous
-        # segment): the flags order the steps of a segment, the stream the rest
-        ps.wait_stream(torch.cuda.current_stream(env.device))
+        ps, es = self.policy_stream, self.env_stream
+        cur = torch.cuda.current_stream(env.device)
+        # both sides start after every earlier write on the caller's stream (reset, the
+        # previous segment, its refill): the flags order the steps of a segment, the
+        # streams the rest
+        ps.wait_stream(cur)
+        es.wait_stream(cur)
         obs = env.obs
         with torch.cuda.stream(ps):
             for k in range(K):
-                for r0, r1, c0, c1 in self.chunks:
-                    self.agent.choose_action_handoff(
-                        obs[r0:r1], eps[k, r0:r1], self.actions[k, r0:r1],
-                        obs_ready=self.step_done[c0:c1], obs_want=q0 + k,
-                        act_ready=self.act_ready[c0:c1], act_value=q0 + k + 1, status=self.status)
-        env.segment_async(self.actions, K, act_ready=self.act_ready, step_done=self.step_done, seq0=q0)
-        torch.cuda.current_stream(env.device).wait_stream(ps)  # the policy's launches are done too
+                self.agent.choose_action_handoff(
+                    obs, eps[k], self.actions[k], obs_ready=self.step_done, obs_want=q0 + k,
+                    act_ready=self.act_ready, act_value=q0 + k + 1, status=self.status)
+        with torch.cuda.stream(es):
+            env.segment_async(self.actions, K, act_ready=self.act_ready, step_done=self.step_done, seq0=q0)
+        cur.wait_stream(es)  # the caller's stream continues after both sides
+        cur.wait_stream(ps)
         self.seq = q0 + K
         self._keep = [eps]

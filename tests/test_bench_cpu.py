@@ -139,6 +139,9 @@ def test_driver_command_world2_gloo_segment_pooling():
     assert out["pooling"]["received_GBps_per_rank"] > 0
     # the no-exchange rate of the same segments, measured after the timed region
     ne = out["pooling"]["no_exchange"]
+    sh = ne["sharded_exchange"]     # one all-reduce of a segment's 128 learn() batches
+    assert sh["bytes_per_segment"] == 128 * 1024 * 26 * 4 and sh["allreduce_ms_per_segment"] > 0
+    assert 0 < sh["value"] < ne["value"] * 1.01
     assert ne["value"] > 0 and ne["steps"] % 128 == 0 and ne["ms_per_step"] > 0
     for _, _, steps, refills in res:
         assert steps % 128 == 0 and refills == steps // 128

@@ -34,7 +34,7 @@ def declared_functions():
 def test_library_exports_header(built_lib):
     from sacenv import _lib
     names = declared_functions()
-    assert len(names) == 35
+    assert len(names) == 37
     assert set(names) == set(_lib.EXPORTS)
     for n in names:
         assert hasattr(built_lib, n), n
@@ -269,11 +269,11 @@ def _interval_extrema_py(y, m, n, L, j):
     step = (n - 1) / (L - 1)
     jf = lambda i: min(int(i * step), n - 2)
 
-    inv = 1 / step
-    lo = max(math.ceil(j * inv) - 2, 0)
+    inv = (L - 1) / (n - 1)        # the host's knot_inv (sacenv/config.py)
+    lo = max(math.ceil(j * inv) - 1, 0)
     while lo < L and jf(lo) < j:
         lo += 1
-    hi = min(math.floor((j + 1) * inv) + 2, L - 1)
+    hi = min(math.floor((j + 1) * inv) + 1, L - 1)
     while hi >= 0 and jf(hi) > j:
         hi -= 1
     if lo > hi:
@@ -300,6 +300,28 @@ def _interval_extrema_py(y, m, n, L, j):
         for d in (-1, 0, 1, 2):
             cand.append(min(max(i0 + d, lo), hi))
     return cand, (lo, hi)
+
+
+def test_interval_bound_starts_never_overshoot():
+    """interval_extrema starts its first/last grid-index searches one below ceil(j inv)
+    and one above floor((j+1) inv) and only walks inward from there: exhaustively, for
+    4..16 knots and every L up to 20 000, neither start lies past the true bound."""
+    bad = 0
+    for n in range(4, 17):
+        for L in range(n, 20001):
+            step, inv = (n - 1) / (L - 1), (L - 1) / (n - 1)
+            jf = lambda i: min(int(i * step), n - 2)  # noqa: E731
+            for j in range(n - 1):
+                lo0 = max(math.ceil(j * inv) - 1, 0)
+                i = max(lo0 - 5, 0)
+                while jf(i) < j:
+                    i += 1
+                hi0 = min(math.floor((j + 1) * inv) + 1, L - 1)
+                k = min(hi0 + 5, L - 1)
+                while k >= 0 and jf(k) > j:
+                    k -= 1
+                bad += lo0 > i or hi0 < k
+    assert bad == 0
 
 
 @pytest.mark.parametrize("L", [10000, 20, 37])
@@ -476,20 +498,19 @@ def test_native_sac_views_follow_the_c_layout(built_lib):
 
 
 def test_closed_loop_co_residency_plan_arithmetic():
-    """sacenv.closed_loop's plan (no GPU): the segment grid's even share per CU plus one
-    policy launch's share must fit one CU; the policy is split into launches that do."""
-    from sacenv.closed_loop import make_plan, max_envs
-    p = make_plan(256, 8, 1024, 2, 1024, 65536)       # 4 owner waves/CU of 8: room for 1 act WG
-    assert p.seg_frac == 0.5 and p.chunk_waves == 256 and p.chunks == 4
-    p = make_plan(256, 16, 1024, 4, 1024, 65536)      # 4 of 16: 3 act WGs per CU
-    assert p.chunk_waves == 768 and p.chunks == 2
-    p = make_plan(256, 16, 100, 4, 100, 6400)         # small grids: one launch
-    assert p.chunk_waves == 100 and p.chunks == 1
+    """sacenv.closed_loop's plan (no GPU): every owner wave resident with room for one
+    policy wave per SIMD (512 VGPRs, granule 8) and one padded policy workgroup per CU."""
+    from sacenv import _lib
+    from sacenv.closed_loop import make_plan
+    p = make_plan(256, 1024, 318, 2816, 1024, 150, 84 * 1024, 65536)   # the measured kernels
+    assert p.seg_vgprs == 320 and p.act_vgprs == 152 and p.owner_waves_per_simd == 1
+    assert p.max_envs == 65536
     with pytest.raises(ValueError):
-        make_plan(256, 8, 2048, 2, 2048, 131072)      # 8 of 8 per CU: no room
-    assert max_envs(256, 8, 2) == 65536
-    assert max_envs(256, 16, 4) == 64 * 256 * 12
-    n = max_envs(256, 10, 3)
-    make_plan(256, 10, n // 64, 3, n // 64, n)
+        make_plan(256, 1025, 318, 2816, 1025, 150, 84 * 1024, 65600)      # one owner wave more
     with pytest.raises(ValueError):
-        make_plan(256, 10, n // 64 + 256, 3, n // 64 + 256, n + 64 * 256)
+        make_plan(256, 2048, 318, 2816, 2048, 150, 84 * 1024, 131072)     # two per SIMD
+    assert make_plan(256, 2048, 176, 2816, 2048, 150, 84 * 1024).max_envs == 131072  # 2 x 176 + 152
+    with pytest.raises(_lib.SacenvError):
+        make_plan(256, 64, 318, 2816, 64, 150, 80 * 1024)                 # 2 policy WGs would fit a CU
+    with pytest.raises(ValueError):                                      # LDS: owners + one policy WG
+        make_plan(256, 1024, 100, 40 * 1024, 1024, 150, 84 * 1024)

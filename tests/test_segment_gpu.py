@@ -122,7 +122,12 @@ def test_closed_loop_equals_eager_loop(N, K, segs, gpu, built_lib):
         a_env.refill()
         b_env.refill()
         torch.cuda.synchronize()
-        assert torch.equal(loop.actions[:K], torch.stack(acts_b[-K:])), s
+        if not torch.equal(loop.actions[:K], torch.stack(acts_b[-K:])):
+            nz = [(loop.actions[k] != 0).sum().item() for k in range(min(K, 6))]
+            raise AssertionError(
+                f"segment {s}: actions differ; rows nonzero {nz}, status {int(a_env.status[1])}, step_done "
+                f"{sorted(set(loop.step_done.tolist()))[:6]}, act_ready {sorted(set(loop.act_ready.tolist()))[:6]}, "
+                f"plan {loop.plan}")
         assert torch.equal(a_env.arena, b_env.arena), s
     a_env.check_status()
     assert int(a_env.status[1]) == 0
@@ -174,31 +179,30 @@ def test_closed_loop_after_a_timeout_refuses_and_steps_nothing(gpu, built_lib):
 
 
 def test_closed_loop_at_the_largest_co_resident_size(gpu, built_lib):
-    """the co-residency plan from both kernels' occupancy; at the
-    largest env count it accepts, the closed loop equals the eager loop bit for bit
-    (the policy split into launches that fit beside the segment grid); one owner wave
-    per CU more is refused."""
+    """the co-residency plan from both kernels' VGPRs and LDS (the
+    library's hipFuncGetAttributes); at the largest env count it admits -- the bench's
+    65 536, one owner wave per SIMD beside one lean policy wave -- the closed loop
+    equals the eager loop bit for bit; one owner wave more is refused."""
     from sacenv import VecBoatEnv
-    from sacenv.closed_loop import ClosedLoop, make_plan, max_envs, occupancy
+    from sacenv.closed_loop import ClosedLoop, make_plan, occupancy
     from sacenv.sac_native import NativeSAC
     cfg = {"base_settings": {"experiment": 6, "test_mode": 0}}
     kw = dict(seed=5, device=gpu, max_episode_steps=40, n_helpers=2048, auto_refill=False)
     probe = VecBoatEnv(cfg, 64, **kw)
     cus = torch.cuda.get_device_properties(gpu).multi_processor_count
-    bs, _, ba, _ = occupancy(probe.params, 64)
-    N = max_envs(cus, bs, ba)
-    print(f"segment {bs}/CU, act {ba}/CU, {cus} CUs: largest closed loop {N} envs")
+    o = occupancy(probe.params, 64)
+    print(f"kernels: {o}, {cus} CUs")
+    N = make_plan(cus, 1, o["seg_vgprs"], o["seg_lds"], 1, o["act_vgprs"], o["act_lds"]).max_envs
+    print(f"largest closed loop: {N} envs")
     assert N >= 65536                                 # the bench's size runs closed loop
     with pytest.raises(ValueError):
-        nw = N // 64 + cus
-        make_plan(cus, bs, nw, ba, nw, N + 64 * cus)
+        make_plan(cus, N // 64 + 1, o["seg_vgprs"], o["seg_lds"], N // 64 + 1, o["act_vgprs"], o["act_lds"], N + 64)
     a_env, b_env = VecBoatEnv(cfg, N, **kw), VecBoatEnv(cfg, N, **kw)
     a_env.reset()
     b_env.reset()
     agent = NativeSAC(gpu, init_seed=3, with_memory=False)
     K = 16
     loop = ClosedLoop(a_env, agent, segment=K)
-    print(f"plan: {loop.plan}, {len(loop.chunks)} policy launches per step")
     g = torch.Generator(device=gpu)
     g.manual_seed(1)
     for s in range(2):
@@ -211,3 +215,40 @@ def test_closed_loop_at_the_largest_co_resident_size(gpu, built_lib):
         torch.cuda.synchronize()
         assert torch.equal(a_env.arena, b_env.arena), s
     loop.check()
+
+
+def test_closed_loop_survives_shared_hardware_queues(gpu, built_lib):
+    """Ordinary HIP streams are spread over GPU_MAX_HW_QUEUES shared hardware queues; a
+    policy stream that landed on the env stream's queue serialised the two and
+    deadlocked the hand-off until its timeout (seen in the full GPU suite). The policy
+    stream now has a queue of its own (sacenv_stream_create_exclusive): with many
+    streams created and used first, every loop still equals the eager loop."""
+    from sacenv import VecBoatEnv
+    from sacenv.closed_loop import ClosedLoop
+    from sacenv.sac_native import NativeSAC
+    streams = [torch.cuda.Stream(device=gpu) for _ in range(9)]
+    for s in streams:
+        with torch.cuda.stream(s):
+            torch.ones(16, device=gpu).sum()
+    cfg = {"base_settings": {"experiment": 6, "test_mode": 0}}
+    kw = dict(seed=9, device=gpu, max_episode_steps=50, n_helpers=256, auto_refill=False)
+    agent = NativeSAC(gpu, init_seed=4, with_memory=False)
+    N, K = 4096, 64
+    g = torch.Generator(device=gpu)
+    g.manual_seed(2)
+    for trial in range(5):
+        a_env, b_env = VecBoatEnv(cfg, N, **kw), VecBoatEnv(cfg, N, **kw)
+        a_env.reset()
+        b_env.reset()
+        loop = ClosedLoop(a_env, agent, segment=K)
+        eps = torch.randn((K, N), generator=g, device=gpu)
+        loop.run(eps)
+        for k in range(K):
+            b_env.step_async(agent.choose_action(b_env.obs, eps=eps[k]).reshape(-1).contiguous())
+        torch.cuda.synchronize()
+        loop.check()
+        assert torch.equal(a_env.arena, b_env.arena), trial
+        extra = torch.cuda.Stream(device=gpu)   # shift the round-robin for the next trial
+        with torch.cuda.stream(extra):
+            torch.ones(16, device=gpu).sum()
+        streams.append(extra)
