@@ -111,6 +111,9 @@ def parse(argv=None):
                     help="time every E-th timed segment's launch (the first always) with HIP events "
                          "for roofline.kernel_avg_us: each pair puts a stream marker on both sides of "
                          "the launch (measured: every segment 1.78 us/step, every 4th 1.74)")
+    ap.add_argument("--no-every-output", action="store_true",
+                    help="skip the every-output rollout measurement after the timed region (PMC passes: its "
+                         "k_rollout launches would mix into the segment kernel's counters)")
     ap.add_argument("--closed-loop", action="store_true",
                     help="a separate line: the SAC actor choosing every step's actions on the device, handing "
                          "off to the persistent env launch through per-wave flags (sacenv.closed_loop)")
@@ -752,7 +755,8 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
     step_s = ev0.ms_to(ev1) * 1e-3 / steps
 
     every = None
-    if world == 1 and run.mode == "segment" and not args.mixed and not args.no_autoreset:
+    if (world == 1 and run.mode == "segment" and not args.mixed and not args.no_autoreset
+            and not args.no_every_output):
         every = every_output_rate(wl, dev, k0=k)
     dinfo = dist_info(world, dev)
     if rank != 0:

@@ -19,9 +19,9 @@ mkdir -p "$OUT"
   -o tools/probes/fetch_calib tools/probes/fetch_calib.hip || exit 1
 MODE=${PMC_KERNEL:-segment}
 if [ "$MODE" = step ]; then LAUNCH="--launch step"; PMCL="--launch step --no-graph"; else LAUNCH=""; PMCL=""; fi
-BENCH="python3 bench.py --steps ${PMC_STEPS:-256} --warmup 128 --no-cpu-baseline $PMCL"
+BENCH="python3 bench.py --steps ${PMC_STEPS:-256} --warmup 128 --no-cpu-baseline --no-every-output $PMCL"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_trace" -o run --output-format csv \
-  -- python3 bench.py --no-cpu-baseline $LAUNCH > "$OUT/prof_trace_bench.json" 2> "$OUT/prof_trace.log" || exit 1
+  -- python3 bench.py --no-cpu-baseline --no-every-output $LAUNCH > "$OUT/prof_trace_bench.json" 2> "$OUT/prof_trace.log" || exit 1
 i=0
 while read -r c; do
   i=$((i+1))
@@ -35,5 +35,6 @@ WRITE_SIZE TCC_HIT_sum TCC_MISS_sum
 FETCH_SIZE
 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64
 SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_INT32
+SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_SALU SQ_INSTS_BRANCH SQ_INSTS_SMEM SQ_INSTS_VALU_INT64
 LIST
 python3 tools/pmc_summary.py "$OUT" "$MODE" || exit 1
