@@ -658,23 +658,33 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
 // critical points need only grid-point accuracy, so approximate rcp/rsq do.
 // Interval j's piece is (y0, y1, a, b) = (y[j], y[j+1], m[j], m[j+1]): every
 // candidate lies in [lo, hi], whose grid samples all fall in interval j.
-template <int S>
-__device__ __forceinline__ void interval_extrema(const SacenvBoatParams& p, int j, int s, double y0,
-                                                 double y1, double a, double b, double& mn,
-                                                 double& mx) {
-  mn = INFINITY;
-  mx = -INFINITY;
+// The grid indices [lo, hi] of interval j (a launch constant per interval: the
+// fit kernel forms it once per lane, not per fit).
+struct IvGrid {
+  double jd, lod, hid;
+  bool valid;
+};
+__device__ __forceinline__ IvGrid interval_grid(const SacenvBoatParams& p, int j) {
   const int L = p.wind_len;
-  const double inv = p.knot_inv;
   // (inv = RN(1/knot_step) puts ceil(j inv) within one of the first grid index of
   // interval j: start one below and step up, and symmetrically for the last)
-  int lo = (int)ceil((double)j * inv) - 1;
+  int lo = (int)ceil((double)j * p.knot_inv) - 1;
   if (lo < 0) lo = 0;
   while (lo < L && knot_coord(p, lo).j < j) ++lo;
-  int hi = (int)floor((double)(j + 1) * inv) + 1;
+  int hi = (int)floor((double)(j + 1) * p.knot_inv) + 1;
   if (hi > L - 1) hi = L - 1;
   while (hi >= 0 && knot_coord(p, hi).j > j) --hi;
-  if (lo > hi) return;
+  return IvGrid{(double)j, (double)lo, (double)hi, lo <= hi};
+}
+
+template <int S>
+__device__ __forceinline__ void interval_extrema_on(const SacenvBoatParams& p, const IvGrid& gr, int s,
+                                                    double y0, double y1, double a, double b, double& mn,
+                                                    double& mx) {
+  mn = INFINITY;
+  mx = -INFINITY;
+  if (!gr.valid) return;
+  const double inv = p.knot_inv;
   const double qa = 3.0 * (b - a), qb = 6.0 * a, qc = y1 - y0 - 2.0 * a - b;
   // the piece in the power basis, f(t) = y0 + c1 t + c2 t^2 + c3 t^3 (spline_piece
   // expanded: c1 = y1 - y0 - 2 m0 - m1, c2 = 3 m0, c3 = m1 - m0): 3 FMAs per
@@ -700,7 +710,7 @@ __device__ __forceinline__ void interval_extrema(const SacenvBoatParams& p, int 
   // i.e. in interval j, so its knot coordinate is t = i * knot_step - j, the same
   // double knot_coord forms -- no integer conversions per candidate (v_cvt costs
   // 8 cycles at one wave per SIMD, tools/ubench/valu_mix.hip)
-  const double jd = (double)j, lod = (double)lo, hid = (double)hi;
+  const double jd = gr.jd, lod = gr.lod, hid = gr.hid;
   const double i0 = ok0 ? floor((jd + r0) * inv) : lod;
   const double i1 = ok1 ? floor((jd + r1) * inv) : lod;
 #pragma unroll
@@ -725,6 +735,12 @@ __device__ __forceinline__ void interval_extrema(const SacenvBoatParams& p, int 
       mx = fmax(mx, v);
     }
   }
+}
+template <int S>
+__device__ __forceinline__ void interval_extrema(const SacenvBoatParams& p, int j, int s, double y0,
+                                                 double y1, double a, double b, double& mn,
+                                                 double& mx) {
+  interval_extrema_on<S>(p, interval_grid(p, j), s, y0, y1, a, b, mn, mx);
 }
 
 // ---------------------------------------------------------------- spline constants
@@ -1281,34 +1297,62 @@ __global__ void __launch_bounds__(kWave) k_refill(SacenvBoatParams p, Arena A) {
 // interval j, the group reduces min/max by shuffles, and lane j folds and
 // stores knot j (the operations of fit_store_wave in the same order:
 // bit-identical coefficients). Grid-stride over the groups.
+//
+// Per lane, what depends only on j (a lane constant: the group's lanes are the
+// knots) is formed once per launch: G's row jj in registers (zero past nk) and
+// interval j's grid range. kFull (nk == GS) drops every per-knot bound check.
+// The group's shuffles are DPP moves inside a 16-lane row (no LDS round trip).
 template <int GS>
-__device__ void fit_group(const SacenvBoatParams& p, const Arena& A, const double* g, int item, int j,
-                          int nc) {
-  const int nk = p.n_knots;
+__device__ __forceinline__ double group_min(double v) {
+  v = fmin(v, dpp_f64<0xB1>(v));  // quad_perm [1,0,3,2]
+  v = fmin(v, dpp_f64<0x4E>(v));  // quad_perm [2,3,0,1]
+  v = fmin(v, dpp_f64<0x141>(v));  // row_half_mirror: the other quad of the 8
+  if (GS == 16) v = fmin(v, dpp_f64<0x140>(v));  // row_mirror: the other 8 of the row
+  return v;
+}
+template <int GS>
+__device__ __forceinline__ double group_max(double v) {
+  v = fmax(v, dpp_f64<0xB1>(v));
+  v = fmax(v, dpp_f64<0x4E>(v));
+  v = fmax(v, dpp_f64<0x141>(v));
+  if (GS == 16) v = fmax(v, dpp_f64<0x140>(v));
+  return v;
+}
+// lane i + 1's value (row_shl:1; the row's last lane keeps its own, unused)
+__device__ __forceinline__ double next_lane_f64(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(__double2loint(v), __double2loint(v), 0x101, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(__double2hiint(v), __double2hiint(v), 0x101, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+template <int GS, bool kFull>
+__device__ __forceinline__ void fit_group(const SacenvBoatParams& p, const Arena& A, const double (&gr)[GS],
+                                          const IvGrid& ig, int item, int j, int jj, int j1, int nc) {
+  const int nk = kFull ? GS : p.n_knots;
   const int rr = item / nc, c = item - rr * nc;
   const int e = A.refill_list(0)[rr], f0 = A.refill_list(1)[rr], f1 = A.refill_list(2)[rr];
   for (int f = f0; f < f1; ++f) {  // uniform across the group
     const int slot = f % kSlots;
-    const double* raw = A.knots_raw();
+    const double* kr = A.knots_raw() + A.wix(slot, c, 0, e);  // the curve's nk knots, contiguous
     double yk[GS];
 #pragma unroll
-    for (int k = 0; k < GS; ++k) yk[k] = k < nk ? raw[A.wix(slot, c, k, e)] : 0.0;
-    const int jj = j < nk ? j : nk - 1, j1 = jj + 1 < nk ? jj + 1 : jj;
-    double yv = raw[A.wix(slot, c, jj, e)];
-    const double y1 = raw[A.wix(slot, c, j1, e)];
+    for (int k = 0; k < GS; ++k) yk[k] = kr[kFull || k < nk ? k : nk - 1];
+    double yv = kr[jj];
+    const double y1 = kr[j1];
+    // m = G @ y in the reference's order (terms past nk: none when kFull; else a
+    // select, so no +0.0 term can turn a -0.0 sum into +0.0)
     double mv = 0.0;
 #pragma unroll
-    for (int k = 0; k < GS; ++k)
-      if (k < nk) mv += g[jj * nk + k] * yk[k];
-    const double m1 = __shfl_down(mv, 1, GS);
-    double mn = INFINITY, mx = -INFINITY;
-    if (j < nk - 1) interval_extrema<1>(p, j, 0, yv, y1, mv, m1, mn, mx);
-#pragma unroll
-    for (int o = GS / 2; o > 0; o >>= 1) {
-      mn = fmin(mn, __shfl_xor(mn, o, GS));
-      mx = fmax(mx, __shfl_xor(mx, o, GS));
+    for (int k = 0; k < GS; ++k) {
+      const double s = mv + gr[k] * yk[k];
+      mv = kFull || k < nk ? s : mv;
     }
-    if (j < nk) {
+    const double m1 = next_lane_f64(mv);
+    double mn, mx;
+    interval_extrema_on<1>(p, ig, 0, yv, y1, mv, m1, mn, mx);  // (ig invalid: +-inf)
+    mn = group_min<GS>(mn);
+    mx = group_max<GS>(mx);
+    if (kFull || j < nk) {
       fold_knot(p, c, mn, mx, yv, mv);
       *reinterpret_cast<double2*>(A.wind_knots() + 2 * A.wix(slot, c, j, e)) = double2{yv, mv};
     }
@@ -1317,12 +1361,11 @@ __device__ void fit_group(const SacenvBoatParams& p, const Arena& A, const doubl
 
 // GS lanes per (env, curve): 8 for up to 8 knots, else 16; one instantiation
 // per width, so the 8-knot launch carries no 16-knot registers
-template <int GS>
+template <int GS, bool kFull>
 __global__ void __launch_bounds__(kWave) k_refill_fit(SacenvBoatParams p, Arena A, Tail T) {
-  __shared__ double g[kMaxK * kMaxK];
   const int lane = threadIdx.x;
   const int nc = p.use_wind_table ? 0 : n_curves(p.experiment);
-  const int nk = p.n_knots;
+  const int nk = kFull ? GS : p.n_knots;
   const int items = A.status()[2] * nc;  // (env, curve) groups
 #ifdef SACENV_STAMPS
   const uint64_t st0 = __builtin_amdgcn_s_memrealtime();
@@ -1331,13 +1374,18 @@ __global__ void __launch_bounds__(kWave) k_refill_fit(SacenvBoatParams p, Arena 
   if (fst_ok) fst[0] = st0, fst[1] = 0;
 #endif
   if (items == 0 || (int)blockIdx.x * (kWave / GS) >= items) return;  // uniform
-  for (int i = lane; i < nk * nk; i += kWave) g[i] = T.g[i];
-  __syncthreads();
+  const int j = lane & (GS - 1);
+  const int jj = j < nk ? j : nk - 1, j1 = jj + 1 < nk ? jj + 1 : jj;
+  double gr[GS];
+#pragma unroll
+  for (int k = 0; k < GS; ++k) gr[k] = kFull || k < nk ? T.g[jj * nk + k] : 0.0;
+  IvGrid ig = interval_grid(p, j < nk - 1 ? j : 0);
+  ig.valid = ig.valid && j < nk - 1;
   const int per = kWave / GS;
   for (int base = blockIdx.x * per; base < items; base += gridDim.x * per) {
     const int item = base + lane / GS;
     if (item >= items) break;
-    fit_group<GS>(p, A, g, item, lane & (GS - 1), nc);
+    fit_group<GS, kFull>(p, A, gr, ig, item, j, jj, j1, nc);
   }
 #ifdef SACENV_STAMPS
   __syncthreads();
@@ -2725,12 +2773,16 @@ int sacenv_boat_refill(const SacenvBoatParams* p, void* arena, void* stream) {
   // (episode, curve) items), grid-stride beyond it; blocks past the count exit
   // at once. Measured 0.12 us/step better than one block per owner wave.
   constexpr int fit_blocks = 8192;
-  if (p->n_knots > 8)
-    hipLaunchKernelGGL(k_refill_fit<16>, dim3(fit_blocks), dim3(kWave), 0, (hipStream_t)stream, *p, A,
-                       make_tail(*p, arena));
+  const Tail T = make_tail(*p, arena);
+  if (p->n_knots == 8)
+    hipLaunchKernelGGL((k_refill_fit<8, true>), dim3(fit_blocks), dim3(kWave), 0, (hipStream_t)stream, *p, A, T);
+  else if (p->n_knots < 8)
+    hipLaunchKernelGGL((k_refill_fit<8, false>), dim3(fit_blocks), dim3(kWave), 0, (hipStream_t)stream, *p, A, T);
+  else if (p->n_knots == 16)
+    hipLaunchKernelGGL((k_refill_fit<16, true>), dim3(fit_blocks), dim3(kWave), 0, (hipStream_t)stream, *p, A, T);
   else
-    hipLaunchKernelGGL(k_refill_fit<8>, dim3(fit_blocks), dim3(kWave), 0, (hipStream_t)stream, *p, A,
-                       make_tail(*p, arena));
+    hipLaunchKernelGGL((k_refill_fit<16, false>), dim3(fit_blocks), dim3(kWave), 0, (hipStream_t)stream, *p, A,
+                       T);
   return launch_status();
 }
 
