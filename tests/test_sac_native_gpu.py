@@ -126,7 +126,10 @@ def test_native_learn_matches_reference_fixture(gpu, built_lib):
         b = tuple(torch.from_numpy(z[f"b{i}_{k}"]) for k in ("state", "action", "reward", "new_state", "done"))
         out = agent.learn(b, noise=(eps[2 * i], eps[2 * i + 1]))
         losses.append([float(x) for x in out])
-    check(agent, np.asarray(losses), z, rtol_w=1e-2, rtol_l=1e-4, init=init)
+    # bar: every weight tensor's two Adam steps within 1e-3 of their
+    # norm; measured worst 6.8e-5 (actor.fc2.weight; tools/sac_fixture_stats.py,
+    # profiles/r04_sac_fixture_stats.json: no entry steps the other way)
+    check(agent, np.asarray(losses), z, rtol_w=1e-3, rtol_l=1e-4, init=init)
 
 
 def test_native_learn_tracks_torch_over_steps(gpu, built_lib):
@@ -144,7 +147,8 @@ def test_native_learn_tracks_torch_over_steps(gpu, built_lib):
         for k in a[n]:
             d_ref, d_nat = a[n][k] - w0[n][k], b[n][k] - w0[n][k]
             nrm = np.linalg.norm(d_ref)
-            assert np.linalg.norm(d_nat - d_ref) <= 2e-2 * nrm + 1e-7, (n, k)
+            # (was 2e-2) measured worst 2.0e-4, value.fc2.weight
+            assert np.linalg.norm(d_nat - d_ref) <= 2e-3 * nrm + 1e-7, (n, k)
 
 
 def test_native_learn_from_device_buffer(gpu, built_lib):
