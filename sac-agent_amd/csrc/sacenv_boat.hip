@@ -1797,7 +1797,7 @@ __device__ uint32_t wait_flag(const uint32_t* f, uint32_t want, uint32_t seen, i
 // kHand (kRoll only): rows published step by step and/or done flags (the
 // closed loop); without it the loop carries no flag code at all (the launch
 // checked that every row was already published).
-template <bool kRoll, int kNc, bool kTIdx, bool kHand = false, bool kTrans = true>
+template <bool kRoll, int kNc, bool kTIdx, bool kHand = false, bool kTrans = true, bool kVc = kRoll>
 __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Arena& A, const Tail& Tin,
                                            const float* __restrict__ action, OwnerLds& l, int ob,
                                            int lane, int n_steps = 1, const RollArgs* ra = nullptr,
@@ -1875,8 +1875,8 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   // one-step launch: plain constants (the compiler places them; the VGPR copies
   // cost their moves in every launch: k_step 5.02 -> 5.36 us measured), the
   // multi-step loop: VGPR copies, moved once per launch
-  const TrigK K = trig_k<kRoll>();
-  const ObsConst oc = kRoll ? obs_const_v(T) : obs_const(T);
+  const TrigK K = trig_k<kVc>();
+  const ObsConst oc = kVc ? obs_const_v(T) : obs_const(T);
   // Wind.get_wind(index) (wind.py:20-24, IndexError guard) of this step. Curves:
   // from the lane's copy of its spline piece (wind_coef, loaded with the
   // state). The copy is refreshed from the active slot at the end of a step
@@ -2340,10 +2340,16 @@ __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, Arena A, Tai
 // n_steps BoatEnv.step launches fused, the state in registers between the
 // steps: open-loop rollouts (records per step) and the segment
 // launch (the arena's record every step, actions behind per-wave flags)
-template <int kNc, bool kTIdx, bool kTrans>
-__global__ void __launch_bounds__(kWave) k_rollout(SacenvBoatParams p, Arena A, Tail T,
-                                                   const float* __restrict__ action, int n_steps, RollArgs ra) {
-  __shared__ OwnerLds slds;
+//
+// kVc: the fp64 constants as VGPR copies (one owner wave per SIMD: k_rollout), or
+// as literals and scalar registers (k_rollout_dense: 238 VGPRs, two owner waves
+// per SIMD, for grids with more owner waves than SIMDs -- 131 072 envs: 48.5
+// against 44.4 G env-steps/s; at one wave per SIMD the copies win, 1.34 against
+// 2.04 us per step). The same arithmetic either way: results are bit-identical.
+template <int kNc, bool kTIdx, bool kTrans, bool kVc>
+__device__ __forceinline__ void rollout_body(const SacenvBoatParams& p, const Arena& A, const Tail& T,
+                                             const float* __restrict__ action, int n_steps, const RollArgs& ra,
+                                             OwnerLds& slds) {
   const int ob = blockIdx.x, lane = threadIdx.x;
   uint32_t seen = 0u;
   bool hand = ra.done != nullptr;
@@ -2371,12 +2377,31 @@ __global__ void __launch_bounds__(kWave) k_rollout(SacenvBoatParams p, Arena A, 
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     hand = hand || seen < ra.seq0 + (uint32_t)n_steps;
   }
-  if (hand)
-    owner_wave<true, kNc, kTIdx, true, kTrans>(vreg_params(p), A, vreg_tail(T), action, slds, ob, lane, n_steps,
-                                               &ra, nullptr, seen);
-  else
-    owner_wave<true, kNc, kTIdx, false, kTrans>(vreg_params(p), A, vreg_tail(T), action, slds, ob, lane, n_steps,
-                                                &ra);
+  if (hand) {
+    if (kVc)
+      owner_wave<true, kNc, kTIdx, true, kTrans, true>(vreg_params(p), A, vreg_tail(T), action, slds, ob, lane,
+                                                       n_steps, &ra, nullptr, seen);
+    else
+      owner_wave<true, kNc, kTIdx, true, kTrans, false>(p, A, T, action, slds, ob, lane, n_steps, &ra, nullptr, seen);
+  } else {
+    if (kVc)
+      owner_wave<true, kNc, kTIdx, false, kTrans, true>(vreg_params(p), A, vreg_tail(T), action, slds, ob, lane,
+                                                        n_steps, &ra);
+    else
+      owner_wave<true, kNc, kTIdx, false, kTrans, false>(p, A, T, action, slds, ob, lane, n_steps, &ra);
+  }
+}
+template <int kNc, bool kTIdx, bool kTrans>
+__global__ void __launch_bounds__(kWave) k_rollout(SacenvBoatParams p, Arena A, Tail T,
+                                                   const float* __restrict__ action, int n_steps, RollArgs ra) {
+  __shared__ OwnerLds slds;
+  rollout_body<kNc, kTIdx, kTrans, true>(p, A, T, action, n_steps, ra, slds);
+}
+template <int kNc, bool kTIdx, bool kTrans>
+__global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(2, 2)))
+k_rollout_dense(SacenvBoatParams p, Arena A, Tail T, const float* __restrict__ action, int n_steps, RollArgs ra) {
+  __shared__ OwnerLds slds;
+  rollout_body<kNc, kTIdx, kTrans, false>(p, A, T, action, n_steps, ra, slds);
 }
 
 // sacenv_mixed_segment (BASELINE configs[4] as one persistent launch): the
@@ -2656,18 +2681,36 @@ int sacenv_boat_step_pooled(const SacenvBoatParams* p, void* arena, const float*
 }
 
 // k_rollout for the launch's wind kind and t rule
+// More owner waves than the device has SIMDs: the two-waves-per-SIMD
+// instantiation (k_rollout_dense), which keeps every owner wave resident.
+static bool dense_grid(int nb_boat) {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return false;
+  return nb_boat > 4 * cus;
+}
+
 static int launch_multi(const SacenvBoatParams& p, void* arena, const float* actions, int n_steps, const RollArgs& ra,
                         void* stream) {
   const int nb_boat = (int)(pad64(p.n_envs) / kWave);
-#define SACENV_LAUNCH(NC, TI)                                                                              \
+  const bool dense = dense_grid(nb_boat);
+#define SACENV_LAUNCH_K(KER, NC, TI)                                                                       \
   if (ra.trans != nullptr)                                                                                 \
-    hipLaunchKernelGGL((k_rollout<NC, TI, true>), dim3(nb_boat), dim3(kWave), 0, (hipStream_t)stream, p,   \
+    hipLaunchKernelGGL((KER<NC, TI, true>), dim3(nb_boat), dim3(kWave), 0, (hipStream_t)stream, p,         \
                        make_arena(p, arena), make_tail(p, arena), actions, n_steps, ra);                   \
   else                                                                                                     \
-    hipLaunchKernelGGL((k_rollout<NC, TI, false>), dim3(nb_boat), dim3(kWave), 0, (hipStream_t)stream, p,  \
+    hipLaunchKernelGGL((KER<NC, TI, false>), dim3(nb_boat), dim3(kWave), 0, (hipStream_t)stream, p,        \
                        make_arena(p, arena), make_tail(p, arena), actions, n_steps, ra)
+#define SACENV_LAUNCH(NC, TI)                  \
+  if (dense) {                                 \
+    SACENV_LAUNCH_K(k_rollout_dense, NC, TI);  \
+  } else {                                     \
+    SACENV_LAUNCH_K(k_rollout, NC, TI);        \
+  }
   SACENV_OWNER_DISPATCH(p, SACENV_LAUNCH)
 #undef SACENV_LAUNCH
+#undef SACENV_LAUNCH_K
   return launch_status();
 }
 
@@ -2739,16 +2782,24 @@ int sacenv_boat_segment_occupancy(const SacenvBoatParams* p, int32_t with_trans,
   int nb = 0;
   hipError_t e = hipSuccess;
   hipFuncAttributes fa{};
-#define SACENV_OCC(NC, TI)                                                                                  \
+  const bool dense = dense_grid((int)(pad64(p->n_envs) / kWave));  // the kernel launch_multi would pick
+#define SACENV_OCC_K(KER, NC, TI)                                                                            \
   if (with_trans) {                                                                                          \
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_rollout<NC, TI, true>, kWave, 0);                \
-    if (e == hipSuccess) e = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(k_rollout<NC, TI, true>)); \
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, KER<NC, TI, true>, kWave, 0);                      \
+    if (e == hipSuccess) e = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(KER<NC, TI, true>));    \
   } else {                                                                                                   \
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_rollout<NC, TI, false>, kWave, 0);               \
-    if (e == hipSuccess) e = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(k_rollout<NC, TI, false>)); \
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, KER<NC, TI, false>, kWave, 0);                     \
+    if (e == hipSuccess) e = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(KER<NC, TI, false>));   \
+  }
+#define SACENV_OCC(NC, TI)                  \
+  if (dense) {                              \
+    SACENV_OCC_K(k_rollout_dense, NC, TI);  \
+  } else {                                  \
+    SACENV_OCC_K(k_rollout, NC, TI);        \
   }
   SACENV_OWNER_DISPATCH(*p, SACENV_OCC)
 #undef SACENV_OCC
+#undef SACENV_OCC_K
   if (e != hipSuccess) return (int)e;
   *blocks_per_cu = nb;
   *grid = (int32_t)(pad64(p->n_envs) / kWave);

@@ -94,6 +94,43 @@ def test_segment_at_bench_size_equals_steps(gpu, built_lib):
         assert torch.equal(a_env.arena, b_env.arena), s
 
 
+@pytest.mark.parametrize("exp", [1, 4, 6])
+def test_dense_segment_equals_steps(exp, gpu, built_lib):
+    """More owner waves than SIMDs (131 072 envs): the segment launch takes the
+    two-waves-per-SIMD instantiation (k_rollout_dense, constants as literals and
+    scalar registers); bit-identical to step launches, with and without pooled rows."""
+    from sacenv import VecBoatEnv, _lib
+    from sacenv.closed_loop import occupancy
+    N, K = 131072, 64
+    kw = dict(seed=3, device=gpu, max_episode_steps=40, auto_refill=False)
+    cfg = {"base_settings": {"experiment": exp, "test_mode": 0}}
+    a_env, b_env = VecBoatEnv(cfg, N, **kw), VecBoatEnv(cfg, N, **kw)
+    o = occupancy(a_env.params, N)
+    simds = 4 * torch.cuda.get_device_properties(gpu).multi_processor_count
+    if o["seg_grid"] > simds:            # the dense kernel: two owner waves fit per SIMD
+        assert o["seg_vgprs"] <= 256 and o["seg_per_cu"] >= 8, o
+    a_env.reset()
+    b_env.reset()
+    acts = torch.rand((2 * K, N), device=gpu) * 2 - 1
+    ready = torch.full((N // 64,), 0x7FFFFFFF, dtype=torch.int32, device=gpu)
+    row = _lib.trans_bytes(exp) * a_env.n_pad
+    ta = torch.zeros(K * row, dtype=torch.uint8, device=gpu)
+    tb = torch.zeros_like(ta)
+    a_env.segment_async(acts, K, act_ready=ready)
+    for j in range(K):
+        b_env.step_async(acts[j])
+    torch.cuda.synchronize()
+    assert torch.equal(a_env.arena, b_env.arena)
+    a_env.segment_async(acts[K:], K, act_ready=ready, trans=ta, trans_stride=row)
+    for j in range(K):
+        b_env.step_pooled_async(acts[K + j].contiguous(), tb[j * row:(j + 1) * row])
+    a_env.refill()
+    b_env.refill()
+    torch.cuda.synchronize()
+    assert torch.equal(ta, tb)
+    assert torch.equal(a_env.arena, b_env.arena)
+
+
 @pytest.mark.parametrize("N,K,segs", [(8192, 128, 3), (777, 37, 4)])
 def test_closed_loop_equals_eager_loop(N, K, segs, gpu, built_lib):
     """ClosedLoop (the env as segment launches, the SAC policy per step on a second
