@@ -26,14 +26,15 @@ $B --experiment 1 --envs 4096 --cpu-seconds 6 > gpurun_out/bench_c2.json 2> gpur
 $B --mixed --cpu-seconds 6 > gpurun_out/bench_c5.json 2> gpurun_out/bench_c5.log || exit 1
 $B --rollout 128 > gpurun_out/bench_rollout_k128.json 2> gpurun_out/bench_rollout_k128.log || exit 1
 $B --envs 131072 --no-cpu-baseline > gpurun_out/bench_131k.json 2> gpurun_out/bench_131k.log || exit 1
+$B --closed-loop --no-cpu-baseline > gpurun_out/bench_closed.json 2> gpurun_out/bench_closed.log || exit 1
 python - <<'PY'
 import json
-for f in ("driver", "default", "step", "c2", "c5", "rollout_k128", "131k"):
+for f in ("driver", "default", "step", "c2", "c5", "rollout_k128", "131k", "closed"):
     d = json.load(open(f"gpurun_out/bench_{f}.json"))
-    r, c = d["roofline"], d.get("cpu_baseline")
-    k = r.get("kernel_avg_us", r.get("kernel_avg_us_per_step"))
+    r, c = d.get("roofline") or {}, d.get("cpu_baseline")
+    k = r.get("kernel_avg_us", r.get("kernel_avg_us_per_step")) or 0.0
     print(f"{f:13s} {d['value']/1e9:7.3f} G/s {d['ms_per_step']*1e3:6.2f} us/step kernel {k:5.2f} us "
-          f"frac {r['frac']:.3f} cpu {c and round(c['value'])}")
+          f"frac {r.get('frac', 0):.3f} cpu {c and round(c['value'])}")
 PY
 for pe in 128 1; do
   port=$((29500 + pe))
@@ -43,6 +44,10 @@ for pe in 128 1; do
     2> gpurun_out/rehearse_pe$pe.log || { tail -20 gpurun_out/rehearse_pe$pe.log; exit 1; }
   tail -1 gpurun_out/rehearse_pe$pe.json | python -c "import json,sys;d=json.loads(sys.stdin.read());print('rehearse pool_every', d['pooling']['pool_every'], round(d['value']/1e9,3), 'G/s', d['dist']['backend'], d['pooling']['received_GBps_per_rank'])"
 done
-bash tools/pmc.sh > gpurun_out/pmc.log 2>&1 || { tail -20 gpurun_out/pmc.log; exit 1; }
-python -c "import json;d=json.load(open('gpurun_out/pmc_segment.json'));print('pmc', d['trace_avg_ns_per_step'], d['hbm_bytes_per_step'])"
+bash tools/ktrace.sh > gpurun_out/kt_final.txt 2>&1 || { tail -20 gpurun_out/kt_final.txt; exit 1; }
+cat gpurun_out/kt_final.txt
+if [ -n "$RUN_PMC" ]; then
+  bash tools/pmc.sh > gpurun_out/pmc.log 2>&1 || { tail -20 gpurun_out/pmc.log; exit 1; }
+  python -c "import json;d=json.load(open('gpurun_out/pmc_segment.json'));print('pmc', d['trace_avg_ns_per_step'], d['hbm_bytes_per_step'])"
+fi
 echo final_check done
