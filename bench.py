@@ -957,8 +957,11 @@ def bench_closed_loop(args, rank, world, dev):
     handing off per owner wave through device flags (sacenv.closed_loop.ClosedLoop): the
     env as persistent sacenv_boat_segment launches, the policy as one launch per step
     on a second stream, no host synchronisation between steps; the slot refill after
-    each 128-step segment. The policy's noise comes from two pre-drawn [128, N] normal
-    tables (the reference draws it inside choose_action)."""
+    each 128-step segment. Timed beside it: the same loop as main.py orders it
+    (ClosedLoop.run_eager: choose_action then one step launch, one stream), which wins
+    when the policy dominates the step; ``value`` is the faster form, ``modes`` both.
+    The policy's noise comes from two pre-drawn [128, N] normal tables (the reference
+    draws it inside choose_action)."""
     from sacenv import VecBoatEnv
     from sacenv.closed_loop import ClosedLoop
     from sacenv.sac_native import NativeSAC
@@ -974,31 +977,38 @@ def bench_closed_loop(args, rank, world, dev):
     eps = torch.randn((2, SEG, N), generator=g, device=dev)
     state = {"i": 0}
 
-    def segment():
-        loop.run(eps[state["i"] % 2])
+    def segment(mode):
+        e = eps[state["i"] % 2]
+        loop.run(e) if mode == "handoff" else loop.run_eager(e)
         env.refill()
         state["i"] += 1
 
-    for _ in range(segs(args.warmup)):
-        segment()
-    _sync(dev)
-    loop.check()
-    barrier(world)
     n_timed = timed_segs(args.steps)
-    t0 = time.perf_counter()
-    for _ in range(n_timed):
-        segment()
-    _sync(dev)
-    barrier(world)
-    el = time.perf_counter() - t0
-    loop.check()
     steps = n_timed * SEG
-    el_max = el
-    if world > 1:
-        import torch.distributed as dist
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el_max = float(t.item())
+    rates = {}
+    # both forms of the loop (the same results, bit for bit: tests/test_segment_gpu.py),
+    # each warmed up and timed over the same number of segments
+    for mode in ("handoff", "eager"):
+        for _ in range(segs(args.warmup)):
+            segment(mode)
+        _sync(dev)
+        loop.check()
+        barrier(world)
+        t0 = time.perf_counter()
+        for _ in range(n_timed):
+            segment(mode)
+        _sync(dev)
+        barrier(world)
+        el = time.perf_counter() - t0
+        loop.check()
+        if world > 1:
+            import torch.distributed as dist
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        rates[mode] = {"value": world * N * steps / el, "unit": "env-steps/s", "ms_per_step": el / steps * 1e3}
+    best = max(rates, key=lambda m: rates[m]["value"])
+    el_max = rates[best]["ms_per_step"] * steps / 1e3
     # the policy alone (sacenv_sac_act on the env's obs, one launch per step) for the split
     ea, eb = _Clock(dev), _Clock(dev)
     st = torch.cuda.current_stream(dev)
@@ -1025,11 +1035,16 @@ def bench_closed_loop(args, rank, world, dev):
                                "episodes, in-kernel auto-reset; policy: NativeSAC choose_action (256-256 actor, "
                                "tanh-squashed Normal) per step",
                    "envs_per_gpu": N, "parallelism": f"env-dp{world}",
-                   "launch": "one persistent sacenv_boat_segment launch per 128 steps (act_ready / step_done "
-                             "flags per owner wave) + one sacenv_sac_act_handoff launch per step on a second "
-                             "stream + the 3 refill launches per segment",
+                   "launch": {"handoff": "one persistent sacenv_boat_segment launch per 128 steps "
+                                         "(act_ready / step_done flags per owner wave) + one "
+                                         "sacenv_sac_act_handoff launch per step on a second stream + the 3 "
+                                         "refill launches per segment",
+                              "eager": "per step one sacenv_sac_act launch then one sacenv_boat_step launch "
+                                       "(main.py:78-81's order, one stream) + the 3 refill launches per segment"},
+                   "value_mode": best,
                    "co_residency": {k: getattr(loop.plan, k) for k in ("seg_vgprs", "act_vgprs", "act_lds",
                                                                        "owner_waves_per_simd", "max_envs")}},
+        "modes": rates,
         "policy_alone_us_per_step": act_us,
         "cpu_baseline": None}
 

@@ -171,6 +171,34 @@ def test_closed_loop_equals_eager_loop(N, K, segs, gpu, built_lib):
     assert int(loop.step_done.min()) == segs * K and int(loop.act_ready.max()) == segs * K
 
 
+def test_closed_loop_run_eager_equals_run(gpu, built_lib):
+    """``ClosedLoop.run_eager`` (choose_action then one step launch per step, one
+    stream: the form bench.py --closed-loop reports when the policy dominates) and
+    the hand-off ``run`` give the same arena, bit for bit."""
+    from sacenv import VecBoatEnv
+    from sacenv.closed_loop import ClosedLoop
+    from sacenv.sac_native import NativeSAC
+    N, K, segs = 8192, 64, 2
+    cfg = {"base_settings": {"experiment": 6, "test_mode": 0}}
+    kw = dict(seed=9, device=gpu, max_episode_steps=50, n_helpers=256, auto_refill=False)
+    a_env, b_env = VecBoatEnv(cfg, N, **kw), VecBoatEnv(cfg, N, **kw)
+    a_env.reset()
+    b_env.reset()
+    agent = NativeSAC(gpu, init_seed=4, with_memory=False)
+    la, lb = ClosedLoop(a_env, agent, segment=K), ClosedLoop(b_env, agent, segment=K)
+    g = torch.Generator(device=gpu)
+    g.manual_seed(2)
+    eps = torch.randn((segs, K, N), generator=g, device=gpu)
+    for s in range(segs):
+        la.run(eps[s])
+        lb.run_eager(eps[s])
+        a_env.refill()
+        b_env.refill()
+        torch.cuda.synchronize()
+        assert torch.equal(a_env.arena, b_env.arena), s
+    la.check()
+
+
 def test_segment_handoff_timeout_sets_status(gpu, built_lib):
     """A row whose flag never comes: the launch gives up after ~seconds of polling,
     flags SACENV_STATUS_HANDOFF_TIMEOUT and returns (no hang)."""
