@@ -10,10 +10,10 @@ action and terminal obs -- for a shared replay buffer over RCCL).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
-Timing. Steps run in whole 128-step segments: each segment is one hipGraph of
-128 step launches followed by the slot refill (k_need_masks + k_refill +
+Timing. Steps run in whole 256-step segments: each segment is one hipGraph of
+256 step launches followed by the slot refill (k_need_masks + k_refill +
 k_refill_fit: the RNG draws and spline fits of the episodes that replace the
-ended ones), which the engine needs at least every 128 steps. W and K are
+ended ones), which the engine needs at least every 256 steps. W and K are
 rounded UP to whole segments (at least one each), so the timed region always
 starts on a segment boundary and always holds its share of refills; the JSON
 ``steps`` / ``warmup`` are the step counts actually executed (the requested
@@ -25,7 +25,7 @@ per-step duration from HIP events on the kernel's stream (refills excluded;
 they are in ``ms_per_step``). ``--launch step``: SURVEY.md §8(d)'s 222 B per
 boat env-step (state read and written every step). ``--launch segment`` (the
 default): the same components with the state resident in registers for the
-128-step launch, 70 B per step + 152 B per launch (SURVEY's 222-B equivalent
+256-step launch, 70 B per step + 152 B per launch (SURVEY's 222-B equivalent
 rate is reported beside it). ``traffic`` = HBM bytes per step from the
 committed rocprofv3 PMC passes (tools/pmc.sh).
 
@@ -50,14 +50,14 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "sac-agent_amd"))
 
 BYTES_PER_ENV_STEP = 222      # state r+w 152, action 4, wind 16, obs 44, reward 4, done+term 2
-SEG_MIN_BYTES = 70 + 152 / 128  # the same with the state in registers for a 128-step persistent launch
+SEG_MIN_BYTES = 70 + 152 / 256  # the same with the state in registers for a 256-step persistent launch
 TOY_BYTES = {"parachute": 86, "car": 102}
 # the toys in the persistent mixed launch: obs 8 + reward 4 + done/term 2 per step, state r+w once
-TOY_SEG_BYTES = {"parachute": 14 + 72 / 128, "car": 14 + 88 / 128}
+TOY_SEG_BYTES = {"parachute": 14 + 72 / 256, "car": 14 + 88 / 256}
 HBM_PEAK = 8.0e12             # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 EPISODE_STEPS = 500
-SEG = 128              # step launches per refill (sacenv _lib.REFILL_PERIOD); one graph per segment
-ACTION_STEPS = 512     # the pre-generated action table cycles every 512 steps (4 segments)
+SEG = 256              # step launches per refill (sacenv _lib.REFILL_PERIOD); one graph per segment
+ACTION_STEPS = 512     # the pre-generated action table cycles every 512 steps (2 segments)
 TRANS_ROW = ("45-B/env transition row (s' entries 0..8 f32, reward, action, term; rudder, fuel and "
              "done rebuilt by the receiver)")
 
@@ -82,9 +82,9 @@ def parse(argv=None):
     ap.add_argument("--experiment", type=int, default=6)
     ap.add_argument("--no-graph", action="store_true", help="eager per-step launches (--launch step)")
     ap.add_argument("--launch", choices=("segment", "step"), default="segment",
-                    help="segment: one persistent sacenv_boat_segment launch per 128 steps (state in "
+                    help="segment: one persistent sacenv_boat_segment launch per 256 steps (state in "
                          "registers, actions behind per-wave flags); step: one k_step launch per step, "
-                         "128 of them per hipGraph replay")
+                         "256 of them per hipGraph replay")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="total CPU-baseline budget (4 C1 legs + the vectorised port)")
@@ -99,14 +99,14 @@ def parse(argv=None):
     ap.add_argument("--rollout", type=int, default=0,
                     help="K > 0: open-loop K-step rollouts (sacenv_boat_rollout), a separate line")
     ap.add_argument("--pooling", choices=("gather", "none"), default="gather",
-                    help="N>1: all-gather the full transitions per 128-step segment (configs[3]), "
+                    help="N>1: all-gather the full transitions per 256-step segment (configs[3]), "
                          "or none (sharded per-GPU replay, SURVEY.md §8(e)'s alternative)")
     ap.add_argument("--refill-overlap", type=int, default=0, choices=(0, 1),
                     help="--launch segment: two 64-step launches per segment, each refill on a side "
                          "stream concurrent with the next launch (1), or the refill between launches (0)")
     ap.add_argument("--pool-every", type=int, default=SEG,
                     help="N>1 gather pooling: steps per all-gather (1 = one all-gather per step, "
-                         "SURVEY.md §8(e); 128 = one per segment, overlapped with the next)")
+                         "SURVEY.md §8(e); 256 = one per segment, overlapped with the next)")
     ap.add_argument("--event-every", type=int, default=4,
                     help="time every E-th timed segment's launch (the first always) with HIP events "
                          "for roofline.kernel_avg_us: each pair puts a stream marker on both sides of "
@@ -122,7 +122,10 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
-MIN_TIMED_SEGS = 8   # the timed region holds at least 1 024 steps
+MIN_TIMED_SEGS = 8   # the timed region holds at least 2 048 steps
+MIN_WARMUP_SEGS = 2  # and at least 512 warm-up steps: the driver's --steps 20 --warmup 5 then
+                     # times the default line's region (the episode-length transient of the
+                     # first ~1 000 steps -- every env starts at step 0 -- is behind it)
 
 
 def segs(n_steps: int) -> int:
@@ -130,10 +133,15 @@ def segs(n_steps: int) -> int:
     return max(1, -(-int(n_steps) // SEG))
 
 
+def warm_segs(n_steps: int) -> int:
+    """Warm-up segments for --warmup n: whole segments, at least MIN_WARMUP_SEGS."""
+    return max(MIN_WARMUP_SEGS, segs(n_steps))
+
+
 def timed_segs(n_steps: int) -> int:
     """Timed segments for --steps n: whole segments, at least MIN_TIMED_SEGS. A single
-    128-step segment is a ~0.25-ms region in which the first launch's submission after an
-    idle stream and the closing synchronize (~44 us) were 13 % of the time."""
+    128-step segment (round 3) was a ~0.25-ms region in which the first launch's submission
+    after an idle stream and the closing synchronize (~44 us) were 13 % of the time."""
     return max(MIN_TIMED_SEGS, segs(n_steps))
 
 
@@ -288,7 +296,7 @@ def load_traffic(n_envs: int, experiment: int, launch: str = "step"):
             continue
         key = "hbm_bytes_per_step" if launch == "segment" else "hbm_bytes_per_launch"
         if int(d.get("envs", -1)) == n_envs and int(d.get("experiment", 6)) == experiment and key in d:
-            # per step of all envs (a k_step launch; 1/128 of a persistent launch)
+            # per step of all envs (a k_step launch; 1/SEG of a persistent launch)
             return {"hbm_bytes_per_launch": float(d[key]), "source": os.path.relpath(path, ROOT)}
     return None
 
@@ -671,7 +679,7 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
     st = run.st
     seg_events = run.seg_events
     segment = run.segment
-    n_warm, n_timed = segs(args.warmup), timed_segs(args.steps)
+    n_warm, n_timed = warm_segs(args.warmup), timed_segs(args.steps)
     k = 0
     for _ in range(n_warm):
         k = segment(k, False)
@@ -705,7 +713,7 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
         el_max = float(t.item())
 
     # k_step average launch duration from events on the stream the kernel runs on,
-    # around 128-launch graph segments (refills excluded). N=1: the segments of
+    # around 256-launch graph segments (refills excluded). N=1: the segments of
     # the timed region itself. N>1 (the segments also stage the pooled rows) or
     # eager: k_step-only segments replayed after the timed region.
     what = ("persistent sacenv_boat_segment launches" if run.mode == "segment" else
@@ -764,7 +772,7 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
     seg_mode = run.mode == "segment"
     # the persistent launch keeps the carried state (152 of SURVEY §8(d)'s 222 B) in
     # registers between its steps: its algorithmic bytes are the same components
-    # with the state read and written once per 128-step launch
+    # with the state read and written once per 256-step launch
     N = wl.envs[0].num_envs
     algo_step = SEG_MIN_BYTES * N if seg_mode else wl.bytes_per_launch
     if seg_mode and args.mixed:  # + the toys with their state resident: record 14 B per step
@@ -785,7 +793,7 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
         "warmup": n_warm * SEG,
         "requested": {"steps": args.steps, "warmup": args.warmup,
                       "rule": f"rounded up to whole {SEG}-step segments (each ends with its refill); "
-                              f"at least {MIN_TIMED_SEGS * SEG} timed steps"},
+                              f"at least {MIN_TIMED_SEGS * SEG} timed and {MIN_WARMUP_SEGS * SEG} warm-up steps"},
         "setup": {"graph_first_replays": run.first_replays,
                   "note": "steps of the first pass over the action table (a captured graph's first "
                           "replay carries its device upload), run before the warm-up, untimed"},
@@ -838,9 +846,9 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
                                  else None),
                      "unit": "GB/s", "frac": achieved / HBM_PEAK,
                      "traffic": None if traffic is None else traffic["hbm_bytes_per_launch"],
-                     "kernel": ("k_rollout_mixed (sacenv_mixed_segment, 128 steps per launch; per step below)"
+                     "kernel": ("k_rollout_mixed (sacenv_mixed_segment, 256 steps per launch; per step below)"
                                 if seg_mode and args.mixed else
-                                "k_rollout (sacenv_boat_segment, 128 steps per launch; per step below)"
+                                "k_rollout (sacenv_boat_segment, 256 steps per launch; per step below)"
                                 if seg_mode else "k_step<true> (mixed)" if args.mixed else "k_step"),
                      "bytes_per_step": algo_step,
                      "bytes_per_env_step": (dict(boat=SEG_MIN_BYTES, **TOY_SEG_BYTES) if seg_mode and args.mixed
@@ -854,7 +862,7 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
                      "algorithmic_bytes": (
                          "SURVEY §8(d)'s per-step components with the state resident: action 4 + wind "
                          "sample 16 + obs 44 + reward 4 + done/term 2 per env-step, state r+w 152 once "
-                         "per 128-step launch" if seg_mode else "SURVEY §8(d): 222 B per boat env-step"),
+                         "per 256-step launch" if seg_mode else "SURVEY §8(d): 222 B per boat env-step"),
                      # SURVEY §8(d)'s per-step contract (the state re-read and re-written every
                      # step, as a step launch must): the equivalent rate of the persistent launch
                      "survey_222B": None if not seg_mode else {
@@ -884,11 +892,11 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
 
 
 # ---------------------------------------------------------------- every-output rate
-def every_output_rate(wl: Workload, dev, n_segs: int = 8, k0: int = 0) -> dict | None:
-    """The same engine with EVERY step's outputs landing in HBM: K = 128-step
+def every_output_rate(wl: Workload, dev, n_segs: int = 4, k0: int = 0) -> dict | None:
+    """The same engine with EVERY step's outputs landing in HBM: K = SEG-step
     sacenv_boat_rollout launches writing each step's 50-B record (obs, reward, done,
     term) and terminal obs to their own rows (the persistent segment rewrites one
-    record in place, so 127 of 128 steps' rows never leave L2), each followed by the
+    record in place, so all but the last step's rows stay in L2), each followed by the
     refill; wall-timed between synchronizes."""
     if dev.type != "cuda":
         return None
@@ -911,7 +919,7 @@ def every_output_rate(wl: Workload, dev, n_segs: int = 8, k0: int = 0) -> dict |
     steps = n_segs * SEG
     return {"value": env.num_envs * steps / el, "unit": "env-steps/s", "steps": steps,
             "ms_per_step": el / steps * 1e3,
-            "note": "sacenv_boat_rollout, 128 steps per launch, every step's record and terminal obs "
+            "note": f"sacenv_boat_rollout, {SEG} steps per launch, every step's record and terminal obs "
                     "written to its own rows, + the refill per launch; after the timed region, wall time"}
 
 
@@ -923,8 +931,8 @@ SHARD_WORDS = 2 * 11 + 1 + 2 + 1   # state, new_state (f32 x 11 each), action, r
 def sharded_exchange(world: int, dev, seg_s: float, n_envs: int) -> dict:
     """The exact lighter exchange: ShardedReplayBuffer keeps each
     rank's transitions on its GPU and assembles every sampled batch with one SUM all-reduce;
-    sample_many batches one segment's 128 learn() batches into ONE all-reduce of
-    128 x 1024 x 26 words (13.6 MB). Timed here on the run's own backend (RCCL on the node),
+    sample_many batches one segment's 256 learn() batches into ONE all-reduce of
+    256 x 1024 x 26 words (27.3 MB). Timed here on the run's own backend (RCCL on the node),
     then charged in series to the measured no-exchange segment time."""
     import torch.distributed as dist
     n = SEG * SHARD_BATCH * SHARD_WORDS
@@ -944,7 +952,7 @@ def sharded_exchange(world: int, dev, seg_s: float, n_envs: int) -> dict:
     return {"value": world * n_envs * SEG / (seg_s + el), "unit": "env-steps/s",
             "allreduce_ms_per_segment": el * 1e3, "bytes_per_segment": words.numel() * 4,
             "segment_ms_no_exchange": seg_s * 1e3,
-            "note": "the no-exchange segment time + one SUM all-reduce of the segment's 128 learn() batches "
+            "note": "the no-exchange segment time + one SUM all-reduce of the segment's 256 learn() batches "
                     "(ShardedReplayBuffer.sample_many: the pooled buffer's batches bit for bit, "
                     "tests/test_sharded_replay_gpu.py), in series (not overlapped), max over ranks"}
 
@@ -957,10 +965,10 @@ def bench_closed_loop(args, rank, world, dev):
     handing off per owner wave through device flags (sacenv.closed_loop.ClosedLoop): the
     env as persistent sacenv_boat_segment launches, the policy as one launch per step
     on a second stream, no host synchronisation between steps; the slot refill after
-    each 128-step segment. Timed beside it: the same loop as main.py orders it
+    each 256-step segment. Timed beside it: the same loop as main.py orders it
     (ClosedLoop.run_eager: choose_action then one step launch, one stream), which wins
     when the policy dominates the step; ``value`` is the faster form, ``modes`` both.
-    The policy's noise comes from two pre-drawn [128, N] normal tables (the reference
+    The policy's noise comes from two pre-drawn [256, N] normal tables (the reference
     draws it inside choose_action)."""
     from sacenv import VecBoatEnv
     from sacenv.closed_loop import ClosedLoop
@@ -989,7 +997,7 @@ def bench_closed_loop(args, rank, world, dev):
     # both forms of the loop (the same results, bit for bit: tests/test_segment_gpu.py),
     # each warmed up and timed over the same number of segments
     for mode in ("handoff", "eager"):
-        for _ in range(segs(args.warmup)):
+        for _ in range(warm_segs(args.warmup)):
             segment(mode)
         _sync(dev)
         loop.check()
@@ -1027,7 +1035,7 @@ def bench_closed_loop(args, rank, world, dev):
         "metric": f"env-steps/sec (whole node), boat_env exp-{args.experiment} closed loop (SAC actor + env "
                   f"step per step, device hand-off), {N:,} envs/GPU".replace(",", " "),
         "value": world * N * steps / el_max, "unit": "env-steps/s", "n_gpus": world, "steps": steps,
-        "warmup": segs(args.warmup) * SEG, "ms_per_step": el_max / steps * 1e3, "higher_is_better": True,
+        "warmup": warm_segs(args.warmup) * SEG, "ms_per_step": el_max / steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f64 env, f32 policy",
         "data": "synthetic: random-init actor (torch.manual_seed), N(0,1) policy noise tables, per-env MT19937 "
                 "wind/start draws",
@@ -1035,7 +1043,7 @@ def bench_closed_loop(args, rank, world, dev):
                                "episodes, in-kernel auto-reset; policy: NativeSAC choose_action (256-256 actor, "
                                "tanh-squashed Normal) per step",
                    "envs_per_gpu": N, "parallelism": f"env-dp{world}",
-                   "launch": {"handoff": "one persistent sacenv_boat_segment launch per 128 steps "
+                   "launch": {"handoff": "one persistent sacenv_boat_segment launch per 256 steps "
                                          "(act_ready / step_done flags per owner wave) + one "
                                          "sacenv_sac_act_handoff launch per step on a second stream + the 3 "
                                          "refill launches per segment",
@@ -1077,7 +1085,7 @@ def bench_rollout(args, wl: Workload, rank, world, dev):
             env.refill()
         return k
 
-    k = run(segs(args.warmup), 0)
+    k = run(warm_segs(args.warmup), 0)
     _sync(dev)
     barrier(world)
     n_timed = segs(args.steps)
@@ -1101,7 +1109,7 @@ def bench_rollout(args, wl: Workload, rank, world, dev):
         "metric": f"env-steps/sec (whole node), boat_env exp-{args.experiment} open-loop K-step rollout, "
                   f"{N} envs/GPU",
         "value": world * N * steps / el_max, "unit": "env-steps/s", "n_gpus": world,
-        "steps": steps, "warmup": segs(args.warmup) * SEG, "ms_per_step": el_max / steps * 1e3,
+        "steps": steps, "warmup": warm_segs(args.warmup) * SEG, "ms_per_step": el_max / steps * 1e3,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic: U(-1,1) f32 actions, per-env MT19937 wind/start draws",
         "config": {"workload": f"boat_env exp {args.experiment}, {N} envs/GPU, open-loop actions, "

@@ -40,8 +40,8 @@ extern "C" {
 #define SACENV_MT_N 624        /* MT19937 words per env (numpy legacy RNG) */
 #define SACENV_MAX_KNOTS 16    /* wind.fixed_points upper bound */
 #define SACENV_N_COUNTERS 5    /* info-dict termination counters, boat_env.py:24-32 */
-#define SACENV_SLOTS 129       /* episode slots per env in autoreset mode (active + 128 ahead) */
-#define SACENV_REFILL_PERIOD 128 /* autoreset: at most this many step launches between refills */
+#define SACENV_SLOTS 257       /* episode slots per env in autoreset mode (active + 256 ahead) */
+#define SACENV_REFILL_PERIOD 256 /* autoreset: at most this many step launches between refills */
 #define SACENV_RECORD_BYTES 50 /* packed per-env step record (see layout.record) */
 #define SACENV_TRANS_OBS 9      /* s' entries in the transition row (obs 0..8) */
 #define SACENV_TRANS_BYTES 45   /* per-env transition row of sacenv_boat_step_pooled */

@@ -3,11 +3,11 @@
 // The step launch (k_step) runs owner waves only: one lane per env, 64
 // consecutive envs per wave, BoatEnv.step (boat_env.py:67-115) on float64
 // SoA state. In autoreset mode an env that ends (terminated or truncated)
-// starts its next episode at once from a PRE-DRAWN slot (SLOTS = 129 per env:
-// the active episode + 128 ahead), so no RNG or spline work ever sits on the
+// starts its next episode at once from a PRE-DRAWN slot (SLOTS = 257 per env:
+// the active episode + 256 ahead), so no RNG or spline work ever sits on the
 // step's path, and the step keeps no refill bookkeeping beyond the episode
 // counter `cons`.
-// The refill launches (at least every 128 steps): k_need_masks marks the envs
+// The refill launches (at least every 256 steps): k_need_masks marks the envs
 // whose ring is short (fill < cons + SLOTS); k_refill ranks them from those
 // masks (DPP scans, no atomics) and, one wave per env, draws
 // the replacement episodes from the env's own numpy-legacy MT19937 stream
@@ -1051,7 +1051,7 @@ __global__ void __launch_bounds__(kWave) k_draw(SacenvBoatParams p, Arena A, Tai
     } else if (mode == 0) {
       // the first episode here; sacenv_boat_init's refill draws the next SLOTS-1 in
       // the env's order (all envs in parallel, the fits spread over lane groups:
-      // seconds faster at 65 536 envs than 129 serial draw-and-fits per wave)
+      // seconds faster at 65 536 envs than SLOTS serial draw-and-fits per wave)
       start_y = draw_episode_wave(p, A, lds, e, 0, lane, nullptr, nullptr);
       if (lane == 0) {
         A.i32(U_CONS)[e] = 0;

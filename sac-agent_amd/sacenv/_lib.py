@@ -19,8 +19,8 @@ OBS_DIM = 11
 MT_N = 624
 MAX_KNOTS = 16
 N_COUNTERS = 5
-SLOTS = 129
-REFILL_PERIOD = 128  # autoreset: step launches allowed between sacenv_boat_refill calls
+SLOTS = 257
+REFILL_PERIOD = 256  # autoreset: step launches allowed between sacenv_boat_refill calls
 STATUS_SLOT_UNDERFLOW = 1
 STATUS_HANDOFF_TIMEOUT = 2
 STATUS_LIST_TIMEOUT = 4

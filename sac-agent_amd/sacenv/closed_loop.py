@@ -2,7 +2,7 @@
 device-side pipelines handing off through per-owner-wave flags.
 
 The env runs as persistent segment launches (``VecBoatEnv.segment_async``,
-``sacenv_boat_segment``: up to 128 steps per launch, the carried state in
+``sacenv_boat_segment``: up to 256 steps per launch, the carried state in
 registers), the policy as ``NativeSAC.choose_action_handoff`` launches on a second
 stream. For owner wave w (64 envs) and sequence number q:
 

@@ -203,7 +203,7 @@ class SegmentPool:
     (``step_records`` slices it back per step). Two staging buffers alternate;
     ``begin`` makes the stepping stream wait for the gather that last used the
     buffer about to be refilled. Fewer, larger collectives than one per step:
-    at 65 536 envs a segment of 128 steps is 420 MB per rank.
+    at 65 536 envs a segment of 256 steps is 840 MB per rank.
     """
 
     def __init__(self, record_bytes: int, seg: int, device, group=None, n_buffers: int = 2):

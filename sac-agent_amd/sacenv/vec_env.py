@@ -38,7 +38,7 @@ class VecBoatEnv:
     autoreset : start the next episode inside ``step`` for envs that end
         (gym vector-env semantics: the returned obs row is the new episode's
         first obs, the terminal obs is ``info['final_obs']``). Episodes are
-        pre-drawn up to 128 ahead per env (``_lib.SLOTS``), from the env's own
+        pre-drawn up to 256 ahead per env (``_lib.SLOTS``), from the env's own
         RNG stream in the reference's order, so draws match the reference
         exactly; a refill launch tops the slots up (see ``refill``).
     env_id_offset : global id of this rank's first env (multi-GPU sharding).

@@ -65,11 +65,11 @@ def _run(rank, world, argv):
 
 def test_driver_command_world1_rounds_to_whole_segments():
     out, env = _run(0, 1, ["--gpus", "1", "--steps", "20", "--warmup", "5"])
-    assert out["steps"] == 8 * 128 and out["warmup"] == 128   # at least 8 timed segments
+    assert out["steps"] == 8 * 256 and out["warmup"] == 512   # at least 8 timed, 2 warm-up segments
     assert out["requested"] == {"steps": 20, "warmup": 5, "rule": out["requested"]["rule"]}
     # every segment ends with its refill; timed region = eight whole segments (+ k_step segs after)
-    assert all(s % 128 == 0 for s in env.refill_at), env.refill_at
-    assert env.refill_at[:2] == [128, 256]
+    assert all(s % 256 == 0 for s in env.refill_at), env.refill_at
+    assert env.refill_at[:2] == [256, 512]
     assert out["value"] > 0 and out["ms_per_step"] > 0
     assert out["roofline"]["frac"] > 0 and out["roofline"]["kernel_avg_us"] > 0
     assert out["metric"].startswith("env-steps/sec (whole node), boat_env exp-6, 65 536 envs/GPU")
@@ -84,12 +84,12 @@ def test_metric_follows_the_config():
     assert "mixed batch" in bench.metric_name(m) and "32 768" in bench.metric_name(m)
 
 
-@pytest.mark.parametrize("steps,warmup,n_timed", [(20, 5, 8), (300, 0, 8), (1100, 0, 9)])
+@pytest.mark.parametrize("steps,warmup,n_timed", [(20, 5, 8), (300, 0, 8), (2100, 0, 9)])
 def test_segment_rounding(steps, warmup, n_timed):
     out, env = _run(0, 1, ["--steps", str(steps), "--warmup", str(warmup), "--kernel-launches", "1"])
-    assert out["steps"] == n_timed * 128
+    assert out["steps"] == n_timed * 256
     # warmup segs + timed segs + 2 k_step-only segments (eager path), each with a refill
-    assert env.refills == out["warmup"] // 128 + n_timed + 2
+    assert env.refills == out["warmup"] // 256 + n_timed + 2
 
 
 def _free_port():
@@ -129,7 +129,7 @@ def test_driver_command_world2_gloo_segment_pooling():
         assert p.exitcode == 0
     out = res[0][1]
     assert res[1][1] is None
-    assert out["steps"] == 8 * 128 and out["n_gpus"] == 2
+    assert out["steps"] == 8 * 256 and out["n_gpus"] == 2
     assert out["value"] > 0
     assert "8 in the timed region" in out["config"]["collective"]
     assert "gloo" in out["config"]["collective"]
@@ -139,9 +139,9 @@ def test_driver_command_world2_gloo_segment_pooling():
     assert out["pooling"]["received_GBps_per_rank"] > 0
     # the no-exchange rate of the same segments, measured after the timed region
     ne = out["pooling"]["no_exchange"]
-    sh = ne["sharded_exchange"]     # one all-reduce of a segment's 128 learn() batches
-    assert sh["bytes_per_segment"] == 128 * 1024 * 26 * 4 and sh["allreduce_ms_per_segment"] > 0
+    sh = ne["sharded_exchange"]     # one all-reduce of a segment's 256 learn() batches
+    assert sh["bytes_per_segment"] == 256 * 1024 * 26 * 4 and sh["allreduce_ms_per_segment"] > 0
     assert 0 < sh["value"] < ne["value"] * 1.01
-    assert ne["value"] > 0 and ne["steps"] % 128 == 0 and ne["ms_per_step"] > 0
+    assert ne["value"] > 0 and ne["steps"] % 256 == 0 and ne["ms_per_step"] > 0
     for _, _, steps, refills in res:
-        assert steps % 128 == 0 and refills == steps // 128
+        assert steps % 256 == 0 and refills == steps // 256

@@ -26,7 +26,7 @@ def test_driver_bench_command():
     assert r.returncode == 0, r.stderr[-3000:]
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
     d = json.loads(line)
-    assert d["steps"] == 8 * 128 and d["warmup"] == 128 and d["n_gpus"] == 1   # >= 8 timed segments
+    assert d["steps"] == 8 * 256 and d["warmup"] == 512 and d["n_gpus"] == 1   # >= 8 timed, 2 warm-up segments
     assert d["value"] > 0 and d["unit"] == "env-steps/s"
     assert d["ms_per_step"] * d["steps"] * 1e-3 <= wall
     # every captured graph (4 action-table segments) ran once before the warm-up
@@ -34,7 +34,7 @@ def test_driver_bench_command():
     rf = d["roofline"]
     assert rf["bound"] == "hbm" and 0 < rf["frac"] < 1 and rf["kernel_avg_us"] > 0
     if rf["kernel"].startswith("k_rollout"):  # the persistent launch: resident-state bytes headline
-        assert abs(rf["bytes_per_env_step"] - (70 + 152 / 128)) < 1e-9
+        assert abs(rf["bytes_per_env_step"] - (70 + 152 / 256)) < 1e-9
         assert rf["survey_222B"]["bytes_per_env_step"] == 222
     # the timed step includes its refill: never faster than the kernel alone
     assert rf["step_us_incl_refill"] >= rf["kernel_avg_us"]
@@ -62,7 +62,7 @@ def test_bench_two_ranks_gloo_on_one_device():
                        capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
-    assert d["n_gpus"] == 2 and d["steps"] == 8 * 128 and d["value"] > 0
+    assert d["n_gpus"] == 2 and d["steps"] == 8 * 256 and d["value"] > 0
     assert d["config"]["global_envs"] == 2 * 8192
-    assert "gloo all_gather per 128-step segment (8 in the timed region)" in d["config"]["collective"]
+    assert "gloo all_gather per 256-step segment (8 in the timed region)" in d["config"]["collective"]
     assert "45-B/env transition row" in d["config"]["collective"]

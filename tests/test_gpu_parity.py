@@ -167,8 +167,8 @@ def test_spline_g_on_device(gpu, built_lib):
 
 def test_autoreset_every_step_one_step_episodes(gpu, built_lib):
     """|action| > 10.5 breaks the rudder on the first step: every env ends in every
-    launch, the worst case for the slot ring (128 episodes consumed between two
-    refills, then 128 drawn per env by one refill wave). Draws must stay exact."""
+    launch, the worst case for the slot ring (REFILL_PERIOD = 256 episodes consumed
+    between two refills, then 256 drawn per env by one refill). Draws must stay exact."""
     from sacenv import VecBoatEnv
     E, S = 70, 270
     seeds = np.arange(E, dtype=np.uint64) * 7 + 3
@@ -191,7 +191,7 @@ def test_autoreset_every_step_one_step_episodes(gpu, built_lib):
 
 
 @pytest.mark.parametrize("period", [1, 7, 32])
-def test_refill_schedule_any_period_up_to_128(period, gpu, built_lib):
+def test_refill_schedule_any_period_within_the_ring(period, gpu, built_lib):
     """Refills placed by hand (auto_refill off) every `period` steps, once doubled,
     give the same episodes as the oracle; a ring that runs dry sets the status bit."""
     from sacenv import VecBoatEnv, _lib

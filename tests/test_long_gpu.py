@@ -11,7 +11,7 @@ Three launch paths replay them, all through the C ABI:
 * ``sacenv_boat_step`` (``VecBoatEnv.step_async``), one launch per step, ended envs
   reset by the host (``sacenv_boat_reset``) as the reference's main loop does;
 * ``sacenv_boat_segment`` (the timed kernel), driven by bench.py's own
-  ``SegmentRunner`` -- one persistent 128-step launch plus the slot refill per
+  ``SegmentRunner`` -- one persistent 256-step launch plus the slot refill per
   segment, in-kernel auto-reset -- each step's pooled transition row (obs entries
   0..8 before any reset, reward, term) written by the launch itself;
 * the same segments with ``VecBoatEnv.segment_async`` and per-wave hand-off flags
@@ -34,7 +34,7 @@ pytestmark = pytest.mark.gpu
 STATE_TOL = 1e-5
 OBS_TOL = 1e-6
 CARRIED = ("s_x", "s_y", "s_r", "v_x", "v_y", "v_r", "rudder_angle", "index")
-SEG = 128
+SEG = 256   # bench.SEG: one persistent launch + the refill per 256 steps
 
 
 def _cfg_dict(z):
@@ -179,7 +179,7 @@ def _carried(env):
 @pytest.mark.parametrize("name", long_fixtures())
 def test_long_fixture_bench_segment_runner(name, gpu, built_lib):
     """bench.py's timed path: SegmentRunner in its default mode (one persistent
-    sacenv_boat_segment launch + the refill per 128 steps)."""
+    sacenv_boat_segment launch + the refill per 256 steps)."""
     import ctypes as C
 
     import bench
