@@ -1,7 +1,7 @@
 """Reduce tools/pmc.sh's rocprofv3 output to per-launch figures for the bench kernel.
 
 Mode "step": k_step, gpurun_out/pmc_k_step.json. Mode "segment": the persistent
-k_rollout of sacenv_boat_segment (128 steps per launch), gpurun_out/pmc_segment.json,
+k_rollout of sacenv_boat_segment (bench.SEG = 256 steps per launch), gpurun_out/pmc_segment.json,
 with the per-launch figures also divided into per-step ones. Either holds:
 * the kernel trace's mean duration;
 * per-launch counter means for the kernel and for the calibration kernels of
@@ -114,5 +114,5 @@ def main(out_dir):
 
 if __name__ == "__main__":
     if len(sys.argv) > 2 and sys.argv[2] == "segment":
-        KERNEL, STEPS_PER_LAUNCH = "k_rollout", 128
+        KERNEL, STEPS_PER_LAUNCH = "k_rollout", 256   # bench.SEG
     main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out")
