@@ -36,7 +36,7 @@ for f in ("driver", "default", "step", "c2", "c5", "rollout_k128", "131k", "clos
     print(f"{f:13s} {d['value']/1e9:7.3f} G/s {d['ms_per_step']*1e3:6.2f} us/step kernel {k:5.2f} us "
           f"frac {r.get('frac', 0):.3f} cpu {c and round(c['value'])}")
 PY
-for pe in 128 1; do
+for pe in 256 1; do
   port=$((29500 + pe))
   SACENV_BENCH_BACKEND=gloo SACENV_BENCH_ONE_DEVICE=1 timeout -k 10 300 python -m torch.distributed.run \
     --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port $port bench.py --gpus 2 \
