@@ -291,6 +291,9 @@ int sacenv_boat_segment(const SacenvBoatParams *p, void *arena, const float *act
  * workgroups per CU the segment launch's kernel can keep resident for these
  * params (with or without pooled rows), its grid (n_pad / 64 one-wave
  * workgroups), its VGPRs per lane as allocated and its LDS bytes per workgroup.
+ * It describes the kernel sacenv_boat_segment launches for these params: with
+ * more owner waves than the device has SIMDs that is the two-waves-per-SIMD
+ * instantiation (constants as literals, <= 256 VGPRs), else the one-wave form.
  * The hand-off only makes progress when every owner wave and every policy
  * workgroup it waits on can be resident at once; sacenv.ClosedLoop plans the
  * policy launches by per-SIMD VGPR and per-CU LDS accounting and refuses a
