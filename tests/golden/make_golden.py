@@ -565,6 +565,16 @@ def make_long():
              [prog_slalom, prog_slalom], np.array([5, 12345], np.uint64))
 
 
+def make_long_wind1():
+    """Round 4: the one-curve wind experiments on the same programs (exp 4: the
+    speed curve; exp 5: the rectified angle), default configs."""
+    base = {"experiment": 4, "test_mode": 0}
+    run_long("exp4", {"base_settings": dict(base)}, [lambda: prog_hold(0.9, 4500), prog_uturn],
+             np.array([7, 2**31 + 5], np.uint64))
+    run_long("exp5", {"base_settings": dict(base, experiment=5)},
+             [lambda: prog_hold(-0.9, 4500), lambda: prog_orbit(True)], np.array([9, 123456789], np.uint64))
+
+
 def sys_modules_box():
     import sys
     return sys.modules["gym.spaces"].Box
@@ -586,12 +596,17 @@ def main():
         return
     if sys.argv[1:] == ["long"]:
         make_long()
+        make_long_wind1()
+        return
+    if sys.argv[1:] == ["long_wind1"]:
+        make_long_wind1()
         return
     run_toys()
     run_replay()
     run_main_loop()
     run_sac_learn()
     make_long()
+    make_long_wind1()
     for exp in range(1, 7):
         run_seeded(f"exp{exp}_uniform", {"base_settings": {"experiment": exp, "test_mode": 0}},
                    400, "uniform", action_seed=100 + exp)
