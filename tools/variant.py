@@ -2,6 +2,7 @@
 
     python tools/variant.py name 'old text' 'new text' ['old2' 'new2' ...]
     python tools/variant.py name --src FILE     (a whole sacenv_boat.hip)
+    python tools/variant.py name --file sacenv_sac.hip 'old' 'new' ...   (another source)
 
 Copies the sources to a temp dir, applies the substitutions to sacenv_boat.hip
 (each must match exactly once), and builds sac-agent_amd/build/libsacenv_<name>.so.
@@ -21,7 +22,9 @@ import __graft_entry__ as g  # noqa: E402
 
 def main(argv):
     name, subs = argv[0], argv[1:]
-    src = None
+    src, target = None, "sacenv_boat.hip"
+    if subs[:1] == ["--file"]:   # the source the substitutions apply to (default sacenv_boat.hip)
+        target, subs = subs[1], subs[2:]
     if subs[:1] == ["--src"]:
         src, subs = subs[1], subs[2:]
     if len(subs) % 2:
@@ -29,7 +32,7 @@ def main(argv):
     with tempfile.TemporaryDirectory() as d:
         for f in g.SOURCES + ["mt19937.h"]:
             shutil.copy(os.path.join(g.CSRC, f), d)
-        p = os.path.join(d, "sacenv_boat.hip")
+        p = os.path.join(d, target)
         s = open(src or p).read()
         for a, b in zip(subs[::2], subs[1::2]):
             if s.count(a) != 1:
