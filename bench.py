@@ -58,8 +58,7 @@ HBM_PEAK = 8.0e12             # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 EPISODE_STEPS = 500
 SEG = 256              # step launches per refill (sacenv _lib.REFILL_PERIOD); one graph per segment
 ACTION_STEPS = 512     # the pre-generated action table cycles every 512 steps (2 segments)
-TRANS_ROW = ("45-B/env transition row (s' entries 0..8 f32, reward, action, term; rudder, fuel and "
-             "done rebuilt by the receiver)")
+TRANS_ROW = "53-B/env transition row (s' f32 x 11, reward, action, term; done = term != 0)"
 
 
 def metric_name(args) -> str:
@@ -98,9 +97,19 @@ def parse(argv=None):
                     help="diagnostic: no in-kernel auto-reset (ended envs keep stepping)")
     ap.add_argument("--rollout", type=int, default=0,
                     help="K > 0: open-loop K-step rollouts (sacenv_boat_rollout), a separate line")
-    ap.add_argument("--pooling", choices=("gather", "none"), default="gather",
-                    help="N>1: all-gather the full transitions per 256-step segment (configs[3]), "
-                         "or none (sharded per-GPU replay, SURVEY.md §8(e)'s alternative)")
+    ap.add_argument("--pooling", choices=("sharded", "gather", "none"), default="sharded",
+                    help="N>1: sharded = the pooled replay buffer sampled out of each rank's staged "
+                         "segments, one SUM all-reduce of the segment's learn() batches (StagedReplay; the "
+                         "all-gather rate is measured beside it); gather = all-gather every transition per "
+                         "256-step segment (configs[3]'s literal exchange); none = no exchange")
+    ap.add_argument("--replay-mem", type=int, default=1_000_000,
+                    help="pooled ReplayBuffer(max_size) (configs/original_config.yaml: 1 000 000)")
+    ap.add_argument("--replay-batch", type=int, default=1024, help="learn() batch (agent.batch_size: 1024)")
+    ap.add_argument("--exchange-segs", type=int, default=4,
+                    help="segments per side measurement after the timed region (the other exchanges)")
+    ap.add_argument("--stub", action="store_true",
+                    help="CPU control-flow rehearsal: a stub workload, no kernels (tools/bench_stub.py); "
+                         "the line says data: stub")
     ap.add_argument("--refill-overlap", type=int, default=0, choices=(0, 1),
                     help="--launch segment: two 64-step launches per segment, each refill on a side "
                          "stream concurrent with the next launch (1), or the refill between launches (0)")
@@ -146,24 +155,71 @@ def timed_segs(n_steps: int) -> int:
 
 
 # ---------------------------------------------------------------- distributed
-def init_dist(n_gpus: int):
+def init_dist(n_gpus: int, stub: bool = False):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != n_gpus:
-        raise SystemExit(f"--gpus {n_gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
-    if os.environ.get("SACENV_BENCH_ONE_DEVICE"):  # rehearsal of the N>1 path on a 1-GPU box
-        local = 0
-    torch.cuda.set_device(local)
+        raise SystemExit(f"--gpus {n_gpus} but WORLD_SIZE={world}")
+    if stub:
+        dev = torch.device("cpu")
+    else:
+        if os.environ.get("SACENV_BENCH_ONE_DEVICE"):  # rehearsal of the N>1 path on a 1-GPU box
+            local = 0
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = os.environ.get("SACENV_BENCH_BACKEND", "nccl")  # gloo: rehearsal on one GPU
+        backend = "gloo" if stub else os.environ.get("SACENV_BENCH_BACKEND", "nccl")  # gloo: rehearsal
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
-    return rank, world, torch.device("cuda", local)
+    return rank, world, dev
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """``--gpus N`` with no launcher (WORLD_SIZE unset): start N rank processes of this
+    script (RANK = LOCAL_RANK = r, WORLD_SIZE = N, a free 127.0.0.1 port) and wait for
+    them. The parent touches no GPU (nothing here initialises HIP), rank 0 prints the
+    line on the inherited stdout, and the exit status is the first failing rank's. A
+    rank that fails ends the others (their own PIDs), so a broken collective cannot
+    leave the rest waiting on it."""
+    env = dict(os.environ, WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    procs = []
+    for r in range(n):
+        e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=e))
+    rc = 0
+    live = list(procs)
+    while live:
+        time.sleep(0.2)
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:      # the others would wait on the failed rank's collectives
+                    q.terminate()
+    for p in procs:
+        try:
+            p.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            p.kill()
+    return rc if rc > 0 else (1 if rc else 0)
 
 
 XGMI_LINK_GBPS = 153.0  # the task brief's MI355X xGMI figure: 7 links x ~153 GB/s per GPU
@@ -332,6 +388,7 @@ def load_compute(n_envs: int, experiment: int, kernel_s: float):
                 "f64_valu_per_wave_step": (pw["INSTS_VALU_FMA_F64"] + pw["INSTS_VALU_MUL_F64"]
                                            + pw["INSTS_VALU_ADD_F64"]) / K,
                 "issue_floor_us_per_step": (valu + salu) * UBENCH_F64_FMA_CYC_1WAVE / 2.26e9 * 1e6,
+                "issue_floor_frac": (valu + salu) * UBENCH_F64_FMA_CYC_1WAVE / 2.26e9 / kernel_s,
                 "source": os.path.relpath(path, ROOT),
                 "note": "one owner wave per SIMD issues in order: ~5 shader cycles per f64 instruction at best "
                         "(8 for 64-bit moves/conversions, ~7 for SALU between VALU), so the step is bound by "
@@ -461,19 +518,22 @@ class SegmentRunner:
     after it (``SegmentPool``, on a side stream); P < SEG (e.g. 1, SURVEY.md §8(e)'s
     one all-gather per step) steps eagerly and gathers every P steps."""
 
-    def __init__(self, args, wl: Workload, dev, pool=None, pool_every: int = SEG):
+    def __init__(self, args, wl: Workload, dev, pool=None, pool_every: int = SEG, exchange=None):
         if SEG % pool_every:
             raise ValueError(f"--pool-every must divide {SEG}")
         self.args, self.wl, self.dev, self.pool = args, wl, dev, pool
+        self.exchange = exchange   # sacenv.dist.SegmentExchange (the staged replay's exchange)
         self.pool_every = int(pool_every)
         # launch mode: "segment" (one persistent launch per segment, or per P steps
         # when pooling every P), "graph" (SEG k_step launches per hipGraph replay),
         # "eager" (SEG k_step launches)
         # (the mixed batch: sacenv_mixed_segment; with pooled rows it steps per launch)
+        rows = pool is not None or exchange is not None
         want_seg = (getattr(args, "launch", "step") == "segment" and not args.no_graph
-                    and wl.segment_step is not None and (pool is None or wl.segment_pools))
+                    and wl.segment_step is not None and (not rows or wl.segment_pools))
         self.mode = ("segment" if want_seg and dev.type == "cuda" else
-                     "graph" if dev.type == "cuda" and not args.no_graph and (pool is None or pool_every == SEG)
+                     "graph" if (dev.type == "cuda" and not args.no_graph and exchange is None
+                                 and (pool is None or pool_every == SEG))
                      else "eager")
         self.use_graph = self.mode == "graph"
         # segment mode, refill overlap: launches of HALF steps; the refill after
@@ -531,6 +591,17 @@ class SegmentRunner:
     def _steps(self, k0: int, with_pool: bool, buf=None, on_step=None, timed: bool = False) -> None:
         """The SEG steps of one segment, enqueued (captured, eager or persistent)."""
         wl, p = self.wl, self.pool if with_pool else None
+        x = self.exchange if with_pool else None
+        if x is not None:   # the segment's rows go to the staged replay's buffer
+            rows, rb = x.rows(), wl.row_bytes()
+            if self.mode == "segment":
+                wl.segment_step(k0, SEG, trans=rows)
+                return
+            for j, k in enumerate(range(k0, k0 + SEG)):
+                wl.pooled_step(k, rows[j * rb:(j + 1) * rb])
+                if on_step is not None:
+                    on_step(k)
+            return
         if self.mode == "segment":
             if p is None and self.overlap:
                 for j0 in range(0, SEG, SEG // 2):
@@ -629,8 +700,23 @@ class SegmentRunner:
                     self.first_replays += SEG
         _sync(dev)
 
+    def finish(self) -> None:
+        """The stepping stream waits for everything a segment left in flight (the last
+        all-gathers / replay exchanges, overlapped refills)."""
+        if self.pool is not None:
+            self.pool.wait()
+        if self.exchange is not None:
+            self.exchange.wait()
+        self.drain_refills()
+
     def segment(self, k0: int, timed: bool = False, with_pool: bool = True, on_step=None) -> int:
-        """Steps k0 .. k0+SEG-1 (k0 % SEG == 0), then the refill, then the pooling."""
+        """Steps k0 .. k0+SEG-1 (k0 % SEG == 0), then the refill, then the pooling
+        (all-gather) or the replay exchange."""
+        x = self.exchange if with_pool else None
+        if x is not None:
+            if not x.started:  # the replay buffer starts here: s of its first row = the current obs
+                x.start(self.wl.envs[0].obs)
+            x.before()
         p = self.pool if with_pool else None
         if p is not None and self.pool_every == SEG:
             p.begin()
@@ -658,22 +744,91 @@ class SegmentRunner:
         if p is not None and self.pool_every == SEG:
             p.fill = SEG
             p.flush()
+        if x is not None:
+            x.after()
         return k0 + SEG
 
 
 # ---------------------------------------------------------------- timing loop
+def _max_over_ranks(x: float, world: int, dev) -> float:
+    if world <= 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def make_exchange(args, wl: Workload, rank: int, world: int, dev):
+    """The sharded pooling's replay exchange: a StagedReplay over this rank's envs (the
+    pooled ReplayBuffer(--replay-mem) of every rank's envs, one learn() of
+    --replay-batch per step) behind a SegmentExchange (its side stream)."""
+    from sacenv.dist import SegmentExchange
+    if args.stub:
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from bench_stub import StubSampler
+        sampler = StubSampler(wl.row_bytes(), SEG, args.replay_batch, world)
+    else:
+        from sacenv.replay import StagedReplay
+        env = wl.envs[0]
+        sampler = StagedReplay(env.num_envs, env.n_pad, args.experiment, env.first_obs_template(), rank=rank,
+                               world=world, mem_size=args.replay_mem, batch=args.replay_batch, seg=SEG, seed=0,
+                               device=dev)
+    return SegmentExchange(sampler, dev)
+
+
+def timed_rate(run: "SegmentRunner", k: int, n_segs: int, world: int, dev, wl: Workload):
+    """One warm segment, then n_segs segments of ``run`` wall-timed between barriers
+    (what they leave in flight included), max over ranks -> (rate dict, k, seconds)."""
+    k = run.segment(k, False)
+    run.finish()
+    _sync(dev)
+    barrier(world)
+    _sync(dev)
+    t0 = time.perf_counter()
+    for _ in range(n_segs):
+        k = run.segment(k, True)
+    run.finish()
+    _sync(dev)
+    barrier(world)
+    el = _max_over_ranks(time.perf_counter() - t0, world, dev)
+    steps = n_segs * SEG
+    return ({"value": world * wl.per_gpu_envs * steps / el, "unit": "env-steps/s", "steps": steps,
+             "ms_per_step": el / steps * 1e3}, k, el)
+
+
+def _xgmi(bytes_per_rank: float, seconds: float, links: int) -> dict:
+    """Bytes a rank moves per second over its point-to-point xGMI links."""
+    rate = bytes_per_rank / seconds / 1e9 if seconds > 0 else 0.0
+    per_link = rate / max(1, links)
+    return {"link_peak_GBps": XGMI_LINK_GBPS, "links_used": links, "GBps_per_rank": rate,
+            "per_link_GBps": per_link, "per_link_frac": per_link / XGMI_LINK_GBPS}
+
+
 def run_bench(args, rank: int, world: int, dev, wl: Workload):
-    """Warm up, time whole segments, measure k_step; rank 0 returns the JSON dict."""
-    pool = None
+    """Warm up, time whole segments, measure the kernel; rank 0 returns the JSON dict.
+
+    N>1 (``--pooling sharded``, the default): every segment's transition rows go into
+    the rank's StagedReplay buffer and the segment's learn() batches are exchanged
+    with ONE SUM all-reduce on a side stream, overlapped with the next segment --
+    inside the timed region. Beside it (after the timed region, same segments):
+    the all-gather of every transition (configs[3]'s literal exchange) and no
+    exchange at all. N=1: the replay path without a collective is measured the same
+    way (``replay_path``), so the per-GPU cost of the exchange is on the N=1 line."""
     pool_every = int(getattr(args, "pool_every", SEG))
-    if world > 1:
-        if args.pooling == "gather":
-            from sacenv.dist import SegmentPool
-            # each step's full transitions are written into row j of a [P][row]
-            # staging buffer (graph-captured with the steps when P = SEG); ONE
-            # all-gather per P steps pools them on a side stream
-            pool = SegmentPool(wl.row_bytes(), pool_every, dev)
-    run = SegmentRunner(args, wl, dev, pool, pool_every)
+    pooling = args.pooling if world > 1 else "none"
+    if pooling == "sharded" and (args.mixed or not wl.segment_pools):
+        pooling = "gather"   # the toys of the mixed batch have no staged replay: their rows are gathered
+    pool = exchange = None
+    if pooling == "gather":
+        from sacenv.dist import SegmentPool
+        # each step's full transitions are written into row j of a [P][row] staging
+        # buffer; ONE all-gather per P steps pools them on a side stream
+        pool = SegmentPool(wl.row_bytes(), pool_every, dev)
+    elif pooling == "sharded":
+        exchange = make_exchange(args, wl, rank, world, dev)
+        pool_every = SEG
+    run = SegmentRunner(args, wl, dev, pool, pool_every, exchange)
     use_graph = run.use_graph
     run.prepare()
     st = run.st
@@ -683,9 +838,7 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
     k = 0
     for _ in range(n_warm):
         k = segment(k, False)
-    run.drain_refills()
-    if pool is not None:
-        pool.wait()
+    run.finish()
     _sync(dev)
     barrier(world)
     _sync(dev)
@@ -694,32 +847,27 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
     t0 = time.perf_counter()
     ev0.record(st)
     g0 = pool.flushes if pool is not None else 0
+    x0 = exchange.exchanges if exchange is not None else 0
     for _ in range(n_timed):
         k = segment(k, True)
-    if pool is not None:
-        pool.wait()  # the last segment's transitions are pooled inside the timed region
-    run.drain_refills()  # the last refills are inside the timed region too
+    run.finish()  # the last segment's all-gather / exchange and the last refills are inside the timed region
     ev1.record(st)
     gathers_timed = (pool.flushes if pool is not None else 0) - g0
+    exchanges_timed = (exchange.exchanges if exchange is not None else 0) - x0
     _sync(dev)
     barrier(world)
     el = time.perf_counter() - t0
     steps = n_timed * SEG
-    el_max = el
-    if world > 1:
-        import torch.distributed as dist
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el_max = float(t.item())
+    el_max = _max_over_ranks(el, world, dev)
 
-    # k_step average launch duration from events on the stream the kernel runs on,
-    # around 256-launch graph segments (refills excluded). N=1: the segments of
-    # the timed region itself. N>1 (the segments also stage the pooled rows) or
-    # eager: k_step-only segments replayed after the timed region.
+    # the kernel's average launch duration from events on the stream it runs on,
+    # refills excluded. N=1: the launches of the timed region itself. N>1 (the
+    # segments also write the exchanged rows) or eager: launches after the timed
+    # region with no exchange.
     what = ("persistent sacenv_boat_segment launches" if run.mode == "segment" else
             f"graph-replayed {SEG}-launch k_step segments")
-    no_exchange = None
-    if pool is not None or run.mode == "eager":
+    no_exchange = all_gather = None
+    if pool is not None or exchange is not None or run.mode == "eager":
         if run.mode == "eager" and dev.type == "cuda" and not args.no_graph:
             run.capture_all(with_pool=False)
             run.mode, use_graph = "graph", True
@@ -728,7 +876,7 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
         run.timed_segments = 0  # (the event stride restarts: the first of these is timed)
         k = segment(k, False, with_pool=False)
         # (N>1) the same segments and refills with no exchange, wall-timed like the
-        # timed region: the sharded-replay rate (--pooling none), reported beside
+        # timed region: N x the one-GPU rate, reported beside
         n_ne = segs(args.kernel_launches)
         _sync(dev)
         barrier(world)
@@ -738,34 +886,49 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
             k = segment(k, True, with_pool=False)
         _sync(dev)
         barrier(world)
-        el_ne = time.perf_counter() - t_ne
-        if world > 1:
-            import torch.distributed as dist
-            t = torch.tensor([el_ne], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el_ne = float(t.item())
-        sharded = None
-        if world > 1:
-            sharded = sharded_exchange(world, dev, el_ne / n_ne, wl.per_gpu_envs)
+        el_ne = _max_over_ranks(time.perf_counter() - t_ne, world, dev)
         no_exchange = {"value": world * wl.per_gpu_envs * n_ne * SEG / el_ne, "steps": n_ne * SEG,
                        "ms_per_step": el_ne / (n_ne * SEG) * 1e3,
-                       "note": "the same persistent segments and refills after the timed region with no "
-                               "all_gather (each rank's transitions stay on its GPU: --pooling none, or "
-                               "ShardedReplayBuffer's B-row exchange per learn()), wall-timed between "
-                               "barriers, max over ranks",
-                       "sharded_exchange": sharded}
+                       "note": "the same persistent segments and refills after the timed region with no exchange "
+                               "(each rank's transitions stay on its GPU, nothing sampled), wall-timed between "
+                               "barriers, max over ranks"}
         kern_src = (f"events around {len(seg_events)} {what if dev.type == 'cuda' else 'eager'} after the "
-                    "timed region (no staging copy, no collective; refills between segments excluded)")
+                    "timed region (no rows, no collective; refills between segments excluded)")
+        if exchange is not None:
+            # beside it: configs[3]'s literal exchange, every transition all-gathered per segment
+            from sacenv.dist import SegmentPool
+            gpool = SegmentPool(wl.row_bytes(), SEG, dev)
+            grun = SegmentRunner(args, wl, dev, gpool, SEG)
+            if grun.mode == "graph":        # (no captured graphs for this side run)
+                grun.mode, grun.use_graph = "eager", False
+            rate, k, el_g = timed_rate(grun, k, max(1, args.exchange_segs), world, dev, wl)
+            recv = (world - 1) * wl.row_bytes() * rate["steps"]
+            all_gather = dict(rate, gathers=gpool.flushes - 1, row_bytes_per_rank_step=wl.row_bytes(),
+                              received_bytes_per_rank=recv, xgmi=_xgmi(recv, el_g, world - 1),
+                              note=f"each segment's {TRANS_ROW} of every rank all-gathered (one "
+                                   f"all_gather_into_tensor per {SEG}-step segment on a side stream, overlapped "
+                                   "with the next segment), after the timed region, wall-timed, max over ranks")
     else:
         kern_src = (f"HIP events around the {len(seg_events)} {what} of the timed region (refills "
                     "between segments excluded)")
     kern_s = sum(a.ms_to(b) for a, b, _ in seg_events) * 1e-3 / sum(n for _, _, n in seg_events)
     step_s = ev0.ms_to(ev1) * 1e-3 / steps
 
-    every = None
+    every = replay_path = None
     if (world == 1 and run.mode == "segment" and not args.mixed and not args.no_autoreset
             and not args.no_every_output):
         every = every_output_rate(wl, dev, k0=k)
+    if world == 1 and not args.mixed and not args.no_autoreset and not args.no_every_output and (
+            run.mode == "segment" or args.stub):
+        # the sharded pooling's replay path on one GPU (no collective): rows staged, the
+        # segment's learns sampled on a side stream overlapped with the next segment
+        xrun = SegmentRunner(args, wl, dev, None, SEG, make_exchange(args, wl, rank, 1, dev))
+        rate, k, _ = timed_rate(xrun, k, max(1, args.exchange_segs), world, dev, wl)
+        replay_path = dict(rate, note=(
+            f"the N>1 line's replay path at one GPU (--pooling sharded without the collective): each "
+            f"segment's {TRANS_ROW} staged by the segment launch, its {SEG} learn() batches of "
+            f"{args.replay_batch} sampled from the pooled ReplayBuffer({args.replay_mem}) on a side stream "
+            "overlapped with the next segment (StagedReplay), after the timed region, wall time"))
     dinfo = dist_info(world, dev)
     if rank != 0:
         return None
@@ -778,12 +941,51 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
     if seg_mode and args.mixed:  # + the toys with their state resident: record 14 B per step
         algo_step += sum(TOY_SEG_BYTES.values()) * N
     achieved = algo_step / kern_s
-    traffic = None if args.mixed else load_traffic(wl.envs[0].num_envs, args.experiment,
-                                                   "segment" if seg_mode else "step")
+    traffic = None if args.mixed or args.stub else load_traffic(N, args.experiment, "segment" if seg_mode else "step")
+    compute = load_compute(N, args.experiment, kern_s) if seg_mode and not args.mixed and not args.stub else None
+    if compute is not None and world > 1:
+        compute["note"] += f" (PMC from the one-GPU run in {compute['source']}, applied to this run's kernel time)"
     backend = None
     if world > 1:
         import torch.distributed as dist
         backend = "RCCL" if dist.get_backend() == "nccl" else dist.get_backend()
+    if exchange is not None:
+        payload = exchange.sampler.bytes_per_segment
+        collective = (f"{backend} SUM all_reduce of each {SEG}-step segment's {SEG} learn() batches ({args.replay_batch} "
+                      f"rows, {payload} B) sampled from the pooled ReplayBuffer({args.replay_mem}) of every rank's "
+                      f"envs out of each rank's staged {TRANS_ROW}s (sacenv.replay.StagedReplay, the pooled buffer's "
+                      f"batches bit for bit): one per segment on a side stream, overlapped with the next segment "
+                      f"({exchanges_timed} in the timed region)")
+    elif pool is not None:
+        collective = (f"all_gather of each step's full transitions (the {TRANS_ROW} written by the step kernel, "
+                      f"{wl.row_bytes()} B per rank-step): one {backend} all_gather per {pool_every}-step "
+                      + ("segment" if pool_every == SEG else "group") +
+                      f" ({gathers_timed} in the timed region) on a side stream"
+                      + (", overlapped with the next segment" if pool_every == SEG else ""))
+    else:
+        collective = "none: no exchange (--pooling none)" if world > 1 else None
+    pooling_out = None
+    if world > 1:
+        pooling_out = {"mode": pooling, "no_exchange": no_exchange}
+        if exchange is not None:
+            payload = exchange.sampler.bytes_per_segment
+            bus = 2 * (world - 1) / world * payload * exchanges_timed  # a ring all-reduce's bytes per rank
+            pooling_out.update({
+                "exchanges_timed": exchanges_timed, "bytes_per_segment": payload,
+                "staged_row_bytes_per_rank_step": wl.row_bytes(),
+                "allreduce_bus_bytes_per_rank": bus, "xgmi": _xgmi(bus, el_max, world - 1),
+                "all_gather": all_gather,
+                "note": "value = the timed region with this exchange; all_gather and no_exchange are the same "
+                        "segments with the other exchanges, after the timed region"})
+        elif pool is not None:
+            recv = (world - 1) * wl.row_bytes() * steps
+            pooling_out.update({
+                "pool_every": pool_every, "gathers_timed": gathers_timed,
+                "row_bytes_per_rank_step": wl.row_bytes(), "received_bytes_per_rank": recv,
+                "received_GBps_per_rank": recv / el_max / 1e9,
+                # each peer's rows arrive over its own point-to-point link
+                "xgmi": _xgmi(recv, el_max, world - 1),
+                "note": "the timed region ends when the last all_gather has landed"})
     return {
         "metric": metric_name(args),
         "value": world * wl.per_gpu_envs * steps / el_max,
@@ -802,22 +1004,17 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic: U(-1,1) f32 actions, per-env MT19937 wind/start draws (seeds = global env id)",
+        "data": ("stub: CPU control-flow rehearsal, no kernels (tools/bench_stub.py)" if args.stub else
+                 "synthetic: U(-1,1) f32 actions, per-env MT19937 wind/start draws (seeds = global env id)"),
         "config": {"workload": (f"mixed batch in one launch: boat_env exp {args.experiment} + "
                                 f"toy_parachute + toy_car, {N} envs each/GPU" if args.mixed else
                                 f"boat_env exp {args.experiment}, {N} envs/GPU") +
-                               f", {args.episode_steps}-step episodes, in-kernel auto-reset",
+                               f", {args.episode_steps}-step episodes, in-kernel auto-reset" +
+                               (f", pooled replay exchange per {SEG}-step segment" if exchange is not None else ""),
                    "experiment": args.experiment, "envs_per_gpu": wl.per_gpu_envs,
                    "global_envs": world * wl.per_gpu_envs,
                    "episode_steps": args.episode_steps, "parallelism": f"env-dp{world}",
-                   "collective": (f"all_gather of each step's full transitions (the {TRANS_ROW} written by the "
-                                  f"step kernel, {wl.row_bytes()} B per rank-step): one "
-                                  f"{backend} all_gather per {pool_every}-step "
-                                  + ("segment" if pool_every == SEG else "group") +
-                                  f" ({gathers_timed} in the timed region) on a side stream"
-                                  + (", overlapped with the next segment" if pool_every == SEG else ""))
-                   if pool is not None else (
-                       "none: sharded per-GPU replay (--pooling none)" if world > 1 else None),
+                   "collective": collective,
                    "launch": ((f"two persistent sacenv_boat_segment launches of {SEG // 2} steps per {SEG}-step "
                                "segment" if run.overlap else
                                f"one persistent sacenv_mixed_segment launch per {SEG} steps (the boat's owner "
@@ -827,6 +1024,8 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
                               "action-row flag, all rows published) + the 3 refill launches after each"
                               + (f"; one launch per {pool_every} steps when pooling" if pool is not None
                                  and pool_every < SEG else "")
+                              + ("; the launch writes each step's transition rows into the staged replay buffer"
+                                 if exchange is not None else "")
                               if seg_mode else
                               (f"hipGraph segments of {SEG} k_step launches" +
                                (" (sacenv_boat_step_pooled: the step writes its pooled row)"
@@ -839,12 +1038,24 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
                        "timed region" if run.overlap else
                        f"k_need_masks + k_refill + k_refill_fit after every {SEG}-step segment, inside the "
                        "timed region")},
-        "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
-                     "limiter": ("FP64 VALU instruction issue of one owner wave per SIMD (see compute)"
-                                 if seg_mode else "launch + latency chains (DESIGN.md §4.2)"),
-                     "compute": (load_compute(N, args.experiment, kern_s) if seg_mode and not args.mixed
-                                 else None),
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK,
+        "roofline": {"bound": "fp64-issue" if compute is not None else "hbm",
+                     "achieved": compute["achieved"] if compute is not None else achieved / 1e9,
+                     "peak": compute["peak"] if compute is not None else HBM_PEAK / 1e9,
+                     "unit": "TFLOP/s" if compute is not None else "GB/s",
+                     "frac": compute["frac"] if compute is not None else achieved / HBM_PEAK,
+                     "issue_floor_frac": None if compute is None else compute["issue_floor_frac"],
+                     "limiter": ("FP64 VALU instruction issue of one owner wave per SIMD: achieved FP64 flop/s "
+                                 "against the 78.6-TF FP64 vector datasheet peak; issue_floor_frac = the issue "
+                                 "floor of the measured instruction stream / the kernel's time (compute); the "
+                                 "byte rates and the PMC traffic are under hbm"
+                                 if compute is not None else
+                                 "launch + latency chains (DESIGN.md §4.2)" if not seg_mode else
+                                 "instruction issue (no committed PMC pass for this shape)"),
+                     "compute": compute,
+                     "hbm": {"achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                             "frac": achieved / HBM_PEAK,
+                             "traffic_frac": (None if traffic is None else
+                                              traffic["hbm_bytes_per_launch"] / kern_s / HBM_PEAK)},
                      "traffic": None if traffic is None else traffic["hbm_bytes_per_launch"],
                      "kernel": ("k_rollout_mixed (sacenv_mixed_segment, 256 steps per launch; per step below)"
                                 if seg_mode and args.mixed else
@@ -873,21 +1084,10 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
                                  "reach this rate at 8 TB/s; the persistent launch is bound by its "
                                  "instruction issue (one owner wave per SIMD), not by HBM"}},
         "every_output": every,
+        "replay_path": replay_path,
         "cpu_baseline": None,
-        # N>1: what the pooled transitions cost -- every rank receives (world - 1) rows per step
         "dist": dinfo,
-        "pooling": None if pool is None else {
-            "pool_every": pool_every,
-            "gathers_timed": gathers_timed,
-            "row_bytes_per_rank_step": wl.row_bytes(),
-            "received_bytes_per_rank": (world - 1) * wl.row_bytes() * steps,
-            "received_GBps_per_rank": (world - 1) * wl.row_bytes() * steps / el_max / 1e9,
-            # xGMI accounting: each peer's rows arrive over its own point-to-point link
-            "xgmi": {"link_peak_GBps": XGMI_LINK_GBPS, "links_used": world - 1,
-                     "per_link_GBps": wl.row_bytes() * steps / el_max / 1e9,
-                     "per_link_frac": wl.row_bytes() * steps / el_max / 1e9 / XGMI_LINK_GBPS},
-            "note": "the timed region ends when the last all_gather has landed",
-            "no_exchange": no_exchange},
+        "pooling": pooling_out,
     }
 
 
@@ -921,40 +1121,6 @@ def every_output_rate(wl: Workload, dev, n_segs: int = 4, k0: int = 0) -> dict |
             "ms_per_step": el / steps * 1e3,
             "note": f"sacenv_boat_rollout, {SEG} steps per launch, every step's record and terminal obs "
                     "written to its own rows, + the refill per launch; after the timed region, wall time"}
-
-
-# ---------------------------------------------------------------- sharded replay exchange
-SHARD_BATCH = 1024      # agent.batch_size (configs/original_config.yaml)
-SHARD_WORDS = 2 * 11 + 1 + 2 + 1   # state, new_state (f32 x 11 each), action, reward (f64), terminal
-
-
-def sharded_exchange(world: int, dev, seg_s: float, n_envs: int) -> dict:
-    """The exact lighter exchange: ShardedReplayBuffer keeps each
-    rank's transitions on its GPU and assembles every sampled batch with one SUM all-reduce;
-    sample_many batches one segment's 256 learn() batches into ONE all-reduce of
-    256 x 1024 x 26 words (27.3 MB). Timed here on the run's own backend (RCCL on the node),
-    then charged in series to the measured no-exchange segment time."""
-    import torch.distributed as dist
-    n = SEG * SHARD_BATCH * SHARD_WORDS
-    words = torch.zeros(n + (n & 1), dtype=torch.int32, device=dev)
-    dist.all_reduce(words)                      # warm the communicator for this size
-    _sync(dev)
-    reps = 4
-    barrier(world)
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        dist.all_reduce(words)
-    _sync(dev)
-    el = (time.perf_counter() - t0) / reps
-    t = torch.tensor([el], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    el = float(t.item())
-    return {"value": world * n_envs * SEG / (seg_s + el), "unit": "env-steps/s",
-            "allreduce_ms_per_segment": el * 1e3, "bytes_per_segment": words.numel() * 4,
-            "segment_ms_no_exchange": seg_s * 1e3,
-            "note": "the no-exchange segment time + one SUM all-reduce of the segment's 256 learn() batches "
-                    "(ShardedReplayBuffer.sample_many: the pooled buffer's batches bit for bit, "
-                    "tests/test_sharded_replay_gpu.py), in series (not overlapped), max over ranks"}
 
 
 # ---------------------------------------------------------------- closed-loop line
@@ -1125,14 +1291,29 @@ def bench_rollout(args, wl: Workload, rank, world, dev):
 
 
 def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
     args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: start the N rank processes here (before anything touches a GPU)
+        sys.exit(spawn_ranks(args.gpus, argv))
     cpu = None
     if (int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.no_cpu_baseline and not args.rollout
-            and not args.closed_loop):
+            and not args.closed_loop and not args.stub):
         # before anything touches the GPU: the C1 legs are child processes, and an
         # idle host keeps them from competing with the timed region's launches
         cpu = cpu_baseline(args, args.mixed_envs if args.mixed else args.envs)
-    rank, world, dev = init_dist(args.gpus)
+    rank, world, dev = init_dist(args.gpus, args.stub)
+    if args.stub:
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import bench_stub
+        _, wl = bench_stub.workload(sys.modules[__name__], rank)
+        out = run_bench(args, rank, world, dev, wl)
+        if out is not None:
+            print(json.dumps(out), flush=True)
+        if world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return
     if args.closed_loop:
         out = bench_closed_loop(args, rank, world, dev)
         if out is not None:

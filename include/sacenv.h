@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SACENV_ABI_VERSION 15
+#define SACENV_ABI_VERSION 16
 #define SACENV_OBS_DIM 11      /* Boat.return_state, boat_env.py:308-323 */
 #define SACENV_MT_N 624        /* MT19937 words per env (numpy legacy RNG) */
 #define SACENV_MAX_KNOTS 16    /* wind.fixed_points upper bound */
@@ -43,9 +43,9 @@ extern "C" {
 #define SACENV_SLOTS 257       /* episode slots per env in autoreset mode (active + 256 ahead) */
 #define SACENV_REFILL_PERIOD 256 /* autoreset: at most this many step launches between refills */
 #define SACENV_RECORD_BYTES 50 /* packed per-env step record (see layout.record) */
-#define SACENV_TRANS_OBS 9      /* s' entries in the transition row (obs 0..8) */
-#define SACENV_TRANS_BYTES 45   /* per-env transition row of sacenv_boat_step_pooled */
-#define SACENV_TRANS_BYTES_EXP2 49 /* the same in experiment 2 (+ obs3_next) */
+#define SACENV_TRANS_OBS 11     /* s' entries in the transition row (the whole obs) */
+#define SACENV_TRANS_BYTES 53   /* per-env transition row of sacenv_boat_step_pooled */
+#define SACENV_TRANS_BYTES_EXP2 57 /* the same in experiment 2 (+ obs3_next) */
 #define SACENV_PAIR_STRIDE 16  /* bytes between envs in the paired f64 state fields */
 
 /* termination codes; 1..5 follow the info-dict key order boat_env.py:24-32,
@@ -223,8 +223,8 @@ int sacenv_boat_step(const SacenvBoatParams *p, void *arena, const float *action
  * replay buffer (main.py:81-88 -> agent/buffer.py:13-22) to
  * the device row `trans` (SACENV_TRANS_BYTES x n_pad bytes, experiment 2:
  * SACENV_TRANS_BYTES_EXP2; 16-B aligned):
- *   s'       f32 [n_pad][9]   obs entries 0..8 after the step, BEFORE any
- *                             auto-reset (the terminal obs of envs that ended)
+ *   s'       f32 [n_pad][11]  the obs after the step, BEFORE any auto-reset
+ *                             (the terminal obs of envs that ended)
  *   reward   f32 [n_pad]
  *   action   f32 [n_pad]      the step's action
  *   term     u8  [n_pad]      termination code; done = term != 0
@@ -232,12 +232,12 @@ int sacenv_boat_step(const SacenvBoatParams *p, void *arena, const float *action
  *                             (normalised start s_y) of the new episode's
  *                             first obs (its other entries are fixed by the
  *                             config: a fresh Boat, boat_env.py:152-198)
- * The receiver rebuilds the rest exactly: s'[9] (rudder) from its f64 rudder
- * (0 at an episode start, += f64(action) / 10 per step with test_mode 0) as
- * (rudder + pi/3) * (1 / (2 pi / 3)), s'[10] (fuel) as (fuel0 - steps) / fuel0;
- * each env's s is the previous row's s', or the fresh-Boat obs for envs that
- * ended there (sacenv/dist.py TransitionStream). 45 B per env instead of the
- * record + action + terminal obs (98 B), written by the step launch itself. */
+ * Each env's s is the previous row's s', or the fresh-Boat obs for envs that
+ * ended there (sacenv/dist.py TransitionStream; the staged replay sampler).
+ * 53 B per env instead of the record + action + terminal obs (98 B), written
+ * by the step launch itself. (ABI 15 and before: s' entries 0..8 only, 45 B,
+ * rudder and fuel rebuilt on the receiver; a sampler that gathers single rows
+ * out of a segment cannot rebuild them.) */
 int sacenv_boat_step_pooled(const SacenvBoatParams *p, void *arena, const float *action, void *trans,
                             void *stream);
 
@@ -480,6 +480,55 @@ int sacenv_replay_sample_shard(const SacenvReplayParams *p, void *arena, int32_t
                                int64_t offset, int64_t n, int64_t period, int64_t *idx, float *state,
                                float *action, double *reward, float *new_state, uint8_t *terminal,
                                void *stream);
+
+/* The pooled buffer sampled out of STAGED SEGMENTS (the exchange that scales,
+ * DESIGN.md §6): main.py:78-90 with every rank's envs storing their transitions
+ * into one ReplayBuffer(mem_size) (buffer.py:13-22) each step and one learn() --
+ * sample_buffer(batch), buffer.py:24-35 -- after every step, WITHOUT a ring: a
+ * persistent step launch writes each step's transition rows (the
+ * sacenv_boat_step_pooled format) into a segment buffer [seg][row] (row =
+ * SACENV_TRANS_BYTES(_EXP2) x n_pad), and the segment's learns are sampled from
+ * it afterwards. The pooled ring appends `period` = world x n rows per step in
+ * global env order; with mem_size <= seg x period every row learn k of segment
+ * g can reach was written in segment g or g - 1, so those two buffers are the
+ * ring. Global step numbers: segment g holds steps g*seg .. g*seg + seg - 1. */
+typedef struct SacenvStagedParams {
+  int64_t period;        /* pooled rows per step: world x n */
+  int64_t offset;        /* this rank's first global env (rank x n) */
+  int32_t n;             /* this rank's envs */
+  int32_t n_pad;         /* the env arena's n_pad: the rows' field stride */
+  int32_t seg;           /* steps (rows) per segment buffer */
+  int32_t experiment;    /* 2: the rows carry obs3_next */
+  float first_obs[SACENV_OBS_DIM]; /* a fresh Boat's obs (boat_env.py:152-198 -> return_state) */
+} SacenvStagedParams;
+
+/* The reference's stored terminal of each row of a segment (main.py:83-88:
+ * info['termination'] == 'reached_goal', the info dict keeping the last
+ * termination across steps and resets): terminal[j][e] (u8 [seg][n_pad]) =
+ * (terminal_mask >> last_term) & 1 after row j's code updated last_term[e]
+ * (u8 [n], carried from segment to segment, zero-initialised). Call once per
+ * segment, in segment order, before sampling it. */
+int sacenv_replay_stage_terminal(const SacenvReplayParams *p, const SacenvStagedParams *sp, const void *rows,
+                                 int32_t n_steps, uint8_t *last_term, uint8_t *terminal, void *stream);
+/* The batches of the n_batches learn() calls after steps g*seg .. g*seg +
+ * n_batches - 1: batch k = np.random.choice(min(c_k, mem_size), batch) on the
+ * arena's sampling stream with c_k = (g*seg + k + 1) x period transitions stored
+ * (fewer than `batch`: learn() returns before sampling, idx = -1, zero words).
+ * Each sampled ring row resolves to the transition the pooled ring holds there
+ * at learn k; this rank's are gathered from rows_cur (segment g) / rows_prev
+ * (segment g - 1; for g = 0 its last row holds the reset obs with term 0): s' =
+ * the row's obs, s = the previous step's s' or, where that step ended, the
+ * fresh-Boat obs (first_obs; experiment 2 with that row's obs3_next), reward,
+ * action, terminal (sacenv_replay_stage_terminal's bytes). Output `words`
+ * (u32, n_batches x 26 batch), per batch: reward f64 [batch] (two words each) |
+ * state f32 [batch][11] | new_state f32 [batch][11] | action f32 [batch] |
+ * terminal u32 [batch]; other ranks' rows are zero words, so an integer SUM
+ * all-reduce over the ranks is the pooled buffer's batches, bit for bit, on
+ * every rank. Needs obs_dim 11, act_dim 1, mem_size <= seg x period. */
+int sacenv_replay_sample_staged(const SacenvReplayParams *p, void *arena, const SacenvStagedParams *sp, int64_t g,
+                                const void *rows_cur, const uint8_t *term_cur, const void *rows_prev,
+                                const uint8_t *term_prev, int32_t batch, int32_t n_batches, int64_t *idx,
+                                uint32_t *words, void *stream);
 
 /* ------------------------------------------------------------------------
  * SAC agent on the device: the batched

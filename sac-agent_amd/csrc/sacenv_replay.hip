@@ -234,6 +234,219 @@ __global__ void __launch_bounds__(256) k_rb_gather(SacenvReplayParams p, RB r, i
   }
 }
 
+// ---------------------------------------------------------------------------
+// The staged sampler (sacenv_replay_sample_staged): the pooled buffer of
+// main.py:81-90 -- every rank's envs storing one transition each per step, one
+// learn() (sample_buffer, buffer.py:24-35) after every step -- sampled straight
+// out of the segments of transition rows the persistent step launch wrote
+// (sacenv_boat_segment's `trans`), with no store into a ring. A ring of M rows
+// that takes `period` rows per step holds the last M sequence numbers; with M <=
+// seg * period every row learn k can reach lies in this segment's or the
+// previous segment's rows, so the two staged segments ARE the ring.
+
+// The persistent info['termination'] (main.py:83, boat_env.py:24-32,84-105,
+// 120-126) per row: codes 1..5 overwrite the env's last termination, 0 and 6
+// keep it; terminal = (terminal_mask >> last) & 1. One thread per 4 envs walks
+// the segment's rows in order: u32 loads (4 envs' codes, coalesced across the
+// threads of a row), kChunk rows in flight before the serial carry.
+__global__ void __launch_bounds__(256) k_rb_stage_terminal(const uint8_t* __restrict__ rows, int64_t row_bytes,
+                                                           int64_t term_off, int n_steps, int n, int n_pad,
+                                                           uint32_t terminal_mask, uint8_t* __restrict__ last_term,
+                                                           uint8_t* __restrict__ terminal) {
+  constexpr int kChunk = 32;
+  const int e0 = 4 * (blockIdx.x * blockDim.x + threadIdx.x);
+  if (e0 >= n) return;
+  uint32_t lt[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) lt[q] = e0 + q < n ? last_term[e0 + q] : 0u;
+  for (int j0 = 0; j0 < n_steps; j0 += kChunk) {
+    uint32_t c[kChunk];
+#pragma unroll
+    for (int j = 0; j < kChunk; ++j)
+      c[j] = j0 + j < n_steps ? *reinterpret_cast<const uint32_t*>(rows + (int64_t)(j0 + j) * row_bytes + term_off + e0)
+                              : 0u;
+#pragma unroll
+    for (int j = 0; j < kChunk; ++j) {
+      uint32_t out = 0u;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t cq = (c[j] >> (8 * q)) & 0xFFu;
+        lt[q] = (cq >= 1u && cq <= 5u) ? cq : lt[q];
+        out |= ((terminal_mask >> lt[q]) & 1u) << (8 * q);
+      }
+      if (j0 + j < n_steps) *reinterpret_cast<uint32_t*>(terminal + (int64_t)(j0 + j) * n_pad + e0) = out;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (e0 + q < n) last_term[e0 + q] = (uint8_t)lt[q];
+}
+
+// mt19937_gen over one block with a whole workgroup (>= 227 threads): the three
+// lane-parallel phases of mt_twist_wave, one word per thread each.
+__device__ __forceinline__ void mt_twist_block(const uint32_t* __restrict__ o, uint32_t* __restrict__ n, int tid) {
+  constexpr int kD = kMtN - kMtM;  // 227
+  if (tid < kD) n[tid] = mt_mix(o[tid], o[tid + 1], o[tid + kMtM]);
+  __syncthreads();
+  if (tid < kD) n[kD + tid] = mt_mix(o[kD + tid], o[kD + tid + 1], n[tid]);
+  __syncthreads();
+  if (tid < kMtN - 1 - 2 * kD) n[2 * kD + tid] = mt_mix(o[2 * kD + tid], o[2 * kD + tid + 1], n[kD + tid]);
+  __syncthreads();
+  if (tid == 0) n[kMtN - 1] = mt_mix(o[kMtN - 1], n[0], n[kMtM - 1]);
+  __syncthreads();
+}
+
+// n_batches consecutive np.random.choice(min(cntr_k, M), batch) calls on one
+// stream, cntr_k = cntr0 + (k + 1) * period (learn k follows step k's stores).
+// One workgroup of kDrawThreads: a whole 624-word block is tempered and tested
+// at once (thread i: word i), accepted words are ranked with a ballot per wave
+// and a prefix over the waves; a batch that completes inside the block ends at
+// its last accepted word, and the next batch re-tests the block from there
+// (its range may differ while cntr < M). The stream advances exactly as numpy's.
+constexpr int kDrawThreads = 1024;
+__global__ void __launch_bounds__(kDrawThreads) k_rb_draw_many(SacenvReplayParams p, RB r, int batch, int nb,
+                                                               int64_t cntr0, int64_t period,
+                                                               int64_t* __restrict__ idx) {
+  __shared__ uint32_t blk[2][kMtN];
+  __shared__ int wcnt[kDrawThreads / kWave];
+  __shared__ int s_end;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
+  constexpr int kWaves = kDrawThreads / kWave;
+  for (int i = tid; i < kMtN; i += kDrawThreads) blk[0][i] = r.key()[i];
+  int cur = 0, pos = *r.pos();
+  bool advanced = false;
+  __syncthreads();
+  int k = 0, filled = 0;
+  while (k < nb) {
+    const int64_t c = cntr0 + (int64_t)(k + 1) * period;
+    const int64_t max_mem = c < p.mem_size ? c : p.mem_size;
+    const uint32_t rng = (uint32_t)(max_mem - 1);
+    if (c < batch || rng == 0u) {  // learn() returns before sampling (continuous_agent.py:97-98),
+      // or numpy's off + 0: no words consumed
+      for (int i = tid; i < batch; i += kDrawThreads) idx[(int64_t)k * batch + i] = c < batch ? -1 : 0;
+      ++k;
+      continue;
+    }
+    uint32_t mask = rng;
+    mask |= mask >> 1;
+    mask |= mask >> 2;
+    mask |= mask >> 4;
+    mask |= mask >> 8;
+    mask |= mask >> 16;
+    if (pos >= kMtN) {
+      mt_twist_block(blk[cur], blk[cur ^ 1], tid);
+      cur ^= 1;
+      pos = 0;
+      advanced = true;
+    }
+    const bool valid = tid >= pos && tid < kMtN;
+    const uint32_t w = valid ? (mt_temper(blk[cur][tid]) & mask) : 0u;
+    const bool acc = valid && w <= rng;
+    const unsigned long long bal = __ballot(acc);
+    if (lane == 0) wcnt[wv] = __popcll(bal);
+    __syncthreads();
+    int excl = 0, total = 0;
+#pragma unroll
+    for (int q = 0; q < kWaves; ++q) {
+      const int v = wcnt[q];
+      excl += q < wv ? v : 0;
+      total += v;
+    }
+    const int rank = excl + __popcll(bal & ((1ull << lane) - 1ull));
+    const int take = batch - filled;
+    if (acc && rank < take) idx[(int64_t)k * batch + filled + rank] = (int64_t)w;
+    if (total >= take) {  // the take-th accepted word ends batch k
+      if (acc && rank == take - 1) s_end = tid;
+      __syncthreads();
+      pos = s_end + 1;
+      ++k;
+      filled = 0;
+    } else {
+      filled += total;
+      pos = kMtN;
+    }
+    __syncthreads();  // wcnt / s_end are rewritten by the next round
+  }
+  if (advanced)
+    for (int i = tid; i < kMtN; i += kDrawThreads) r.key()[i] = blk[cur][i];
+  if (tid == 0) *r.pos() = pos;
+}
+
+struct Staged {
+  const char* cur;         // rows of segment g
+  const char* prev;        // rows of segment g - 1 (g = 0: row seg-1 holds the reset obs, term 0)
+  const uint8_t* tcur;     // k_rb_stage_terminal's terminal bytes [seg][n_pad] of segment g
+  const uint8_t* tprev;    // ... of segment g - 1
+  int64_t row_bytes, period, offset, g;
+  int n, n_pad, seg, exp2;
+  float first[SACENV_OBS_DIM];
+};
+
+// One thread per sampled row (batch b, row i): ring row idx -> the sequence
+// number it holds at learn b (the latest s = idx mod M below cntr_b) -> (step,
+// global env); this rank's rows are read from the staged segments: s' the row's
+// obs, s the previous step's s' (or the fresh-Boat obs where that step ended:
+// first_obs, exp 2 with that row's obs3_next), the reward and action, the
+// terminal byte. Output per batch, 32-bit words (sample_many's packing):
+// reward f64 [B] | state [B][11] | new_state [B][11] | action [B] | terminal [B];
+// rows of other ranks are zero words, so a SUM all-reduce assembles the batch.
+__global__ void __launch_bounds__(256) k_rb_gather_staged(SacenvReplayParams p, Staged S, int batch, int nb,
+                                                          const int64_t* __restrict__ idx,
+                                                          uint32_t* __restrict__ words, int64_t per) {
+  constexpr int D = SACENV_OBS_DIM;
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t >= (int64_t)batch * nb) return;
+  const int b = (int)(t / batch), i = (int)(t - (int64_t)b * batch);
+  const int64_t M = p.mem_size;
+  const int64_t cntr = (S.g * S.seg + b + 1) * S.period;
+  const int64_t row = idx[t];  // -1: no learn at this step (fewer rows than a batch)
+  const int64_t s = row < 0 ? 0 : row + M * ((cntr - 1 - row) / M);
+  const int64_t q = s / S.period, u = s - q * S.period;
+  const bool own = row >= 0 && u >= S.offset && u < S.offset + S.n;
+  uint32_t* const W = words + (int64_t)b * per;
+  float sn[D], sv[D];
+  float rw = 0.f, ac = 0.f;
+  uint32_t tm = 0u;
+#pragma unroll
+  for (int k = 0; k < D; ++k) sn[k] = sv[k] = 0.f;
+  if (own) {
+    const int e = (int)(u - S.offset);
+    int64_t j = q - S.g * S.seg;  // >= -seg + 1 (M <= seg * period)
+    const bool in_cur = j >= 0;
+    j = in_cur ? j : j + S.seg;
+    const char* R = (in_cur ? S.cur : S.prev) + j * S.row_bytes;
+    // the previous step's row: same segment, or the last row of the previous one
+    const char* P = j > 0 ? R - S.row_bytes : S.prev + (int64_t)(S.seg - 1) * S.row_bytes;
+    const float* rs = reinterpret_cast<const float*>(R) + (int64_t)e * D;
+    const float* ps = reinterpret_cast<const float*>(P) + (int64_t)e * D;
+    const int64_t np = S.n_pad;
+    rw = reinterpret_cast<const float*>(R + 44 * np)[e];
+    ac = reinterpret_cast<const float*>(R + 48 * np)[e];
+    tm = (in_cur ? S.tcur : S.tprev)[j * np + e];
+    const bool pdone = reinterpret_cast<const uint8_t*>(P + 52 * np)[e] != 0;
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      sn[k] = rs[k];
+      sv[k] = pdone ? S.first[k] : ps[k];
+    }
+    if (S.exp2 && pdone) sv[3] = reinterpret_cast<const float*>(P + 53 * np)[e];
+  }
+  const double r64 = (double)rw;
+  uint64_t rb;
+  __builtin_memcpy(&rb, &r64, 8);
+  W[2 * i] = (uint32_t)rb;
+  W[2 * i + 1] = (uint32_t)(rb >> 32);
+  uint32_t* const st = W + 2 * batch + (int64_t)i * D;
+  uint32_t* const ns = W + 2 * batch + (int64_t)batch * D + (int64_t)i * D;
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    st[k] = __float_as_uint(sv[k]);
+    ns[k] = __float_as_uint(sn[k]);
+  }
+  W[2 * batch + 2 * (int64_t)batch * D + i] = __float_as_uint(ac);
+  W[2 * batch + 2 * (int64_t)batch * D + batch + i] = tm;
+}
+
 int check_replay(const SacenvReplayParams* p) {
   if (p == nullptr) return SACENV_E_NULL;
   if (p->mem_size <= 0 || p->mem_size > 0x7FFFFFFFLL || p->obs_dim <= 0 || p->act_dim <= 0)
@@ -349,6 +562,70 @@ int sacenv_replay_sample_shard(const SacenvReplayParams* p, void* arena, int32_t
   if (offset < 0 || n < 0 || period <= 0 || offset + n > period) return SACENV_E_RANGE;
   return sample(p, arena, batch, stored, idx, state, action, reward, new_state, terminal,
                 Shard{period, offset, offset + n}, stream);
+}
+
+static int check_staged(const SacenvReplayParams* p, const SacenvStagedParams* sp) {
+  int rc = check_replay(p);
+  if (rc) return rc;
+  if (sp == nullptr) return SACENV_E_NULL;
+  if (p->obs_dim != SACENV_OBS_DIM || p->act_dim != 1) return SACENV_E_SIZE;  // the boat's rows
+  if (sp->n <= 0 || sp->n_pad < sp->n || (sp->n_pad & 63) != 0 || sp->seg <= 0) return SACENV_E_SIZE;
+  if (sp->offset < 0 || sp->period <= 0 || sp->offset + sp->n > sp->period) return SACENV_E_RANGE;
+  return SACENV_OK;
+}
+
+static int64_t staged_row_bytes(const SacenvStagedParams* sp) {
+  return (int64_t)(sp->experiment == 2 ? SACENV_TRANS_BYTES_EXP2 : SACENV_TRANS_BYTES) * sp->n_pad;
+}
+
+int sacenv_replay_stage_terminal(const SacenvReplayParams* p, const SacenvStagedParams* sp, const void* rows,
+                                 int32_t n_steps, uint8_t* last_term, uint8_t* terminal, void* stream) {
+  int rc = check_staged(p, sp);
+  if (rc) return rc;
+  if (n_steps < 0 || n_steps > sp->seg) return SACENV_E_SIZE;
+  if (!rows || !last_term || !terminal) return SACENV_E_NULL;
+  if (n_steps == 0) return SACENV_OK;
+  hipLaunchKernelGGL(k_rb_stage_terminal, dim3((unsigned)((sp->n + 1023) / 1024)), dim3(256), 0, (hipStream_t)stream,
+                     static_cast<const uint8_t*>(rows), staged_row_bytes(sp), (int64_t)52 * sp->n_pad, n_steps, sp->n,
+                     sp->n_pad, p->terminal_mask, last_term, terminal);
+  return status();
+}
+
+int sacenv_replay_sample_staged(const SacenvReplayParams* p, void* arena, const SacenvStagedParams* sp, int64_t g,
+                                const void* rows_cur, const uint8_t* term_cur, const void* rows_prev,
+                                const uint8_t* term_prev, int32_t batch, int32_t n_batches, int64_t* idx,
+                                uint32_t* words, void* stream) {
+  int rc = check_staged(p, sp);
+  if (rc) return rc;
+  if (g < 0 || batch < 0 || n_batches < 0 || n_batches > sp->seg) return SACENV_E_SIZE;
+  // every row learn k can reach lies in segments g and g-1 (and a row's predecessor too)
+  if (p->mem_size > (int64_t)sp->seg * sp->period) return SACENV_E_RANGE;
+  if (!arena || !rows_cur || !term_cur || !rows_prev || !term_prev || !idx || !words) return SACENV_E_NULL;
+  if (batch == 0 || n_batches == 0) return SACENV_OK;
+  if ((g * sp->seg + 1) * sp->period > (int64_t)1 << 62) return SACENV_E_RANGE;
+  const RB r = make_rb(*p, arena);
+  hipLaunchKernelGGL(k_rb_draw_many, dim3(1), dim3(kDrawThreads), 0, (hipStream_t)stream, *p, r, batch, n_batches,
+                     g * sp->seg * sp->period, sp->period, idx);
+  if ((rc = status())) return rc;
+  Staged S;
+  S.cur = static_cast<const char*>(rows_cur);
+  S.prev = static_cast<const char*>(rows_prev);
+  S.tcur = term_cur;
+  S.tprev = term_prev;
+  S.row_bytes = staged_row_bytes(sp);
+  S.period = sp->period;
+  S.offset = sp->offset;
+  S.g = g;
+  S.n = sp->n;
+  S.n_pad = sp->n_pad;
+  S.seg = sp->seg;
+  S.exp2 = sp->experiment == 2;
+  for (int k = 0; k < SACENV_OBS_DIM; ++k) S.first[k] = sp->first_obs[k];
+  const int64_t total = (int64_t)batch * n_batches;
+  const int64_t per = (int64_t)batch * (2 * SACENV_OBS_DIM + 1 + 3);
+  hipLaunchKernelGGL(k_rb_gather_staged, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     *p, S, batch, n_batches, idx, words, per);
+  return status();
 }
 
 }  // extern "C"

@@ -14,7 +14,7 @@ PKG_ROOT = _build.PKG_ROOT
 LIB_PATH = os.environ.get("SACENV_LIB", _build.LIB)
 LOADED_DIGEST = None  # source digest of the loaded library (the in-tree build)
 
-ABI_VERSION = 15
+ABI_VERSION = 16
 OBS_DIM = 11
 MT_N = 624
 MAX_KNOTS = 16
@@ -26,9 +26,9 @@ STATUS_HANDOFF_TIMEOUT = 2
 STATUS_LIST_TIMEOUT = 4
 FLAG_ABORT = 0xFFFFFFFF  # hand-off flag of a wave / workgroup that gave up (sacenv.h)
 RECORD_BYTES = 50
-TRANS_OBS = 9           # s' entries in the pooled row (obs 0..8; 9 and 10 rebuilt by the receiver)
-TRANS_BYTES = 45        # sacenv_boat_step_pooled's per-env transition row
-TRANS_BYTES_EXP2 = 49   # experiment 2 (+ obs3_next)
+TRANS_OBS = 11          # s' entries in the pooled row (the whole obs)
+TRANS_BYTES = 53        # sacenv_boat_step_pooled's per-env transition row
+TRANS_BYTES_EXP2 = 57   # experiment 2 (+ obs3_next)
 
 
 def trans_bytes(experiment: int) -> int:
@@ -107,6 +107,11 @@ class ReplayParams(C.Structure):
                 ("terminal_mask", C.c_uint32)]
 
 
+class StagedParams(C.Structure):
+    _fields_ = [("period", _i64), ("offset", _i64), ("n", _i32), ("n_pad", _i32), ("seg", _i32),
+                ("experiment", _i32), ("first_obs", C.c_float * OBS_DIM)]
+
+
 REPLAY_LAYOUT_FIELDS = ("total_bytes", "state", "new_state", "action", "reward", "terminal",
                         "mem_cntr", "mt_key", "mt_pos")
 
@@ -139,7 +144,7 @@ EXPORTS = ("sacenv_abi_version", "sacenv_error_string", "sacenv_boat_layout",
            "sacenv_toy_reset", "sacenv_toy_step", "sacenv_mixed_step", "sacenv_mixed_step_pooled",
            "sacenv_mixed_segment", "sacenv_replay_layout",
            "sacenv_replay_init", "sacenv_replay_store", "sacenv_replay_store_env", "sacenv_replay_sample", "sacenv_replay_store_shard",
-           "sacenv_replay_sample_shard",
+           "sacenv_replay_sample_shard", "sacenv_replay_stage_terminal", "sacenv_replay_sample_staged",
            "sacenv_compact_done", "sacenv_boat_reset_list", "sacenv_sac_layout", "sacenv_sac_sync",
            "sacenv_sac_act", "sacenv_sac_act_handoff", "sacenv_sac_act_occupancy", "sacenv_sac_learn")
 
@@ -179,6 +184,7 @@ def load(path: str | None = None):
     P = C.POINTER(BoatParams)
     TP = C.POINTER(ToyParams)
     RP = C.POINTER(ReplayParams)
+    SP = C.POINTER(StagedParams)
     sig = {
         "sacenv_abi_version": (C.c_int, []),
         "sacenv_error_string": (C.c_char_p, [C.c_int]),
@@ -212,6 +218,8 @@ def load(path: str | None = None):
         "sacenv_replay_store_shard": (C.c_int, [RP, _p, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p]),
         "sacenv_replay_sample_shard": (C.c_int, [RP, _p, _i32, _i64, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p,
                                                  _p]),
+        "sacenv_replay_stage_terminal": (C.c_int, [RP, SP, _p, _i32, _p, _p, _p]),
+        "sacenv_replay_sample_staged": (C.c_int, [RP, _p, SP, _i64, _p, _p, _p, _p, _i32, _i32, _p, _p, _p]),
         "sacenv_sac_layout": (C.c_int, [C.POINTER(SacParams), C.POINTER(SacLayout)]),
         "sacenv_sac_sync": (C.c_int, [C.POINTER(SacParams), _p, _p]),
         "sacenv_sac_act": (C.c_int, [C.POINTER(SacParams), _p, _p, _i32, _p, _p, _p, _p]),

@@ -16,12 +16,12 @@ The shared replay buffer consumes whole transitions (s, a, r, s', terminal)
 (main.py:83-88, agent/buffer.py:13-22). The record alone cannot form them:
 for an env that ended (and auto-reset) its obs is already the NEXT episode's
 first obs. The pooled row of a step is the transition row the step kernel
-writes itself (``sacenv_boat_step_pooled``, ``TransitionLayout``: s' entries
-0..8 before the reset, reward, action, term, and in experiment 2 the one obs
-entry a fresh Boat does not fix; 45 B per env, 49 in experiment 2);
+writes itself (``sacenv_boat_step_pooled``, ``TransitionLayout``: s' -- the
+obs before any reset --, reward, action, term, and in experiment 2 the one obs
+entry a fresh Boat does not fix; 53 B per env, 57 in experiment 2);
 ``TransitionStream`` turns consecutive pooled rows back into (s, a, r, s',
-code), rebuilding s'[9] (rudder) and s'[10] (fuel) exactly from the actions
-and episode starts.
+code). ``sacenv.replay.StagedReplay`` samples the pooled replay buffer straight
+out of a segment's rows (the exchange that scales).
 """
 from __future__ import annotations
 
@@ -29,9 +29,7 @@ from dataclasses import dataclass
 
 import torch
 
-import math
-
-from ._lib import TRANS_OBS, trans_bytes
+from ._lib import TRANS_OBS, trans_bytes  # noqa: F401
 from .vec_env import RECORD_BYTES
 
 
@@ -79,13 +77,12 @@ class TransitionLayout:
     """One rank's pooled row for one step, as ``sacenv_boat_step_pooled`` writes it
     (per-field arrays of n_pad entries; ``_lib.trans_bytes(experiment)`` per env):
 
-        [ s' f32 [n_pad][9] | reward f32 | action f32 | term u8 | obs3_next f32 (exp 2) ]
+        [ s' f32 [n_pad][11] | reward f32 | action f32 | term u8 | obs3_next f32 (exp 2) ]
 
-    s' holds obs entries 0..8 BEFORE any auto-reset (the terminal obs of envs
-    that ended); entries 9 (rudder) and 10 (fuel) and done (= term != 0) are
-    rebuilt by ``TransitionStream``. In experiment 2 the next transition's s of
-    an env that ended is the fresh-Boat obs (``first_obs_template``) with entry
-    3 = obs3_next; elsewhere the template itself.
+    s' is the obs BEFORE any auto-reset (the terminal obs of envs that ended);
+    done = term != 0. In experiment 2 the next transition's s of an env that
+    ended is the fresh-Boat obs (``first_obs_template``) with entry 3 =
+    obs3_next; elsewhere the template itself.
     """
     n: int            # envs per rank
     n_pad: int        # the arena's padded row count (n rounded up to 64)
@@ -100,22 +97,22 @@ class TransitionLayout:
         return self.per_env * self.n_pad
 
     def views(self, row: torch.Tensor):
-        """(s' entries 0..8 [n,9], reward [n], action [n], term [n], obs3_next [n] or None)."""
+        """(s' [n, 11], reward [n], action [n], term [n], obs3_next [n] or None)."""
         n, NP, K = self.n, self.n_pad, TRANS_OBS
         if row.dtype != torch.uint8 or row.numel() != self.nbytes:
             raise ValueError("row must be uint8 of TransitionLayout.nbytes")
         f = lambda a, b: row[a * NP: b * NP].view(torch.float32)[:n]  # noqa: E731
-        s9 = row[: 4 * K * NP].view(torch.float32).view(NP, K)[:n]
+        sp = row[: 4 * K * NP].view(torch.float32).view(NP, K)[:n]
         o = 4 * K
         obs3 = f(o + 9, o + 13) if self.experiment == 2 else None
-        return s9, f(o, o + 4), f(o + 4, o + 8), row[(o + 8) * NP: (o + 9) * NP][:n], obs3
+        return sp, f(o, o + 4), f(o + 4, o + 8), row[(o + 8) * NP: (o + 9) * NP][:n], obs3
 
     def pack(self, s_next, reward, action, obs3_next, term) -> torch.Tensor:
         """Host-side packing (tests, and hosts without the kernel's buffers); s_next is
-        the full [n, 11] obs (entries 9 and 10 are not carried)."""
+        the [n, 11] obs."""
         row = torch.zeros(self.nbytes, dtype=torch.uint8, device=s_next.device)
-        s9, r, a, t, o3 = self.views(row)
-        s9.copy_(s_next[:, :TRANS_OBS].to(torch.float32))
+        sp, r, a, t, o3 = self.views(row)
+        sp.copy_(s_next[:, :TRANS_OBS].to(torch.float32))
         r.copy_(reward.reshape(r.shape).to(torch.float32))
         a.copy_(action.reshape(a.shape).to(torch.float32))
         t.copy_(term.reshape(t.shape).to(torch.uint8))
@@ -124,15 +121,10 @@ class TransitionLayout:
         return row
 
     def unpack_gathered(self, gathered: torch.Tensor, world: int):
-        """Global (s'[:, :9], reward, action, term, obs3_next or None) in global env-id order."""
+        """Global (s' [world*n, 11], reward, action, term, obs3_next or None) in global env-id order."""
         parts = [self.views(gathered[r * self.nbytes:(r + 1) * self.nbytes]) for r in range(world)]
         cat = lambda i: torch.cat([p[i] for p in parts])  # noqa: E731
         return cat(0), cat(1), cat(2), cat(3), (cat(4) if self.experiment == 2 else None)
-
-
-# the kernel's normalisations of the two rebuilt entries (make_obs, boat_env.py:318-319)
-_RUD_LO = math.pi / 3
-_RUD_SCALE = 1.0 / (math.pi / 3 - (-math.pi / 3))
 
 
 class TransitionStream:
@@ -142,41 +134,26 @@ class TransitionStream:
     env that ended there the first obs of its new episode (``first_obs``, the
     fresh-Boat template, with entry 3 = that row's obs3_next in experiment 2);
     the reset obs for the first step (the stream starts at a reset). ``s'`` is
-    the step's obs before any auto-reset: entries 0..8 from the row, entry 9
-    from the env's f64 rudder (0 at an episode start, += f64(action) / 10 per
-    step with test_mode 0, boat_env.py:72-73) and entry 10 from its step count
-    (fuel = fuel0 - steps, :70), in the kernel's arithmetic (bit-identical).
-    ``code`` is the term code (the replay buffer derives terminal from it,
-    main.py:83-88); done = code != 0."""
+    the step's obs before any auto-reset, as the row holds it. ``code`` is the
+    term code (the replay buffer derives terminal from it, main.py:83-88);
+    done = code != 0."""
 
     def __init__(self, layout: TransitionLayout, world: int, reset_obs: torch.Tensor,
-                 first_obs: torch.Tensor, fuel0: int = 15000, test_mode: int = 0):
+                 first_obs: torch.Tensor):
         self.layout, self.world = layout, int(world)
         self.prev = reset_obs.to(torch.float32).clone()
         dev = self.prev.device
         self.first = first_obs.to(torch.float32).to(dev).reshape(1, -1)
-        n = self.prev.shape[0]
-        self.rudder = torch.zeros(n, dtype=torch.float64, device=dev)
-        self.fuel = torch.full((n,), int(fuel0), dtype=torch.int64, device=dev)
-        self.fuel0, self.test_mode = int(fuel0), int(test_mode)
 
     def push(self, gathered_row: torch.Tensor):
-        s9, reward, action, term, obs3 = self.layout.unpack_gathered(gathered_row, self.world)
-        rud = self.rudder + action.to(torch.float64) / 10.0 if self.test_mode == 0 else self.rudder
-        fuel = self.fuel - 1
-        s_next = torch.empty_like(self.prev)
-        s_next[:, :TRANS_OBS] = s9
-        s_next[:, 9] = ((rud + _RUD_LO) * _RUD_SCALE).to(torch.float32)
-        s_next[:, 10] = (fuel.to(torch.float64) / float(self.fuel0)).to(torch.float32)
+        s_next, reward, action, term, obs3 = self.layout.unpack_gathered(gathered_row, self.world)
         s = self.prev
         done = term != 0
         fresh = self.first.expand_as(s_next).clone()
         if obs3 is not None:
             fresh[:, 3] = obs3
         self.prev = torch.where(done[:, None], fresh, s_next)
-        self.rudder = torch.where(done, torch.zeros_like(rud), rud)
-        self.fuel = torch.where(done, torch.full_like(fuel, self.fuel0), fuel)
-        return s, action.clone(), reward.clone(), s_next, term.clone()
+        return s, action.clone(), reward.clone(), s_next.clone(), term.clone()
 
 
 def gather_records(record: torch.Tensor, out: torch.Tensor | None = None, group=None) -> torch.Tensor:
@@ -298,3 +275,66 @@ def shard_owner(rows, cntr: int, mem_size: int, period: int, n_per_rank: int):
     rows = np.asarray(rows, dtype=np.int64)
     s = rows + mem_size * ((cntr - 1 - rows) // mem_size)
     return (s % period) // n_per_rank
+
+
+class SegmentExchange:
+    """The replay exchange of a segment, run on a side stream while the next segment steps.
+
+    ``sampler`` is a ``sacenv.replay.StagedReplay`` (or anything with ``rows(g)``,
+    ``begin(obs)`` and ``sample_segment(g)``): segment g's step launch writes its
+    transition rows into ``rows(g)``; ``after(g)`` then enqueues the segment's
+    learns' sampling -- terminal scan, index draws, gather, and the one SUM
+    all-reduce over the ranks -- on the side stream, behind the segment.
+    ``before(g)`` makes the stepping stream wait for ``after(g - 2)``, whose
+    gather still reads the buffer segment g is about to overwrite (three
+    buffers: the sampling of segment g overlaps segment g + 1). Segments are
+    counted from ``start`` (the replay buffer starts empty there)."""
+
+    def __init__(self, sampler, device):
+        self.sampler = sampler
+        self.device = torch.device(device)
+        self.cuda = self.device.type == "cuda"
+        self.side = torch.cuda.Stream(device=self.device) if self.cuda else None
+        self.g = 0               # segments exchanged so far
+        self.started = False
+        self._done = {}
+        self.exchanges = 0
+        self.last = None         # the batches of the latest segment
+
+    def _cur(self):
+        return torch.cuda.current_stream(self.device) if self.cuda else None
+
+    def start(self, obs: torch.Tensor) -> None:
+        """The obs every env starts from (the s of the first stored transition)."""
+        self.sampler.begin(obs)
+        self.started, self.g = True, 0
+
+    def rows(self) -> torch.Tensor:
+        """The row buffer of the segment about to be stepped."""
+        return self.sampler.rows(self.g)
+
+    def before(self) -> None:
+        ev = self._done.pop(self.g - 2, None)
+        if ev is not None:
+            self._cur().wait_event(ev)
+
+    def after(self) -> None:
+        g = self.g
+        if self.cuda:
+            self.side.wait_stream(self._cur())
+            with torch.cuda.stream(self.side):
+                self.last = self.sampler.sample_segment(g)
+                ev = torch.cuda.Event()
+                ev.record(self.side)
+            self._done[g] = ev
+        else:
+            self.last = self.sampler.sample_segment(g)
+        self.g += 1
+        self.exchanges += 1
+
+    def wait(self) -> None:
+        """The stepping stream waits for every exchange in flight."""
+        if self.cuda:
+            for ev in self._done.values():
+                self._cur().wait_event(ev)
+        self._done.clear()

@@ -190,11 +190,12 @@ class ShardedReplayBuffer(DeviceReplayBuffer):
         return self.sample_many(batch_size, 1)[0]
 
     def sample_many(self, batch_size: int, n_batches: int):
-        """``n_batches`` consecutive sample_buffer calls (the batches of that many
-        ``learn()`` calls, e.g. one per step of a segment) assembled with ONE SUM
-        all-reduce: the same batches, in the same order, as ``n_batches`` ``sample``
-        calls (the index draws continue the buffer's one MT19937 stream), for one
-        collective's latency instead of ``n_batches``."""
+        """``n_batches`` consecutive sample_buffer calls with NO stores between them,
+        assembled with ONE SUM all-reduce: the same batches, in the same order, as
+        ``n_batches`` ``sample`` calls at this mem_cntr (the index draws continue the
+        buffer's one MT19937 stream), for one collective's latency instead of
+        ``n_batches``. (The reference's loop stores a step's rows before each learn();
+        ``StagedReplay`` samples a segment's learns with the buffer each of them saw.)"""
         import torch.distributed as dist
         B, n = int(batch_size), int(n_batches)
         if n < 1:
@@ -202,34 +203,156 @@ class ShardedReplayBuffer(DeviceReplayBuffer):
         if self.mem_cntr == 0 and B > 0:
             raise ValueError("a must be greater than 0 unless no samples are taken")
         D, A = int(np.prod(self.input_shape)), self.n_actions
-        # per batch, 32-bit words: reward (f64 = 2 words, first: 8-B aligned), state,
-        # new_state, action (f32), terminal; each block padded to an even word count
-        per = B * (2 * D + A + 3)
-        per += per & 1
-        words = torch.zeros(n * per, dtype=torch.int32, device=self.device)
+        words, views = _packed_batches(B, n, D, A, self.input_shape, self.device)
         tm = torch.empty(B, dtype=torch.uint8, device=self.device)
-        views = []
-        for i in range(n):
-            w = words[i * per: (i + 1) * per]
-            rw = w[: 2 * B].view(torch.float64)
-            o = 2 * B
-            st = w[o: o + B * D].view(torch.float32).view(B, *self.input_shape)
-            o += B * D
-            ns = w[o: o + B * D].view(torch.float32).view(B, *self.input_shape)
-            o += B * D
-            ac = w[o: o + B * A].view(torch.float32).view(B, A)
-            o += B * A
-            tm32 = w[o: o + B]
-            idx = torch.empty(B, dtype=torch.int64, device=self.device)
+        for st, ac, rw, ns, tm32, idx in views:
             _lib.check(self.lib.sacenv_replay_sample_shard(
                 self._pp, self.arena.data_ptr(), B, self.mem_cntr, self.offset, self.n, self.period,
                 idx.data_ptr(), st.data_ptr(), ac.data_ptr(), rw.data_ptr(), ns.data_ptr(), tm.data_ptr(),
                 self.stream))
             tm32.copy_(tm.to(torch.int32))
-            views.append((st, ac, rw, ns, tm32, idx))
         if self.world > 1:
             dist.all_reduce(words, op=dist.ReduceOp.SUM, group=self.group)
         return [(st, ac, rw, ns, tm32.to(torch.bool), idx) for st, ac, rw, ns, tm32, idx in views]
+
+
+def _packed_batches(B: int, n: int, D: int, A: int, shape, device):
+    """n batches packed as 32-bit words, per batch: reward (f64 = 2 words, first:
+    8-B aligned), state, new_state, action (f32), terminal (one word per row);
+    each block padded to an even word count. Returns (words, [(st, ac, rw, ns,
+    tm32, idx)] views)."""
+    per = B * (2 * D + A + 3)
+    per += per & 1
+    words = torch.zeros(n * per, dtype=torch.int32, device=device)
+    views = []
+    for i in range(n):
+        w = words[i * per: (i + 1) * per]
+        rw = w[: 2 * B].view(torch.float64)
+        o = 2 * B
+        st = w[o: o + B * D].view(torch.float32).view(B, *shape)
+        o += B * D
+        ns = w[o: o + B * D].view(torch.float32).view(B, *shape)
+        o += B * D
+        ac = w[o: o + B * A].view(torch.float32).view(B, A)
+        o += B * A
+        tm32 = w[o: o + B]
+        idx = torch.empty(B, dtype=torch.int64, device=device)
+        views.append((st, ac, rw, ns, tm32, idx))
+    return words, views
+
+
+class StagedReplay:
+    """The pooled replay buffer of main.py:78-90 -- every rank's envs storing one
+    transition each per step into ONE agent/buffer.py ring (``ReplayBuffer(mem_size)``,
+    buffer.py:13-22) and one ``learn()`` sampling it after every step (buffer.py:24-35)
+    -- sampled straight out of the segments of transition rows the persistent step
+    launch writes (``sacenv_boat_segment``'s ``trans``), with no ring and no store.
+
+    Segment g's steps write their rows into ``rows(g)`` (one of ``n_buffers``
+    [seg][row] buffers; ``row = _lib.trans_bytes(exp) * n_pad``). ``sample_segment(g)``
+    then enqueues, on the current stream: the reference's stored terminal of every
+    row (``sacenv_replay_stage_terminal``: main.py:83-88 with the persistent
+    ``info['termination']``), the seg learns' index draws (np.random.choice on the
+    buffer's MT19937 stream, seeded like ``np.random.seed(seed)``, each learn with the
+    mem_cntr it saw), the gather of this rank's sampled rows from segments g and g-1,
+    and (world > 1) ONE SUM all-reduce of the packed batches -- the pooled buffer's
+    batches, bit for bit, on every rank (tests/test_staged_replay_gpu.py). Per
+    segment ~27 MB cross the links at batch 1 024, whatever the world size, where
+    the all-gather moves every transition to every rank.
+
+    Buffer reuse: ``sample_segment(g)`` reads rows(g) and rows(g-1), so segment
+    g+2 (which writes rows(g-1) with 3 buffers) must not start before it is done
+    (``done(g)``); with 3 buffers the sampling of segment g overlaps segment g+1."""
+
+    def __init__(self, n: int, n_pad: int, experiment: int, first_obs, *, rank: int = 0, world: int = 1,
+                 mem_size: int = 1_000_000, batch: int = 1024, seg: int = 256, seed: int = 0,
+                 device=None, group=None, n_buffers: int = 3, terminal_mask: int = TERMINAL_GOAL):
+        self.lib = _lib.load()
+        self.device = torch.device(device if device is not None else "cuda")
+        if self.device.type != "cuda":
+            raise RuntimeError("StagedReplay runs on a GPU (HIP); no CPU path")
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        if n_buffers < 3:
+            raise ValueError("the sampling of segment g reads two buffers while g+1 writes a third")
+        self.n, self.n_pad, self.seg, self.batch = int(n), int(n_pad), int(seg), int(batch)
+        self.rank, self.world, self.group = int(rank), int(world), group
+        self.mem_size = int(mem_size)
+        sp = _lib.StagedParams()
+        sp.period, sp.offset = self.world * self.n, self.rank * self.n
+        sp.n, sp.n_pad, sp.seg, sp.experiment = self.n, self.n_pad, self.seg, int(experiment)
+        fo = np.asarray(first_obs.cpu() if isinstance(first_obs, torch.Tensor) else first_obs,
+                        np.float32).reshape(_lib.OBS_DIM)
+        for k in range(_lib.OBS_DIM):
+            sp.first_obs[k] = float(fo[k])
+        if self.mem_size > self.seg * sp.period:
+            raise ValueError(f"mem_size {self.mem_size} > seg * period = {self.seg * sp.period}: a learn could "
+                             "reach rows older than the previous segment")
+        self.sp, self._spp = sp, C.byref(sp)
+        self.period = int(sp.period)
+        # the sampling stream lives in a replay arena (its key / pos fields)
+        self._rb = DeviceReplayBuffer(self.mem_size, (_lib.OBS_DIM,), 1, device=self.device, seed=seed,
+                                      reward_f32=True, terminal_mask=terminal_mask)
+        self.row_bytes = _lib.trans_bytes(experiment) * self.n_pad
+        self.buffers = [torch.zeros(self.seg * self.row_bytes, dtype=torch.uint8, device=self.device)
+                        for _ in range(n_buffers)]
+        self.terminal = [torch.zeros(self.seg * self.n_pad, dtype=torch.uint8, device=self.device)
+                         for _ in range(n_buffers)]
+        self.last_term = torch.zeros(self.n, dtype=torch.uint8, device=self.device)
+        self._words = [_packed_batches(self.batch, self.seg, _lib.OBS_DIM, 1, (_lib.OBS_DIM,), self.device)
+                       for _ in range(2)]
+        self._idx = [torch.empty(self.seg * self.batch, dtype=torch.int64, device=self.device) for _ in range(2)]
+        self._events = {}
+
+    @property
+    def stream(self) -> int:
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def rows(self, g: int) -> torch.Tensor:
+        """Segment g's row buffer: step j of the segment writes row j (stride ``row_bytes``)."""
+        return self.buffers[int(g) % len(self.buffers)]
+
+    def begin(self, reset_obs: torch.Tensor) -> None:
+        """Before segment 0: the obs every env starts from (the s of step 0) go into the
+        last row of the buffer standing for segment -1, with term 0."""
+        b = self.rows(-1)
+        last = b[(self.seg - 1) * self.row_bytes: self.seg * self.row_bytes]
+        np_ = self.n_pad
+        last.zero_()
+        last[: 44 * np_].view(torch.float32).view(np_, _lib.OBS_DIM)[: self.n].copy_(
+            reset_obs.to(device=self.device, dtype=torch.float32))
+        self.terminal[(-1) % len(self.buffers)].zero_()
+        self.last_term.zero_()
+
+    def sample_segment(self, g: int, n_batches: int | None = None):
+        """Enqueue segment g's learns' batches (after its steps were enqueued on this
+        stream); returns [(state, action, reward f64, new_state, terminal bool, idx)],
+        one per learn, views that stay valid until ``sample_segment(g + 2)``."""
+        import torch.distributed as dist
+        g = int(g)
+        nb = self.seg if n_batches is None else int(n_batches)
+        words, views = self._words[g % 2]
+        idx = self._idx[g % 2]
+        nbuf = len(self.buffers)
+        cur, prev = g % nbuf, (g - 1) % nbuf
+        rp = self._rb._pp
+        _lib.check(self.lib.sacenv_replay_stage_terminal(rp, self._spp, self.buffers[cur].data_ptr(), self.seg,
+                                                         self.last_term.data_ptr(), self.terminal[cur].data_ptr(),
+                                                         self.stream))
+        _lib.check(self.lib.sacenv_replay_sample_staged(
+            rp, self._rb.arena.data_ptr(), self._spp, g, self.buffers[cur].data_ptr(), self.terminal[cur].data_ptr(),
+            self.buffers[prev].data_ptr(), self.terminal[prev].data_ptr(), self.batch, nb, idx.data_ptr(),
+            words.data_ptr(), self.stream))
+        if self.world > 1:
+            dist.all_reduce(words, op=dist.ReduceOp.SUM, group=self.group)
+        B = self.batch
+        return [(st, ac, rw, ns, tm32.to(torch.bool), idx[i * B: (i + 1) * B])
+                for i, (st, ac, rw, ns, tm32, _) in enumerate(views[:nb])]
+
+    @property
+    def bytes_per_segment(self) -> int:
+        """The all-reduce payload of one segment's batches."""
+        return int(self._words[0][0].numel()) * 4
 
 
 class ReplayBuffer:
@@ -267,4 +390,4 @@ class ReplayBuffer:
                 rewards.cpu().numpy(), states_.cpu().numpy().astype(np.float64), dones.cpu().numpy())
 
 
-__all__ = ["DeviceReplayBuffer", "ReplayBuffer", "TERMINAL_GOAL"]
+__all__ = ["DeviceReplayBuffer", "ReplayBuffer", "ShardedReplayBuffer", "StagedReplay", "TERMINAL_GOAL"]

@@ -239,8 +239,8 @@ class VecBoatEnv:
         self._after_step()
 
     def step_pooled_async(self, actions: torch.Tensor, trans_row: torch.Tensor) -> None:
-        """``step_async`` that also writes the step's transition row (s' entries 0..8,
-        reward, action, term, and obs3_next in experiment 2; ``sacenv_boat_step_pooled``,
+        """``step_async`` that also writes the step's transition row (s', reward,
+        action, term, and obs3_next in experiment 2; ``sacenv_boat_step_pooled``,
         ``sacenv.dist.TransitionLayout``) into ``trans_row``, a 16-B aligned uint8
         device tensor of ``_lib.trans_bytes(experiment) * n_pad`` bytes (e.g. a row
         of a pooling buffer: no copy launches)."""

@@ -9,6 +9,8 @@ N>1 segment pooling -- with a stub workload at world sizes 1 and 2 (gloo).
 import json
 import os
 import socket
+import subprocess
+import sys
 
 import pytest
 import torch
@@ -17,42 +19,12 @@ import torch.multiprocessing as mp
 
 from conftest import ROOT
 
-N_ENVS, N_PAD = 70, 128
-
-
-class _StubEnv:
-    """Stands in for VecBoatEnv: the record / terminal-obs regions the pool reads."""
-
-    def __init__(self, rank):
-        self.num_envs, self.n_pad = N_ENVS, N_PAD
-        self.record = torch.zeros(50 * N_PAD, dtype=torch.uint8)
-        self.final_obs_bytes = torch.zeros(44 * N_PAD, dtype=torch.uint8)
-        self.rank, self.steps, self.refills, self.refill_at = rank, 0, 0, []
-
-    def step_async(self, actions):
-        assert actions.dtype == torch.float32 and actions.numel() == N_ENVS
-        self.steps += 1
-        self.record.fill_((self.steps + 31 * self.rank) % 251)
-        self.final_obs_bytes.fill_((self.steps * 7 + self.rank) % 253)
-
-    def refill(self):
-        self.refills += 1
-        self.refill_at.append(self.steps)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+from bench_stub import N_PAD, workload as _stub_workload  # noqa: E402
 
 
 def _workload(bench, rank):
-    from sacenv.dist import TransitionLayout
-    env = _StubEnv(rank)
-    actions = torch.rand((bench.ACTION_STEPS, N_ENVS), generator=torch.Generator().manual_seed(rank))
-    lay = TransitionLayout(N_ENVS, N_PAD)
-
-    def pooled_step(k, row):
-        assert row.numel() == lay.nbytes
-        env.step_async(actions[k % bench.ACTION_STEPS])
-        row.fill_((env.steps * 3 + rank) % 255)
-
-    return env, bench.Workload([env], env.step_async, env.refill, actions, pooled_step, lay.nbytes,
-                               N_ENVS, bench.BYTES_PER_ENV_STEP * N_ENVS)
+    return _stub_workload(bench, rank)
 
 
 def _run(rank, world, argv):
@@ -100,7 +72,7 @@ def _free_port():
     return p
 
 
-def _dist_worker(rank, world, port, q):
+def _dist_worker(rank, world, port, q, extra):
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "sac-agent_amd"))
@@ -108,40 +80,83 @@ def _dist_worker(rank, world, port, q):
                       WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        out, env = _run(rank, world, ["--gpus", str(world), "--steps", "20", "--warmup", "5"])
+        out, env = _run(rank, world, ["--gpus", str(world), "--steps", "20", "--warmup", "5", "--stub",
+                                      "--replay-batch", "64", *extra])
         q.put((rank, out, env.steps, env.refills))
     finally:
         dist.destroy_process_group()
 
 
-def test_driver_command_world2_gloo_segment_pooling():
-    """The N>1 path (SegmentPool of full transitions) with the driver's short command."""
+def _world2(extra):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_dist_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_dist_worker, args=(r, world, port, q, extra)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted((q.get(timeout=300) for _ in range(world)), key=lambda x: x[0])
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    out = res[0][1]
     assert res[1][1] is None
+    for _, _, steps, refills in res:
+        assert steps % 256 == 0 and refills == steps // 256
+    return res[0][1]
+
+
+def test_driver_command_world2_gloo_segment_gather():
+    """The all-gather pooling (--pooling gather) with the driver's short command."""
+    out = _world2(["--pooling", "gather"])
     assert out["steps"] == 8 * 256 and out["n_gpus"] == 2
     assert out["value"] > 0
     assert "8 in the timed region" in out["config"]["collective"]
     assert "gloo" in out["config"]["collective"]
-    # the row is the step kernel's 45-B/env transition row
-    assert f"{45 * N_PAD} B per rank-step" in out["config"]["collective"]
-    assert out["pooling"]["received_bytes_per_rank"] == (world - 1) * 45 * N_PAD * out["steps"]
-    assert out["pooling"]["received_GBps_per_rank"] > 0
-    # the no-exchange rate of the same segments, measured after the timed region
-    ne = out["pooling"]["no_exchange"]
-    sh = ne["sharded_exchange"]     # one all-reduce of a segment's 256 learn() batches
-    assert sh["bytes_per_segment"] == 256 * 1024 * 26 * 4 and sh["allreduce_ms_per_segment"] > 0
-    assert 0 < sh["value"] < ne["value"] * 1.01
+    # the row is the step kernel's 53-B/env transition row
+    assert f"{53 * N_PAD} B per rank-step" in out["config"]["collective"]
+    po = out["pooling"]
+    assert po["mode"] == "gather" and po["received_bytes_per_rank"] == 53 * N_PAD * out["steps"]
+    assert po["received_GBps_per_rank"] > 0
+    ne = po["no_exchange"]     # the no-exchange rate of the same segments, after the timed region
     assert ne["value"] > 0 and ne["steps"] % 256 == 0 and ne["ms_per_step"] > 0
-    for _, _, steps, refills in res:
-        assert steps % 256 == 0 and refills == steps // 256
+
+
+def test_driver_command_world2_gloo_sharded_exchange():
+    """The default N>1 pooling: each segment's rows staged per rank and the segment's
+    learn() batches exchanged with one all-reduce, inside the timed region; the
+    all-gather and no-exchange rates measured beside it."""
+    out = _world2([])
+    assert out["steps"] == 8 * 256 and out["n_gpus"] == 2 and out["value"] > 0
+    po = out["pooling"]
+    assert po["mode"] == "sharded" and po["exchanges_timed"] == 8
+    assert po["bytes_per_segment"] == 256 * 64 * 26 * 4
+    assert "8 in the timed region" in out["config"]["collective"] and "all_reduce" in out["config"]["collective"]
+    assert po["xgmi"]["GBps_per_rank"] > 0
+    ag = po["all_gather"]
+    assert ag["value"] > 0 and ag["received_bytes_per_rank"] == 53 * N_PAD * ag["steps"]
+    assert po["no_exchange"]["value"] > 0
+    assert out["data"].startswith("stub")
+
+
+def test_bench_self_launches_its_ranks():
+    """python bench.py --gpus 2 with no launcher (WORLD_SIZE unset): bench starts its two
+    rank processes itself; rank 0 prints the one JSON line."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--stub", "--steps", "20",
+                        "--warmup", "5", "--replay-batch", "32", "--exchange-segs", "1"],
+                       capture_output=True, text=True, env=env, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["pooling"]["mode"] == "sharded" and out["value"] > 0
+
+
+def test_bench_self_launch_fails_loudly():
+    """Ranks that die end the run with a non-zero status and no line."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--stub",
+                        "--pooling", "gather", "--pool-every", "7"], capture_output=True, text=True, env=env,
+                       timeout=300, cwd=ROOT)
+    assert r.returncode != 0 and "must divide" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

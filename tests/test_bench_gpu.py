@@ -32,7 +32,13 @@ def test_driver_bench_command():
     # every captured graph (4 action-table segments) ran once before the warm-up
     assert d["setup"]["graph_first_replays"] == 512
     rf = d["roofline"]
-    assert rf["bound"] == "hbm" and 0 < rf["frac"] < 1 and rf["kernel_avg_us"] > 0
+    # the persistent step is bound by FP64 instruction issue (PMC: profiles/*pmc_segment.json);
+    # the byte figures stay beside it
+    assert rf["bound"] == "fp64-issue" and rf["unit"] == "TFLOP/s" and 0 < rf["frac"] < 1
+    assert 0 < rf["issue_floor_frac"] <= 1.05 and rf["kernel_avg_us"] > 0
+    assert 0 < rf["hbm"]["frac"] < 1 and rf["hbm"]["unit"] == "GB/s"
+    # the N>1 replay path at one GPU, measured on the same line
+    assert d["replay_path"]["value"] > 0 and d["every_output"]["value"] > 0
     if rf["kernel"].startswith("k_rollout"):  # the persistent launch: resident-state bytes headline
         assert abs(rf["bytes_per_env_step"] - (70 + 152 / 256)) < 1e-9
         assert rf["survey_222B"]["bytes_per_env_step"] == 222
@@ -44,25 +50,45 @@ def test_driver_bench_command():
         assert d["metric"] == json.load(f)["metric"]
 
 
+def _two_rank_env():
+    return dict(os.environ, SACENV_BENCH_BACKEND="gloo", SACENV_BENCH_ONE_DEVICE="1")
+
+
 @pytest.mark.gpu
 def test_bench_two_ranks_gloo_on_one_device():
-    """The N>1 bench path (segment pooling of the kernel-written transition rows, max-over-
-    ranks timing) as two processes sharing the one GPU over gloo, under the launcher the
-    driver uses (torch.distributed.run). RCCL needs one device per rank; the driver's
-    8-GPU run is the RCCL one."""
+    """The N>1 bench path (the staged replay exchange of the kernel-written transition rows,
+    max-over-ranks timing; the all-gather beside it) as two processes sharing the one GPU
+    over gloo, under the launcher the driver uses (torch.distributed.run). RCCL needs one
+    device per rank; the driver's 8-GPU run is the RCCL one."""
     import socket
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    env = dict(os.environ, SACENV_BENCH_BACKEND="gloo", SACENV_BENCH_ONE_DEVICE="1")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
                         "--gpus", "2", "--steps", "20", "--warmup", "5", "--envs", "8192"],
-                       capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+                       capture_output=True, text=True, timeout=600, cwd=ROOT, env=_two_rank_env())
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert d["n_gpus"] == 2 and d["steps"] == 8 * 256 and d["value"] > 0
     assert d["config"]["global_envs"] == 2 * 8192
-    assert "gloo all_gather per 256-step segment (8 in the timed region)" in d["config"]["collective"]
-    assert "45-B/env transition row" in d["config"]["collective"]
+    c = d["config"]["collective"]
+    assert "gloo SUM all_reduce" in c and "(8 in the timed region)" in c and "53-B/env transition row" in c
+    po = d["pooling"]
+    assert po["mode"] == "sharded" and po["exchanges_timed"] == 8
+    assert po["all_gather"]["value"] > 0 and po["no_exchange"]["value"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_self_launch_two_ranks_on_one_device():
+    """``python bench.py --gpus 2`` with no launcher: bench starts its own two ranks."""
+    env = {k: v for k, v in _two_rank_env().items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "20",
+                        "--warmup", "5", "--envs", "4096", "--exchange-segs", "1"],
+                       capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["pooling"]["mode"] == "sharded" and d["value"] > 0

@@ -925,11 +925,10 @@ def test_c5_mixed_32768_each_vs_oracles(gpu, built_lib):
 
 @pytest.mark.parametrize("exp", [2, 6])
 def test_step_pooled_row_equals_step_outputs(exp, gpu, built_lib):
-    """sacenv_boat_step_pooled = sacenv_boat_step (arena bit-identical) + the 45-B
-    transition row: s' entries 0..8 = the pre-reset obs (final_obs where done),
-    reward, action, term, obs3_next = the new episode's obs[3] (experiment 2);
-    TransitionStream rebuilds s' (rudder and fuel entries included) and each next s
-    (the returned obs) bit-exactly from consecutive rows."""
+    """sacenv_boat_step_pooled = sacenv_boat_step (arena bit-identical) + the 53-B
+    transition row: s' = the pre-reset obs (final_obs where done), reward, action,
+    term, obs3_next = the new episode's obs[3] (experiment 2); TransitionStream
+    rebuilds each next s (the returned obs) bit-exactly from consecutive rows."""
     from sacenv import VecBoatEnv, _lib
     from sacenv.dist import TransitionLayout, TransitionStream
     cfg = {"base_settings": {"experiment": exp, "test_mode": 0}, "boat_env": {"track_width": 30}}
@@ -941,7 +940,7 @@ def test_step_pooled_row_equals_step_outputs(exp, gpu, built_lib):
     lay = TransitionLayout(N, b_env.n_pad, exp)
     row = torch.empty(lay.nbytes, dtype=torch.uint8, device=gpu)
     stream = TransitionStream(lay, 1, obs0, b_env.first_obs_template())
-    assert lay.nbytes == (49 if exp == 2 else 45) * b_env.n_pad
+    assert lay.nbytes == (57 if exp == 2 else 53) * b_env.n_pad
     g = torch.Generator(device=gpu)
     g.manual_seed(5)
     ended = 0
@@ -951,17 +950,16 @@ def test_step_pooled_row_equals_step_outputs(exp, gpu, built_lib):
         b_env.step_pooled_async(act, row)
         torch.cuda.synchronize()
         assert torch.equal(a_env.arena, b_env.arena), f"step {k}"
-        s9, rew, ac, term, obs3 = lay.views(row)
+        sp, rew, ac, term, obs3 = lay.views(row)
         d = a_env.done.bool()
         assert torch.equal(term != 0, d) and torch.equal(term, a_env.term)
         assert torch.equal(rew, a_env.reward) and torch.equal(ac, act)
-        assert torch.equal(s9[d], a_env.final_obs[d][:, :9]) and torch.equal(s9[~d], a_env.obs[~d][:, :9])
+        assert torch.equal(sp[d], a_env.final_obs[d]) and torch.equal(sp[~d], a_env.obs[~d])
         if exp == 2:
             assert torch.equal(obs3[d], a_env.obs[d][:, 3])
         else:
             assert obs3 is None
         s, a2, r2, sn, code = stream.push(row)
-        # the rebuilt s' (rudder and fuel entries from the actions / steps) is the kernel's, bit for bit
         assert torch.equal(sn[d], a_env.final_obs[d]) and torch.equal(sn[~d], a_env.obs[~d]), f"step {k}: s'"
         assert torch.equal(stream.prev, a_env.obs), f"step {k}: rebuilt next s"
         ended += int(d.sum())

@@ -34,12 +34,34 @@ def declared_functions():
 def test_library_exports_header(built_lib):
     from sacenv import _lib
     names = declared_functions()
-    assert len(names) == 37
+    assert len(names) == 39
     assert set(names) == set(_lib.EXPORTS)
     for n in names:
         assert hasattr(built_lib, n), n
     assert built_lib.sacenv_abi_version() == _lib.ABI_VERSION
     assert built_lib.sacenv_error_string(-2).decode().startswith("Well someone")
+
+
+def test_staged_sampler_argument_errors_without_gpu(built_lib):
+    """sacenv_replay_stage_terminal / _sample_staged validate on the host, never launching."""
+    from sacenv import _lib
+    rp = _lib.ReplayParams(mem_size=1_000_000, obs_dim=11, act_dim=1, reward_f32=1, terminal_mask=2)
+    sp = _lib.StagedParams(period=4096, offset=0, n=4096, n_pad=4096, seg=256, experiment=6)
+    R, S = ctypes.byref(rp), ctypes.byref(sp)
+    args = (1, 1, 1, 1, 1024, 256, 1, 1, None)
+    sp.period = sp.n = sp.n_pad = 64      # mem_size > seg * period: a learn could reach older rows
+    assert built_lib.sacenv_replay_sample_staged(R, 1, S, 0, *args) == -5
+    sp.period = sp.n = sp.n_pad = 4096
+    rp.obs_dim = 10                       # the boat's rows only
+    assert built_lib.sacenv_replay_sample_staged(R, 1, S, 0, *args) == -4
+    rp.obs_dim = 11
+    sp.n_pad = 4000                       # not a multiple of 64
+    assert built_lib.sacenv_replay_stage_terminal(R, S, 1, 256, 1, 1, None) == -4
+    sp.n_pad, sp.offset = 4096, 1         # offset + n > period
+    assert built_lib.sacenv_replay_stage_terminal(R, S, 1, 256, 1, 1, None) == -5
+    sp.offset = 0
+    assert built_lib.sacenv_replay_stage_terminal(R, S, None, 256, 1, 1, None) == -1
+    assert built_lib.sacenv_replay_sample_staged(R, None, S, 0, *args) == -1
 
 
 def test_argument_errors_without_gpu(built_lib):

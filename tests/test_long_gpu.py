@@ -139,19 +139,19 @@ def _check_segment_outputs(name, z, env, rows, seg_state):
     keep = {int(k): j for j, k in enumerate(z["keep"])}
     term = np.empty((E, S), np.uint8)
     rew = np.empty((E, S), np.float32)
-    s9 = {}
+    sp = {}
     for k in range(S):
         v = lay.views(rows[k])
         term[:, k] = v[3].numpy()
         rew[:, k] = v[1].numpy()
         if k in keep:
-            s9[keep[k]] = v[0].numpy()
+            sp[keep[k]] = v[0].numpy()
     for e in range(E):
         bad = np.flatnonzero(term[e] != z["term"][e])
         assert bad.size == 0, f"{name} env {e}: term differs first at step {bad[:1]}"
     np.testing.assert_allclose(rew, z["reward"], rtol=OBS_TOL, atol=1e-5)
-    for j, o in s9.items():
-        np.testing.assert_allclose(o, z["obs"][:, j, :9], rtol=OBS_TOL, atol=OBS_TOL,
+    for j, o in sp.items():
+        np.testing.assert_allclose(o, z["obs"][:, j, :], rtol=OBS_TOL, atol=OBS_TOL,
                                    err_msg=f"{name} step {z['keep'][j]}")
     fields = [str(f) for f in z["state_fields"]]
     cols = [fields.index(f) for f in CARRIED]

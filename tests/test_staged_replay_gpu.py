@@ -1,0 +1,130 @@
+"""StagedReplay: the pooled replay buffer sampled out of staged segments.
+
+The reference loop (main.py:78-90) stores every env's transition (buffer.py:13-22)
+and runs one learn() -- sample_buffer(batch), buffer.py:24-35 -- after EVERY step,
+each on the buffer as that step left it. StagedReplay draws a segment's learns
+after the segment from the transition rows the persistent launch wrote
+(sacenv_boat_segment's ``trans``), with no ring. The reference side here is the
+literal loop on the device: a VecBoatEnv stepped one launch at a time, a
+DeviceReplayBuffer fed every step (store_env_step: the reference's persistent
+terminal rule, new_state = the terminal obs of envs that reset) and sampled
+after every step. Batches and indices must agree bit for bit, across the ring's
+wrap (mem_size not a multiple of the rows per step), ranges below mem_size at
+the start, learns skipped while fewer rows than a batch are stored, auto-resets
+(experiment 2's start-y obs entry included) and, over two gloo ranks sharing the
+box's GPU, the SUM all-reduce of the ranks' shares.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+SEG = 64
+
+
+def _cfg(exp):
+    return {"base_settings": {"experiment": exp, "test_mode": 0}, "boat_env": {"track_width": 30}}
+
+
+def _run(rank, world, exp, N, M, B, n_segs, dev, group=None):
+    """Returns (n learns checked, n skipped) on rank 0 (None elsewhere)."""
+    from sacenv import VecBoatEnv
+    from sacenv.replay import DeviceReplayBuffer, StagedReplay
+    kw = dict(seed=3, device=dev, max_episode_steps=40, n_helpers=64, auto_refill=False)
+    env = VecBoatEnv(_cfg(exp), N, env_id_offset=rank * N, **kw)
+    obs0 = env.reset().clone()
+    rep = StagedReplay(N, env.n_pad, exp, env.first_obs_template(), rank=rank, world=world, mem_size=M,
+                       batch=B, seg=SEG, seed=5, device=dev, group=group)
+    rep.begin(obs0)
+    ref = ref_rb = None
+    if rank == 0:
+        ref = VecBoatEnv(_cfg(exp), world * N, **kw)
+        ref.reset()
+        ref_rb = DeviceReplayBuffer(M, (11,), 1, device=dev, seed=5)
+    g = torch.Generator(device=dev)
+    g.manual_seed(9)
+    checked = skipped = 0
+    for s in range(n_segs):
+        acts = torch.rand((SEG, world * N), generator=g, device=dev) * 2 - 1
+        mine = acts[:, rank * N:(rank + 1) * N].contiguous()
+        env.segment_async(mine, SEG, trans=rep.rows(s), trans_stride=rep.row_bytes)
+        env.refill()
+        got = rep.sample_segment(s)
+        if ref is None:
+            continue
+        for k in range(SEG):
+            prev = ref.obs.clone()
+            ref.step(acts[k].contiguous())
+            ref_rb.store_env_step(prev, acts[k].contiguous(), ref)
+            st, ac, rw, ns, tm, idx = got[k]
+            if ref_rb.mem_cntr < B:     # continuous_agent.learn returns before sampling
+                torch.cuda.synchronize()
+                assert bool((idx == -1).all()) and not bool(st.any()), (s, k)
+                skipped += 1
+                continue
+            want = ref_rb.sample(B)
+            torch.cuda.synchronize()
+            assert torch.equal(idx, want[5]), f"segment {s} learn {k}: indices"
+            for i, (x, y) in enumerate(zip((st, ac, rw, ns, tm), want[:5])):
+                assert torch.equal(x.reshape(-1), y.reshape(-1).to(x.dtype)), (s, k, i)
+            checked += 1
+        ref.refill()
+    torch.cuda.synchronize()
+    env.check_status()
+    return (checked, skipped) if rank == 0 else None
+
+
+@pytest.mark.parametrize("exp,N,M,B", [(6, 3000, 50_021, 256), (2, 2000, 40_000, 511), (6, 700, 20_000, 1024)])
+def test_staged_replay_equals_per_step_learns(exp, N, M, B, gpu, built_lib):
+    checked, skipped = _run(0, 1, exp, N, M, B, 4, gpu)
+    assert checked + skipped == 4 * SEG
+    assert skipped == (1 if N < B else 0)
+
+
+def test_staged_replay_refuses_a_ring_older_than_one_segment(gpu, built_lib):
+    from sacenv.replay import StagedReplay
+    with pytest.raises(ValueError):
+        StagedReplay(100, 128, 6, torch.zeros(11), mem_size=SEG * 100 + 1, seg=SEG, device=gpu)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "sac-agent_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank, _run(rank, world, 6, 1000, 30_011, 333, 3, torch.device("cuda", 0))))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_staged_replay_two_ranks_equal_pooled_buffer(gpu, built_lib):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert res[0] == (3 * SEG, 0) and res[1] is None, res
