@@ -470,16 +470,19 @@ def make_workload(args, rank: int, dev) -> Workload:
     # the arguments are built right here (table [512, N] f32 contiguous, one flag per owner wave)
     assert actions.is_contiguous() and ready.numel() == env.n_pad // 64
 
-    def segment_step(k0: int, n: int, trans=None):
+    def segment_step(k0: int, n: int, trans=None, stage=None, marks=None):
         # sacenv_boat_segment (VecBoatEnv.segment_async without its per-call Python
         # checks): the timed loop pays one ctypes call
         r0 = k0 % ACTION_STEPS
         assert r0 + n <= ACTION_STEPS
         if trans is not None and trans.numel() < (n - 1) * row_bytes + lay.nbytes:
             raise ValueError("pooled rows buffer too small")
+        if stage is not None and (stage.numel() < n * 64 * env.n_pad or (marks is not None and marks.numel() < n * env.n_pad // 64)):
+            raise ValueError("staged rows / marks buffer too small")
         _lib.check(seg_fn(env._pp, env._ptr, C.c_void_p(a0 + 4 * r0 * astride), astride, n, ready.data_ptr(),
                           None, 0, None if trans is None else trans.data_ptr(),
-                          0 if trans is None else row_bytes, torch.cuda.current_stream(dev).cuda_stream))
+                          0 if trans is None else row_bytes, None if stage is None else stage.data_ptr(),
+                          None if marks is None else marks.data_ptr(), torch.cuda.current_stream(dev).cuda_stream))
 
     if args.mixed:
         # the whole batch as ONE persistent launch per segment (sacenv_mixed_segment: the boat's
@@ -592,11 +595,12 @@ class SegmentRunner:
         """The SEG steps of one segment, enqueued (captured, eager or persistent)."""
         wl, p = self.wl, self.pool if with_pool else None
         x = self.exchange if with_pool else None
-        if x is not None:   # the segment's rows go to the staged replay's buffer
-            rows, rb = x.rows(), wl.row_bytes()
+        if x is not None:   # the segment writes the staged replay's rows
+            sa = x.stage_args()
             if self.mode == "segment":
-                wl.segment_step(k0, SEG, trans=rows)
+                wl.segment_step(k0, SEG, stage=sa["stage"], marks=sa["marks"])
                 return
+            rows, rb = sa["rows"], wl.row_bytes()   # (the CPU stub: pooled rows per step)
             for j, k in enumerate(range(k0, k0 + SEG)):
                 wl.pooled_step(k, rows[j * rb:(j + 1) * rb])
                 if on_step is not None:
@@ -926,9 +930,10 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
         rate, k, _ = timed_rate(xrun, k, max(1, args.exchange_segs), world, dev, wl)
         replay_path = dict(rate, note=(
             f"the N>1 line's replay path at one GPU (--pooling sharded without the collective): each "
-            f"segment's {TRANS_ROW} staged by the segment launch, its {SEG} learn() batches of "
-            f"{args.replay_batch} sampled from the pooled ReplayBuffer({args.replay_mem}) on a side stream "
-            "overlapped with the next segment (StagedReplay), after the timed region, wall time"))
+            f"segment's {SEG} learn() batches of {args.replay_batch} drawn ahead from the pooled "
+            f"ReplayBuffer({args.replay_mem})'s sampling stream, the segment launch writing the 64-B rows they "
+            "read, the batches gathered on a side stream overlapped with the next segment (StagedReplay), "
+            "after the timed region, wall time"))
     dinfo = dist_info(world, dev)
     if rank != 0:
         return None
@@ -952,9 +957,10 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
     if exchange is not None:
         payload = exchange.sampler.bytes_per_segment
         collective = (f"{backend} SUM all_reduce of each {SEG}-step segment's {SEG} learn() batches ({args.replay_batch} "
-                      f"rows, {payload} B) sampled from the pooled ReplayBuffer({args.replay_mem}) of every rank's "
-                      f"envs out of each rank's staged {TRANS_ROW}s (sacenv.replay.StagedReplay, the pooled buffer's "
-                      f"batches bit for bit): one per segment on a side stream, overlapped with the next segment "
+                      f"rows, {payload} B) of the pooled ReplayBuffer({args.replay_mem}) of every rank's envs, "
+                      "gathered from the rows each rank's segment launch staged (sacenv.replay.StagedReplay: the "
+                      "index draws made ahead, only the rows they read written; the pooled buffer's batches bit "
+                      f"for bit): one per segment on a side stream, overlapped with the next segment "
                       f"({exchanges_timed} in the timed region)")
     elif pool is not None:
         collective = (f"all_gather of each step's full transitions (the {TRANS_ROW} written by the step kernel, "
@@ -972,7 +978,7 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
             bus = 2 * (world - 1) / world * payload * exchanges_timed  # a ring all-reduce's bytes per rank
             pooling_out.update({
                 "exchanges_timed": exchanges_timed, "bytes_per_segment": payload,
-                "staged_row_bytes_per_rank_step": wl.row_bytes(),
+                "staged_row_bytes": 64,
                 "allreduce_bus_bytes_per_rank": bus, "xgmi": _xgmi(bus, el_max, world - 1),
                 "all_gather": all_gather,
                 "note": "value = the timed region with this exchange; all_gather and no_exchange are the same "

@@ -74,7 +74,7 @@ enum {
 enum {
   SACENV_OUT_ACCEL = 1,      /* layout.accel: a_x, a_y, a_r of the step (f64) */
   SACENV_OUT_REWARD64 = 2,   /* layout.reward64: reward in f64 */
-  SACENV_OUT_KNOTS = 4       /* layout.knots_raw: drawn knot values per slot */
+  SACENV_OUT_KNOTS = 4       /* layout.knots_raw: drawn knot values per slot (allocated only then) */
 };
 
 /* Everything the hot path reads from the reference config
@@ -140,8 +140,9 @@ typedef struct SacenvBoatLayout {
   int64_t wind_knots;         /* f64 [n_pad][SLOTS][2][n_knots][2]: per episode slot and curve, each
                                  knot's folded value and 2nd derivative / 6 (episode-contiguous:
                                  the refill writes whole lines) */
-  int64_t knots_raw;          /* f64 [n_pad][SLOTS][2][n_knots] drawn knot values (autoreset refills
-                                 always; init / host resets with SACENV_OUT_KNOTS) */
+  int64_t knots_raw;          /* f64 [n_pad][SLOTS][2][n_knots] drawn knot values, only with
+                                 SACENV_OUT_KNOTS (else -1: no storage; a refill's fit reads the drawn
+                                 knots from the slot's own wind_knots y fields) */
   int64_t mt_key;             /* u32 [n_pad][624] per-env MT19937 state */
   int64_t record;             /* u8 [50 n_pad]: obs f32 [n_pad][11] | reward f32 [n_pad]
                                  | done u8 [n_pad] | term u8 [n_pad]  (the all-gather payload) */
@@ -156,6 +157,10 @@ typedef struct SacenvBoatLayout {
                                  [2] envs listed by the last refill */
   int64_t spline_g;           /* f64 [n_knots][n_knots]: (m/6) = G @ knots (written by init) */
   int64_t wind_table;         /* f64 [2][wind_len] (velocity, angle), if use_wind_table */
+  int64_t last_term;          /* i32 [n_pad] info['termination'] as the reference's info dict keeps it:
+                                 the env's last termination code 1..5 (0: none yet); every step
+                                 updates it, resets never clear it (boat_env.py:24-32,84-105,120-126;
+                                 main.py:83 reads it) */
 } SacenvBoatLayout;
 
 /* status bits (layout.status[1]); sticky until the arena is re-initialised */
@@ -281,11 +286,18 @@ int sacenv_boat_rollout(const SacenvBoatParams *p, void *arena, const float *act
  *   reads the rows behind it). The host learns of it from the status bit.
  * trans (nullable, 16-B aligned, trans_stride a multiple of 16): step ks's
  * pooled transition row (sacenv_boat_step_pooled's format) at trans + ks *
- * trans_stride. Counts as n_steps step launches for the refill contract
- * (autoreset: n_steps <= SACENV_REFILL_PERIOD). */
+ * trans_stride. stage (nullable, 16-B aligned, not with trans): the staged
+ * replay rows of sacenv_replay_sample_staged -- step ks, env e at stage + (ks *
+ * n_pad + e) * 64: s' f32 [11] (the obs before any auto-reset), reward f32,
+ * action f32, u32 term | last_term << 8 (last_term: layout.last_term after the
+ * step), obs3_next f32 (experiment 2), 0 -- written only where bit e % 64 of
+ * stage_marks[ks * n_pad / 64 + e / 64] is set (sacenv_replay_stage_mark: the rows
+ * a learn will sample; stage_marks == NULL: every row). Counts as n_steps step
+ * launches for the refill contract (autoreset: n_steps <= SACENV_REFILL_PERIOD). */
 int sacenv_boat_segment(const SacenvBoatParams *p, void *arena, const float *actions, int64_t action_stride,
                         int32_t n_steps, const uint32_t *act_ready, uint32_t *step_done, uint32_t seq0,
-                        void *trans, int64_t trans_stride, void *stream);
+                        void *trans, int64_t trans_stride, void *stage, const uint64_t *stage_marks,
+                        void *stream);
 
 /* Co-residency data for the closed loop (main.py:70-91 on the device): the
  * workgroups per CU the segment launch's kernel can keep resident for these
@@ -308,6 +320,7 @@ int sacenv_boat_segment(const SacenvBoatParams *p, void *arena, const float *act
 int sacenv_stream_create_exclusive(void **stream);
 int sacenv_stream_destroy(void *stream);
 
+/* with_trans: 0 no rows, 1 pooled transition rows, 2 staged replay rows */
 int sacenv_boat_segment_occupancy(const SacenvBoatParams *p, int32_t with_trans, int32_t *blocks_per_cu,
                                   int32_t *grid, int32_t *vgprs, int32_t *lds_bytes);
 
@@ -484,11 +497,10 @@ int sacenv_replay_sample_shard(const SacenvReplayParams *p, void *arena, int32_t
 /* The pooled buffer sampled out of STAGED SEGMENTS (the exchange that scales,
  * DESIGN.md §6): main.py:78-90 with every rank's envs storing their transitions
  * into one ReplayBuffer(mem_size) (buffer.py:13-22) each step and one learn() --
- * sample_buffer(batch), buffer.py:24-35 -- after every step, WITHOUT a ring: a
- * persistent step launch writes each step's transition rows (the
- * sacenv_boat_step_pooled format) into a segment buffer [seg][row] (row =
- * SACENV_TRANS_BYTES(_EXP2) x n_pad), and the segment's learns are sampled from
- * it afterwards. The pooled ring appends `period` = world x n rows per step in
+ * sample_buffer(batch), buffer.py:24-35 -- after every step, WITHOUT a ring: the
+ * index draws are made ahead, the persistent step launch writes the rows they
+ * will read (sacenv_boat_segment's stage: 64 B per step and env), and the
+ * segment's learns are gathered from them afterwards. The pooled ring appends `period` = world x n rows per step in
  * global env order; with mem_size <= seg x period every row learn k of segment
  * g can reach was written in segment g or g - 1, so those two buffers are the
  * ring. Global step numbers: segment g holds steps g*seg .. g*seg + seg - 1. */
@@ -502,33 +514,47 @@ typedef struct SacenvStagedParams {
   float first_obs[SACENV_OBS_DIM]; /* a fresh Boat's obs (boat_env.py:152-198 -> return_state) */
 } SacenvStagedParams;
 
-/* The reference's stored terminal of each row of a segment (main.py:83-88:
- * info['termination'] == 'reached_goal', the info dict keeping the last
- * termination across steps and resets): terminal[j][e] (u8 [seg][n_pad]) =
- * (terminal_mask >> last_term) & 1 after row j's code updated last_term[e]
- * (u8 [n], carried from segment to segment, zero-initialised). Call once per
- * segment, in segment order, before sampling it. */
-int sacenv_replay_stage_terminal(const SacenvReplayParams *p, const SacenvStagedParams *sp, const void *rows,
-                                 int32_t n_steps, uint8_t *last_term, uint8_t *terminal, void *stream);
-/* The batches of the n_batches learn() calls after steps g*seg .. g*seg +
- * n_batches - 1: batch k = np.random.choice(min(c_k, mem_size), batch) on the
- * arena's sampling stream with c_k = (g*seg + k + 1) x period transitions stored
- * (fewer than `batch`: learn() returns before sampling, idx = -1, zero words).
- * Each sampled ring row resolves to the transition the pooled ring holds there
- * at learn k; this rank's are gathered from rows_cur (segment g) / rows_prev
- * (segment g - 1; for g = 0 its last row holds the reset obs with term 0): s' =
- * the row's obs, s = the previous step's s' or, where that step ended, the
- * fresh-Boat obs (first_obs; experiment 2 with that row's obs3_next), reward,
- * action, terminal (sacenv_replay_stage_terminal's bytes). Output `words`
- * (u32, n_batches x 26 batch), per batch: reward f64 [batch] (two words each) |
- * state f32 [batch][11] | new_state f32 [batch][11] | action f32 [batch] |
- * terminal u32 [batch]; other ranks' rows are zero words, so an integer SUM
- * all-reduce over the ranks is the pooled buffer's batches, bit for bit, on
- * every rank. Needs obs_dim 11, act_dim 1, mem_size <= seg x period. */
-int sacenv_replay_sample_staged(const SacenvReplayParams *p, void *arena, const SacenvStagedParams *sp, int64_t g,
-                                const void *rows_cur, const uint8_t *term_cur, const void *rows_prev,
-                                const uint8_t *term_prev, int32_t batch, int32_t n_batches, int64_t *idx,
-                                uint32_t *words, void *stream);
+/* Device scratch of sacenv_replay_stage_draw for this buffer and batch shape. */
+int sacenv_replay_stage_scratch_bytes(const SacenvReplayParams *p, int32_t batch, int32_t n_batches,
+                                      int64_t *bytes);
+/* The index draws of the n_batches learn() calls after steps g*seg ..
+ * g*seg + n_batches - 1: batch k = np.random.choice(min(c_k, mem_size), batch)
+ * on the arena's sampling stream (seeded like np.random.seed), c_k = (g*seg +
+ * k + 1) x period transitions stored; fewer than `batch`: learn() returns
+ * before sampling (continuous_agent.py:97-98), idx = -1 and no words drawn.
+ * idx: i64 [n_batches][batch]. Call for g = 0, 1, 2, ... in order; the draws
+ * depend only on the stream and the counts, so segment g's may be drawn
+ * before it steps. Once every learn of the segment samples [0, mem_size),
+ * the stream's MT blocks are generated by one wave and the accepted words
+ * ranked over the whole stream by many workgroups (scratch: a device buffer of
+ * sacenv_replay_stage_scratch_bytes); before that, one workgroup draws them in
+ * order. */
+int sacenv_replay_stage_draw(const SacenvReplayParams *p, void *arena, const SacenvStagedParams *sp, int64_t g,
+                             int32_t batch, int32_t n_batches, int64_t *idx, void *scratch, int64_t scratch_bytes,
+                             void *stream);
+/* The rows of segment g some learn will read (u64 [seg][n_pad/64], one bit per
+ * env; cleared first): every row the draws of segment g (idx_g) and g + 1
+ * (idx_next, nullable) sample that lies in segment g on this rank, and the row
+ * before it (its s). sacenv_boat_segment writes exactly these (stage_marks). */
+int sacenv_replay_stage_mark(const SacenvReplayParams *p, const SacenvStagedParams *sp, int64_t g,
+                             const int64_t *idx_g, const int64_t *idx_next, int32_t batch, int32_t n_batches,
+                             uint64_t *marks, void *stream);
+/* The batches of segment g's learns (idx from sacenv_replay_stage_draw): each
+ * sampled ring row resolves to the transition the pooled ring holds there at
+ * learn k; this rank's are read from the staged rows of stage_cur (segment g)
+ * and stage_prev (segment g - 1; for g = 0 its last row holds the obs every env
+ * starts from, term 0): s' = the row's obs, s = the previous step's s' or,
+ * where that step ended, the fresh-Boat obs (first_obs; experiment 2 with that
+ * row's obs3_next), reward, action, terminal = (terminal_mask >> last_term) & 1
+ * (main.py:83-88). Output `words` (u32, n_batches x 26 batch), per batch:
+ * reward f64 [batch] (two words each) | state f32 [batch][11] | new_state f32
+ * [batch][11] | action f32 [batch] | terminal u32 [batch]; other ranks' rows
+ * are zero words, so an integer SUM all-reduce over the ranks is the pooled
+ * buffer's batches, bit for bit, on every rank. Needs obs_dim 11, act_dim 1,
+ * mem_size <= seg x period. */
+int sacenv_replay_sample_staged(const SacenvReplayParams *p, const SacenvStagedParams *sp, int64_t g,
+                                const void *stage_cur, const void *stage_prev, const int64_t *idx, int32_t batch,
+                                int32_t n_batches, uint32_t *words, void *stream);
 
 /* ------------------------------------------------------------------------
  * SAC agent on the device: the batched

@@ -56,7 +56,8 @@ constexpr int U_SX = 0, U_SY = 8, U_SR = 16, U_VX = 24, U_VY = 32, U_VR = 40, U_
               U_EP = 56, U_COEF = 64, U_W0N = 128, U_T = 144, U_IDX = 152,
               U_CONS = 156, U_FILL = 160, U_MTPOS = 164, U_SYN = 168, U_STARTY = 172,
               U_CNT = U_STARTY + 4 * kSlots,
-              U_LIST = U_CNT + 4 * SACENV_N_COUNTERS, U_CSNAP = U_LIST + 12, U_WIND = U_CSNAP + 4;
+              U_LIST = U_CNT + 4 * SACENV_N_COUNTERS, U_CSNAP = U_LIST + 12, U_LTERM = U_CSNAP + 4,
+              U_WIND = U_LTERM + 4;
 constexpr int U_MT_BYTES = 4 * kMtN;
 // The f64 fields below U_PAIRED are stored as 16-B pairs per env, [n_pad][2]:
 // (s_x, s_y) (s_r, v_x) (v_y, v_r) (rudder, ep_reward), the spline piece as
@@ -69,7 +70,8 @@ constexpr int64_t kWindUnits = 16LL * kSlots;  // f64 x 2 curves x slots, per kn
 __host__ __device__ inline int64_t pad64(int64_t n) { return (n + 63) / 64 * 64; }
 __host__ __device__ inline int64_t align256(int64_t x) { return (x + 255) / 256 * 256; }
 
-__host__ __device__ inline void compute_layout(int n, int nk, int L, int use_table, SacenvBoatLayout* o) {
+__host__ __device__ inline void compute_layout(int n, int nk, int L, int use_table, int raw_knots,
+                                               SacenvBoatLayout* o) {
   const int64_t np = pad64(n), nw = np / 64;
   o->n_pad = np;
   // paired fields: the offset of env 0's element; consecutive envs are 16 B apart
@@ -93,11 +95,13 @@ __host__ __device__ inline void compute_layout(int n, int nk, int L, int use_tab
   o->start_y = U_STARTY * np;
   o->counters = U_CNT * np;
   o->refill_list = U_LIST * np;
-  const int64_t uw = U_WIND, wk = kWindUnits * nk;
+  // the drawn knots (raw, before the fit) are kept per slot only when asked for
+  // (SACENV_OUT_KNOTS); the refill's fit reads them from the slot's own y fields
+  const int64_t uw = U_WIND, wk = kWindUnits * nk, rk = raw_knots ? 1 : 0;
   o->wind_knots = uw * np;
-  o->knots_raw = (uw + 2 * wk) * np;
-  o->mt_key = (uw + 3 * wk) * np;
-  const int64_t ur = uw + 3 * wk + U_MT_BYTES;
+  o->knots_raw = raw_knots ? (uw + 2 * wk) * np : -1;
+  o->mt_key = (uw + (2 + rk) * wk) * np;
+  const int64_t ur = uw + (2 + rk) * wk + U_MT_BYTES;
   o->record = ur * np;
   o->obs = ur * np;
   o->reward = (ur + 44) * np;
@@ -117,6 +121,7 @@ __host__ __device__ inline void compute_layout(int n, int nk, int L, int use_tab
   o->wind_table = off;
   off += use_table ? align256(16LL * L) : 0;
   o->total_bytes = off;
+  o->last_term = U_LTERM * np;
 }
 
 // Device view: pointers are recomputed from (base, n_pad, n_knots) at use,
@@ -125,6 +130,7 @@ struct Arena {
   char* b;
   int64_t np;
   int nk;
+  int rk;  // 1: knots_raw is allocated (SACENV_OUT_KNOTS)
   template <class T>
   __device__ __forceinline__ T* at(int64_t units) const { return reinterpret_cast<T*>(b + units * np); }
   __device__ __forceinline__ double* f64(int u) const { return at<double>(u); }
@@ -134,8 +140,8 @@ struct Arena {
   // episode-contiguous slot storage: [env][slot][curve][knot] (+ [y, m] pairs)
   __device__ __forceinline__ double* wind_knots() const { return at<double>(U_WIND); }
   __device__ __forceinline__ double* knots_raw() const { return at<double>(U_WIND + 2 * wk()); }
-  __device__ __forceinline__ uint32_t* mt_key() const { return at<uint32_t>(U_WIND + 3 * wk()); }
-  __device__ __forceinline__ int64_t ur() const { return U_WIND + 3 * wk() + U_MT_BYTES; }
+  __device__ __forceinline__ uint32_t* mt_key() const { return at<uint32_t>(U_WIND + (2 + rk) * wk()); }
+  __device__ __forceinline__ int64_t ur() const { return U_WIND + (2 + rk) * wk() + U_MT_BYTES; }
   __device__ __forceinline__ float* obs() const { return at<float>(ur()); }
   __device__ __forceinline__ float* reward() const { return at<float>(ur() + 44); }
   __device__ __forceinline__ uint8_t* done() const { return at<uint8_t>(ur() + 48); }
@@ -222,7 +228,7 @@ struct Arena {
 };
 
 __host__ inline Arena make_arena(const SacenvBoatParams& p, void* base) {
-  return Arena{static_cast<char*>(base), pad64(p.n_envs), p.n_knots};
+  return Arena{static_cast<char*>(base), pad64(p.n_envs), p.n_knots, (p.out_flags & SACENV_OUT_KNOTS) ? 1 : 0};
 }
 
 // Launch constants built on the host: the small tables whose offsets depend
@@ -917,8 +923,10 @@ __device__ __forceinline__ void store_draw(const SacenvBoatParams& p, const Aren
   const int ncurves = p.use_wind_table ? 0 : n_curves(p.experiment);
   if (lane == 0) A.i32(U_STARTY)[(int64_t)slot * A.np + e] = start_y;
   const int c = lane >> 4, j = lane & 15;
-  if (c < ncurves && j < nk && (raw || (p.out_flags & SACENV_OUT_KNOTS)))
-    A.knots_raw()[A.wix(slot, c, j, e)] = l.y[c][j];
+  if (c < ncurves && j < nk) {
+    if (raw) A.wind_knots()[2 * A.wix(slot, c, j, e)] = l.y[c][j];  // the fit's input, in the slot's y
+    if (A.rk) A.knots_raw()[A.wix(slot, c, j, e)] = l.y[c][j];
+  }
 }
 
 // Boat(config) in one go (init / host-driven resets): draw + fit into slot.
@@ -1238,7 +1246,9 @@ __global__ void __launch_bounds__(kWave) k_refill(SacenvBoatParams p, Arena A) {
         if (cc < ncurves && jj < nk) {
           const int src = k + 1 + cc * 2 * nk + 2 * jj;  // np.random.sample: res53 of two words
           const double a = (double)(gw[src] >> 5), bb = (double)(gw[src + 1] >> 6);
-          A.knots_raw()[A.wix(slot, cc, jj, e)] = (a * 67108864.0 + bb) / 9007199254740992.0;
+          const double kv = (a * 67108864.0 + bb) / 9007199254740992.0;
+          A.wind_knots()[2 * A.wix(slot, cc, jj, e)] = kv;  // k_refill_fit's input, in the slot's y
+          if (A.rk) A.knots_raw()[A.wix(slot, cc, jj, e)] = kv;
         }
         if (gl == 0) {
           A.i32(U_STARTY)[(int64_t)slot * A.np + e] = -p.start_y_half + (int32_t)(gw[k] & mask);
@@ -1333,12 +1343,14 @@ __device__ __forceinline__ void fit_group(const SacenvBoatParams& p, const Arena
   const int e = A.refill_list(0)[rr], f0 = A.refill_list(1)[rr], f1 = A.refill_list(2)[rr];
   for (int f = f0; f < f1; ++f) {  // uniform across the group
     const int slot = f % kSlots;
-    const double* kr = A.knots_raw() + A.wix(slot, c, 0, e);  // the curve's nk knots, contiguous
+    // the curve's nk drawn knots, in the slot's y fields (k_refill put them there);
+    // every lane of the group reads them all before any lane writes the fitted pairs
+    const double* kr = A.wind_knots() + 2 * A.wix(slot, c, 0, e);
     double yk[GS];
 #pragma unroll
-    for (int k = 0; k < GS; ++k) yk[k] = kr[kFull || k < nk ? k : nk - 1];
-    double yv = kr[jj];
-    const double y1 = kr[j1];
+    for (int k = 0; k < GS; ++k) yk[k] = kr[2 * (kFull || k < nk ? k : nk - 1)];
+    double yv = kr[2 * jj];
+    const double y1 = kr[2 * j1];
     // m = G @ y in the reference's order (terms past nk: none when kFull; else a
     // select, so no +0.0 term can turn a -0.0 sum into +0.0)
     double mv = 0.0;
@@ -1743,6 +1755,10 @@ struct RollArgs {
   int64_t fin_stride;     // floats
   char* trans;            // pooled transition row of step ks at trans + ks * trans_stride (or null)
   int64_t trans_stride;   // bytes
+  // staged replay rows (kRows == 2): env e's 64-B row of step ks at stage + (ks * n_pad + e) * 64,
+  // written where bit (e % 64) of marks[ks * n_pad / 64 + e / 64] is set (marks == null: every row)
+  char* stage;
+  const unsigned long long* marks;
   int64_t act_stride;     // floats between consecutive action rows
   // Action hand-off (sacenv_boat_segment): owner wave w steps ks only once
   // ready[w] >= seq0 + ks + 1, and publishes done[w] = seq0 + ks + 1 once step
@@ -1797,7 +1813,7 @@ __device__ uint32_t wait_flag(const uint32_t* f, uint32_t want, uint32_t seen, i
 // kHand (kRoll only): rows published step by step and/or done flags (the
 // closed loop); without it the loop carries no flag code at all (the launch
 // checked that every row was already published).
-template <bool kRoll, int kNc, bool kTIdx, bool kHand = false, bool kTrans = true, bool kVc = kRoll>
+template <bool kRoll, int kNc, bool kTIdx, bool kHand = false, int kRows = 1, bool kVc = kRoll>
 __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Arena& A, const Tail& Tin,
                                            const float* __restrict__ action, OwnerLds& l, int ob,
                                            int lane, int n_steps = 1, const RollArgs* ra = nullptr,
@@ -1827,6 +1843,9 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   // wave's hand-off flag covers -- and step with action 0, so padding state
   // never depends on another wave's row.
   const char* const abase = reinterpret_cast<const char*>(action) + (active ? eo4 : (uint32_t)ob * 256u);
+  // info['termination'] as the reference's info dict keeps it (main.py:83): the last
+  // termination code 1..5, carried across steps and auto-resets
+  uint32_t lt = (uint32_t)A.i32e(U_LTERM, eo4);
   const uint32_t* const rdy = kHand ? (ra->ready != nullptr ? ra->ready + ob : nullptr) : nullptr;
   const int64_t arow = kRoll ? ra->act_stride * 4 : 0;  // bytes between action rows
   // kHand: the latest value of this wave's ready flag (the launch waited for row 0)
@@ -2088,6 +2107,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
                            __HIP_MEMORY_SCOPE_AGENT);
   if (term == SACENV_TERM_NONE && active && p.max_episode_steps > 0 && index >= p.max_episode_steps)
     term = SACENV_TERM_TRUNCATED;
+  lt = (uint32_t)term - 1u < 5u ? (uint32_t)term : lt;  // codes 1..5 overwrite it, 0 and 6 keep it
   const bool ended = term != SACENV_TERM_NONE;
   PHASE(3);
 
@@ -2096,8 +2116,8 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   char* const R = kRoll ? ra->rec + (int64_t)ks * ra->rec_stride : A.b + A.ur() * A.np;
   float* const fin = kRoll ? (ra->fin != nullptr ? ra->fin + (int64_t)ks * ra->fin_stride : nullptr)
                            : A.final_obs();
-  // (kRoll: kTrans compiles the pooled row in or out; the step launch decides at run time)
-  char* const trans = !kTrans ? nullptr
+  // (kRoll: kRows compiles the pooled row in or out; the step launch decides at run time)
+  char* const trans = kRows != 1 ? nullptr
                               : kRoll ? (ra->trans != nullptr ? ra->trans + (int64_t)ks * ra->trans_stride : nullptr)
                                       : trans1;
   if (p.out_flags & SACENV_OUT_REWARD64) A.at_e<double>(A.ur() + 126, eo) = reward;
@@ -2157,6 +2177,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
     st_out(A.i32e(U_CONS, eo4), cons_out);
   }
   if (!kRoll) {
+    st_out(A.i32e(U_LTERM, eo4), (int32_t)lt);
     EARLY_STORE2(U_RUD, rudder, ep);
     if (restart && nc > 0) {  // the new episode's first wind: the piece's y0 = y(0); at
       // t = 0 the piece is exactly y0 whatever (finite) m0, y1, m1 it still holds
@@ -2252,6 +2273,19 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
   }
+  if (kRoll && kRows == 2) {
+    // the staged replay row of this step (sacenv_replay_sample_staged reads it), only
+    // where a learn of this or the next segment samples it or its successor: one
+    // 64-B line per row, s' (the pre-reset obs), reward, action, term | lt << 8, obs3_next
+    const unsigned long long mk = ra->marks != nullptr ? ra->marks[(int64_t)ks * A.nwaves() + ob] : ~0ull;
+    if (((mk >> lane) & 1ull) != 0ull) {
+      float4* const S = reinterpret_cast<float4*>(ra->stage + ((int64_t)ks * A.np + e) * 64);
+      S[0] = make_float4(o.v[0], o.v[1], o.v[2], o.v[3]);
+      S[1] = make_float4(o.v[4], o.v[5], o.v[6], o.v[7]);
+      S[2] = make_float4(o.v[8], o.v[9], o.v[10], (float)reward);
+      S[3] = make_float4(act, __uint_as_float((uint32_t)term | (lt << 8)), row3_new, 0.0f);
+    }
+  }
   if (kHand && ra->done != nullptr) {
     // step ks's outputs visible device-wide (release: L2 write-back + wait for
     // the stores), then its done flag, write-through
@@ -2280,6 +2314,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
     if (!t_idx) A.f64e(U_T, eo) = t;
     A.f64e(U_EP, eo) = ep;
     A.i32e(U_IDX, eo4) = index;
+    A.i32e(U_LTERM, eo4) = (int32_t)lt;
     if (p.autoreset) A.i32e(U_CONS, eo4) = cons;
 #pragma unroll
     for (int k = 0; k < kCoef; ++k)
@@ -2346,7 +2381,7 @@ __global__ void __launch_bounds__(kWave) k_step(SacenvBoatParams p, Arena A, Tai
 // per SIMD, for grids with more owner waves than SIMDs -- 131 072 envs: 48.5
 // against 44.4 G env-steps/s; at one wave per SIMD the copies win, 1.34 against
 // 2.04 us per step). The same arithmetic either way: results are bit-identical.
-template <int kNc, bool kTIdx, bool kTrans, bool kVc>
+template <int kNc, bool kTIdx, int kRows, bool kVc>
 __device__ __forceinline__ void rollout_body(const SacenvBoatParams& p, const Arena& A, const Tail& T,
                                              const float* __restrict__ action, int n_steps, const RollArgs& ra,
                                              OwnerLds& slds) {
@@ -2379,29 +2414,29 @@ __device__ __forceinline__ void rollout_body(const SacenvBoatParams& p, const Ar
   }
   if (hand) {
     if (kVc)
-      owner_wave<true, kNc, kTIdx, true, kTrans, true>(vreg_params(p), A, vreg_tail(T), action, slds, ob, lane,
+      owner_wave<true, kNc, kTIdx, true, kRows, true>(vreg_params(p), A, vreg_tail(T), action, slds, ob, lane,
                                                        n_steps, &ra, nullptr, seen);
     else
-      owner_wave<true, kNc, kTIdx, true, kTrans, false>(p, A, T, action, slds, ob, lane, n_steps, &ra, nullptr, seen);
+      owner_wave<true, kNc, kTIdx, true, kRows, false>(p, A, T, action, slds, ob, lane, n_steps, &ra, nullptr, seen);
   } else {
     if (kVc)
-      owner_wave<true, kNc, kTIdx, false, kTrans, true>(vreg_params(p), A, vreg_tail(T), action, slds, ob, lane,
+      owner_wave<true, kNc, kTIdx, false, kRows, true>(vreg_params(p), A, vreg_tail(T), action, slds, ob, lane,
                                                         n_steps, &ra);
     else
-      owner_wave<true, kNc, kTIdx, false, kTrans, false>(p, A, T, action, slds, ob, lane, n_steps, &ra);
+      owner_wave<true, kNc, kTIdx, false, kRows, false>(p, A, T, action, slds, ob, lane, n_steps, &ra);
   }
 }
-template <int kNc, bool kTIdx, bool kTrans>
+template <int kNc, bool kTIdx, int kRows>
 __global__ void __launch_bounds__(kWave) k_rollout(SacenvBoatParams p, Arena A, Tail T,
                                                    const float* __restrict__ action, int n_steps, RollArgs ra) {
   __shared__ OwnerLds slds;
-  rollout_body<kNc, kTIdx, kTrans, true>(p, A, T, action, n_steps, ra, slds);
+  rollout_body<kNc, kTIdx, kRows, true>(p, A, T, action, n_steps, ra, slds);
 }
-template <int kNc, bool kTIdx, bool kTrans>
+template <int kNc, bool kTIdx, int kRows>
 __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(2, 2)))
 k_rollout_dense(SacenvBoatParams p, Arena A, Tail T, const float* __restrict__ action, int n_steps, RollArgs ra) {
   __shared__ OwnerLds slds;
-  rollout_body<kNc, kTIdx, kTrans, false>(p, A, T, action, n_steps, ra, slds);
+  rollout_body<kNc, kTIdx, kRows, false>(p, A, T, action, n_steps, ra, slds);
 }
 
 // sacenv_mixed_segment (BASELINE configs[4] as one persistent launch): the
@@ -2415,7 +2450,7 @@ __global__ void __launch_bounds__(kWave) k_rollout_mixed(SacenvBoatParams p, Are
   const int lane = threadIdx.x;
   int b = (int)blockIdx.x;
   if (b < nb_boat) {
-    owner_wave<true, kNc, kTIdx, false, false>(vreg_params(p), A, vreg_tail(T), action, slds, b, lane, n_steps,
+    owner_wave<true, kNc, kTIdx, false, 0>(vreg_params(p), A, vreg_tail(T), action, slds, b, lane, n_steps,
                                                &ra);
     return;
   }
@@ -2481,7 +2516,7 @@ int check_params(const SacenvBoatParams* p) {
 
 Tail make_tail(const SacenvBoatParams& p, void* arena) {
   SacenvBoatLayout L;
-  compute_layout(p.n_envs, p.n_knots, p.wind_len, p.use_wind_table, &L);
+  compute_layout(p.n_envs, p.n_knots, p.wind_len, p.use_wind_table, (p.out_flags & SACENV_OUT_KNOTS) != 0, &L);
   char* b = static_cast<char*>(arena);
   Tail T;
   T.g = reinterpret_cast<const double*>(b + L.spline_g);
@@ -2570,7 +2605,7 @@ int sacenv_boat_layout(const SacenvBoatParams* p, SacenvBoatLayout* out) {
   const int rc = check_params(p);
   if (rc) return rc;
   if (out == nullptr) return SACENV_E_NULL;
-  compute_layout(p->n_envs, p->n_knots, p->wind_len, p->use_wind_table, out);
+  compute_layout(p->n_envs, p->n_knots, p->wind_len, p->use_wind_table, (p->out_flags & SACENV_OUT_KNOTS) != 0, out);
   return SACENV_OK;
 }
 
@@ -2696,11 +2731,14 @@ static int launch_multi(const SacenvBoatParams& p, void* arena, const float* act
   const int nb_boat = (int)(pad64(p.n_envs) / kWave);
   const bool dense = dense_grid(nb_boat);
 #define SACENV_LAUNCH_K(KER, NC, TI)                                                                       \
-  if (ra.trans != nullptr)                                                                                 \
-    hipLaunchKernelGGL((KER<NC, TI, true>), dim3(nb_boat), dim3(kWave), 0, (hipStream_t)stream, p,         \
+  if (ra.stage != nullptr)                                                                                 \
+    hipLaunchKernelGGL((KER<NC, TI, 2>), dim3(nb_boat), dim3(kWave), 0, (hipStream_t)stream, p,            \
+                       make_arena(p, arena), make_tail(p, arena), actions, n_steps, ra);                   \
+  else if (ra.trans != nullptr)                                                                            \
+    hipLaunchKernelGGL((KER<NC, TI, 1>), dim3(nb_boat), dim3(kWave), 0, (hipStream_t)stream, p,            \
                        make_arena(p, arena), make_tail(p, arena), actions, n_steps, ra);                   \
   else                                                                                                     \
-    hipLaunchKernelGGL((KER<NC, TI, false>), dim3(nb_boat), dim3(kWave), 0, (hipStream_t)stream, p,        \
+    hipLaunchKernelGGL((KER<NC, TI, 0>), dim3(nb_boat), dim3(kWave), 0, (hipStream_t)stream, p,            \
                        make_arena(p, arena), make_tail(p, arena), actions, n_steps, ra)
 #define SACENV_LAUNCH(NC, TI)                  \
   if (dense) {                                 \
@@ -2717,12 +2755,12 @@ static int launch_multi(const SacenvBoatParams& p, void* arena, const float* act
 // byte offsets of the record and the status words in the arena
 static int64_t A_ur_bytes(const SacenvBoatParams& p) {
   SacenvBoatLayout L;
-  compute_layout(p.n_envs, p.n_knots, p.wind_len, p.use_wind_table, &L);
+  compute_layout(p.n_envs, p.n_knots, p.wind_len, p.use_wind_table, (p.out_flags & SACENV_OUT_KNOTS) != 0, &L);
   return L.record;
 }
 static int64_t status_offset(const SacenvBoatParams& p) {
   SacenvBoatLayout L;
-  compute_layout(p.n_envs, p.n_knots, p.wind_len, p.use_wind_table, &L);
+  compute_layout(p.n_envs, p.n_knots, p.wind_len, p.use_wind_table, (p.out_flags & SACENV_OUT_KNOTS) != 0, &L);
   return L.status;
 }
 
@@ -2744,7 +2782,8 @@ int sacenv_boat_rollout(const SacenvBoatParams* p, void* arena, const float* act
 
 int sacenv_boat_segment(const SacenvBoatParams* p, void* arena, const float* actions, int64_t action_stride,
                         int32_t n_steps, const uint32_t* act_ready, uint32_t* step_done, uint32_t seq0,
-                        void* trans, int64_t trans_stride, void* stream) {
+                        void* trans, int64_t trans_stride, void* stage, const uint64_t* stage_marks,
+                        void* stream) {
   int rc = check_params(p);
   if (rc) return rc;
   if (arena == nullptr || actions == nullptr) return SACENV_E_NULL;
@@ -2754,6 +2793,8 @@ int sacenv_boat_segment(const SacenvBoatParams* p, void* arena, const float* act
     return SACENV_E_RANGE;
   if (trans != nullptr && ((reinterpret_cast<uintptr_t>(trans) & 15u) != 0u || (trans_stride & 15) != 0))
     return SACENV_E_RANGE;  // float4 row stores
+  if (stage != nullptr && (trans != nullptr || (reinterpret_cast<uintptr_t>(stage) & 15u) != 0u))
+    return SACENV_E_RANGE;  // one kind of rows per launch; float4 stores
   const Arena A = make_arena(*p, arena);
   RollArgs ra{};
   ra.rec = static_cast<char*>(arena) + A_ur_bytes(*p);
@@ -2762,6 +2803,8 @@ int sacenv_boat_segment(const SacenvBoatParams* p, void* arena, const float* act
   ra.fin_stride = 0;
   ra.trans = static_cast<char*>(trans);
   ra.trans_stride = trans_stride;
+  ra.stage = static_cast<char*>(stage);
+  ra.marks = reinterpret_cast<const unsigned long long*>(stage_marks);
   ra.act_stride = action_stride;
   ra.ready = act_ready;
   ra.done = step_done;
@@ -2784,12 +2827,15 @@ int sacenv_boat_segment_occupancy(const SacenvBoatParams* p, int32_t with_trans,
   hipFuncAttributes fa{};
   const bool dense = dense_grid((int)(pad64(p->n_envs) / kWave));  // the kernel launch_multi would pick
 #define SACENV_OCC_K(KER, NC, TI)                                                                            \
-  if (with_trans) {                                                                                          \
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, KER<NC, TI, true>, kWave, 0);                      \
-    if (e == hipSuccess) e = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(KER<NC, TI, true>));    \
+  if (with_trans == 2) {                                                                                     \
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, KER<NC, TI, 2>, kWave, 0);                         \
+    if (e == hipSuccess) e = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(KER<NC, TI, 2>));       \
+  } else if (with_trans) {                                                                                   \
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, KER<NC, TI, 1>, kWave, 0);                         \
+    if (e == hipSuccess) e = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(KER<NC, TI, 1>));       \
   } else {                                                                                                   \
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, KER<NC, TI, false>, kWave, 0);                     \
-    if (e == hipSuccess) e = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(KER<NC, TI, false>));   \
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, KER<NC, TI, 0>, kWave, 0);                         \
+    if (e == hipSuccess) e = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(KER<NC, TI, 0>));       \
   }
 #define SACENV_OCC(NC, TI)                  \
   if (dense) {                              \

@@ -235,55 +235,39 @@ __global__ void __launch_bounds__(256) k_rb_gather(SacenvReplayParams p, RB r, i
 }
 
 // ---------------------------------------------------------------------------
-// The staged sampler (sacenv_replay_sample_staged): the pooled buffer of
-// main.py:81-90 -- every rank's envs storing one transition each per step, one
-// learn() (sample_buffer, buffer.py:24-35) after every step -- sampled straight
-// out of the segments of transition rows the persistent step launch wrote
-// (sacenv_boat_segment's `trans`), with no store into a ring. A ring of M rows
-// that takes `period` rows per step holds the last M sequence numbers; with M <=
-// seg * period every row learn k can reach lies in this segment's or the
-// previous segment's rows, so the two staged segments ARE the ring.
+// The staged sampler: the pooled buffer of main.py:78-90 -- every rank's envs
+// storing one transition each per step, one learn() (sample_buffer,
+// buffer.py:24-35) after every step -- sampled out of the rows the persistent
+// step launch wrote (sacenv_boat_segment's `stage`), with no ring. A ring of M
+// rows that takes `period` rows per step holds the last M sequence numbers;
+// with M <= seg * period every row learn k of segment g can reach (and the row
+// before it, for s) lies in segment g or g - 1, so two staged segments ARE the
+// ring. The index draws depend only on the sampling stream and the counts
+// stored, so segment g's are drawn before it steps, and the launch writes only
+// the rows some learn will read (sacenv_replay_stage_mark).
 
-// The persistent info['termination'] (main.py:83, boat_env.py:24-32,84-105,
-// 120-126) per row: codes 1..5 overwrite the env's last termination, 0 and 6
-// keep it; terminal = (terminal_mask >> last) & 1. One thread per 4 envs walks
-// the segment's rows in order: u32 loads (4 envs' codes, coalesced across the
-// threads of a row), kChunk rows in flight before the serial carry.
-__global__ void __launch_bounds__(256) k_rb_stage_terminal(const uint8_t* __restrict__ rows, int64_t row_bytes,
-                                                           int64_t term_off, int n_steps, int n, int n_pad,
-                                                           uint32_t terminal_mask, uint8_t* __restrict__ last_term,
-                                                           uint8_t* __restrict__ terminal) {
-  constexpr int kChunk = 32;
-  const int e0 = 4 * (blockIdx.x * blockDim.x + threadIdx.x);
-  if (e0 >= n) return;
-  uint32_t lt[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) lt[q] = e0 + q < n ? last_term[e0 + q] : 0u;
-  for (int j0 = 0; j0 < n_steps; j0 += kChunk) {
-    uint32_t c[kChunk];
-#pragma unroll
-    for (int j = 0; j < kChunk; ++j)
-      c[j] = j0 + j < n_steps ? *reinterpret_cast<const uint32_t*>(rows + (int64_t)(j0 + j) * row_bytes + term_off + e0)
-                              : 0u;
-#pragma unroll
-    for (int j = 0; j < kChunk; ++j) {
-      uint32_t out = 0u;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint32_t cq = (c[j] >> (8 * q)) & 0xFFu;
-        lt[q] = (cq >= 1u && cq <= 5u) ? cq : lt[q];
-        out |= ((terminal_mask >> lt[q]) & 1u) << (8 * q);
-      }
-      if (j0 + j < n_steps) *reinterpret_cast<uint32_t*>(terminal + (int64_t)(j0 + j) * n_pad + e0) = out;
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-    if (e0 + q < n) last_term[e0 + q] = (uint8_t)lt[q];
+struct StagedGeom {
+  int64_t period, offset, g;
+  int n, n_pad, seg, exp2;
+};
+
+// ring row `row` at learn time (cntr rows stored) -> (global step q, global env u)
+__device__ __forceinline__ void resolve(int64_t row, int64_t cntr, int64_t M, int64_t period, int64_t* q,
+                                        int64_t* u) {
+  const int64_t s = row + M * ((cntr - 1 - row) / M);  // the latest sequence number = row (mod M)
+  *q = s / period;
+  *u = s - *q * period;
 }
 
-// mt19937_gen over one block with a whole workgroup (>= 227 threads): the three
-// lane-parallel phases of mt_twist_wave, one word per thread each.
+// n_batches consecutive np.random.choice(min(cntr_k, M), batch) calls on one
+// stream, cntr_k = cntr0 + (k + 1) * period (learn k follows step k's stores),
+// learns with cntr_k < batch skipped (continuous_agent.py:97-98: idx = -1, no
+// words). The general path (ranges that change between learns): one workgroup;
+// a whole 624-word block is tempered and tested at once (thread i: word i),
+// accepted words are ranked with a ballot per wave and a prefix over the
+// waves; a batch that completes inside the block ends at its last accepted
+// word, and the next batch re-tests the block from there.
+constexpr int kDrawThreads = 1024;
 __device__ __forceinline__ void mt_twist_block(const uint32_t* __restrict__ o, uint32_t* __restrict__ n, int tid) {
   constexpr int kD = kMtN - kMtM;  // 227
   if (tid < kD) n[tid] = mt_mix(o[tid], o[tid + 1], o[tid + kMtM]);
@@ -296,14 +280,6 @@ __device__ __forceinline__ void mt_twist_block(const uint32_t* __restrict__ o, u
   __syncthreads();
 }
 
-// n_batches consecutive np.random.choice(min(cntr_k, M), batch) calls on one
-// stream, cntr_k = cntr0 + (k + 1) * period (learn k follows step k's stores).
-// One workgroup of kDrawThreads: a whole 624-word block is tempered and tested
-// at once (thread i: word i), accepted words are ranked with a ballot per wave
-// and a prefix over the waves; a batch that completes inside the block ends at
-// its last accepted word, and the next batch re-tests the block from there
-// (its range may differ while cntr < M). The stream advances exactly as numpy's.
-constexpr int kDrawThreads = 1024;
 __global__ void __launch_bounds__(kDrawThreads) k_rb_draw_many(SacenvReplayParams p, RB r, int batch, int nb,
                                                                int64_t cntr0, int64_t period,
                                                                int64_t* __restrict__ idx) {
@@ -321,8 +297,7 @@ __global__ void __launch_bounds__(kDrawThreads) k_rb_draw_many(SacenvReplayParam
     const int64_t c = cntr0 + (int64_t)(k + 1) * period;
     const int64_t max_mem = c < p.mem_size ? c : p.mem_size;
     const uint32_t rng = (uint32_t)(max_mem - 1);
-    if (c < batch || rng == 0u) {  // learn() returns before sampling (continuous_agent.py:97-98),
-      // or numpy's off + 0: no words consumed
+    if (c < batch || rng == 0u) {  // learn() returns before sampling, or numpy's off + 0: no words
       for (int i = tid; i < batch; i += kDrawThreads) idx[(int64_t)k * batch + i] = c < batch ? -1 : 0;
       ++k;
       continue;
@@ -372,66 +347,255 @@ __global__ void __launch_bounds__(kDrawThreads) k_rb_draw_many(SacenvReplayParam
   if (tid == 0) *r.pos() = pos;
 }
 
-struct Staged {
-  const char* cur;         // rows of segment g
-  const char* prev;        // rows of segment g - 1 (g = 0: row seg-1 holds the reset obs, term 0)
-  const uint8_t* tcur;     // k_rb_stage_terminal's terminal bytes [seg][n_pad] of segment g
-  const uint8_t* tprev;    // ... of segment g - 1
-  int64_t row_bytes, period, offset, g;
-  int n, n_pad, seg, exp2;
+// The steady-state path (every learn of the segment draws from the same range
+// [0, M)): the accepted words are numbered over the whole stream, word by word,
+// so the draws split into (1) the MT blocks the segment may need, generated
+// by one wave -- the only sequential part, the recurrence itself; (2) accepted
+// words counted per 1 024-word tile, all tiles at once; (3) a prefix over the
+// tiles; (4) every tile ranking its accepted words and writing idx[rank] for
+// rank < n_batches * batch, the tile holding the last one handing the stream
+// on (the block it lies in and the position after it).
+constexpr int kTile = 1024, kTileThreads = 256;
+
+__global__ void __launch_bounds__(kWave) k_mt_chain(RB r, uint32_t* __restrict__ out, int n_blocks,
+                                                    int* __restrict__ ctrl) {
+  __shared__ DrawLds l;
+  const int lane = threadIdx.x;
+  for (int i = lane; i < kMtN; i += kWave) l.blk[0][i] = r.key()[i];
+  int cur = 0;
+  const int pos = *r.pos();
+  if (lane == 0) {
+    ctrl[2] = 0;                          // no shortfall yet
+    ctrl[3] = pos >= kMtN ? 0 : pos;      // p0: the next word's position in block 0
+  }
+  __syncthreads();
+  if (pos >= kMtN) {  // the stream's next word is in the next block
+    mt_twist_wave(l.blk[0], l.blk[1], lane);
+    cur = 1;
+  }
+  for (int b = 0; b < n_blocks; ++b) {
+    uint32_t* const o = out + (int64_t)b * kMtN;
+    for (int i = lane; i < kMtN; i += kWave) o[i] = l.blk[cur][i];
+    if (b + 1 < n_blocks) {
+      mt_twist_wave(l.blk[cur], l.blk[cur ^ 1], lane);
+      cur ^= 1;
+    }
+  }
+}
+
+struct DrawPlan {
+  const uint32_t* blocks;  // the generated blocks; stream word t is block (p0 + t) / 624, word (p0 + t) % 624
+  int p0;                  // position of the stream's next word in block 0 (ctrl[3], set by k_mt_chain)
+  int64_t n_words;         // words generated from p0 on
+  uint32_t rng, mask;
+  int64_t need;            // accepted words wanted: n_batches * batch
+  int* tile_cnt;           // [tiles]
+  int* tile_off;           // [tiles] exclusive prefix
+  int* ctrl;               // [0] tile holding the last wanted word (-1: too few words), [1] total accepted,
+                           // [2] 1 = too few words generated (no draw made), [3] p0
+};
+
+__device__ __forceinline__ void plan_start(DrawPlan& d, int64_t n_blocks) {
+  d.p0 = d.ctrl[3];
+  d.n_words = n_blocks * kMtN - d.p0;
+}
+
+__device__ __forceinline__ uint32_t plan_word(const DrawPlan& d, int64_t t, bool* acc) {
+  const int64_t gp = d.p0 + t;
+  const int64_t b = gp / kMtN;
+  const uint32_t w = mt_temper(d.blocks[b * kMtN + (gp - b * kMtN)]) & d.mask;
+  *acc = t < d.n_words && w <= d.rng;
+  return w;
+}
+
+__global__ void __launch_bounds__(kTileThreads) k_draw_count(DrawPlan d, int64_t n_blocks) {
+  __shared__ int wc[kTileThreads / kWave];
+  plan_start(d, n_blocks);
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
+  const int64_t t0 = (int64_t)blockIdx.x * kTile;
+  int c = 0;
+#pragma unroll
+  for (int q = 0; q < kTile / kTileThreads; ++q) {
+    bool acc;
+    const int64_t t = t0 + q * kTileThreads + tid;
+    if (t < d.n_words) plan_word(d, t, &acc);
+    else acc = false;
+    c += acc ? 1 : 0;
+  }
+  // wave sum, then the workgroup's
+  for (int o = kWave / 2; o > 0; o >>= 1) c += __shfl_xor(c, o);
+  if (lane == 0) wc[wv] = c;
+  __syncthreads();
+  if (tid == 0) {
+    int t = 0;
+    for (int i = 0; i < kTileThreads / kWave; ++i) t += wc[i];
+    d.tile_cnt[blockIdx.x] = t;
+  }
+}
+
+__global__ void __launch_bounds__(1024) k_draw_scan(DrawPlan d, int tiles) {
+  __shared__ int part[1024 / kWave];
+  __shared__ int carry;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
+  if (tid == 0) {
+    carry = 0;
+    d.ctrl[0] = -1;
+  }
+  __syncthreads();
+  for (int base = 0; base < tiles; base += 1024) {
+    const int i = base + tid;
+    const int v = i < tiles ? d.tile_cnt[i] : 0;
+    int x = v;  // inclusive scan in the wave
+    for (int o = 1; o < kWave; o <<= 1) {
+      const int y = __shfl_up(x, o);
+      x += lane >= o ? y : 0;
+    }
+    if (lane == kWave - 1) part[wv] = x;
+    __syncthreads();
+    int before = carry;
+    for (int w = 0; w < wv; ++w) before += part[w];
+    const int excl = before + x - v;
+    if (i < tiles) {
+      d.tile_off[i] = excl;
+      if (excl < d.need && excl + v >= d.need) d.ctrl[0] = i;
+    }
+    __syncthreads();
+    if (tid == 1023) carry = excl + v;
+    __syncthreads();
+  }
+  if (tid == 0) d.ctrl[1] = carry;
+}
+
+__global__ void __launch_bounds__(kTileThreads) k_draw_emit(DrawPlan d, RB r, int64_t n_blocks,
+                                                              int64_t* __restrict__ idx) {
+  __shared__ int wc[kTileThreads / kWave];
+  plan_start(d, n_blocks);
+  __shared__ int64_t s_end;   // stream position after the last wanted word (this tile only)
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
+  const int last = d.ctrl[0];
+  if (last < 0) {  // too few words generated (never at the planned margin): report, draw nothing
+    if (blockIdx.x == 0 && tid == 0) d.ctrl[2] = 1;
+    return;
+  }
+  if ((int)blockIdx.x > last) return;
+  const int64_t t0 = (int64_t)blockIdx.x * kTile;
+  int run = d.tile_off[blockIdx.x];
+  if (tid == 0) s_end = -1;
+#pragma unroll
+  for (int q = 0; q < kTile / kTileThreads; ++q) {
+    const int64_t t = t0 + q * kTileThreads + tid;
+    bool acc = false;
+    uint32_t w = 0u;
+    if (t < d.n_words) w = plan_word(d, t, &acc);
+    const unsigned long long bal = __ballot(acc);
+    __syncthreads();  // wc of the previous round read
+    if (lane == 0) wc[wv] = __popcll(bal);
+    __syncthreads();
+    int before = 0, total = 0;
+#pragma unroll
+    for (int i = 0; i < kTileThreads / kWave; ++i) {
+      before += i < wv ? wc[i] : 0;
+      total += wc[i];
+    }
+    const int64_t rank = (int64_t)run + before + __popcll(bal & ((1ull << lane) - 1ull));
+    if (acc && rank < d.need) idx[rank] = (int64_t)w;
+    if (acc && rank == d.need - 1) s_end = d.p0 + t + 1;
+    run += total;
+  }
+  __syncthreads();
+  if (s_end >= 0) {  // this tile ends the segment's draws: the stream's state after them
+    int64_t b = s_end / kMtN;
+    int pos = (int)(s_end - b * kMtN);
+    if (pos == 0) {  // block b is not generated yet: keep block b-1, twist first next time
+      b -= 1;
+      pos = kMtN;
+    }
+    for (int i = tid; i < kMtN; i += kTileThreads) r.key()[i] = d.blocks[b * kMtN + i];
+    if (tid == 0) *r.pos() = pos;
+  }
+}
+
+// Marks the rows of segment g that a learn will read: every sampled row of
+// the learns of segments g and g + 1 (idx_g, idx_n) that lies in segment g on
+// this rank, and the row before it (its s). One thread per sampled row.
+__global__ void __launch_bounds__(256) k_rb_stage_mark(SacenvReplayParams p, StagedGeom G,
+                                                       const int64_t* __restrict__ idx_g,
+                                                       const int64_t* __restrict__ idx_n, int batch, int nb,
+                                                       unsigned long long* __restrict__ marks, int64_t total) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t per = (int64_t)batch * nb;
+  if (t >= total) return;
+  const bool nxt = t >= per;
+  const int64_t tt = nxt ? t - per : t;
+  const int64_t row = (nxt ? idx_n : idx_g)[tt];
+  if (row < 0) return;  // no learn at that step
+  const int k = (int)(tt / batch);
+  const int64_t cntr = ((G.g + (nxt ? 1 : 0)) * G.seg + k + 1) * G.period;
+  int64_t q, u;
+  resolve(row, cntr, p.mem_size, G.period, &q, &u);
+  if (u < G.offset || u >= G.offset + G.n) return;
+  const int e = (int)(u - G.offset);
+  const int nw = G.n_pad / kWave;
+#pragma unroll
+  for (int d = 0; d < 2; ++d) {  // the row, and its predecessor (s)
+    const int64_t j = q - d - G.g * G.seg;
+    if (j >= 0 && j < G.seg)
+      atomicOr(&marks[j * nw + e / kWave], 1ull << (e % kWave));
+  }
+}
+
+struct StagedRows {
+  const char* cur;   // segment g's 64-B rows [seg][n_pad]
+  const char* prev;  // segment g - 1's (g = 0: its last row holds the reset obs, term 0)
   float first[SACENV_OBS_DIM];
 };
 
-// One thread per sampled row (batch b, row i): ring row idx -> the sequence
-// number it holds at learn b (the latest s = idx mod M below cntr_b) -> (step,
-// global env); this rank's rows are read from the staged segments: s' the row's
-// obs, s the previous step's s' (or the fresh-Boat obs where that step ended:
-// first_obs, exp 2 with that row's obs3_next), the reward and action, the
-// terminal byte. Output per batch, 32-bit words (sample_many's packing):
-// reward f64 [B] | state [B][11] | new_state [B][11] | action [B] | terminal [B];
-// rows of other ranks are zero words, so a SUM all-reduce assembles the batch.
-__global__ void __launch_bounds__(256) k_rb_gather_staged(SacenvReplayParams p, Staged S, int batch, int nb,
-                                                          const int64_t* __restrict__ idx,
+// One thread per sampled row (batch b, row i): the ring row -> (step, global
+// env) at learn b; this rank's rows are read from the staged segments: s' =
+// the row's obs, s = the previous step's s' (or the fresh-Boat obs where that
+// step ended: first_obs, exp 2 with that row's obs3_next), reward, action,
+// terminal = (terminal_mask >> last_term) & 1. Output per batch, 32-bit words
+// (sample_many's packing): reward f64 [B] | state [B][11] | new_state [B][11] |
+// action [B] | terminal [B]; other ranks' rows are zero words, so a SUM
+// all-reduce assembles the batch.
+__global__ void __launch_bounds__(256) k_rb_gather_staged(SacenvReplayParams p, StagedGeom G, StagedRows S,
+                                                          int batch, int nb, const int64_t* __restrict__ idx,
                                                           uint32_t* __restrict__ words, int64_t per) {
   constexpr int D = SACENV_OBS_DIM;
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (t >= (int64_t)batch * nb) return;
   const int b = (int)(t / batch), i = (int)(t - (int64_t)b * batch);
-  const int64_t M = p.mem_size;
-  const int64_t cntr = (S.g * S.seg + b + 1) * S.period;
   const int64_t row = idx[t];  // -1: no learn at this step (fewer rows than a batch)
-  const int64_t s = row < 0 ? 0 : row + M * ((cntr - 1 - row) / M);
-  const int64_t q = s / S.period, u = s - q * S.period;
-  const bool own = row >= 0 && u >= S.offset && u < S.offset + S.n;
+  int64_t q = 0, u = -1;
+  if (row >= 0) resolve(row, (G.g * G.seg + b + 1) * G.period, p.mem_size, G.period, &q, &u);
+  const bool own = u >= G.offset && u < G.offset + G.n;
   uint32_t* const W = words + (int64_t)b * per;
-  float sn[D], sv[D];
-  float rw = 0.f, ac = 0.f;
+  float sn[16], sv[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) sn[k] = sv[k] = 0.f;
   uint32_t tm = 0u;
-#pragma unroll
-  for (int k = 0; k < D; ++k) sn[k] = sv[k] = 0.f;
   if (own) {
-    const int e = (int)(u - S.offset);
-    int64_t j = q - S.g * S.seg;  // >= -seg + 1 (M <= seg * period)
+    const int e = (int)(u - G.offset);
+    int64_t j = q - G.g * G.seg;  // > -seg (M <= seg * period)
     const bool in_cur = j >= 0;
-    j = in_cur ? j : j + S.seg;
-    const char* R = (in_cur ? S.cur : S.prev) + j * S.row_bytes;
-    // the previous step's row: same segment, or the last row of the previous one
-    const char* P = j > 0 ? R - S.row_bytes : S.prev + (int64_t)(S.seg - 1) * S.row_bytes;
-    const float* rs = reinterpret_cast<const float*>(R) + (int64_t)e * D;
-    const float* ps = reinterpret_cast<const float*>(P) + (int64_t)e * D;
-    const int64_t np = S.n_pad;
-    rw = reinterpret_cast<const float*>(R + 44 * np)[e];
-    ac = reinterpret_cast<const float*>(R + 48 * np)[e];
-    tm = (in_cur ? S.tcur : S.tprev)[j * np + e];
-    const bool pdone = reinterpret_cast<const uint8_t*>(P + 52 * np)[e] != 0;
+    j = in_cur ? j : j + G.seg;
+    const float4* R = reinterpret_cast<const float4*>((in_cur ? S.cur : S.prev) + (j * G.n_pad + e) * 64);
+    const float4* P = j > 0 ? reinterpret_cast<const float4*>((in_cur ? S.cur : S.prev) + ((j - 1) * G.n_pad + e) * 64)
+                            : reinterpret_cast<const float4*>(S.prev + ((int64_t)(G.seg - 1) * G.n_pad + e) * 64);
 #pragma unroll
-    for (int k = 0; k < D; ++k) {
-      sn[k] = rs[k];
-      sv[k] = pdone ? S.first[k] : ps[k];
+    for (int k = 0; k < 4; ++k) {
+      const float4 x = R[k], y = P[k];
+      sn[4 * k] = x.x, sn[4 * k + 1] = x.y, sn[4 * k + 2] = x.z, sn[4 * k + 3] = x.w;
+      sv[4 * k] = y.x, sv[4 * k + 1] = y.y, sv[4 * k + 2] = y.z, sv[4 * k + 3] = y.w;
     }
-    if (S.exp2 && pdone) sv[3] = reinterpret_cast<const float*>(P + 53 * np)[e];
+    const bool pdone = (__float_as_uint(sv[13]) & 0xFFu) != 0u;
+    const float o3 = sv[14];
+#pragma unroll
+    for (int k = 0; k < D; ++k) sv[k] = pdone ? S.first[k] : sv[k];
+    if (G.exp2 && pdone) sv[3] = o3;
+    tm = (p.terminal_mask >> ((__float_as_uint(sn[13]) >> 8) & 0xFFu)) & 1u;
   }
-  const double r64 = (double)rw;
+  const double r64 = (double)sn[11];
   uint64_t rb;
   __builtin_memcpy(&rb, &r64, 8);
   W[2 * i] = (uint32_t)rb;
@@ -443,7 +607,7 @@ __global__ void __launch_bounds__(256) k_rb_gather_staged(SacenvReplayParams p, 
     st[k] = __float_as_uint(sv[k]);
     ns[k] = __float_as_uint(sn[k]);
   }
-  W[2 * batch + 2 * (int64_t)batch * D + i] = __float_as_uint(ac);
+  W[2 * batch + 2 * (int64_t)batch * D + i] = __float_as_uint(sn[12]);
   W[2 * batch + 2 * (int64_t)batch * D + batch + i] = tm;
 }
 
@@ -571,60 +735,135 @@ static int check_staged(const SacenvReplayParams* p, const SacenvStagedParams* s
   if (p->obs_dim != SACENV_OBS_DIM || p->act_dim != 1) return SACENV_E_SIZE;  // the boat's rows
   if (sp->n <= 0 || sp->n_pad < sp->n || (sp->n_pad & 63) != 0 || sp->seg <= 0) return SACENV_E_SIZE;
   if (sp->offset < 0 || sp->period <= 0 || sp->offset + sp->n > sp->period) return SACENV_E_RANGE;
+  // every row a learn can reach (and the row before it) lies in this segment or the previous one
+  if (p->mem_size > (int64_t)sp->seg * sp->period) return SACENV_E_RANGE;
   return SACENV_OK;
 }
 
-static int64_t staged_row_bytes(const SacenvStagedParams* sp) {
-  return (int64_t)(sp->experiment == 2 ? SACENV_TRANS_BYTES_EXP2 : SACENV_TRANS_BYTES) * sp->n_pad;
+static StagedGeom geom(const SacenvStagedParams* sp, int64_t g) {
+  StagedGeom G;
+  G.period = sp->period;
+  G.offset = sp->offset;
+  G.g = g;
+  G.n = sp->n;
+  G.n_pad = sp->n_pad;
+  G.seg = sp->seg;
+  G.exp2 = sp->experiment == 2;
+  return G;
 }
 
-int sacenv_replay_stage_terminal(const SacenvReplayParams* p, const SacenvStagedParams* sp, const void* rows,
-                                 int32_t n_steps, uint8_t* last_term, uint8_t* terminal, void* stream) {
-  int rc = check_staged(p, sp);
+// the steady-state draw's generated blocks: enough for n_batches * batch accepted
+// words with a 20 % margin over the expected count (the standard deviation of the
+// count is ~0.1 % of it), + 2 blocks for the start position
+static int64_t draw_blocks(const SacenvReplayParams* p, int32_t batch, int32_t n_batches) {
+  const uint64_t rng = (uint64_t)(p->mem_size - 1);
+  uint64_t mask = rng;
+  for (int sh = 1; sh < 64; sh <<= 1) mask |= mask >> sh;
+  const double acc = (double)(rng + 1) / (double)(mask + 1);
+  const double need = (double)batch * n_batches;
+  return (int64_t)(need / acc * 1.2 / kMtN) + 3;
+}
+
+static int64_t draw_tiles(int64_t blocks) { return (blocks * kMtN + kTile - 1) / kTile; }
+
+static int64_t scratch_bytes(const SacenvReplayParams* p, int32_t batch, int32_t n_batches) {
+  const int64_t K = draw_blocks(p, batch, n_batches), T = draw_tiles(K);
+  return align256(4 * K * kMtN) + 2 * align256(4 * T) + 256;
+}
+
+int sacenv_replay_stage_scratch_bytes(const SacenvReplayParams* p, int32_t batch, int32_t n_batches,
+                                      int64_t* bytes) {
+  const int rc = check_replay(p);
   if (rc) return rc;
-  if (n_steps < 0 || n_steps > sp->seg) return SACENV_E_SIZE;
-  if (!rows || !last_term || !terminal) return SACENV_E_NULL;
-  if (n_steps == 0) return SACENV_OK;
-  hipLaunchKernelGGL(k_rb_stage_terminal, dim3((unsigned)((sp->n + 1023) / 1024)), dim3(256), 0, (hipStream_t)stream,
-                     static_cast<const uint8_t*>(rows), staged_row_bytes(sp), (int64_t)52 * sp->n_pad, n_steps, sp->n,
-                     sp->n_pad, p->terminal_mask, last_term, terminal);
-  return status();
+  if (bytes == nullptr) return SACENV_E_NULL;
+  if (batch < 0 || n_batches < 0) return SACENV_E_SIZE;
+  *bytes = scratch_bytes(p, batch, n_batches);
+  return SACENV_OK;
 }
 
-int sacenv_replay_sample_staged(const SacenvReplayParams* p, void* arena, const SacenvStagedParams* sp, int64_t g,
-                                const void* rows_cur, const uint8_t* term_cur, const void* rows_prev,
-                                const uint8_t* term_prev, int32_t batch, int32_t n_batches, int64_t* idx,
-                                uint32_t* words, void* stream) {
+int sacenv_replay_stage_draw(const SacenvReplayParams* p, void* arena, const SacenvStagedParams* sp, int64_t g,
+                             int32_t batch, int32_t n_batches, int64_t* idx, void* scratch, int64_t scratch_size,
+                             void* stream) {
   int rc = check_staged(p, sp);
   if (rc) return rc;
   if (g < 0 || batch < 0 || n_batches < 0 || n_batches > sp->seg) return SACENV_E_SIZE;
-  // every row learn k can reach lies in segments g and g-1 (and a row's predecessor too)
-  if (p->mem_size > (int64_t)sp->seg * sp->period) return SACENV_E_RANGE;
-  if (!arena || !rows_cur || !term_cur || !rows_prev || !term_prev || !idx || !words) return SACENV_E_NULL;
+  if (!arena || !idx) return SACENV_E_NULL;
   if (batch == 0 || n_batches == 0) return SACENV_OK;
-  if ((g * sp->seg + 1) * sp->period > (int64_t)1 << 62) return SACENV_E_RANGE;
+  if ((g * sp->seg + sp->seg + 1) * sp->period > (int64_t)1 << 62) return SACENV_E_RANGE;
   const RB r = make_rb(*p, arena);
-  hipLaunchKernelGGL(k_rb_draw_many, dim3(1), dim3(kDrawThreads), 0, (hipStream_t)stream, *p, r, batch, n_batches,
-                     g * sp->seg * sp->period, sp->period, idx);
+  const int64_t cntr0 = g * sp->seg * sp->period;
+  const int64_t M = p->mem_size;
+  const bool steady = cntr0 + sp->period >= M && cntr0 + sp->period >= batch && M >= 2;
+  if (!steady) {  // the first learns of a buffer (ranges below M, skipped learns): one workgroup
+    hipLaunchKernelGGL(k_rb_draw_many, dim3(1), dim3(kDrawThreads), 0, (hipStream_t)stream, *p, r, batch,
+                       n_batches, cntr0, sp->period, idx);
+    return status();
+  }
+  if (!scratch) return SACENV_E_NULL;
+  if (scratch_size < scratch_bytes(p, batch, n_batches)) return SACENV_E_SIZE;
+  const int64_t K = draw_blocks(p, batch, n_batches), T = draw_tiles(K);
+  char* sc = static_cast<char*>(scratch);
+  DrawPlan d;
+  d.blocks = reinterpret_cast<const uint32_t*>(sc);
+  d.tile_cnt = reinterpret_cast<int*>(sc + align256(4 * K * kMtN));
+  d.tile_off = reinterpret_cast<int*>(sc + align256(4 * K * kMtN) + align256(4 * T));
+  d.ctrl = reinterpret_cast<int*>(sc + align256(4 * K * kMtN) + 2 * align256(4 * T));
+  d.rng = (uint32_t)(M - 1);
+  uint32_t mask = d.rng;
+  for (int sh = 1; sh < 32; sh <<= 1) mask |= mask >> sh;
+  d.mask = mask;
+  d.need = (int64_t)batch * n_batches;
+  d.p0 = -1;       // (read by the kernels from ctrl[3], which k_mt_chain sets)
+  d.n_words = -1;
+  hipLaunchKernelGGL(k_mt_chain, dim3(1), dim3(kWave), 0, (hipStream_t)stream, r,
+                     reinterpret_cast<uint32_t*>(sc), (int)K, d.ctrl);
   if ((rc = status())) return rc;
-  Staged S;
-  S.cur = static_cast<const char*>(rows_cur);
-  S.prev = static_cast<const char*>(rows_prev);
-  S.tcur = term_cur;
-  S.tprev = term_prev;
-  S.row_bytes = staged_row_bytes(sp);
-  S.period = sp->period;
-  S.offset = sp->offset;
-  S.g = g;
-  S.n = sp->n;
-  S.n_pad = sp->n_pad;
-  S.seg = sp->seg;
-  S.exp2 = sp->experiment == 2;
+  hipLaunchKernelGGL(k_draw_count, dim3((unsigned)T), dim3(kTileThreads), 0, (hipStream_t)stream, d, (int64_t)K);
+  if ((rc = status())) return rc;
+  hipLaunchKernelGGL(k_draw_scan, dim3(1), dim3(1024), 0, (hipStream_t)stream, d, (int)T);
+  if ((rc = status())) return rc;
+  hipLaunchKernelGGL(k_draw_emit, dim3((unsigned)T), dim3(kTileThreads), 0, (hipStream_t)stream, d, r, (int64_t)K,
+                     idx);
+  return status();
+}
+
+int sacenv_replay_stage_mark(const SacenvReplayParams* p, const SacenvStagedParams* sp, int64_t g,
+                             const int64_t* idx_g, const int64_t* idx_next, int32_t batch, int32_t n_batches,
+                             uint64_t* marks, void* stream) {
+  int rc = check_staged(p, sp);
+  if (rc) return rc;
+  if (g < 0 || batch < 0 || n_batches < 0 || n_batches > sp->seg) return SACENV_E_SIZE;
+  if (!idx_g || !marks) return SACENV_E_NULL;
+  const hipError_t e = hipMemsetAsync(marks, 0, (size_t)sp->seg * (sp->n_pad / kWave) * 8, (hipStream_t)stream);
+  if (e != hipSuccess) return (int)e;
+  const int64_t per = (int64_t)batch * n_batches;
+  if (per == 0) return SACENV_OK;
+  // without the next segment's draws, only this segment's learns mark
+  const int64_t total = idx_next != nullptr ? 2 * per : per;
+  hipLaunchKernelGGL(k_rb_stage_mark, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     *p, geom(sp, g), idx_g, idx_next != nullptr ? idx_next : idx_g, batch, n_batches,
+                     reinterpret_cast<unsigned long long*>(marks), total);
+  return status();
+}
+
+int sacenv_replay_sample_staged(const SacenvReplayParams* p, const SacenvStagedParams* sp, int64_t g,
+                                const void* stage_cur, const void* stage_prev, const int64_t* idx, int32_t batch,
+                                int32_t n_batches, uint32_t* words, void* stream) {
+  int rc = check_staged(p, sp);
+  if (rc) return rc;
+  if (g < 0 || batch < 0 || n_batches < 0 || n_batches > sp->seg) return SACENV_E_SIZE;
+  if (!stage_cur || !stage_prev || !idx || !words) return SACENV_E_NULL;
+  if (((reinterpret_cast<uintptr_t>(stage_cur) | reinterpret_cast<uintptr_t>(stage_prev)) & 15u) != 0u)
+    return SACENV_E_RANGE;
+  if (batch == 0 || n_batches == 0) return SACENV_OK;
+  StagedRows S;
+  S.cur = static_cast<const char*>(stage_cur);
+  S.prev = static_cast<const char*>(stage_prev);
   for (int k = 0; k < SACENV_OBS_DIM; ++k) S.first[k] = sp->first_obs[k];
   const int64_t total = (int64_t)batch * n_batches;
   const int64_t per = (int64_t)batch * (2 * SACENV_OBS_DIM + 1 + 3);
   hipLaunchKernelGGL(k_rb_gather_staged, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                     *p, S, batch, n_batches, idx, words, per);
+                     *p, geom(sp, g), S, batch, n_batches, idx, words, per);
   return status();
 }
 

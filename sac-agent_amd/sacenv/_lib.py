@@ -72,7 +72,7 @@ LAYOUT_FIELDS = (
     "refill_list",
     "wind_knots", "knots_raw", "mt_key", "record", "obs", "reward", "done", "term",
     "final_obs", "final_ep_reward", "accel", "reward64", "refill_mask", "status",
-    "spline_g", "wind_table")
+    "spline_g", "wind_table", "last_term")
 
 
 class BoatLayout(C.Structure):
@@ -144,7 +144,8 @@ EXPORTS = ("sacenv_abi_version", "sacenv_error_string", "sacenv_boat_layout",
            "sacenv_toy_reset", "sacenv_toy_step", "sacenv_mixed_step", "sacenv_mixed_step_pooled",
            "sacenv_mixed_segment", "sacenv_replay_layout",
            "sacenv_replay_init", "sacenv_replay_store", "sacenv_replay_store_env", "sacenv_replay_sample", "sacenv_replay_store_shard",
-           "sacenv_replay_sample_shard", "sacenv_replay_stage_terminal", "sacenv_replay_sample_staged",
+           "sacenv_replay_sample_shard", "sacenv_replay_stage_scratch_bytes", "sacenv_replay_stage_draw",
+           "sacenv_replay_stage_mark", "sacenv_replay_sample_staged",
            "sacenv_compact_done", "sacenv_boat_reset_list", "sacenv_sac_layout", "sacenv_sac_sync",
            "sacenv_sac_act", "sacenv_sac_act_handoff", "sacenv_sac_act_occupancy", "sacenv_sac_learn")
 
@@ -196,7 +197,7 @@ def load(path: str | None = None):
         "sacenv_boat_step_pooled": (C.c_int, [P, _p, _p, _p, _p]),
         "sacenv_boat_refill": (C.c_int, [P, _p, _p]),
         "sacenv_boat_rollout": (C.c_int, [P, _p, _p, _i32, _p, _p, _p]),
-        "sacenv_boat_segment": (C.c_int, [P, _p, _p, _i64, _i32, _p, _p, C.c_uint32, _p, _i64, _p]),
+        "sacenv_boat_segment": (C.c_int, [P, _p, _p, _i64, _i32, _p, _p, C.c_uint32, _p, _i64, _p, _p, _p]),
         "sacenv_boat_segment_occupancy": (C.c_int, [P, _i32] + [C.POINTER(_i32)] * 4),
         "sacenv_stream_create_exclusive": (C.c_int, [C.POINTER(_p)]),
         "sacenv_stream_destroy": (C.c_int, [_p]),
@@ -218,8 +219,10 @@ def load(path: str | None = None):
         "sacenv_replay_store_shard": (C.c_int, [RP, _p, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p]),
         "sacenv_replay_sample_shard": (C.c_int, [RP, _p, _i32, _i64, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p,
                                                  _p]),
-        "sacenv_replay_stage_terminal": (C.c_int, [RP, SP, _p, _i32, _p, _p, _p]),
-        "sacenv_replay_sample_staged": (C.c_int, [RP, _p, SP, _i64, _p, _p, _p, _p, _i32, _i32, _p, _p, _p]),
+        "sacenv_replay_stage_scratch_bytes": (C.c_int, [RP, _i32, _i32, C.POINTER(_i64)]),
+        "sacenv_replay_stage_draw": (C.c_int, [RP, _p, SP, _i64, _i32, _i32, _p, _p, _i64, _p]),
+        "sacenv_replay_stage_mark": (C.c_int, [RP, SP, _i64, _p, _p, _i32, _i32, _p, _p]),
+        "sacenv_replay_sample_staged": (C.c_int, [RP, SP, _i64, _p, _p, _p, _i32, _i32, _p, _p]),
         "sacenv_sac_layout": (C.c_int, [C.POINTER(SacParams), C.POINTER(SacLayout)]),
         "sacenv_sac_sync": (C.c_int, [C.POINTER(SacParams), _p, _p]),
         "sacenv_sac_act": (C.c_int, [C.POINTER(SacParams), _p, _p, _i32, _p, _p, _p, _p]),

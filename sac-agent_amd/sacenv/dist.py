@@ -280,15 +280,16 @@ def shard_owner(rows, cntr: int, mem_size: int, period: int, n_per_rank: int):
 class SegmentExchange:
     """The replay exchange of a segment, run on a side stream while the next segment steps.
 
-    ``sampler`` is a ``sacenv.replay.StagedReplay`` (or anything with ``rows(g)``,
-    ``begin(obs)`` and ``sample_segment(g)``): segment g's step launch writes its
-    transition rows into ``rows(g)``; ``after(g)`` then enqueues the segment's
-    learns' sampling -- terminal scan, index draws, gather, and the one SUM
-    all-reduce over the ranks -- on the side stream, behind the segment.
-    ``before(g)`` makes the stepping stream wait for ``after(g - 2)``, whose
-    gather still reads the buffer segment g is about to overwrite (three
-    buffers: the sampling of segment g overlaps segment g + 1). Segments are
-    counted from ``start`` (the replay buffer starts empty there)."""
+    ``sampler`` is a ``sacenv.replay.StagedReplay`` (or anything with ``begin(obs)``,
+    ``stage_args(g)``, ``prepare(g)`` and ``sample_segment(g)``). Per segment g:
+    ``before()`` makes the stepping stream wait for the marks of segment g's rows and
+    for ``sample_segment(g - 2)`` (its gather still reads the buffer segment g is about
+    to overwrite); the launch writes its rows (``stage_args()``); ``after()`` enqueues on
+    the side stream, without waiting for the launch, the next segment's draws and marks
+    (``prepare(g + 1)``), then -- behind the launch -- the segment's batches: the gather
+    and the one SUM all-reduce over the ranks. So the draws, the gather and the
+    collective all overlap the next segment. Segments are counted from ``start`` (the
+    replay buffer starts empty there)."""
 
     def __init__(self, sampler, device):
         self.sampler = sampler
@@ -298,6 +299,7 @@ class SegmentExchange:
         self.g = 0               # segments exchanged so far
         self.started = False
         self._done = {}
+        self._ready = {}
         self.exchanges = 0
         self.last = None         # the batches of the latest segment
 
@@ -305,22 +307,28 @@ class SegmentExchange:
         return torch.cuda.current_stream(self.device) if self.cuda else None
 
     def start(self, obs: torch.Tensor) -> None:
-        """The obs every env starts from (the s of the first stored transition)."""
+        """The obs every env starts from (the s of the first stored transition); the
+        first segments' draws and marks, on the stepping stream."""
         self.sampler.begin(obs)
         self.started, self.g = True, 0
 
-    def rows(self) -> torch.Tensor:
-        """The row buffer of the segment about to be stepped."""
-        return self.sampler.rows(self.g)
+    def stage_args(self) -> dict:
+        """The row arguments of the segment about to be stepped."""
+        return self.sampler.stage_args(self.g)
 
     def before(self) -> None:
-        ev = self._done.pop(self.g - 2, None)
-        if ev is not None:
-            self._cur().wait_event(ev)
+        for ev in (self._done.pop(self.g - 2, None), self._ready.pop(self.g, None)):
+            if ev is not None:
+                self._cur().wait_event(ev)
 
     def after(self) -> None:
         g = self.g
         if self.cuda:
+            with torch.cuda.stream(self.side):
+                self.sampler.prepare(g + 1)       # independent of the launch: overlaps it
+                ev = torch.cuda.Event()
+                ev.record(self.side)
+            self._ready[g + 1] = ev
             self.side.wait_stream(self._cur())
             with torch.cuda.stream(self.side):
                 self.last = self.sampler.sample_segment(g)
@@ -328,6 +336,7 @@ class SegmentExchange:
                 ev.record(self.side)
             self._done[g] = ev
         else:
+            self.sampler.prepare(g + 1)
             self.last = self.sampler.sample_segment(g)
         self.g += 1
         self.exchanges += 1
@@ -335,6 +344,7 @@ class SegmentExchange:
     def wait(self) -> None:
         """The stepping stream waits for every exchange in flight."""
         if self.cuda:
-            for ev in self._done.values():
+            for ev in list(self._done.values()) + list(self._ready.values()):
                 self._cur().wait_event(ev)
         self._done.clear()
+        self._ready.clear()

@@ -245,36 +245,38 @@ class StagedReplay:
     """The pooled replay buffer of main.py:78-90 -- every rank's envs storing one
     transition each per step into ONE agent/buffer.py ring (``ReplayBuffer(mem_size)``,
     buffer.py:13-22) and one ``learn()`` sampling it after every step (buffer.py:24-35)
-    -- sampled straight out of the segments of transition rows the persistent step
-    launch writes (``sacenv_boat_segment``'s ``trans``), with no ring and no store.
+    -- served from the rows the persistent step launch writes, with no ring and no
+    store of rows nobody reads.
 
-    Segment g's steps write their rows into ``rows(g)`` (one of ``n_buffers``
-    [seg][row] buffers; ``row = _lib.trans_bytes(exp) * n_pad``). ``sample_segment(g)``
-    then enqueues, on the current stream: the reference's stored terminal of every
-    row (``sacenv_replay_stage_terminal``: main.py:83-88 with the persistent
-    ``info['termination']``), the seg learns' index draws (np.random.choice on the
-    buffer's MT19937 stream, seeded like ``np.random.seed(seed)``, each learn with the
-    mem_cntr it saw), the gather of this rank's sampled rows from segments g and g-1,
-    and (world > 1) ONE SUM all-reduce of the packed batches -- the pooled buffer's
-    batches, bit for bit, on every rank (tests/test_staged_replay_gpu.py). Per
-    segment ~27 MB cross the links at batch 1 024, whatever the world size, where
-    the all-gather moves every transition to every rank.
+    The batches' indices depend only on the sampling stream (np.random.choice on an
+    MT19937 state seeded like ``np.random.seed(seed)``) and on how many rows were
+    stored before each learn, so they are drawn AHEAD: ``prepare(g)`` draws segment
+    g+1's learns and marks the rows of segment g that the learns of segments g and
+    g+1 will read (``sacenv_replay_stage_draw`` / ``_stage_mark``); segment g's launch
+    (``sacenv_boat_segment`` with ``**stage_args(g)``) writes exactly those rows (64 B
+    each); ``sample_segment(g)`` gathers this rank's share of segment g's batches from
+    segments g and g-1 (``sacenv_replay_sample_staged``) and, with world > 1, ONE SUM
+    all-reduce of the packed batches makes them the pooled buffer's batches, bit for
+    bit, on every rank (tests/test_staged_replay_gpu.py). ~27 MB cross the links per
+    256-step segment at batch 1 024, whatever the world size.
 
-    Buffer reuse: ``sample_segment(g)`` reads rows(g) and rows(g-1), so segment
-    g+2 (which writes rows(g-1) with 3 buffers) must not start before it is done
-    (``done(g)``); with 3 buffers the sampling of segment g overlaps segment g+1."""
+    Order per segment g (``begin`` did draws 0 and 1 and the marks of segment 0):
+    ``stage_args(g)`` -> the launch -> ``prepare(g + 1)`` -> ``sample_segment(g)``.
+    Buffers: the staged rows of segment g are read by ``sample_segment(g)`` and
+    ``(g + 1)``, so the launch of segment g + 2 (3 buffers) must follow
+    ``sample_segment(g)`` in stream order (``sacenv.dist.SegmentExchange`` arranges it)."""
+
+    N_BUFFERS = 3
 
     def __init__(self, n: int, n_pad: int, experiment: int, first_obs, *, rank: int = 0, world: int = 1,
                  mem_size: int = 1_000_000, batch: int = 1024, seg: int = 256, seed: int = 0,
-                 device=None, group=None, n_buffers: int = 3, terminal_mask: int = TERMINAL_GOAL):
+                 device=None, group=None, terminal_mask: int = TERMINAL_GOAL):
         self.lib = _lib.load()
         self.device = torch.device(device if device is not None else "cuda")
         if self.device.type != "cuda":
             raise RuntimeError("StagedReplay runs on a GPU (HIP); no CPU path")
         if self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
-        if n_buffers < 3:
-            raise ValueError("the sampling of segment g reads two buffers while g+1 writes a third")
         self.n, self.n_pad, self.seg, self.batch = int(n), int(n_pad), int(seg), int(batch)
         self.rank, self.world, self.group = int(rank), int(world), group
         self.mem_size = int(mem_size)
@@ -293,61 +295,76 @@ class StagedReplay:
         # the sampling stream lives in a replay arena (its key / pos fields)
         self._rb = DeviceReplayBuffer(self.mem_size, (_lib.OBS_DIM,), 1, device=self.device, seed=seed,
                                       reward_f32=True, terminal_mask=terminal_mask)
-        self.row_bytes = _lib.trans_bytes(experiment) * self.n_pad
-        self.buffers = [torch.zeros(self.seg * self.row_bytes, dtype=torch.uint8, device=self.device)
-                        for _ in range(n_buffers)]
-        self.terminal = [torch.zeros(self.seg * self.n_pad, dtype=torch.uint8, device=self.device)
-                         for _ in range(n_buffers)]
-        self.last_term = torch.zeros(self.n, dtype=torch.uint8, device=self.device)
+        nb = self.N_BUFFERS
+        self.stage = [torch.zeros(self.seg * self.n_pad * 64, dtype=torch.uint8, device=self.device)
+                      for _ in range(nb)]
+        self.marks = [torch.zeros(self.seg * self.n_pad // 64, dtype=torch.int64, device=self.device)
+                      for _ in range(nb)]
+        self._idx = [torch.empty(self.seg * self.batch, dtype=torch.int64, device=self.device) for _ in range(4)]
         self._words = [_packed_batches(self.batch, self.seg, _lib.OBS_DIM, 1, (_lib.OBS_DIM,), self.device)
                        for _ in range(2)]
-        self._idx = [torch.empty(self.seg * self.batch, dtype=torch.int64, device=self.device) for _ in range(2)]
-        self._events = {}
+        nbytes = C.c_int64()
+        _lib.check(self.lib.sacenv_replay_stage_scratch_bytes(self._rb._pp, self.batch, self.seg, C.byref(nbytes)))
+        self._scratch = torch.empty(int(nbytes.value), dtype=torch.uint8, device=self.device)
+        self.drawn = 0   # segments whose learns are drawn
 
     @property
     def stream(self) -> int:
         return torch.cuda.current_stream(self.device).cuda_stream
 
-    def rows(self, g: int) -> torch.Tensor:
-        """Segment g's row buffer: step j of the segment writes row j (stride ``row_bytes``)."""
-        return self.buffers[int(g) % len(self.buffers)]
+    def _draw(self) -> None:
+        g = self.drawn
+        _lib.check(self.lib.sacenv_replay_stage_draw(
+            self._rb._pp, self._rb.arena.data_ptr(), self._spp, g, self.batch, self.seg,
+            self._idx[g % 4].data_ptr(), self._scratch.data_ptr(), self._scratch.numel(), self.stream))
+        self.drawn += 1
 
-    def begin(self, reset_obs: torch.Tensor) -> None:
-        """Before segment 0: the obs every env starts from (the s of step 0) go into the
-        last row of the buffer standing for segment -1, with term 0."""
-        b = self.rows(-1)
-        last = b[(self.seg - 1) * self.row_bytes: self.seg * self.row_bytes]
-        np_ = self.n_pad
+    def _mark(self, g: int) -> None:
+        _lib.check(self.lib.sacenv_replay_stage_mark(
+            self._rb._pp, self._spp, g, self._idx[g % 4].data_ptr(), self._idx[(g + 1) % 4].data_ptr(),
+            self.batch, self.seg, self.marks[g % self.N_BUFFERS].data_ptr(), self.stream))
+
+    def begin(self, obs: torch.Tensor) -> None:
+        """The buffer starts empty here: the obs every env starts from (the s of its first
+        stored transition) go into the last row of the buffer standing for segment -1,
+        with term 0; segment 0 and 1's learns are drawn and segment 0's rows marked."""
+        nb = self.N_BUFFERS
+        last = self.stage[(-1) % nb][(self.seg - 1) * self.n_pad * 64:].view(torch.float32).view(self.n_pad, 16)
         last.zero_()
-        last[: 44 * np_].view(torch.float32).view(np_, _lib.OBS_DIM)[: self.n].copy_(
-            reset_obs.to(device=self.device, dtype=torch.float32))
-        self.terminal[(-1) % len(self.buffers)].zero_()
-        self.last_term.zero_()
+        last[: self.n, : _lib.OBS_DIM].copy_(obs.to(device=self.device, dtype=torch.float32))
+        self.drawn = 0
+        self._draw()
+        self._draw()
+        self._mark(0)
 
-    def sample_segment(self, g: int, n_batches: int | None = None):
-        """Enqueue segment g's learns' batches (after its steps were enqueued on this
-        stream); returns [(state, action, reward f64, new_state, terminal bool, idx)],
-        one per learn, views that stay valid until ``sample_segment(g + 2)``."""
+    def stage_args(self, g: int) -> dict:
+        """The staged-row arguments of segment g's launch (VecBoatEnv.segment_async /
+        sacenv_boat_segment): its 64-B row buffer and the marks of the rows to write."""
+        return {"stage": self.stage[g % self.N_BUFFERS], "marks": self.marks[g % self.N_BUFFERS]}
+
+    def prepare(self, g: int) -> None:
+        """Before segment g steps (after segment g - 1 was launched): draw segment g+1's
+        learns and mark segment g's rows."""
+        while self.drawn < g + 2:
+            self._draw()
+        self._mark(g)
+
+    def sample_segment(self, g: int):
+        """Enqueue segment g's learns' batches (after its launch, on this stream); returns
+        [(state, action, reward f64, new_state, terminal int32 0/1, idx)], one per learn,
+        views valid until ``sample_segment(g + 2)``."""
         import torch.distributed as dist
         g = int(g)
-        nb = self.seg if n_batches is None else int(n_batches)
         words, views = self._words[g % 2]
-        idx = self._idx[g % 2]
-        nbuf = len(self.buffers)
-        cur, prev = g % nbuf, (g - 1) % nbuf
-        rp = self._rb._pp
-        _lib.check(self.lib.sacenv_replay_stage_terminal(rp, self._spp, self.buffers[cur].data_ptr(), self.seg,
-                                                         self.last_term.data_ptr(), self.terminal[cur].data_ptr(),
-                                                         self.stream))
+        idx = self._idx[g % 4]
+        nb = self.N_BUFFERS
         _lib.check(self.lib.sacenv_replay_sample_staged(
-            rp, self._rb.arena.data_ptr(), self._spp, g, self.buffers[cur].data_ptr(), self.terminal[cur].data_ptr(),
-            self.buffers[prev].data_ptr(), self.terminal[prev].data_ptr(), self.batch, nb, idx.data_ptr(),
-            words.data_ptr(), self.stream))
+            self._rb._pp, self._spp, g, self.stage[g % nb].data_ptr(), self.stage[(g - 1) % nb].data_ptr(),
+            idx.data_ptr(), self.batch, self.seg, words.data_ptr(), self.stream))
         if self.world > 1:
             dist.all_reduce(words, op=dist.ReduceOp.SUM, group=self.group)
         B = self.batch
-        return [(st, ac, rw, ns, tm32.to(torch.bool), idx[i * B: (i + 1) * B])
-                for i, (st, ac, rw, ns, tm32, _) in enumerate(views[:nb])]
+        return [(st, ac, rw, ns, tm32, idx[i * B: (i + 1) * B]) for i, (st, ac, rw, ns, tm32, _) in enumerate(views)]
 
     @property
     def bytes_per_segment(self) -> int:

@@ -101,8 +101,11 @@ class VecBoatEnv:
         self.mt_pos = view(L.mt_pos, i32, NP)[:N]
         self.start_y_slots = view(L.start_y, i32, _lib.SLOTS, NP)[:, :N]
         self.counters = view(L.counters, i32, _lib.N_COUNTERS, NP)[:, :N]
+        # info['termination'] as the reference keeps it: the last code 1..5 (0: none yet)
+        self.last_term = view(L.last_term, i32, NP)[:N]
         self.wind_knots = view(L.wind_knots, f64, NP, _lib.SLOTS, 2, nk, 2)
-        self.knots_raw_slots = view(L.knots_raw, f64, NP, _lib.SLOTS, 2, nk)
+        # the drawn knots per slot exist only with record_knots (SACENV_OUT_KNOTS)
+        self.knots_raw_slots = view(L.knots_raw, f64, NP, _lib.SLOTS, 2, nk) if record_knots else None
         self.mt_key = view(L.mt_key, i32, NP, _lib.MT_N)[:N]
         self.spline_g = view(L.spline_g, f64, nk, nk)
         # outputs: the packed record (the all-gather payload) and extras
@@ -169,6 +172,8 @@ class VecBoatEnv:
     @property
     def knots_raw(self) -> torch.Tensor:
         """Knot values [2, n_knots, N] of each env's current episode (record_knots)."""
+        if self.knots_raw_slots is None:
+            raise RuntimeError("construct the env with record_knots=True to keep the drawn knots")
         slot = (self.cons % _lib.SLOTS).long() if self.autoreset else torch.zeros_like(self.cons).long()
         k = self.knots_raw_slots[: self.num_envs]                     # [N, SLOTS, 2, nk]
         return k[torch.arange(self.num_envs, device=k.device), slot].permute(1, 2, 0)
@@ -286,7 +291,8 @@ class VecBoatEnv:
         return records, final_obs
 
     def segment_async(self, actions: torch.Tensor, n_steps: int | None = None, *, act_ready=None,
-                      step_done=None, seq0: int = 0, trans=None, trans_stride: int = 0) -> None:
+                      step_done=None, seq0: int = 0, trans=None, trans_stride: int = 0, stage=None,
+                      stage_marks=None) -> None:
         """``n_steps`` BoatEnv.step calls in ONE persistent launch (``sacenv_boat_segment``):
         the same results as ``n_steps`` ``step_async`` calls, bit for bit, with the
         carried state in registers between the steps and each step's outputs in the
@@ -297,7 +303,9 @@ class VecBoatEnv:
         [n_pad/64]) the wave steps ks only once ``act_ready[w] >= seq0 + ks + 1``;
         with ``step_done`` it publishes ``seq0 + ks + 1`` there once step ks's outputs
         are visible. ``trans`` (u8 device, 16-B aligned): step ks's pooled transition
-        row at ``trans[ks * trans_stride:]``."""
+        row at ``trans[ks * trans_stride:]``. ``stage`` / ``stage_marks``: the staged
+        replay rows (64 B per step and env, written where the mark bit is set;
+        ``sacenv.replay.StagedReplay``)."""
         K = int(actions.shape[0]) if n_steps is None else int(n_steps)
         if (not isinstance(actions, torch.Tensor) or actions.dtype != torch.float32
                 or actions.device != self.device or actions.dim() != 2
@@ -318,12 +326,22 @@ class VecBoatEnv:
             if (trans.dtype != torch.uint8 or trans.device != self.device or not trans.is_contiguous()
                     or trans.numel() < (K - 1) * int(trans_stride) + nb):
                 raise ValueError("trans must be a contiguous uint8 device tensor holding K rows")
+        if stage is not None:
+            if (stage.dtype != torch.uint8 or stage.device != self.device or not stage.is_contiguous()
+                    or stage.numel() < K * 64 * self.n_pad):
+                raise ValueError("stage must be a contiguous uint8 device tensor of n_steps x 64 x n_pad bytes")
+            if stage_marks is not None and (stage_marks.dtype != torch.int64 or stage_marks.device != self.device
+                                            or not stage_marks.is_contiguous()
+                                            or stage_marks.numel() < K * self.n_pad // 64):
+                raise ValueError("stage_marks must be a contiguous int64 device tensor of n_steps x n_pad/64")
         _lib.check(self.lib.sacenv_boat_segment(
             self._pp, self._ptr, actions.data_ptr(), int(actions.stride(0)), K,
             None if act_ready is None else act_ready.data_ptr(),
             None if step_done is None else step_done.data_ptr(), int(seq0) & 0xFFFFFFFF,
-            None if trans is None else trans.data_ptr(), int(trans_stride), self.stream))
-        self._keep_seg = (actions, act_ready, step_done, trans)
+            None if trans is None else trans.data_ptr(), int(trans_stride),
+            None if stage is None else stage.data_ptr(), None if stage_marks is None else stage_marks.data_ptr(),
+            self.stream))
+        self._keep_seg = (actions, act_ready, step_done, trans, stage, stage_marks)
         if self.autoreset:
             self._since_refill += K
 

@@ -34,7 +34,7 @@ def declared_functions():
 def test_library_exports_header(built_lib):
     from sacenv import _lib
     names = declared_functions()
-    assert len(names) == 39
+    assert len(names) == 41
     assert set(names) == set(_lib.EXPORTS)
     for n in names:
         assert hasattr(built_lib, n), n
@@ -43,25 +43,32 @@ def test_library_exports_header(built_lib):
 
 
 def test_staged_sampler_argument_errors_without_gpu(built_lib):
-    """sacenv_replay_stage_terminal / _sample_staged validate on the host, never launching."""
+    """sacenv_replay_stage_draw / _stage_mark / _sample_staged validate on the host, never launching."""
     from sacenv import _lib
     rp = _lib.ReplayParams(mem_size=1_000_000, obs_dim=11, act_dim=1, reward_f32=1, terminal_mask=2)
     sp = _lib.StagedParams(period=4096, offset=0, n=4096, n_pad=4096, seg=256, experiment=6)
     R, S = ctypes.byref(rp), ctypes.byref(sp)
-    args = (1, 1, 1, 1, 1024, 256, 1, 1, None)
+    gather = (0, 1, 1, 1, 1024, 256, 1, None)
     sp.period = sp.n = sp.n_pad = 64      # mem_size > seg * period: a learn could reach older rows
-    assert built_lib.sacenv_replay_sample_staged(R, 1, S, 0, *args) == -5
+    assert built_lib.sacenv_replay_sample_staged(R, S, *gather) == -5
+    assert built_lib.sacenv_replay_stage_draw(R, 1, S, 0, 1024, 256, 1, 1, 1 << 30, None) == -5
     sp.period = sp.n = sp.n_pad = 4096
     rp.obs_dim = 10                       # the boat's rows only
-    assert built_lib.sacenv_replay_sample_staged(R, 1, S, 0, *args) == -4
+    assert built_lib.sacenv_replay_sample_staged(R, S, *gather) == -4
     rp.obs_dim = 11
     sp.n_pad = 4000                       # not a multiple of 64
-    assert built_lib.sacenv_replay_stage_terminal(R, S, 1, 256, 1, 1, None) == -4
+    assert built_lib.sacenv_replay_stage_mark(R, S, 0, 1, 1, 1024, 256, 1, None) == -4
     sp.n_pad, sp.offset = 4096, 1         # offset + n > period
-    assert built_lib.sacenv_replay_stage_terminal(R, S, 1, 256, 1, 1, None) == -5
+    assert built_lib.sacenv_replay_stage_mark(R, S, 0, 1, 1, 1024, 256, 1, None) == -5
     sp.offset = 0
-    assert built_lib.sacenv_replay_stage_terminal(R, S, None, 256, 1, 1, None) == -1
-    assert built_lib.sacenv_replay_sample_staged(R, None, S, 0, *args) == -1
+    assert built_lib.sacenv_replay_stage_mark(R, S, 0, None, 1, 1024, 256, 1, None) == -1
+    assert built_lib.sacenv_replay_sample_staged(R, S, 0, None, 1, 1, 1024, 256, 1, None) == -1
+    assert built_lib.sacenv_replay_stage_draw(R, None, S, 0, 1024, 256, 1, 1, 1 << 30, None) == -1
+    # steady state (g >= 1 here) needs the scratch the library asks for
+    need = ctypes.c_int64()
+    assert built_lib.sacenv_replay_stage_scratch_bytes(R, 1024, 256, ctypes.byref(need)) == 0
+    assert need.value > 4 * 624 * 256 * 1024 / 0.95 / 624
+    assert built_lib.sacenv_replay_stage_draw(R, 1, S, 300, 1024, 256, 1, 1, need.value - 1, None) == -4
 
 
 def test_argument_errors_without_gpu(built_lib):
@@ -152,12 +159,15 @@ def test_ctypes_structs_match_c_layout(tmp_path):
             assert got[(cname, fname)] == getattr(py, fname).offset, (cname, fname)
 
 
-@pytest.mark.parametrize("n", [1, 63, 64, 65536, 100000])
-def test_arena_layout(built_lib, n):
-    """Fields are aligned, disjoint and inside total_bytes; record is contiguous."""
+@pytest.mark.parametrize("n,knots", [(1, False), (63, True), (64, False), (65536, False), (65536, True),
+                                     (100000, False)])
+def test_arena_layout(built_lib, n, knots):
+    """Fields are aligned, disjoint and inside total_bytes; record is contiguous; the
+    drawn knots get storage only when recorded (SACENV_OUT_KNOTS)."""
     from sacenv import _lib
     from sacenv.config import BoatConfig, make_params
-    p = make_params(BoatConfig(experiment=6), n, use_wind_table=True)
+    p = make_params(BoatConfig(experiment=6), n, use_wind_table=True,
+                    out_flags=_lib.OUT_KNOTS if knots else 0)
     L = _lib.layout(p)
     np_ = L.n_pad
     assert np_ % 64 == 0 and n <= np_ < n + 64
@@ -170,8 +180,12 @@ def test_arena_layout(built_lib, n):
              "wind_coef": 64, "wind0_next": 16, "start_y_next": 4,
              "index": 4, "cons": 4, "fill": 4, "mt_pos": 4,
              "start_y": 4 * S, "counters": 20, "refill_list": 12, "wind_knots": 32 * S * nk,
-             "knots_raw": 16 * S * nk, "mt_key": 2496, "obs": 44, "reward": 4, "done": 1, "term": 1,
-             "final_obs": 44, "final_ep_reward": 8, "accel": 24, "reward64": 8}
+             "mt_key": 2496, "obs": 44, "reward": 4, "done": 1, "term": 1,
+             "final_obs": 44, "final_ep_reward": 8, "accel": 24, "reward64": 8, "last_term": 4}
+    if knots:
+        sizes["knots_raw"] = 16 * S * nk
+    else:
+        assert L.knots_raw == -1
     spans = sorted((getattr(L, f), getattr(L, f) + w * np_, f) for f, w in sizes.items())
     for (a0, a1, f), (b0, b1, g) in zip(spans, spans[1:]):
         assert a1 <= b0, (f, g)
@@ -186,6 +200,9 @@ def test_arena_layout(built_lib, n):
         assert off >= end and off % 256 == 0, f
         end = off + w
     assert end <= L.total_bytes
+    if n == 65536:   # per env: the wind slots dominate (<= 75 KB without recorded knots)
+        per_env = (L.total_bytes - 16 * 10000) / n
+        assert per_env <= (103 * 1024 if knots else 70 * 1024), per_env
 
 
 # ---------------------------------------------------------------- MT19937

@@ -201,7 +201,7 @@ def test_long_fixture_bench_segment_runner(name, gpu, built_lib):
         # each step's transition row written by the launch into rows[k]
         _lib.check(env.lib.sacenv_boat_segment(
             env._pp, env._ptr, C.c_void_p(table.data_ptr() + 4 * k0 * E), E, n, ready.data_ptr(),
-            None, 0, C.c_void_p(rows.data_ptr() + k0 * rb), rb,
+            None, 0, C.c_void_p(rows.data_ptr() + k0 * rb), rb, None, None,
             torch.cuda.current_stream(gpu).cuda_stream))
 
     wl = bench.Workload([env], env.step_async, env.refill, table, None, 0, E, 0, segment_step)

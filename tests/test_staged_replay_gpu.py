@@ -3,8 +3,10 @@
 The reference loop (main.py:78-90) stores every env's transition (buffer.py:13-22)
 and runs one learn() -- sample_buffer(batch), buffer.py:24-35 -- after EVERY step,
 each on the buffer as that step left it. StagedReplay draws a segment's learns
-after the segment from the transition rows the persistent launch wrote
-(sacenv_boat_segment's ``trans``), with no ring. The reference side here is the
+after the segment from the rows the persistent launch wrote
+(sacenv_boat_segment's ``stage``), with no ring. The learns' index draws are
+made ahead (they depend only on the sampling stream and the stored counts), and
+the launch writes only the rows those learns read. The reference side here is the
 literal loop on the device: a VecBoatEnv stepped one launch at a time, a
 DeviceReplayBuffer fed every step (store_env_step: the reference's persistent
 terminal rule, new_state = the terminal obs of envs that reset) and sampled
@@ -29,6 +31,13 @@ pytestmark = pytest.mark.gpu
 SEG = 64
 
 
+_BITS = torch.tensor([bin(i).count("1") for i in range(256)], dtype=torch.int64)
+
+
+def _popcount(t: torch.Tensor) -> int:
+    return int(_BITS.to(t.device)[t.view(torch.uint8).long()].sum())
+
+
 def _cfg(exp):
     return {"base_settings": {"experiment": exp, "test_mode": 0}, "boat_env": {"track_width": 30}}
 
@@ -43,6 +52,7 @@ def _run(rank, world, exp, N, M, B, n_segs, dev, group=None):
     rep = StagedReplay(N, env.n_pad, exp, env.first_obs_template(), rank=rank, world=world, mem_size=M,
                        batch=B, seg=SEG, seed=5, device=dev, group=group)
     rep.begin(obs0)
+    assert bool((env.last_term == 0).all())
     ref = ref_rb = None
     if rank == 0:
         ref = VecBoatEnv(_cfg(exp), world * N, **kw)
@@ -50,13 +60,16 @@ def _run(rank, world, exp, N, M, B, n_segs, dev, group=None):
         ref_rb = DeviceReplayBuffer(M, (11,), 1, device=dev, seed=5)
     g = torch.Generator(device=dev)
     g.manual_seed(9)
-    checked = skipped = 0
+    checked = skipped = written = 0
     for s in range(n_segs):
         acts = torch.rand((SEG, world * N), generator=g, device=dev) * 2 - 1
         mine = acts[:, rank * N:(rank + 1) * N].contiguous()
-        env.segment_async(mine, SEG, trans=rep.rows(s), trans_stride=rep.row_bytes)
+        sa = rep.stage_args(s)
+        env.segment_async(mine, SEG, stage=sa["stage"], stage_marks=sa["marks"])
         env.refill()
+        rep.prepare(s + 1)
         got = rep.sample_segment(s)
+        written += _popcount(sa["marks"])
         if ref is None:
             continue
         for k in range(SEG):
@@ -76,8 +89,14 @@ def _run(rank, world, exp, N, M, B, n_segs, dev, group=None):
                 assert torch.equal(x.reshape(-1), y.reshape(-1).to(x.dtype)), (s, k, i)
             checked += 1
         ref.refill()
+        torch.cuda.synchronize()
+        # the arena carries info['termination'] as the buffer's per-env byte does
+        assert torch.equal(ref.last_term.to(torch.uint8), ref_rb._last_term[ref]), s
     torch.cuda.synchronize()
     env.check_status()
+    if rank == 0 and world == 1:
+        # only the rows a learn reads were written: a small share of the segment's rows
+        assert 0 < written < 0.5 * n_segs * SEG * N, written
     return (checked, skipped) if rank == 0 else None
 
 

@@ -44,11 +44,14 @@ class StubSampler:
         self.words = torch.zeros(seg * batch * 26, dtype=torch.int32)
         self.sampled = []
 
-    def rows(self, g):
-        return self.buffers[g % len(self.buffers)]
+    def stage_args(self, g):
+        return {"rows": self.buffers[g % len(self.buffers)]}
 
     def begin(self, obs):
         self.sampled.clear()
+
+    def prepare(self, g):
+        pass
 
     def sample_segment(self, g):
         import torch.distributed as dist

@@ -26,26 +26,37 @@ def main():
     rep, env = x.sampler, wl.envs[0]
     rep.begin(env.obs)
     k = 0
-    for g in range(6):     # serialised: one stream
-        wl.segment_step(k % bench.ACTION_STEPS, bench.SEG, trans=rep.rows(g))
+
+    def seg(g):
+        nonlocal k
+        sa = rep.stage_args(g)
+        wl.segment_step(k % bench.ACTION_STEPS, bench.SEG, stage=sa["stage"], marks=sa["marks"])
         wl.refill()
+        rep.prepare(g + 1)
         rep.sample_segment(g)
         k += bench.SEG
+
+    for g in range(6):     # serialised: one stream
+        seg(g)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for g in range(6, 12):
-        wl.segment_step(k % bench.ACTION_STEPS, bench.SEG, trans=rep.rows(g))
-        wl.refill()
-        rep.sample_segment(g)
-        k += bench.SEG
+        seg(g)
     torch.cuda.synchronize()
     ser = (time.perf_counter() - t0) / (6 * bench.SEG)
+    # the no-exchange segment for reference
+    t0 = time.perf_counter()
+    for g in range(6):
+        wl.segment_step(k % bench.ACTION_STEPS, bench.SEG)
+        wl.refill()
+        k += bench.SEG
+    torch.cuda.synchronize()
+    plain = (time.perf_counter() - t0) / (6 * bench.SEG)
+    x = bench.make_exchange(args, wl, 0, 1, dev)
     run = bench.SegmentRunner(args, wl, dev, None, bench.SEG, x)
-    x.g = 12
-    x.started = True
     rate, k, _ = bench.timed_rate(run, k, 6, 1, dev, wl)
-    print(f"serialised {ser * 1e6:.3f} us/step; overlapped {rate['ms_per_step'] * 1e3:.3f} us/step "
-          f"({rate['value'] / 1e9:.2f} G env-steps/s)", flush=True)
+    print(f"no exchange {plain * 1e6:.3f} us/step; serialised {ser * 1e6:.3f} us/step; overlapped "
+          f"{rate['ms_per_step'] * 1e3:.3f} us/step ({rate['value'] / 1e9:.2f} G env-steps/s)", flush=True)
 
 
 if __name__ == "__main__":
