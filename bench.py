@@ -126,6 +126,9 @@ def parse(argv=None):
     ap.add_argument("--closed-loop", action="store_true",
                     help="a separate line: the SAC actor choosing every step's actions on the device, handing "
                          "off to the persistent env launch through per-wave flags (sacenv.closed_loop)")
+    ap.add_argument("--train", action="store_true",
+                    help="a separate line: main.py:78-90's whole loop per step on the device -- NativeSAC "
+                         "choose_action, the env step, the transitions stored, one learn() on a sampled batch")
     ap.add_argument("--episode-steps", type=int, default=EPISODE_STEPS,
                     help="truncation length (0 = none)")
     return ap.parse_args(argv)
@@ -1151,7 +1154,7 @@ def bench_closed_loop(args, rank, world, dev):
                      n_helpers=args.helpers, auto_refill=False)
     env.reset()
     agent = NativeSAC(dev, init_seed=rank, with_memory=False)
-    loop = ClosedLoop(env, agent, segment=SEG)
+    loop = ClosedLoop(env, agent, segment=SEG, handoff=True)
     g = torch.Generator(device=dev)
     g.manual_seed(77 + rank)
     eps = torch.randn((2, SEG, N), generator=g, device=dev)
@@ -1159,7 +1162,7 @@ def bench_closed_loop(args, rank, world, dev):
 
     def segment(mode):
         e = eps[state["i"] % 2]
-        loop.run(e) if mode == "handoff" else loop.run_eager(e)
+        loop.run_handoff(e) if mode == "handoff" else loop.run_eager(e)
         env.refill()
         state["i"] += 1
 
@@ -1226,6 +1229,103 @@ def bench_closed_loop(args, rank, world, dev):
                                                                        "owner_waves_per_simd", "max_envs")}},
         "modes": rates,
         "policy_alone_us_per_step": act_us,
+        "cpu_baseline": None}
+
+
+# ---------------------------------------------------------------- training-loop line
+def bench_train(args, rank, world, dev):
+    """main.py:78-90's loop, every step, for every env of the rank at once:
+    NativeSAC choose_action on the [N, 11] obs (continuous_agent.py:57-61, one MFMA launch),
+    VecBoatEnv.step (one launch, auto-reset in-kernel; the slot refill every 256 steps),
+    DeviceReplayBuffer.store_env_step (agent/buffer.py:13-22 with main.py:83-88's terminal:
+    one launch for the N transitions), then one learn() (continuous_agent.py:96-154:
+    sample_buffer(1 024) on the device + the four losses and Adam steps on MFMA kernels).
+    The policy noise of choose_action and learn comes from pre-drawn tables (the reference
+    draws it inside). Beside the loop's rate: each part timed alone with HIP events."""
+    from sacenv import VecBoatEnv
+    from sacenv.sac_native import NativeSAC
+    N = args.envs
+    env = VecBoatEnv({"base_settings": {"experiment": args.experiment, "test_mode": args.test_mode}}, N,
+                     seed=0, device=dev, max_episode_steps=args.episode_steps, env_id_offset=rank * N,
+                     n_helpers=args.helpers)
+    env.reset()
+    agent = NativeSAC(dev, init_seed=rank)
+    B = agent.cfg.batch_size
+    g = torch.Generator(device=dev)
+    g.manual_seed(99 + rank)
+    eps = torch.randn((SEG, N), generator=g, device=dev)
+    noise = torch.randn((SEG, 2, B), generator=g, device=dev)
+    prev = torch.empty_like(env.obs)
+    counts = {"learns": 0}
+
+    def step(k):
+        prev.copy_(env.obs)
+        a = agent.choose_action(env.obs, eps=eps[k % SEG])
+        env.step_async(a.view(-1))
+        agent.memory.store_env_step(prev, a, env)
+        if agent.learn(noise=(noise[k % SEG, 0], noise[k % SEG, 1])) is not None:
+            counts["learns"] += 1
+
+    k = 0
+    for _ in range(warm_segs(args.warmup) * SEG):
+        step(k)
+        k += 1
+    _sync(dev)
+    barrier(world)
+    n_timed = timed_segs(args.steps)
+    steps = n_timed * SEG
+    l0 = counts["learns"]
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(k)
+        k += 1
+    _sync(dev)
+    barrier(world)
+    el = _max_over_ranks(time.perf_counter() - t0, world, dev)
+    learns = counts["learns"] - l0
+    env.check_status()
+
+    # each part alone (HIP events on the stream they run on), 64 repetitions
+    st = torch.cuda.current_stream(dev)
+
+    def timed(fn, reps=64):
+        fn()
+        ea, eb = _Clock(dev), _Clock(dev)
+        ea.record(st)
+        for _ in range(reps):
+            fn()
+        eb.record(st)
+        _sync(dev)
+        return ea.ms_to(eb) * 1e3 / reps
+
+    a0 = agent.choose_action(env.obs, eps=eps[0]).view(-1).contiguous()
+    parts = {"choose_action_us": timed(lambda: agent.choose_action(env.obs, eps=eps[0])),
+             "env_step_us": timed(lambda: env.step_async(a0)),
+             "store_us": timed(lambda: agent.memory.store_env_step(prev, a0, env)),
+             "sample_us": timed(lambda: agent.memory.sample(B)),
+             "learn_us": timed(lambda: agent.learn(noise=(noise[0, 0], noise[0, 1])))}
+    if rank != 0:
+        return None
+    return {
+        "metric": f"env-steps/sec (whole node), boat_env exp-{args.experiment} training loop (act + step + store "
+                  f"+ sample + learn per step), {N:,} envs/GPU".replace(",", " "),
+        "value": world * N * steps / el, "unit": "env-steps/s", "n_gpus": world, "steps": steps,
+        "warmup": warm_segs(args.warmup) * SEG, "ms_per_step": el / steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64 env, f32 agent",
+        "data": "synthetic: random-init SAC networks (torch.manual_seed), N(0,1) policy noise tables, per-env "
+                "MT19937 wind/start draws",
+        "config": {"workload": f"boat_env exp {args.experiment}, {N} envs/GPU, {args.episode_steps}-step episodes, "
+                               f"in-kernel auto-reset; NativeSAC (256-256 MLPs, batch {B}, ReplayBuffer"
+                               f"({agent.memory.mem_size})), one learn() per step",
+                   "envs_per_gpu": N, "parallelism": f"env-dp{world}" + (" (independent replicas)" if world > 1
+                                                                          else ""),
+                   "launch": "per step: sacenv_sac_act, sacenv_boat_step, sacenv_replay_store_env, "
+                             "sacenv_replay_sample (draw + gather), sacenv_sac_learn (4 launches); the slot refill "
+                             "every 256 steps"},
+        "learns_timed": learns,
+        "parts": parts,
+        "note": "the loop is learn-bound: one learn() of a 1 024-row batch per step of all N envs (the "
+                "reference's ratio is one learn per env step of ONE env)",
         "cpu_baseline": None}
 
 
@@ -1304,7 +1404,7 @@ def main(argv=None):
         sys.exit(spawn_ranks(args.gpus, argv))
     cpu = None
     if (int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.no_cpu_baseline and not args.rollout
-            and not args.closed_loop and not args.stub):
+            and not args.closed_loop and not args.train and not args.stub):
         # before anything touches the GPU: the C1 legs are child processes, and an
         # idle host keeps them from competing with the timed region's launches
         cpu = cpu_baseline(args, args.mixed_envs if args.mixed else args.envs)
@@ -1320,8 +1420,8 @@ def main(argv=None):
             import torch.distributed as dist
             dist.destroy_process_group()
         return
-    if args.closed_loop:
-        out = bench_closed_loop(args, rank, world, dev)
+    if args.closed_loop or args.train:
+        out = (bench_closed_loop if args.closed_loop else bench_train)(args, rank, world, dev)
         if out is not None:
             print(json.dumps(out), flush=True)
         if world > 1:

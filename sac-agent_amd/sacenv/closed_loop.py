@@ -37,6 +37,20 @@ Then all owner waves are resident, each policy workgroup's wait ends, and the
 policy launches drain. A configuration that fails is refused (65 536 envs fit:
 one owner wave of ~320 VGPRs per SIMD beside one ~152-VGPR policy wave).
 
+Which form runs. ``ClosedLoop(env, agent)`` runs the EAGER form
+by default (``run_eager``: one ``choose_action`` launch at full occupancy, then one
+step launch, on one stream -- main.py:78-81's order, bit-identical to the hand-off):
+with the reference's 256-256 actor on 65 536 envs the policy (~75 us) dwarfs the env
+step (~1.3 us), the launch boundary the hand-off removes costs nothing by comparison,
+and the hand-off's policy -- one workgroup per CU beside the resident owner waves --
+runs at 0.43x its full-occupancy rate (measured 0.38 G vs 0.80 G env-steps/s). The
+hand-off form (``handoff=True``) pays where the policy is cheaper than the env step
+(a small actor, or far more envs per policy row). Its co-residency rests on one more
+assumption than the plan can check: that the dispatcher spreads a policy workgroup's
+4 waves over the CU's 4 SIMDs (two on one SIMD leave 208 VGPRs, below an owner
+wave's 320); the abort protocol bounds what a violation costs (an error after ~seconds,
+not a hang).
+
 Timeouts. A flag that never comes (~seconds) sets SACENV_STATUS_HANDOFF_TIMEOUT;
 from then on every hand-off launch is a no-op on the device (sacenv.h's abort
 protocol), ``check()`` raises, and ``run()`` refuses to enqueue more steps once
@@ -116,12 +130,23 @@ def plan(env, n_cu: int | None = None) -> CoResidencyPlan:
 
 
 class ClosedLoop:
-    """Drives ``env`` (a ``VecBoatEnv``) with ``agent`` (a ``NativeSAC``)."""
+    """Drives ``env`` (a ``VecBoatEnv``) with ``agent`` (a ``NativeSAC``): ``run`` is the
+    eager form unless ``handoff=True`` (module docstring). A context manager: ``close``
+    (or leaving the ``with`` block) releases the hand-off's policy queue."""
 
-    def __init__(self, env, agent, segment: int = _lib.REFILL_PERIOD, n_cu: int | None = None):
+    def __init__(self, env, agent, segment: int = _lib.REFILL_PERIOD, n_cu: int | None = None,
+                 handoff: bool = False):
         if segment < 1 or (env.autoreset and segment > _lib.REFILL_PERIOD):
             raise ValueError(f"segment must be 1..{_lib.REFILL_PERIOD}")
         self.env, self.agent, self.K = env, agent, int(segment)
+        self.handoff = bool(handoff)
+        self.seq = 0
+        self.failed = False
+        self._keep = []
+        self._policy_handle = None
+        self.plan = None
+        if not self.handoff:
+            return
         self.plan = plan(env, n_cu)
         dev = env.device
         nw = env.n_pad // 64
@@ -141,19 +166,28 @@ class ClosedLoop:
             _lib.check(_lib.load().sacenv_stream_create_exclusive(C.byref(h)))
         self._policy_handle = h
         self.policy_stream = torch.cuda.ExternalStream(h.value, device=dev)
-        self.seq = 0
-        self.failed = False
-        self._keep = []
 
-    def __del__(self):
+    def close(self) -> None:
+        """Release the policy's hardware queue once its work is done (waits for that
+        stream only, not the device)."""
         h = getattr(self, "_policy_handle", None)
         if h is not None and h.value:
-            try:
-                torch.cuda.synchronize(self.env.device)
-                _lib.load().sacenv_stream_destroy(h)
-            except Exception:  # noqa: BLE001  (interpreter shutdown)
-                pass
-            self._policy_handle = None
+            self.policy_stream.synchronize()
+            _lib.check(_lib.load().sacenv_stream_destroy(h))
+        self._policy_handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
+
+    def __del__(self):  # a fallback for loops never closed: this stream's sync only
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001  (interpreter shutdown)
+            pass
 
     def check(self) -> None:
         """Synchronise and raise if a hand-off timed out (then this loop stays refused)."""
@@ -165,9 +199,19 @@ class ClosedLoop:
         self.env.check_status()
 
     def run(self, eps: torch.Tensor) -> None:
-        """``eps.shape[0]`` (<= segment) steps: policy draws ``eps[k]`` (f32 [N]) for step k.
-        Enqueues everything; the env's refill (autoreset) follows each segment on the
-        env's stream."""
+        """``eps.shape[0]`` (<= segment) steps: policy draws ``eps[k]`` (f32 [N]) for step k,
+        in this loop's form (the hand-off with ``handoff=True``, else ``run_eager``)."""
+        if self.handoff:
+            self.run_handoff(eps)
+        else:
+            self.run_eager(eps)
+
+    def run_handoff(self, eps: torch.Tensor) -> None:
+        """The hand-off form: the policy launches and ONE persistent env launch, handing
+        off through the per-wave flags. Enqueues everything; the env's refill
+        (autoreset) follows each segment on the env's stream."""
+        if not self.handoff:
+            raise RuntimeError("construct the ClosedLoop with handoff=True for the hand-off form")
         if self.failed:
             raise _lib.SacenvError("closed loop refused: an earlier hand-off timed out")
         K = int(eps.shape[0])

@@ -286,28 +286,49 @@ def test_full_size_subsample_vs_oracle(gpu, built_lib):
     assert n_trunc > 0
 
 
+SHIM_FIELDS = ("s_x", "s_y", "s_r", "v_x", "v_y", "v_r", "a_x", "a_y", "a_r", "rudder_angle", "t", "fuel", "index")
+
+
+def _shim_state(env):
+    """The fixture's 13 state fields read through the drop-in's env.boat (boat_env.py:143-306)."""
+    b = env.boat
+    return np.array([getattr(b, f) for f in SHIM_FIELDS], np.float64)
+
+
 def test_dropin_boatenv_shares_global_rng(gpu, built_lib):
-    """BoatEnv shim driven like main.py:70-91 reproduces the seeded reference run,
-    and leaves numpy's global stream exactly where the reference would."""
+    """BoatEnv shim driven like main.py:70-91 reproduces the seeded reference run --
+    all 13 state fields through env.boat.* and the obs, every step, the state after
+    every reset -- and leaves numpy's global stream exactly where the reference would."""
     from sacenv import BoatEnv
     z = golden("seeded_exp6_uniform.npz")
+    assert tuple(str(f) for f in z["state_fields"]) == SHIM_FIELDS
     e = 1
     np.random.seed(int(z["seeds"][e]))
     env = BoatEnv(_cfg_dict(z), None, device=gpu)
     obs = env.reset()
     np.testing.assert_allclose(obs, z["init_obs"][e], atol=OBS_TOL)
+    np.testing.assert_allclose(_shim_state(env), z["init_state"][e], rtol=0, atol=STATE_TOL)
     assert env.action_space.shape == (1,) and env.observation_space.shape == (11,)
     S = z["reward"].shape[1]
+    resets = 0
     for k in range(S):
         o, r, d, info = env.step(np.array([z["actions"][e, k]], np.float32))
         assert d == bool(z["done"][e, k])
-        assert abs(env.boat.s_x - z["state"][e, k, 0]) <= STATE_TOL
+        np.testing.assert_allclose(_shim_state(env), z["state"][e, k], rtol=0, atol=STATE_TOL,
+                                   err_msg=f"step {k}")
+        np.testing.assert_allclose(o, z["obs"][e, k], rtol=0, atol=OBS_TOL, err_msg=f"step {k}")
         assert abs(r - z["reward"][e, k]) <= STATE_TOL
+        assert abs(info["episode_reward"] - z["ep_reward"][e, k]) <= STATE_TOL
         assert info is env.info
         if d:
             assert info["termination"] == "rudder_broken"
-            env.reset()
+            ro = env.reset()
             assert env.info["episode_reward"] == 0
+            np.testing.assert_allclose(ro, z["reset_obs"][e, k], rtol=0, atol=OBS_TOL)
+            np.testing.assert_allclose(_shim_state(env), z["reset_state"][e, k], rtol=0, atol=STATE_TOL)
+            assert env.boat.s_y_start == int(z["start_y"][e, k])
+            resets += 1
+    assert resets > 0
     ora = OracleVecBoat(OracleConfig(experiment=6), z["seeds"][e:e + 1])
     ora.reset()
     for k in range(S):
@@ -318,6 +339,45 @@ def test_dropin_boatenv_shares_global_rng(gpu, built_lib):
                         "boat_velocity_y", "boat_angle", "action_rudder", "reward",
                         "rudder_angle", "n"}
     assert len(env.boat.wind.wind_velocity) == 10000
+
+
+def test_dropin_boatenv_long_reference_run(gpu, built_lib):
+    """The drop-in over 10 000 steps of a recorded reference run (long_exp6.npz env 1:
+    the U-turn program, episodes ended by s_x < 0 and the default-t_max timeout), driven
+    as main.py:70-91 drives the reference: one step() per action, reset() when done
+    (numpy's global stream draws the next Boat). Every step: done, termination and
+    reward; at the kept steps: the 13 state fields through env.boat.* and the obs, and
+    after each reset the fresh Boat."""
+    from sacenv import BoatEnv
+    z = golden("long_exp6.npz")
+    keep = {int(k): j for j, k in enumerate(z["keep"])}
+    e = 1
+    np.random.seed(int(z["seeds"][e]))
+    env = BoatEnv(_cfg_dict(z), None, device=gpu)
+    obs = env.reset()
+    np.testing.assert_allclose(obs, z["init_obs"][e], atol=OBS_TOL)
+    names = {v: k for k, v in {"reached_goal": 1, "out_of_bounds": 2, "out_of_fuel": 3, "rudder_broken": 4,
+                               "timeout": 5}.items()}
+    S = int(z["n_steps"])
+    ends = 0
+    for k in range(S):
+        o, r, d, info = env.step(np.array([z["actions"][e, k]], np.float32))
+        assert d == bool(z["done"][e, k]), f"step {k}"
+        assert abs(r - z["reward"][e, k]) <= STATE_TOL, f"step {k}"
+        j = keep.get(k)
+        if j is not None:
+            np.testing.assert_allclose(_shim_state(env), z["state"][e, j], rtol=0, atol=STATE_TOL,
+                                       err_msg=f"step {k}")
+            np.testing.assert_allclose(o, z["obs"][e, j], rtol=0, atol=OBS_TOL, err_msg=f"step {k}")
+        if d:
+            assert info["termination"] == names[int(z["term"][e, k])], f"step {k}"
+            ro = env.reset()
+            np.testing.assert_allclose(ro, z["reset_obs"][e, j], rtol=0, atol=OBS_TOL)
+            np.testing.assert_allclose(_shim_state(env), z["reset_state"][e, j], rtol=0, atol=STATE_TOL)
+            ends += 1
+    assert ends == int(z["done"][e].sum()) > 0
+    assert [env.info[n] for n in ("reached_goal", "out_of_bounds", "out_of_fuel", "rudder_broken",
+                                  "timeout")] == [int(c) for c in z["counters"][e]]
 
 
 def test_bad_config_raises(gpu, built_lib):

@@ -145,7 +145,7 @@ def test_closed_loop_equals_eager_loop(N, K, segs, gpu, built_lib):
     a_env.reset()
     b_env.reset()
     agent = NativeSAC(gpu, init_seed=3, with_memory=False)
-    loop = ClosedLoop(a_env, agent, segment=K)
+    loop = ClosedLoop(a_env, agent, segment=K, handoff=True)
     g = torch.Generator(device=gpu)
     g.manual_seed(1)
     eps = torch.randn((segs, K, N), generator=g, device=gpu)
@@ -185,13 +185,16 @@ def test_closed_loop_run_eager_equals_run(gpu, built_lib):
     a_env.reset()
     b_env.reset()
     agent = NativeSAC(gpu, init_seed=4, with_memory=False)
-    la, lb = ClosedLoop(a_env, agent, segment=K), ClosedLoop(b_env, agent, segment=K)
+    la, lb = ClosedLoop(a_env, agent, segment=K, handoff=True), ClosedLoop(b_env, agent, segment=K)
+    assert lb.plan is None and not lb.handoff      # no co-residency plan, no exclusive queue
+    with pytest.raises(RuntimeError):
+        lb.run_handoff(torch.zeros((1, b_env.num_envs), device=gpu))
     g = torch.Generator(device=gpu)
     g.manual_seed(2)
     eps = torch.randn((segs, K, N), generator=g, device=gpu)
     for s in range(segs):
         la.run(eps[s])
-        lb.run_eager(eps[s])
+        lb.run(eps[s])          # the default form: eager
         a_env.refill()
         b_env.refill()
         torch.cuda.synchronize()
@@ -224,7 +227,7 @@ def test_closed_loop_after_a_timeout_refuses_and_steps_nothing(gpu, built_lib):
     env = VecBoatEnv({"base_settings": {"experiment": 1}}, 128, device=gpu, autoreset=False)
     env.reset()
     agent = NativeSAC(gpu, init_seed=3, with_memory=False)
-    loop = ClosedLoop(env, agent, segment=8)
+    loop = ClosedLoop(env, agent, segment=8, handoff=True)
     ready = torch.zeros(2, dtype=torch.int32, device=gpu)
     ready[0] = 3                                      # wave 1's rows never come: timeout
     env.segment_async(torch.zeros((8, 128), device=gpu), 8, act_ready=ready)
@@ -267,19 +270,20 @@ def test_closed_loop_at_the_largest_co_resident_size(gpu, built_lib):
     b_env.reset()
     agent = NativeSAC(gpu, init_seed=3, with_memory=False)
     K = 16
-    loop = ClosedLoop(a_env, agent, segment=K)
     g = torch.Generator(device=gpu)
     g.manual_seed(1)
-    for s in range(2):
-        eps = torch.randn((K, N), generator=g, device=gpu)
-        loop.run(eps)
-        for k in range(K):
-            b_env.step_async(agent.choose_action(b_env.obs, eps=eps[k]).reshape(-1).contiguous())
-        a_env.refill()
-        b_env.refill()
-        torch.cuda.synchronize()
-        assert torch.equal(a_env.arena, b_env.arena), s
-    loop.check()
+    with ClosedLoop(a_env, agent, segment=K, handoff=True) as loop:   # releases its queue on exit
+        for s in range(2):
+            eps = torch.randn((K, N), generator=g, device=gpu)
+            loop.run(eps)
+            for k in range(K):
+                b_env.step_async(agent.choose_action(b_env.obs, eps=eps[k]).reshape(-1).contiguous())
+            a_env.refill()
+            b_env.refill()
+            torch.cuda.synchronize()
+            assert torch.equal(a_env.arena, b_env.arena), s
+        loop.check()
+    assert loop._policy_handle is None
 
 
 def test_closed_loop_survives_shared_hardware_queues(gpu, built_lib):
@@ -305,7 +309,7 @@ def test_closed_loop_survives_shared_hardware_queues(gpu, built_lib):
         a_env, b_env = VecBoatEnv(cfg, N, **kw), VecBoatEnv(cfg, N, **kw)
         a_env.reset()
         b_env.reset()
-        loop = ClosedLoop(a_env, agent, segment=K)
+        loop = ClosedLoop(a_env, agent, segment=K, handoff=True)
         eps = torch.randn((K, N), generator=g, device=gpu)
         loop.run(eps)
         for k in range(K):
