@@ -1938,8 +1938,15 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   const int slot0 = cons % kSlots;
   int nslot = slot0 + 1 == kSlots ? 0 : slot0 + 1;
   uint32_t so = lane_ring + (uint32_t)slot0 * slot_bytes, sno = lane_ring + (uint32_t)nslot * slot_bytes;
+  // staged replay rows: the wave's mark word of each step, loaded a step ahead (a
+  // scalar load of a line the mark launch wrote: ~1 us from HBM, as long as a step)
+  unsigned long long mk_cur = ~0ull;
+  if (kRoll && kRows == 2 && ra->marks != nullptr) mk_cur = ra->marks[ob];
   for (int ks = 0; ks < (kRoll ? n_steps : 1) && (!kHand || !failed); ++ks) {
   PHASE(0);
+  unsigned long long mk_nxt = ~0ull;
+  if (kRoll && kRows == 2 && ra->marks != nullptr && ks + 1 < n_steps)
+    mk_nxt = ra->marks[(int64_t)(ks + 1) * A.nwaves() + ob];
   const float act = active ? act_cur : 0.0f;
   // the next step's action, a step ahead: open-loop rows at once; a handed-off
   // row if its flag already said so, else after this step's outputs (below)
@@ -2137,6 +2144,25 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   // its next episode. The restart's ~45 per-lane selects (state, row, slot ring)
   // sit behind ONE wave-uniform branch: in most steps no lane of the wave ends
   // its episode (an episode runs up to 500 steps), and the selects are skipped.
+  // the staged replay row of this step (sacenv_replay_sample_staged reads it), only
+  // where a learn of this or the next segment samples it or its successor: one 64-B
+  // line per row, s' (the pre-reset obs), reward, action, term | lt << 8, obs3_next
+  // (written by a restarting lane below); stored before the restart selects, so the
+  // pre-reset obs need not stay live across them
+  bool staged = false;
+  float4* stage_row = nullptr;
+  if (kRoll && kRows == 2) {
+    const unsigned long long mk = mk_cur;
+    mk_cur = mk_nxt;
+    staged = ((mk >> lane) & 1ull) != 0ull;
+    stage_row = reinterpret_cast<float4*>(ra->stage + ((int64_t)ks * A.np + e) * 64);
+    if (staged) {
+      stage_row[0] = make_float4(o.v[0], o.v[1], o.v[2], o.v[3]);
+      stage_row[1] = make_float4(o.v[4], o.v[5], o.v[6], o.v[7]);
+      stage_row[2] = make_float4(o.v[8], o.v[9], o.v[10], (float)reward);
+      stage_row[3] = make_float4(act, __uint_as_float((uint32_t)term | (lt << 8)), 0.0f, 0.0f);
+    }
+  }
   float row[SACENV_OBS_DIM];
 #pragma unroll
   for (int k = 0; k < SACENV_OBS_DIM; ++k) row[k] = o.v[k];
@@ -2162,6 +2188,8 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
 #pragma unroll
       for (int k = 0; k < SACENV_OBS_DIM; ++k) row[k] = fo.v[k];
       row3_new = fo.v[3];
+      if (kRoll && kRows == 2 && p.experiment == 2 && staged)
+        reinterpret_cast<float*>(stage_row)[14] = row3_new;  // the staged row's obs3_next
       cons_out = cons + 1;
     }
   }
@@ -2271,19 +2299,6 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-  }
-  if (kRoll && kRows == 2) {
-    // the staged replay row of this step (sacenv_replay_sample_staged reads it), only
-    // where a learn of this or the next segment samples it or its successor: one
-    // 64-B line per row, s' (the pre-reset obs), reward, action, term | lt << 8, obs3_next
-    const unsigned long long mk = ra->marks != nullptr ? ra->marks[(int64_t)ks * A.nwaves() + ob] : ~0ull;
-    if (((mk >> lane) & 1ull) != 0ull) {
-      float4* const S = reinterpret_cast<float4*>(ra->stage + ((int64_t)ks * A.np + e) * 64);
-      S[0] = make_float4(o.v[0], o.v[1], o.v[2], o.v[3]);
-      S[1] = make_float4(o.v[4], o.v[5], o.v[6], o.v[7]);
-      S[2] = make_float4(o.v[8], o.v[9], o.v[10], (float)reward);
-      S[3] = make_float4(act, __uint_as_float((uint32_t)term | (lt << 8)), row3_new, 0.0f);
     }
   }
   if (kHand && ra->done != nullptr) {

@@ -357,29 +357,60 @@ __global__ void __launch_bounds__(kDrawThreads) k_rb_draw_many(SacenvReplayParam
 // on (the block it lies in and the position after it).
 constexpr int kTile = 1024, kTileThreads = 256;
 
-__global__ void __launch_bounds__(kWave) k_mt_chain(RB r, uint32_t* __restrict__ out, int n_blocks,
-                                                    int* __restrict__ ctrl) {
-  __shared__ DrawLds l;
-  const int lane = threadIdx.x;
-  for (int i = lane; i < kMtN; i += kWave) l.blk[0][i] = r.key()[i];
-  int cur = 0;
+// The stream's MT blocks for one segment's draws: block 0 is the block holding
+// the next word (the key, or its successor when pos = 624), then one twist per
+// block -- the only sequential part of the draws. Thread l (l < 227) owns the
+// words l, l + 227 and l + 454 of every block: mt19937_gen's word i depends on
+// new word i - 227 from i = 227 on, so the three phases of a twist chain inside
+// the thread (w0 = mix(o[l], o[l+1], o[l+397]), w1 = mix(o[l+227], o[l+228], w0),
+// w2 = mix(o[l+454], o[l+455], w1); word 623 = mix(o[623], new[0], new[396])),
+// and a block costs one LDS round trip (the old block's neighbours) and one
+// barrier instead of three dependent phases.
+constexpr int kChainThreads = 256;
+__global__ void __launch_bounds__(kChainThreads) k_mt_chain(RB r, uint32_t* __restrict__ out, int n_blocks,
+                                                            int* __restrict__ ctrl) {
+  constexpr int kD = kMtN - kMtM;  // 227
+  __shared__ uint32_t buf[2][kMtN];
+  const int l = threadIdx.x;
   const int pos = *r.pos();
-  if (lane == 0) {
+  if (l == 0) {
     ctrl[2] = 0;                          // no shortfall yet
     ctrl[3] = pos >= kMtN ? 0 : pos;      // p0: the next word's position in block 0
   }
-  __syncthreads();
-  if (pos >= kMtN) {  // the stream's next word is in the next block
-    mt_twist_wave(l.blk[0], l.blk[1], lane);
-    cur = 1;
+  for (int i = l; i < kMtN; i += kChainThreads) {
+    const uint32_t v = r.key()[i];
+    buf[0][i] = v;
+    if (pos < kMtN) out[i] = v;
   }
-  for (int b = 0; b < n_blocks; ++b) {
-    uint32_t* const o = out + (int64_t)b * kMtN;
-    for (int i = lane; i < kMtN; i += kWave) o[i] = l.blk[cur][i];
-    if (b + 1 < n_blocks) {
-      mt_twist_wave(l.blk[cur], l.blk[cur ^ 1], lane);
-      cur ^= 1;
+  __syncthreads();
+  int cur = 0;
+  for (int b = pos < kMtN ? 1 : 0; b < n_blocks; ++b) {
+    const uint32_t* o = buf[cur];
+    uint32_t* n = buf[cur ^ 1];
+    uint32_t* g = out + (int64_t)b * kMtN;
+    if (l < kD) {
+      const uint32_t o0 = o[l], o1 = o[l + 1], o397 = o[l + kMtM], o227 = o[l + kD], o228 = o[l + kD + 1];
+      const bool has2 = l < kMtN - 1 - 2 * kD;  // words 454..622
+      const uint32_t o454 = o[has2 ? l + 2 * kD : 0], o455 = o[has2 ? l + 2 * kD + 1 : 0];
+      const uint32_t w0 = mt_mix(o0, o1, o397);
+      const uint32_t w1 = mt_mix(o227, o228, w0);
+      n[l] = w0;
+      g[l] = w0;
+      n[l + kD] = w1;
+      g[l + kD] = w1;
+      if (has2) {
+        const uint32_t w2 = mt_mix(o454, o455, w1);
+        n[l + 2 * kD] = w2;
+        g[l + 2 * kD] = w2;
+      } else if (l == kMtN - 1 - 2 * kD) {  // word 623: new[0] (thread 0's w0) redone here, new[396] = w1
+        const uint32_t n0 = mt_mix(o[0], o[1], o[kMtM]);
+        const uint32_t w2 = mt_mix(o[kMtN - 1], n0, w1);
+        n[kMtN - 1] = w2;
+        g[kMtN - 1] = w2;
+      }
     }
+    __syncthreads();
+    cur ^= 1;
   }
 }
 
@@ -473,8 +504,12 @@ __global__ void __launch_bounds__(kTileThreads) k_draw_emit(DrawPlan d, RB r, in
   __shared__ int64_t s_end;   // stream position after the last wanted word (this tile only)
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
   const int last = d.ctrl[0];
-  if (last < 0) {  // too few words generated (never at the planned margin): report, draw nothing
-    if (blockIdx.x == 0 && tid == 0) d.ctrl[2] = 1;
+  if (last < 0) {  // too few words generated (never at the planned margin): report, draw nothing;
+    // the stream position -1 marks the arena (StagedReplay.check raises)
+    if (blockIdx.x == 0 && tid == 0) {
+      d.ctrl[2] = 1;
+      *r.pos() = -1;
+    }
     return;
   }
   if ((int)blockIdx.x > last) return;
@@ -753,15 +788,16 @@ static StagedGeom geom(const SacenvStagedParams* sp, int64_t g) {
 }
 
 // the steady-state draw's generated blocks: enough for n_batches * batch accepted
-// words with a 20 % margin over the expected count (the standard deviation of the
-// count is ~0.1 % of it), + 2 blocks for the start position
+// words with a 5 % margin over the expected count (at 262 144 draws of [0, 10^6)
+// the count's standard deviation is 0.04 % of it: 120 sigma), + 3 blocks for the
+// start position and small draws
 static int64_t draw_blocks(const SacenvReplayParams* p, int32_t batch, int32_t n_batches) {
   const uint64_t rng = (uint64_t)(p->mem_size - 1);
   uint64_t mask = rng;
   for (int sh = 1; sh < 64; sh <<= 1) mask |= mask >> sh;
   const double acc = (double)(rng + 1) / (double)(mask + 1);
   const double need = (double)batch * n_batches;
-  return (int64_t)(need / acc * 1.2 / kMtN) + 3;
+  return (int64_t)(need / acc * 1.05 / kMtN) + 3;
 }
 
 static int64_t draw_tiles(int64_t blocks) { return (blocks * kMtN + kTile - 1) / kTile; }
@@ -815,7 +851,7 @@ int sacenv_replay_stage_draw(const SacenvReplayParams* p, void* arena, const Sac
   d.need = (int64_t)batch * n_batches;
   d.p0 = -1;       // (read by the kernels from ctrl[3], which k_mt_chain sets)
   d.n_words = -1;
-  hipLaunchKernelGGL(k_mt_chain, dim3(1), dim3(kWave), 0, (hipStream_t)stream, r,
+  hipLaunchKernelGGL(k_mt_chain, dim3(1), dim3(kChainThreads), 0, (hipStream_t)stream, r,
                      reinterpret_cast<uint32_t*>(sc), (int)K, d.ctrl);
   if ((rc = status())) return rc;
   hipLaunchKernelGGL(k_draw_count, dim3((unsigned)T), dim3(kTileThreads), 0, (hipStream_t)stream, d, (int64_t)K);

@@ -371,6 +371,12 @@ class StagedReplay:
         """The all-reduce payload of one segment's batches."""
         return int(self._words[0][0].numel()) * 4
 
+    def check(self) -> None:
+        """Synchronise and raise if a draw ran short of generated MT words (the planned
+        5 % margin is > 100 standard deviations of the count at the bench's shape)."""
+        if int(self._rb.mt_pos.item()) < 0:
+            raise _lib.SacenvError("staged draw: too few MT words generated; the sampling stream is invalid")
+
 
 class ReplayBuffer:
     """Drop-in for agent.buffer.ReplayBuffer (buffer.py:3-35), GPU-backed, numpy I/O,

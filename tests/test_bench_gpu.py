@@ -74,7 +74,7 @@ def test_bench_two_ranks_gloo_on_one_device():
     assert d["n_gpus"] == 2 and d["steps"] == 8 * 256 and d["value"] > 0
     assert d["config"]["global_envs"] == 2 * 8192
     c = d["config"]["collective"]
-    assert "gloo SUM all_reduce" in c and "(8 in the timed region)" in c and "53-B/env transition row" in c
+    assert "gloo SUM all_reduce" in c and "(8 in the timed region)" in c and "StagedReplay" in c
     po = d["pooling"]
     assert po["mode"] == "sharded" and po["exchanges_timed"] == 8
     assert po["all_gather"]["value"] > 0 and po["no_exchange"]["value"] > 0

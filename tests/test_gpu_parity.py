@@ -124,6 +124,31 @@ def test_wind_tables_vs_reference(name, gpu, built_lib):
     np.testing.assert_allclose(a, z["ang"], rtol=0, atol=1e-12)
 
 
+def test_wind_tables_span_their_range_at_scale(gpu, built_lib):
+    """wind.py:86-99's min-max renormalisation makes a renormalised curve's extreme
+    samples exactly 0 and 1 (x max_velocity for the speed, x 2 pi for the angle). The
+    fit finds the grid extrema from the cubic's critical points and folds them into
+    the knots; over 2 048 exp-6 episodes (full 10 000-sample tables through
+    sacenv_boat_wind_eval) every table stays inside its range, and every curve's
+    extreme sample lands on the range's ends within a few ulp."""
+    from sacenv import VecBoatEnv
+    n, L = 2048, 10000
+    env = VecBoatEnv({"base_settings": {"experiment": 6}}, n, seed=41, device=gpu, autoreset=False)
+    ids = torch.arange(n, dtype=torch.int32, device=gpu).repeat_interleave(L)
+    ix = torch.arange(L, dtype=torch.int32, device=gpu).repeat(n)
+    v, a = env.wind_eval(ids, ix)
+    v, a = v.view(n, L), a.view(n, L)
+    for t, top in ((v, float(env.cfg.max_velocity)), (a, 2 * np.pi)):
+        lo, hi = t.min(1).values.cpu().numpy(), t.max(1).values.cpu().numpy()
+        eps = 8 * np.finfo(np.float64).eps * top
+        assert (lo >= -eps).all() and (hi <= top + eps).all(), (lo.min(), hi.max())
+        # a renormalised curve (its raw spline left [0, 1]) touches BOTH ends; a curve
+        # that was not renormalised touches neither (its raw samples lie strictly inside)
+        at_lo, at_hi = lo <= eps, hi >= top - eps
+        assert np.array_equal(at_lo, at_hi), (np.flatnonzero(at_lo != at_hi)[:5], lo, hi)
+        assert at_lo.sum() > n // 4
+
+
 @pytest.mark.parametrize("autoreset", [False, True])
 def test_rng_draws_bit_exact_across_many_resets(autoreset, gpu, built_lib):
     """Knots/start-y of 150 consecutive Boats per env == numpy RandomState (crosses

@@ -94,9 +94,13 @@ def _run(rank, world, exp, N, M, B, n_segs, dev, group=None):
         assert torch.equal(ref.last_term.to(torch.uint8), ref_rb._last_term[ref]), s
     torch.cuda.synchronize()
     env.check_status()
+    rep.check()
     if rank == 0 and world == 1:
-        # only the rows a learn reads were written: a small share of the segment's rows
-        assert 0 < written < 0.5 * n_segs * SEG * N, written
+        # only the rows a learn reads (and their predecessors) were written: at most
+        # 2 x 2 marks per sampled row of two segments' learns
+        assert 0 < written <= min(n_segs * SEG * N, 4 * n_segs * SEG * B), written
+        if 4 * B < N // 2:
+            assert written < 0.5 * n_segs * SEG * N, written
     return (checked, skipped) if rank == 0 else None
 
 

@@ -4,7 +4,8 @@
 #   parity tests (log kept), smoke(), the driver's bench command, the default
 #   bench line (persistent segments) with cpu_baseline, the per-step-launch line,
 #   the config lines (C2, C5 mixed, 131 072 envs, the K=128 rollout), the N=2
-#   rehearsal over gloo on the one GPU (segment pooling and per-step pooling),
+#   rehearsals over gloo on the one GPU (the sharded exchange and the all-gather),
+#   the training loop (--train),
 #   then tools/pmc.sh (kernel trace + calibrated PMC
 #   passes of the persistent segment kernel).
 set -o pipefail
@@ -36,14 +37,26 @@ for f in ("driver", "default", "step", "c2", "c5", "rollout_k128", "131k", "clos
     print(f"{f:13s} {d['value']/1e9:7.3f} G/s {d['ms_per_step']*1e3:6.2f} us/step kernel {k:5.2f} us "
           f"frac {r.get('frac', 0):.3f} cpu {c and round(c['value'])}")
 PY
-for pe in 256 1; do
-  port=$((29500 + pe))
-  SACENV_BENCH_BACKEND=gloo SACENV_BENCH_ONE_DEVICE=1 timeout -k 10 300 python -m torch.distributed.run \
-    --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port $port bench.py --gpus 2 \
-    --envs 65536 --pool-every $pe --steps 256 --warmup 128 > gpurun_out/rehearse_pe$pe.json \
-    2> gpurun_out/rehearse_pe$pe.log || { tail -20 gpurun_out/rehearse_pe$pe.log; exit 1; }
-  tail -1 gpurun_out/rehearse_pe$pe.json | python -c "import json,sys;d=json.loads(sys.stdin.read());print('rehearse pool_every', d['pooling']['pool_every'], round(d['value']/1e9,3), 'G/s', d['dist']['backend'], d['pooling']['received_GBps_per_rank'])"
-done
+# N=2 rehearsals over gloo on the one GPU: the default sharded exchange (bench starting its
+# own ranks, no launcher), and the all-gather under torch.distributed.run
+SACENV_BENCH_BACKEND=gloo SACENV_BENCH_ONE_DEVICE=1 timeout -k 10 400 python bench.py --gpus 2 --envs 65536 \
+  --steps 256 --warmup 128 > gpurun_out/rehearse_sharded.json 2> gpurun_out/rehearse_sharded.log \
+  || { tail -20 gpurun_out/rehearse_sharded.log; exit 1; }
+SACENV_BENCH_BACKEND=gloo SACENV_BENCH_ONE_DEVICE=1 timeout -k 10 400 python -m torch.distributed.run \
+  --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 \
+  --envs 65536 --pooling gather --steps 256 --warmup 128 > gpurun_out/rehearse_gather.json \
+  2> gpurun_out/rehearse_gather.log || { tail -20 gpurun_out/rehearse_gather.log; exit 1; }
+python - <<'PY'
+import json
+for f in ("sharded", "gather"):
+    d = json.loads(open(f"gpurun_out/rehearse_{f}.json").read().strip().splitlines()[-1])
+    p = d["pooling"]
+    print(f"rehearse {f}: {d['value']/1e9:.3f} G/s {d['dist']['backend']} no_exchange "
+          f"{p['no_exchange']['value']/1e9:.3f}" + (f" all_gather {p['all_gather']['value']/1e9:.3f}"
+                                                  if p.get('all_gather') else ""))
+PY
+$B --train > gpurun_out/bench_train.json 2> gpurun_out/bench_train.log || exit 1
+python -c "import json;d=json.load(open('gpurun_out/bench_train.json'));print('train', round(d['value']/1e6,1), 'M/s', d['parts'])"
 bash tools/ktrace.sh > gpurun_out/kt_final.txt 2>&1 || { tail -20 gpurun_out/kt_final.txt; exit 1; }
 cat gpurun_out/kt_final.txt
 if [ -n "$RUN_PMC" ]; then
