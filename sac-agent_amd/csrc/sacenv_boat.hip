@@ -1692,6 +1692,7 @@ struct MixedToys {
 constexpr int kCoef = 8;  // wind_coef fields: 2 curves x (y0, y1, m0, m1)
 struct OwnerLds {
   float obs[kWave * SACENV_OBS_DIM];  // the wave's obs rows, stored as float4
+  unsigned long long mk[SACENV_REFILL_PERIOD];  // staged replay rows: the wave's mark word per step
 };
 
 // t += dt (boat_env.py:69) accumulates exactly when dt = m * 2^e with m < 2^22:
@@ -1938,15 +1939,22 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   const int slot0 = cons % kSlots;
   int nslot = slot0 + 1 == kSlots ? 0 : slot0 + 1;
   uint32_t so = lane_ring + (uint32_t)slot0 * slot_bytes, sno = lane_ring + (uint32_t)nslot * slot_bytes;
-  // staged replay rows: the wave's mark word of each step, loaded a step ahead (a
-  // scalar load of a line the mark launch wrote: ~1 us from HBM, as long as a step)
-  unsigned long long mk_cur = ~0ull;
-  if (kRoll && kRows == 2 && ra->marks != nullptr) mk_cur = ra->marks[ob];
+  // staged replay rows: the wave's mark words of every step of the launch, staged in
+  // LDS once (a per-step global load would sit in the loop's vmcnt accounting, and the
+  // step's first full wait would expose its ~1-us latency every step)
+  if (kRoll && kRows == 2 && ra->marks != nullptr) {
+    for (int q = lane; q < n_steps; q += kWave) l.mk[q] = ra->marks[(int64_t)q * A.nwaves() + ob];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  // every load of the launch's prologue has landed before the step loop: the waitcnt
+  // pass then sees no load pending at the loop's entry, and the loop keeps no wait
+  // for them -- such a wait, on later steps, also waits for the previous step's
+  // stores (vmcnt counts both on gfx950)
+  if (kRoll) __builtin_amdgcn_s_waitcnt(0);
   for (int ks = 0; ks < (kRoll ? n_steps : 1) && (!kHand || !failed); ++ks) {
   PHASE(0);
-  unsigned long long mk_nxt = ~0ull;
-  if (kRoll && kRows == 2 && ra->marks != nullptr && ks + 1 < n_steps)
-    mk_nxt = ra->marks[(int64_t)(ks + 1) * A.nwaves() + ob];
   const float act = active ? act_cur : 0.0f;
   // the next step's action, a step ahead: open-loop rows at once; a handed-off
   // row if its flag already said so, else after this step's outputs (below)
@@ -2152,8 +2160,7 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   bool staged = false;
   float4* stage_row = nullptr;
   if (kRoll && kRows == 2) {
-    const unsigned long long mk = mk_cur;
-    mk_cur = mk_nxt;
+    const unsigned long long mk = ra->marks != nullptr ? l.mk[ks] : ~0ull;
     staged = ((mk >> lane) & 1ull) != 0ull;
     stage_row = reinterpret_cast<float4*>(ra->stage + ((int64_t)ks * A.np + e) * 64);
     if (staged) {

@@ -249,14 +249,26 @@ __global__ void __launch_bounds__(256) k_rb_gather(SacenvReplayParams p, RB r, i
 struct StagedGeom {
   int64_t period, offset, g;
   int n, n_pad, seg, exp2;
+  double r_mem, r_period;  // 1 / mem_size, 1 / period (host IEEE divisions)
 };
 
+// floor(x / d) for 0 <= x < 2^52 and 0 < d < 2^31 from the rounded reciprocal rd:
+// the double estimate is off by at most one, fixed by one step each way (a 64-bit
+// integer division is a ~50-instruction sequence on the GPU)
+__device__ __forceinline__ int64_t div_floor(int64_t x, int64_t d, double rd) {
+  int64_t q = (int64_t)((double)x * rd);
+  q -= q * d > x ? 1 : 0;
+  q += (q + 1) * d <= x ? 1 : 0;
+  return q;
+}
+
 // ring row `row` at learn time (cntr rows stored) -> (global step q, global env u)
-__device__ __forceinline__ void resolve(int64_t row, int64_t cntr, int64_t M, int64_t period, int64_t* q,
+__device__ __forceinline__ void resolve(int64_t row, int64_t cntr, int64_t M, const StagedGeom& G, int64_t* q,
                                         int64_t* u) {
-  const int64_t s = row + M * ((cntr - 1 - row) / M);  // the latest sequence number = row (mod M)
-  *q = s / period;
-  *u = s - *q * period;
+  // the latest sequence number = row (mod M) below cntr
+  const int64_t s = row + M * div_floor(cntr - 1 - row, M, G.r_mem);
+  *q = div_floor(s, G.period, G.r_period);
+  *u = s - *q * G.period;
 }
 
 // n_batches consecutive np.random.choice(min(cntr_k, M), batch) calls on one
@@ -567,7 +579,7 @@ __global__ void __launch_bounds__(256) k_rb_stage_mark(SacenvReplayParams p, Sta
   const int k = (int)(tt / batch);
   const int64_t cntr = ((G.g + (nxt ? 1 : 0)) * G.seg + k + 1) * G.period;
   int64_t q, u;
-  resolve(row, cntr, p.mem_size, G.period, &q, &u);
+  resolve(row, cntr, p.mem_size, G, &q, &u);
   if (u < G.offset || u >= G.offset + G.n) return;
   const int e = (int)(u - G.offset);
   const int nw = G.n_pad / kWave;
@@ -602,7 +614,7 @@ __global__ void __launch_bounds__(256) k_rb_gather_staged(SacenvReplayParams p, 
   const int b = (int)(t / batch), i = (int)(t - (int64_t)b * batch);
   const int64_t row = idx[t];  // -1: no learn at this step (fewer rows than a batch)
   int64_t q = 0, u = -1;
-  if (row >= 0) resolve(row, (G.g * G.seg + b + 1) * G.period, p.mem_size, G.period, &q, &u);
+  if (row >= 0) resolve(row, (G.g * G.seg + b + 1) * G.period, p.mem_size, G, &q, &u);
   const bool own = u >= G.offset && u < G.offset + G.n;
   uint32_t* const W = words + (int64_t)b * per;
   float sn[16], sv[16];
@@ -775,8 +787,16 @@ static int check_staged(const SacenvReplayParams* p, const SacenvStagedParams* s
   return SACENV_OK;
 }
 
-static StagedGeom geom(const SacenvStagedParams* sp, int64_t g) {
+// the sequence numbers of segments g and g + 1 stay below 2^52 (div_floor's range)
+static bool staged_range_ok(const SacenvStagedParams* sp, int64_t g) {
+  if (sp->period >= ((int64_t)1 << 31)) return false;
+  return g < (((int64_t)1 << 52) / ((int64_t)sp->seg * sp->period)) - 2;
+}
+
+static StagedGeom geom(const SacenvReplayParams* p, const SacenvStagedParams* sp, int64_t g) {
   StagedGeom G;
+  G.r_mem = 1.0 / (double)p->mem_size;
+  G.r_period = 1.0 / (double)sp->period;
   G.period = sp->period;
   G.offset = sp->offset;
   G.g = g;
@@ -825,7 +845,7 @@ int sacenv_replay_stage_draw(const SacenvReplayParams* p, void* arena, const Sac
   if (g < 0 || batch < 0 || n_batches < 0 || n_batches > sp->seg) return SACENV_E_SIZE;
   if (!arena || !idx) return SACENV_E_NULL;
   if (batch == 0 || n_batches == 0) return SACENV_OK;
-  if ((g * sp->seg + sp->seg + 1) * sp->period > (int64_t)1 << 62) return SACENV_E_RANGE;
+  if (!staged_range_ok(sp, g)) return SACENV_E_RANGE;
   const RB r = make_rb(*p, arena);
   const int64_t cntr0 = g * sp->seg * sp->period;
   const int64_t M = p->mem_size;
@@ -870,6 +890,7 @@ int sacenv_replay_stage_mark(const SacenvReplayParams* p, const SacenvStagedPara
   if (rc) return rc;
   if (g < 0 || batch < 0 || n_batches < 0 || n_batches > sp->seg) return SACENV_E_SIZE;
   if (!idx_g || !marks) return SACENV_E_NULL;
+  if (!staged_range_ok(sp, g)) return SACENV_E_RANGE;
   const hipError_t e = hipMemsetAsync(marks, 0, (size_t)sp->seg * (sp->n_pad / kWave) * 8, (hipStream_t)stream);
   if (e != hipSuccess) return (int)e;
   const int64_t per = (int64_t)batch * n_batches;
@@ -877,7 +898,7 @@ int sacenv_replay_stage_mark(const SacenvReplayParams* p, const SacenvStagedPara
   // without the next segment's draws, only this segment's learns mark
   const int64_t total = idx_next != nullptr ? 2 * per : per;
   hipLaunchKernelGGL(k_rb_stage_mark, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                     *p, geom(sp, g), idx_g, idx_next != nullptr ? idx_next : idx_g, batch, n_batches,
+                     *p, geom(p, sp, g), idx_g, idx_next != nullptr ? idx_next : idx_g, batch, n_batches,
                      reinterpret_cast<unsigned long long*>(marks), total);
   return status();
 }
@@ -889,6 +910,7 @@ int sacenv_replay_sample_staged(const SacenvReplayParams* p, const SacenvStagedP
   if (rc) return rc;
   if (g < 0 || batch < 0 || n_batches < 0 || n_batches > sp->seg) return SACENV_E_SIZE;
   if (!stage_cur || !stage_prev || !idx || !words) return SACENV_E_NULL;
+  if (!staged_range_ok(sp, g)) return SACENV_E_RANGE;
   if (((reinterpret_cast<uintptr_t>(stage_cur) | reinterpret_cast<uintptr_t>(stage_prev)) & 15u) != 0u)
     return SACENV_E_RANGE;
   if (batch == 0 || n_batches == 0) return SACENV_OK;
@@ -899,7 +921,7 @@ int sacenv_replay_sample_staged(const SacenvReplayParams* p, const SacenvStagedP
   const int64_t total = (int64_t)batch * n_batches;
   const int64_t per = (int64_t)batch * (2 * SACENV_OBS_DIM + 1 + 3);
   hipLaunchKernelGGL(k_rb_gather_staged, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                     *p, geom(sp, g), S, batch, n_batches, idx, words, per);
+                     *p, geom(p, sp, g), S, batch, n_batches, idx, words, per);
   return status();
 }
 
