@@ -364,7 +364,6 @@ FP64_VECTOR_PEAK = 78.6e12   # MI355X datasheet FP64 vector: 256 CUs x 4 SIMDs x
 # measured ceilings (tools/ubench/f64_latency.hip, profiles/r04_ubench_*.txt): v_fma_f64 issue at one
 # wave per SIMD 5.1 shader cycles per wave instruction (dependent 5.8), at two waves 3.5 per SIMD;
 # 64-bit moves, conversions, rndne/ldexp/fract and AGPR reads ~8, v_readfirstlane ~24 (valu_mix.hip)
-UBENCH_F64_FMA_CYC_1WAVE = 5.1
 
 
 def load_compute(n_envs: int, experiment: int, kernel_s: float):
@@ -385,18 +384,31 @@ def load_compute(n_envs: int, experiment: int, kernel_s: float):
         salu = pw["INSTS_SALU"] / K
         flops = (2 * pw["INSTS_VALU_FMA_F64"] + pw["INSTS_VALU_MUL_F64"] + pw["INSTS_VALU_ADD_F64"]) / K
         achieved = flops * n_envs / kernel_s
-        return {"unit": "TFLOP/s (FP64 vector)", "achieved": achieved / 1e12, "peak": FP64_VECTOR_PEAK / 1e12,
-                "frac": achieved / FP64_VECTOR_PEAK,
-                "fp64_flops_per_env_step": flops, "valu_per_wave_step": valu, "salu_per_wave_step": salu,
-                "f64_valu_per_wave_step": (pw["INSTS_VALU_FMA_F64"] + pw["INSTS_VALU_MUL_F64"]
-                                           + pw["INSTS_VALU_ADD_F64"]) / K,
-                "issue_floor_us_per_step": (valu + salu) * UBENCH_F64_FMA_CYC_1WAVE / 2.26e9 * 1e6,
-                "issue_floor_frac": (valu + salu) * UBENCH_F64_FMA_CYC_1WAVE / 2.26e9 / kernel_s,
-                "source": os.path.relpath(path, ROOT),
-                "note": "one owner wave per SIMD issues in order: ~5 shader cycles per f64 instruction at best "
-                        "(8 for 64-bit moves/conversions, ~7 for SALU between VALU), so the step is bound by "
-                        "instruction issue, not by HBM bytes (counter traffic is ~0.1 of the byte figure) nor "
-                        "by FP64 throughput; issue_floor = (VALU + SALU) x 5.1 cycles at 2.26 GHz"}
+        out = {"unit": "TFLOP/s (FP64 vector)", "achieved": achieved / 1e12, "peak": FP64_VECTOR_PEAK / 1e12,
+               "frac": achieved / FP64_VECTOR_PEAK,
+               "fp64_flops_per_env_step": flops, "valu_per_wave_step": valu, "salu_per_wave_step": salu,
+               "f64_valu_per_wave_step": (pw["INSTS_VALU_FMA_F64"] + pw["INSTS_VALU_MUL_F64"]
+                                          + pw["INSTS_VALU_ADD_F64"]) / K,
+               "source": os.path.relpath(path, ROOT)}
+        life, issue = pw.get("WAVE_CYCLES"), pw.get("ACTIVE_INST_ANY")
+        if life and issue and d.get("trace_avg_ns_per_step"):
+            # SQ cycle counters tick once per 4 shader cycles; the clock they imply over
+            # the profiled launches' per-step time (a lower bound: a wave lives a little
+            # less than its launch)
+            clk = 4.0 * life / K / (d["trace_avg_ns_per_step"] * 1e-9)
+            floor = 4.0 * issue / K / clk
+            out.update({
+                "issue_frac_of_wave_life": issue / life, "wait_frac_of_wave_life": pw.get("WAIT_ANY", 0.0) / life,
+                "ifetch_frac_of_wave_life": pw.get("WAIT_INST_ANY", 0.0) / life,
+                "clock_ghz_implied": clk / 1e9,
+                "issue_floor_us_per_step": floor * 1e6, "issue_floor_frac": floor / kernel_s,
+                "note": "one owner wave per SIMD issues in order, one instruction per 4-cycle issue slot at "
+                        "best (f64 VALU ~5 cycles), so the step is bound by its instruction stream, not by HBM "
+                        "bytes (counter traffic is ~0.1 of the byte figure) nor by FP64 throughput; "
+                        "issue_floor = the measured issue cycles (SQ_ACTIVE_INST_ANY x 4) per step at the "
+                        "implied clock; the rest of a wave's life is dependency waits (wait_frac) and "
+                        "instruction fetch"})
+        return out
     return None
 
 

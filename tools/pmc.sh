@@ -1,7 +1,9 @@
 #!/bin/bash
 # rocprofv3 evidence for the bench kernel (run on the GPU box from the repo root):
-#   PMC_KERNEL=segment (default: the persistent k_rollout of --launch segment) or
-#   step (k_step of --launch step);
+#   PMC_KERNEL=segment (default: the persistent k_rollout of --launch segment),
+#   rollout (the same kernel as --rollout 256 runs it: every step's record and
+#   terminal obs to rows of their own, the headline's every_output) or step
+#   (k_step of --launch step);
 #   1. kernel trace + stats of the bench command;
 #   2. PMC passes, one per run, --pmc never combined with a trace domain (pool
 #      rule), each within the per-block limits (<= 4 TCC, <= 8 SQ counters):
@@ -18,7 +20,9 @@ mkdir -p "$OUT"
 [ -x tools/probes/fetch_calib ] || /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 \
   -o tools/probes/fetch_calib tools/probes/fetch_calib.hip || exit 1
 MODE=${PMC_KERNEL:-segment}
-if [ "$MODE" = step ]; then LAUNCH="--launch step"; PMCL="--launch step --no-graph"; else LAUNCH=""; PMCL=""; fi
+if [ "$MODE" = step ]; then LAUNCH="--launch step"; PMCL="--launch step --no-graph"
+elif [ "$MODE" = rollout ]; then LAUNCH="--rollout 256"; PMCL="--rollout 256"
+else LAUNCH=""; PMCL=""; fi
 BENCH="python3 bench.py --steps ${PMC_STEPS:-256} --warmup 128 --no-cpu-baseline --no-every-output $PMCL"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_trace" -o run --output-format csv \
   -- python3 bench.py --no-cpu-baseline --no-every-output $LAUNCH > "$OUT/prof_trace_bench.json" 2> "$OUT/prof_trace.log" || exit 1
