@@ -1275,7 +1275,7 @@ def bench_train(args, rank, world, dev):
         a = agent.choose_action(env.obs, eps=eps[k % SEG])
         env.step_async(a.view(-1))
         agent.memory.store_env_step(prev, a, env)
-        if agent.learn(noise=(noise[k % SEG, 0], noise[k % SEG, 1])) is not None:
+        if agent.learn(noise=(noise[k % SEG, 0], noise[k % SEG, 1]), losses=False) is not None:
             counts["learns"] += 1
 
     k = 0
@@ -1315,7 +1315,7 @@ def bench_train(args, rank, world, dev):
              "env_step_us": timed(lambda: env.step_async(a0)),
              "store_us": timed(lambda: agent.memory.store_env_step(prev, a0, env)),
              "sample_us": timed(lambda: agent.memory.sample(B)),
-             "learn_us": timed(lambda: agent.learn(noise=(noise[0, 0], noise[0, 1])))}
+             "learn_us": timed(lambda: agent.learn(noise=(noise[0, 0], noise[0, 1]), losses=False))}
     if rank != 0:
         return None
     return {

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SACENV_ABI_VERSION 16
+#define SACENV_ABI_VERSION 17
 #define SACENV_OBS_DIM 11      /* Boat.return_state, boat_env.py:308-323 */
 #define SACENV_MT_N 624        /* MT19937 words per env (numpy legacy RNG) */
 #define SACENV_MAX_KNOTS 16    /* wind.fixed_points upper bound */
@@ -465,6 +465,15 @@ int sacenv_replay_store_env(const SacenvReplayParams *p, void *arena, int64_t n,
                             const float *action, const void *reward, const float *new_state,
                             const float *final_state, const uint8_t *code, uint8_t *last_term,
                             void *stream);
+/* sacenv_replay_store_env with the buffer's mem_cntr before this call given by
+ * the caller (`cntr`, which a host that issues every store knows): ONE launch,
+ * which also sets the device count to cntr + n (sacenv_replay_store_env reads
+ * the device count and advances it in a second launch, so it can be captured in
+ * a graph; this form cannot: cntr is a launch argument). */
+int sacenv_replay_store_env_at(const SacenvReplayParams *p, void *arena, int64_t cntr, int64_t n,
+                               const float *state, const float *action, const void *reward,
+                               const float *new_state, const float *final_state, const uint8_t *code,
+                               uint8_t *last_term, void *stream);
 /* sample_buffer(batch) (buffer.py:24-35): indices (i64) and the gathered rows.
  * Any output but idx may be NULL. An empty buffer is an error (SACENV_E_SIZE:
  * np.random.choice(0, n) raises) detected on the host from `stored`. */

@@ -86,8 +86,12 @@ __global__ void __launch_bounds__(kWave) k_rb_init(RB r, uint32_t seed) {
 // (n - first) x (D + A + 1) stored columns with 32-bit index math. mem_cntr
 // advances in a second launch (k_rb_advance), after every workgroup has read
 // it: stream order instead of a grid-wide atomic (one word takes ~90
-// returning atomics/µs) or an agent-scope acq_rel fence per workgroup.
-__global__ void __launch_bounds__(256) k_rb_store(SacenvReplayParams p, RB r, int64_t n, int64_t offset,
+// returning atomics/µs) or an agent-scope acq_rel fence per workgroup. With the
+// count from the host (host_cntr >= 0) no workgroup reads it, so the first one
+// writes the advanced count and the second launch goes (one fixed launch cost,
+// ~5 us, per stored step).
+__global__ void __launch_bounds__(256) k_rb_store(SacenvReplayParams p, RB r, int64_t host_cntr, int64_t advance,
+                                                  int64_t n, int64_t offset,
                                                   const float* __restrict__ state,
                                                   const float* __restrict__ action,
                                                   const void* __restrict__ reward,
@@ -95,7 +99,8 @@ __global__ void __launch_bounds__(256) k_rb_store(SacenvReplayParams p, RB r, in
                                                   const float* __restrict__ final_state,
                                                   const uint8_t* __restrict__ code,
                                                   uint8_t* __restrict__ last_term) {
-  const int64_t M = p.mem_size, c0 = *r.cntr() + offset;
+  const int64_t M = p.mem_size, c0 = (host_cntr >= 0 ? host_cntr : *r.cntr()) + offset;
+  if (host_cntr >= 0 && blockIdx.x == 0 && threadIdx.x == 0) *r.cntr() = host_cntr + advance;  // buffer.py:22
   const int64_t first = n > M ? n - M : 0;
   const uint32_t rows = (uint32_t)(n - first);
   const uint32_t base = (uint32_t)((c0 + first) % M);  // ring row of stored row 0
@@ -699,10 +704,12 @@ int sacenv_replay_init(const SacenvReplayParams* p, void* arena, uint32_t seed, 
 
 static int store(const SacenvReplayParams* p, void* arena, int64_t n, int64_t offset, int64_t advance,
                  const float* state, const float* action, const void* reward, const float* new_state,
-                 const float* final_state, const uint8_t* code, uint8_t* last_term, void* stream) {
+                 const float* final_state, const uint8_t* code, uint8_t* last_term, void* stream,
+                 int64_t host_cntr = -1) {
   int rc = check_replay(p);
   if (rc) return rc;
   if (n < 0) return SACENV_E_SIZE;
+  if (host_cntr >= 0 && n == 0) host_cntr = -1;  // nothing to launch: advance as before
   if (n == 0 && advance == n) return SACENV_OK;
   if (!arena || !state || !action || !reward || !new_state || !code) return SACENV_E_NULL;
   const int64_t rows = n > p->mem_size ? p->mem_size : n;
@@ -712,12 +719,20 @@ static int store(const SacenvReplayParams* p, void* arena, int64_t n, int64_t of
   if (blocks > 8192) blocks = 8192;
   const RB r = make_rb(*p, arena);
   if (n > 0) {
-    hipLaunchKernelGGL(k_rb_store, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *p, r, n, offset,
-                       state, action, reward, new_state, final_state, code, last_term);
+    hipLaunchKernelGGL(k_rb_store, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *p, r, host_cntr,
+                       advance, n, offset, state, action, reward, new_state, final_state, code, last_term);
     if ((rc = status())) return rc;
+    if (host_cntr >= 0) return SACENV_OK;
   }
   hipLaunchKernelGGL(k_rb_advance, dim3(1), dim3(kWave), 0, (hipStream_t)stream, r, advance);
   return status();
+}
+
+int sacenv_replay_store_env_at(const SacenvReplayParams* p, void* arena, int64_t cntr, int64_t n, const float* state,
+                               const float* action, const void* reward, const float* new_state,
+                               const float* final_state, const uint8_t* code, uint8_t* last_term, void* stream) {
+  if (cntr < 0) return SACENV_E_RANGE;
+  return store(p, arena, n, 0, n, state, action, reward, new_state, final_state, code, last_term, stream, cntr);
 }
 
 int sacenv_replay_store_env(const SacenvReplayParams* p, void* arena, int64_t n, const float* state,

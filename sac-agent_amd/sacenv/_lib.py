@@ -14,7 +14,7 @@ PKG_ROOT = _build.PKG_ROOT
 LIB_PATH = os.environ.get("SACENV_LIB", _build.LIB)
 LOADED_DIGEST = None  # source digest of the loaded library (the in-tree build)
 
-ABI_VERSION = 16
+ABI_VERSION = 17
 OBS_DIM = 11
 MT_N = 624
 MAX_KNOTS = 16
@@ -143,7 +143,7 @@ EXPORTS = ("sacenv_abi_version", "sacenv_error_string", "sacenv_boat_layout",
            "sacenv_boat_refill", "sacenv_boat_wind_eval", "sacenv_toy_layout", "sacenv_toy_init",
            "sacenv_toy_reset", "sacenv_toy_step", "sacenv_mixed_step", "sacenv_mixed_step_pooled",
            "sacenv_mixed_segment", "sacenv_replay_layout",
-           "sacenv_replay_init", "sacenv_replay_store", "sacenv_replay_store_env", "sacenv_replay_sample", "sacenv_replay_store_shard",
+           "sacenv_replay_init", "sacenv_replay_store", "sacenv_replay_store_env", "sacenv_replay_store_env_at", "sacenv_replay_sample", "sacenv_replay_store_shard",
            "sacenv_replay_sample_shard", "sacenv_replay_stage_scratch_bytes", "sacenv_replay_stage_draw",
            "sacenv_replay_stage_mark", "sacenv_replay_sample_staged",
            "sacenv_compact_done", "sacenv_boat_reset_list", "sacenv_sac_layout", "sacenv_sac_sync",
@@ -215,6 +215,7 @@ def load(path: str | None = None):
         "sacenv_replay_init": (C.c_int, [RP, _p, C.c_uint32, _p]),
         "sacenv_replay_store": (C.c_int, [RP, _p, _i64, _p, _p, _p, _p, _p, _p, _p]),
         "sacenv_replay_store_env": (C.c_int, [RP, _p, _i64, _p, _p, _p, _p, _p, _p, _p, _p]),
+        "sacenv_replay_store_env_at": (C.c_int, [RP, _p, _i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p]),
         "sacenv_replay_sample": (C.c_int, [RP, _p, _i32, _i64, _p, _p, _p, _p, _p, _p, _p]),
         "sacenv_replay_store_shard": (C.c_int, [RP, _p, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p]),
         "sacenv_replay_sample_shard": (C.c_int, [RP, _p, _i32, _i64, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p,

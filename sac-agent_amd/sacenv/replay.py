@@ -101,10 +101,11 @@ class DeviceReplayBuffer:
             if (lt.dtype != torch.uint8 or lt.device != self.device or lt.numel() != n
                     or not lt.is_contiguous()):
                 raise ValueError("last_term must be a contiguous u8 device tensor with one byte per row")
-        _lib.check(self.lib.sacenv_replay_store_env(
-            self._pp, self.arena.data_ptr(), n, s.data_ptr(), a.data_ptr(), r.data_ptr(), ns.data_ptr(),
-            None if fs is None else fs.data_ptr(), c.data_ptr(), None if lt is None else lt.data_ptr(),
-            self.stream))
+        # the host issues every store, so it knows the count: one launch (sacenv.h)
+        _lib.check(self.lib.sacenv_replay_store_env_at(
+            self._pp, self.arena.data_ptr(), self.mem_cntr, n, s.data_ptr(), a.data_ptr(), r.data_ptr(),
+            ns.data_ptr(), None if fs is None else fs.data_ptr(), c.data_ptr(),
+            None if lt is None else lt.data_ptr(), self.stream))
         self._keep = (s, a, r, ns, c, fs)
         self.mem_cntr += n
 
@@ -128,8 +129,10 @@ class DeviceReplayBuffer:
         self.store_batch(prev_obs, actions, env.reward, env.obs, env.term, final_state=env.final_obs,
                          last_term=last)
 
-    def sample(self, batch_size: int):
-        """sample_buffer (buffer.py:24-35) on device: (states, actions, rewards, states_, dones, idx)."""
+    def sample(self, batch_size: int, as_bool: bool = True):
+        """sample_buffer (buffer.py:24-35) on device: (states, actions, rewards, states_, dones, idx).
+        ``as_bool=False``: dones as the kernel writes them (u8 0/1), with no conversion launch
+        (the agent's learn() reads u8)."""
         B = int(batch_size)
         if self.mem_cntr == 0 and B > 0:
             raise ValueError("a must be greater than 0 unless no samples are taken")
@@ -142,7 +145,7 @@ class DeviceReplayBuffer:
         _lib.check(self.lib.sacenv_replay_sample(
             self._pp, self.arena.data_ptr(), B, self.mem_cntr, idx.data_ptr(), st.data_ptr(),
             ac.data_ptr(), rw.data_ptr(), ns.data_ptr(), tm.data_ptr(), self.stream))
-        return st, ac, rw, ns, tm.bool(), idx
+        return st, ac, rw, ns, (tm.bool() if as_bool else tm), idx
 
 
 class ShardedReplayBuffer(DeviceReplayBuffer):
@@ -185,9 +188,11 @@ class ShardedReplayBuffer(DeviceReplayBuffer):
         self._keep = (s, a, r, ns, c, fs)
         self.mem_cntr += self.period
 
-    def sample(self, batch_size: int):
-        """The pooled buffer's sample_buffer (buffer.py:24-35), identical on every rank."""
-        return self.sample_many(batch_size, 1)[0]
+    def sample(self, batch_size: int, as_bool: bool = True):
+        """The pooled buffer's sample_buffer (buffer.py:24-35), identical on every rank
+        (``as_bool=False``: dones as u8, as DeviceReplayBuffer.sample)."""
+        st, ac, rw, ns, tm, idx = self.sample_many(batch_size, 1)[0]
+        return st, ac, rw, ns, (tm if as_bool else tm.to(torch.uint8)), idx
 
     def sample_many(self, batch_size: int, n_batches: int):
         """``n_batches`` consecutive sample_buffer calls with NO stores between them,

@@ -167,13 +167,15 @@ class NativeSAC:
             None if status is None else status.data_ptr(), self._stream()))
 
     @torch.no_grad()
-    def learn(self, batch=None, noise=None):
-        """continuous_agent.py:96-154 as VecSAC.learn; returns the four losses (device scalars)."""
+    def learn(self, batch=None, noise=None, *, losses: bool = True):
+        """continuous_agent.py:96-154 as VecSAC.learn; returns the four losses (device scalars,
+        independent tensors), or with ``losses=False`` the agent's own f32 [4] loss buffer (no
+        copy launch: the next learn() rewrites it). None while the buffer holds < batch rows."""
         B, D = self.cfg.batch_size, self.params.obs_dim
         if batch is None:
             if self.memory is None or self.memory.mem_cntr < B:
                 return None
-            state, action, reward, state_, done, _ = self.memory.sample(B)
+            state, action, reward, state_, done, _ = self.memory.sample(B, as_bool=False)
         else:
             state, action, reward, state_, done = batch
         state = self._f32(state, B * D)
@@ -193,6 +195,8 @@ class NativeSAC:
             action.data_ptr(), reward.data_ptr(), state_.data_ptr(), done.data_ptr(), e1.data_ptr(),
             e2.data_ptr(), step, self.losses.data_ptr(), self._stream()))
         self.adam_step = step
+        if not losses:
+            return self.losses
         # independent tensors (as VecSAC.learn returns): the next learn() rewrites self.losses
         return tuple(self.losses.clone().unbind(0))
 

@@ -643,6 +643,42 @@ def test_replay_store_env_step_uses_final_obs(gpu, built_lib):
     assert torch.equal(st, rb.state_memory[idx]) and torch.equal(ns, rb.new_state_memory[idx])
 
 
+def test_replay_store_with_host_count_equals_two_launch_store(gpu, built_lib):
+    """sacenv_replay_store_env_at (the count from the host, one launch; what
+    DeviceReplayBuffer.store_batch issues) leaves the arena -- rows, last_term bytes
+    and the device mem_cntr -- exactly as sacenv_replay_store_env (device count, a
+    second launch to advance it), across ring wraps and a call storing more rows
+    than the ring holds."""
+    from sacenv import _lib
+    from sacenv.replay import DeviceReplayBuffer
+    M = 1000
+    a, b = (DeviceReplayBuffer(M, (11,), 1, device=gpu, seed=5) for _ in range(2))
+    a.arena.zero_()            # (unwritten ring rows hold whatever the allocation held)
+    b.arena.copy_(a.arena)
+    lt_a, lt_b = (torch.zeros(2500, dtype=torch.uint8, device=gpu) for _ in range(2))
+    g = torch.Generator(device=gpu).manual_seed(4)
+    for n in (300, 300, 300, 300, 2500, 7, 650):
+        st = torch.rand((n, 11), generator=g, device=gpu)
+        ns = torch.rand((n, 11), generator=g, device=gpu)
+        fo = torch.rand((n, 11), generator=g, device=gpu)
+        ac = torch.rand((n, 1), generator=g, device=gpu)
+        rw = torch.rand(n, generator=g, device=gpu, dtype=torch.float64)
+        rw = rw.float() if a.params.reward_f32 else rw   # as store_batch hands it over
+        cd = torch.randint(0, 7, (n,), generator=g, device=gpu, dtype=torch.uint8)
+        a.store_batch(st, ac, rw, ns, cd, final_state=fo, last_term=lt_a[:n])
+        _lib.check(b.lib.sacenv_replay_store_env(
+            b._pp, b.arena.data_ptr(), n, st.data_ptr(), ac.data_ptr(), rw.data_ptr(), ns.data_ptr(),
+            fo.data_ptr(), cd.data_ptr(), lt_b[:n].data_ptr(), b.stream))
+        b.mem_cntr += n
+        torch.cuda.synchronize()
+        assert torch.equal(a.arena, b.arena) and torch.equal(lt_a, lt_b), n
+        assert int(a._cntr.item()) == a.mem_cntr == b.mem_cntr == int(b._cntr.item())
+    with pytest.raises((ValueError, _lib.SacenvError)):
+        _lib.check(a.lib.sacenv_replay_store_env_at(a._pp, a.arena.data_ptr(), -1, 1, st.data_ptr(),
+                                                    ac.data_ptr(), rw.data_ptr(), ns.data_ptr(), None,
+                                                    cd.data_ptr(), None, a.stream))
+
+
 def test_replay_store_env_step_reference_terminal_vs_main_loop(gpu, built_lib):
     """main.py:70-91 around the reference env + ReplayBuffer (main_loop_goal.npz): the
     device buffer holds the same rows, terminal following the env's persistent
