@@ -754,7 +754,7 @@ class SegmentRunner:
             gset = self.graphs[(k0 % ACTION_STEPS) // SEG]
             gset[p.buf if p is not None else 0].replay()
         else:
-            self._steps(k0, p is not None, buf=buf, on_step=on_step, timed=timed)
+            self._steps(k0, with_pool, buf=buf, on_step=on_step, timed=timed)
         if own:
             eb.record(self.st)
             self.seg_events.append((ea, eb, SEG))

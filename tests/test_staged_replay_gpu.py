@@ -151,3 +151,40 @@ def test_staged_replay_two_ranks_equal_pooled_buffer(gpu, built_lib):
     for p in ps:
         p.join(timeout=60)
     assert res[0] == (3 * SEG, 0) and res[1] is None, res
+
+
+def test_bench_runner_exchange_equals_direct_staged_replay(gpu, built_lib):
+    """bench's timed N>1 path (SegmentRunner with the SegmentExchange of --pooling
+    sharded, at world 1) samples the same batches as the staged replay driven by
+    hand (StagedReplay + segment_async(stage=...) + refill, one stream): the runner's
+    segments must write the staged rows (a runner that stepped plain segments would
+    gather stale rows)."""
+    import bench
+    from sacenv.replay import StagedReplay
+    args = bench.parse(["--no-cpu-baseline", "--envs", "4096", "--replay-mem", "100003",
+                        "--replay-batch", "257"])
+    wl_a, wl_b = (bench.make_workload(args, 0, gpu) for _ in range(2))
+    x = bench.make_exchange(args, wl_a, 0, 1, gpu)
+    run = bench.SegmentRunner(args, wl_a, gpu, None, bench.SEG, x)
+    env_b = wl_b.envs[0]
+    rep = StagedReplay(env_b.num_envs, env_b.n_pad, args.experiment, env_b.first_obs_template(), rank=0,
+                       world=1, mem_size=args.replay_mem, batch=args.replay_batch, seg=bench.SEG, seed=0,
+                       device=gpu)
+    rep.begin(env_b.obs)
+    k = 0
+    for g in range(3):
+        k = run.segment(k, False)
+        run.finish()
+        sa = rep.stage_args(g)
+        wl_b.segment_step(g * bench.SEG % bench.ACTION_STEPS, bench.SEG, stage=sa["stage"], marks=sa["marks"])
+        wl_b.refill()
+        rep.prepare(g + 1)
+        want = rep.sample_segment(g)
+        torch.cuda.synchronize()
+        got = x.last
+        assert len(got) == len(want) == bench.SEG
+        for j in (0, 1, 77, bench.SEG - 1):
+            for u, v in zip(got[j], want[j]):
+                assert torch.equal(u, v), (g, j)
+    rep.check()
+    x.sampler.check()
