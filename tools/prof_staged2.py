@@ -1,0 +1,80 @@
+"""Which side-stream kernel slows the staged segment launch (diagnostic).
+
+bench's workload (exp 6, 65 536 envs) with a StagedReplay; per segment the launch
+is bracketed by HIP events on the stepping stream, and the replay's work is placed:
+  serial  -- everything after the refill on the stepping stream (no overlap);
+  both    -- draws + marks (prepare) and the gather on the side stream, as bench;
+  prep    -- only prepare on the side stream (gather serial after the refill);
+  gather  -- only the gather on the side stream (prepare serial).
+Prints the median launch time per mode (us per 256-step launch) and the wall
+us per step.
+"""
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "sac-agent_amd"))
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+
+
+def main():
+    args = bench.parse(["--no-cpu-baseline"])
+    dev = torch.device("cuda", 0)
+    wl = bench.make_workload(args, 0, dev)
+    env = wl.envs[0]
+    from sacenv.replay import StagedReplay
+    main_st = torch.cuda.current_stream(dev)
+    side = torch.cuda.Stream(device=dev)
+    for mode in ("serial", "both", "prep", "gather", "serial", "both"):
+        rep = StagedReplay(env.num_envs, env.n_pad, args.experiment, env.first_obs_template(), rank=0, world=1,
+                           mem_size=args.replay_mem, batch=args.replay_batch, seg=bench.SEG, seed=0, device=dev)
+        rep.begin(env.obs)
+        k = 0
+        launch = []
+        ready, done = [], {}
+        for g in range(10):
+            for ev in ready:
+                main_st.wait_event(ev)
+            ready = []
+            if g - 2 in done:
+                main_st.wait_event(done.pop(g - 2))
+            sa = rep.stage_args(g)
+            ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ea.record(main_st)
+            wl.segment_step(k % bench.ACTION_STEPS, bench.SEG, stage=sa["stage"], marks=sa["marks"])
+            eb.record(main_st)
+            wl.refill()
+            k += bench.SEG
+            if mode in ("both", "prep"):
+                # as SegmentExchange: prepare(g + 1) does not wait for the launch
+                side.wait_event(ea)
+                with torch.cuda.stream(side):
+                    rep.prepare(g + 1)
+                    e = torch.cuda.Event()
+                    e.record(side)
+                ready.append(e)
+            else:
+                rep.prepare(g + 1)
+            if mode in ("both", "gather"):
+                side.wait_stream(main_st)
+                with torch.cuda.stream(side):
+                    rep.sample_segment(g)
+                    e = torch.cuda.Event()
+                    e.record(side)
+                done[g] = e
+            else:
+                rep.sample_segment(g)
+            launch.append((ea, eb))
+        torch.cuda.synchronize()
+        rep.check()
+        ms = [a.elapsed_time(b) * 1e3 for a, b in launch[3:]]
+        print(f"{mode:7s} launch {statistics.median(ms):7.1f} us (min {min(ms):6.1f})", flush=True)
+
+
+if __name__ == "__main__":
+    main()
