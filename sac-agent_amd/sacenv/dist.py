@@ -310,6 +310,10 @@ class SegmentExchange:
         """The obs every env starts from (the s of the first stored transition); the
         first segments' draws and marks, on the stepping stream."""
         self.sampler.begin(obs)
+        if self.cuda:
+            # the side stream's first prepare() continues the sampling stream begin()'s
+            # draws advance on this stream: it must not run ahead of them
+            self.side.wait_stream(self._cur())
         self.started, self.g = True, 0
 
     def stage_args(self) -> dict:
