@@ -65,10 +65,6 @@ struct RB {
   __device__ int32_t* pos() const { return reinterpret_cast<int32_t*>(b + L.mt_pos); }
 };
 
-struct DrawLds {
-  uint32_t blk[2][kMtN];
-};
-
 __global__ void __launch_bounds__(kWave) k_rb_init(RB r, uint32_t seed) {
   if (threadIdx.x != 0) return;
   uint32_t x = seed;  // init_genrand (numpy RandomState._legacy_seeding)
@@ -152,54 +148,9 @@ __global__ void k_rb_advance(RB r, int64_t n) {
 
 // np.random.choice(max_mem, batch) with replace=True, p=None: numpy legacy
 // randint(0, max_mem) -> masked rejection on 32-bit words (rng = max_mem-1;
-// rng == 0 draws nothing). One wave; words in order, accepted words fill the
-// batch in order, the stream stops after the batch-th accepted word.
-__global__ void __launch_bounds__(kWave) k_rb_draw(SacenvReplayParams p, RB r, int batch,
-                                                   int64_t* __restrict__ idx) {
-  __shared__ DrawLds l;
-  const int lane = threadIdx.x;
-  const int64_t cnt = *r.cntr();
-  const int64_t max_mem = cnt < p.mem_size ? cnt : p.mem_size;
-  const uint64_t rng = (uint64_t)(max_mem - 1);
-  if (rng == 0) {  // numpy: off + 0, no words consumed
-    for (int i = lane; i < batch; i += kWave) idx[i] = 0;
-    return;
-  }
-  uint32_t mask = (uint32_t)rng;
-  mask |= mask >> 1;
-  mask |= mask >> 2;
-  mask |= mask >> 4;
-  mask |= mask >> 8;
-  mask |= mask >> 16;
-  MtStream st;
-  st.gkey = r.key();
-  st.pos = *r.pos();
-  st.cur = 0;
-  st.loaded = false;
-  st.nxt_valid = false;
-  st.advanced = false;
-  int filled = 0;
-  while (filled < batch) {
-    const uint32_t w = mt_fetch(st, l, lane) & mask;
-    const bool acc = w <= (uint32_t)rng;
-    const unsigned long long bal = __ballot(acc);
-    const int before = __popcll(bal & ((1ull << lane) - 1ull));
-    const int take = batch - filled;
-    if (acc && before < take) idx[filled + before] = (int64_t)w;
-    const int total = __popcll(bal);
-    if (total >= take) {
-      // the take-th accepted word ends the draw: consume up to and including it
-      unsigned long long b = bal;
-      for (int t = 1; t < take; ++t) b &= b - 1ull;
-      st.pos += __ffsll((long long)b);
-      filled = batch;
-    } else {
-      st.pos += kWave;
-      filled += total;
-    }
-  }
-  mt_finish(st, l, r.pos(), lane);
-}
+// rng == 0 draws nothing); words in order, accepted words fill the batch in
+// order, the stream stops after the batch-th accepted word: k_rb_draw_many below
+// (one 1 024-thread workgroup).
 
 // Sharded rows (sacenv_replay_sample_shard): ring row p holds the transition
 // with the latest global sequence number s <= mem_cntr - 1, s = p (mod M); this
@@ -297,6 +248,10 @@ __device__ __forceinline__ void mt_twist_block(const uint32_t* __restrict__ o, u
   __syncthreads();
 }
 
+// kSample: one sample_buffer(batch) at the device count (sacenv_replay_sample: no
+// learn() skip below batch rows; graph-capturable like the store), else the nb
+// learns of a staged segment at counts cntr0 + (k + 1) * period.
+template <bool kSample = false>
 __global__ void __launch_bounds__(kDrawThreads) k_rb_draw_many(SacenvReplayParams p, RB r, int batch, int nb,
                                                                int64_t cntr0, int64_t period,
                                                                int64_t* __restrict__ idx) {
@@ -311,11 +266,12 @@ __global__ void __launch_bounds__(kDrawThreads) k_rb_draw_many(SacenvReplayParam
   __syncthreads();
   int k = 0, filled = 0;
   while (k < nb) {
-    const int64_t c = cntr0 + (int64_t)(k + 1) * period;
+    const int64_t c = kSample ? *r.cntr() : cntr0 + (int64_t)(k + 1) * period;
     const int64_t max_mem = c < p.mem_size ? c : p.mem_size;
     const uint32_t rng = (uint32_t)(max_mem - 1);
-    if (c < batch || rng == 0u) {  // learn() returns before sampling, or numpy's off + 0: no words
-      for (int i = tid; i < batch; i += kDrawThreads) idx[(int64_t)k * batch + i] = c < batch ? -1 : 0;
+    const bool skip = !kSample && c < batch;
+    if (skip || rng == 0u) {  // learn() returns before sampling, or numpy's off + 0: no words
+      for (int i = tid; i < batch; i += kDrawThreads) idx[(int64_t)k * batch + i] = skip ? -1 : 0;
       ++k;
       continue;
     }
@@ -767,7 +723,10 @@ static int sample(const SacenvReplayParams* p, void* arena, int32_t batch, int64
   if (arena == nullptr || idx == nullptr) return SACENV_E_NULL;
   if (batch == 0) return SACENV_OK;
   const RB r = make_rb(*p, arena);
-  hipLaunchKernelGGL(k_rb_draw, dim3(1), dim3(kWave), 0, (hipStream_t)stream, *p, r, batch, idx);
+  // one 1 024-thread workgroup: a twist per 624 words and one ballot-and-scan round per
+  // block instead of one wave's 64-word rounds (9.8 -> ~4 us per 1 024 draws)
+  hipLaunchKernelGGL(k_rb_draw_many<true>, dim3(1), dim3(kDrawThreads), 0, (hipStream_t)stream, *p, r, batch, 1,
+                     (int64_t)0, (int64_t)0, idx);
   if ((rc = status())) return rc;
   const int64_t total = (int64_t)batch * (p->obs_dim + p->act_dim + 1);
   hipLaunchKernelGGL(k_rb_gather, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *p,
@@ -866,7 +825,7 @@ int sacenv_replay_stage_draw(const SacenvReplayParams* p, void* arena, const Sac
   const int64_t M = p->mem_size;
   const bool steady = cntr0 + sp->period >= M && cntr0 + sp->period >= batch && M >= 2;
   if (!steady) {  // the first learns of a buffer (ranges below M, skipped learns): one workgroup
-    hipLaunchKernelGGL(k_rb_draw_many, dim3(1), dim3(kDrawThreads), 0, (hipStream_t)stream, *p, r, batch,
+    hipLaunchKernelGGL(k_rb_draw_many<false>, dim3(1), dim3(kDrawThreads), 0, (hipStream_t)stream, *p, r, batch,
                        n_batches, cntr0, sp->period, idx);
     return status();
   }

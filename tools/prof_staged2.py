@@ -5,7 +5,8 @@ is bracketed by HIP events on the stepping stream, and the replay's work is plac
   serial  -- everything after the refill on the stepping stream (no overlap);
   both    -- draws + marks (prepare) and the gather on the side stream, as bench;
   prep    -- only prepare on the side stream (gather serial after the refill);
-  gather  -- only the gather on the side stream (prepare serial).
+  gather  -- only the gather on the side stream (prepare serial);
+  after   -- prepare and gather on the side stream after the launch (beside the refill).
 Prints the median launch time per mode (us per 256-step launch) and the wall
 us per step.
 """
@@ -30,14 +31,18 @@ def main():
     from sacenv.replay import StagedReplay
     main_st = torch.cuda.current_stream(dev)
     side = torch.cuda.Stream(device=dev)
-    for mode in ("serial", "both", "prep", "gather", "serial", "both"):
+    for mode in ("serial", "both", "after", "serial", "both", "after"):
         rep = StagedReplay(env.num_envs, env.n_pad, args.experiment, env.first_obs_template(), rank=0, world=1,
                            mem_size=args.replay_mem, batch=args.replay_batch, seg=bench.SEG, seed=0, device=dev)
         rep.begin(env.obs)
         k = 0
         launch = []
         ready, done = [], {}
+        t_a = t_b = None
         for g in range(10):
+            if g == 3:
+                t_a = torch.cuda.Event(enable_timing=True)
+                t_a.record(main_st)
             for ev in ready:
                 main_st.wait_event(ev)
             ready = []
@@ -50,9 +55,10 @@ def main():
             eb.record(main_st)
             wl.refill()
             k += bench.SEG
-            if mode in ("both", "prep"):
+            if mode in ("both", "prep", "after"):
                 # as SegmentExchange: prepare(g + 1) does not wait for the launch
-                side.wait_event(ea)
+                # ("after": it waits for the launch's end, running beside the refill)
+                side.wait_event(eb if mode == "after" else ea)
                 with torch.cuda.stream(side):
                     rep.prepare(g + 1)
                     e = torch.cuda.Event()
@@ -60,7 +66,7 @@ def main():
                 ready.append(e)
             else:
                 rep.prepare(g + 1)
-            if mode in ("both", "gather"):
+            if mode in ("both", "gather", "after"):
                 side.wait_stream(main_st)
                 with torch.cuda.stream(side):
                     rep.sample_segment(g)
@@ -70,10 +76,16 @@ def main():
             else:
                 rep.sample_segment(g)
             launch.append((ea, eb))
+        for ev in ready + list(done.values()):
+            main_st.wait_event(ev)
+        t_b = torch.cuda.Event(enable_timing=True)
+        t_b.record(main_st)
         torch.cuda.synchronize()
         rep.check()
         ms = [a.elapsed_time(b) * 1e3 for a, b in launch[3:]]
-        print(f"{mode:7s} launch {statistics.median(ms):7.1f} us (min {min(ms):6.1f})", flush=True)
+        per_step = t_a.elapsed_time(t_b) * 1e3 / (7 * bench.SEG)
+        print(f"{mode:7s} launch {statistics.median(ms):7.1f} us (min {min(ms):6.1f}); {per_step:.3f} us/step "
+              f"wall (segments 3-9 with their refills and replay work)", flush=True)
 
 
 if __name__ == "__main__":
