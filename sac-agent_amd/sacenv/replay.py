@@ -308,6 +308,14 @@ class StagedReplay:
         self._idx = [torch.empty(self.seg * self.batch, dtype=torch.int64, device=self.device) for _ in range(4)]
         self._words = [_packed_batches(self.batch, self.seg, _lib.OBS_DIM, 1, (_lib.OBS_DIM,), self.device)
                        for _ in range(2)]
+        # the per-learn views of each (words, idx) buffer pair, built once: a segment's
+        # 256 x 6 tensor views cost ~1 ms of host time, more than the segment's GPU time
+        B = self.batch
+        self._batches = {}
+        for wi, (_, views) in enumerate(self._words):
+            for ii, idx in enumerate(self._idx):
+                self._batches[wi, ii] = [(st, ac, rw, ns, tm32, idx[i * B: (i + 1) * B])
+                                         for i, (st, ac, rw, ns, tm32, _) in enumerate(views)]
         nbytes = C.c_int64()
         _lib.check(self.lib.sacenv_replay_stage_scratch_bytes(self._rb._pp, self.batch, self.seg, C.byref(nbytes)))
         self._scratch = torch.empty(int(nbytes.value), dtype=torch.uint8, device=self.device)
@@ -360,7 +368,7 @@ class StagedReplay:
         views valid until ``sample_segment(g + 2)``."""
         import torch.distributed as dist
         g = int(g)
-        words, views = self._words[g % 2]
+        words = self._words[g % 2][0]
         idx = self._idx[g % 4]
         nb = self.N_BUFFERS
         _lib.check(self.lib.sacenv_replay_sample_staged(
@@ -368,8 +376,7 @@ class StagedReplay:
             idx.data_ptr(), self.batch, self.seg, words.data_ptr(), self.stream))
         if self.world > 1:
             dist.all_reduce(words, op=dist.ReduceOp.SUM, group=self.group)
-        B = self.batch
-        return [(st, ac, rw, ns, tm32, idx[i * B: (i + 1) * B]) for i, (st, ac, rw, ns, tm32, _) in enumerate(views)]
+        return self._batches[g % 2, g % 4]
 
     @property
     def bytes_per_segment(self) -> int:
