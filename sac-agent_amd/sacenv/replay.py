@@ -308,8 +308,8 @@ class StagedReplay:
         self._idx = [torch.empty(self.seg * self.batch, dtype=torch.int64, device=self.device) for _ in range(4)]
         self._words = [_packed_batches(self.batch, self.seg, _lib.OBS_DIM, 1, (_lib.OBS_DIM,), self.device)
                        for _ in range(2)]
-        # the per-learn views of each (words, idx) buffer pair, built once: a segment's
-        # 256 x 6 tensor views cost ~1 ms of host time, more than the segment's GPU time
+        # the per-learn views of each (words, idx) buffer pair, built once instead of
+        # 256 idx slices per segment (host time the persistent launches do not wait for)
         B = self.batch
         self._batches = {}
         for wi, (_, views) in enumerate(self._words):
