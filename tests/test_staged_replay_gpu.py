@@ -104,7 +104,8 @@ def _run(rank, world, exp, N, M, B, n_segs, dev, group=None):
     return (checked, skipped) if rank == 0 else None
 
 
-@pytest.mark.parametrize("exp,N,M,B", [(6, 3000, 50_021, 256), (2, 2000, 40_000, 511), (6, 700, 20_000, 1024)])
+@pytest.mark.parametrize("exp,N,M,B", [(6, 3000, 50_021, 256), (2, 2000, 40_000, 511), (6, 700, 20_000, 1024),
+                                       (5, 1500, 30_011, 300), (1, 1100, 25_000, 128)])
 def test_staged_replay_equals_per_step_learns(exp, N, M, B, gpu, built_lib):
     checked, skipped = _run(0, 1, exp, N, M, B, 4, gpu)
     assert checked + skipped == 4 * SEG
