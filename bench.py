@@ -39,6 +39,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import subprocess
 import sys
@@ -78,6 +79,8 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=2048)
     ap.add_argument("--warmup", type=int, default=512)
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--min-seconds", type=float, default=MIN_TIMED_SECONDS,
+                    help="the timed region lasts at least this long (whole segments; GPU runs only)")
     ap.add_argument("--experiment", type=int, default=6)
     ap.add_argument("--no-graph", action="store_true", help="eager per-step launches (--launch step)")
     ap.add_argument("--launch", choices=("segment", "step"), default="segment",
@@ -135,6 +138,9 @@ def parse(argv=None):
 
 
 MIN_TIMED_SEGS = 8   # the timed region holds at least 2 048 steps
+MIN_TIMED_SECONDS = 1.0  # and lasts at least ~1 s (whole segments, sized from the warm-up's rate), so
+                         # an outside sampler of GPU activity sees the timed phase
+                         # (--min-seconds)
 MIN_WARMUP_SEGS = 2  # and at least 512 warm-up steps: the driver's --steps 20 --warmup 5 then
                      # times the default line's region (the episode-length transient of the
                      # first ~1 000 steps -- every env starts at step 0 -- is behind it)
@@ -855,10 +861,15 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
     segment = run.segment
     n_warm, n_timed = warm_segs(args.warmup), timed_segs(args.steps)
     k = 0
+    t_w = time.perf_counter()
     for _ in range(n_warm):
         k = segment(k, False)
     run.finish()
     _sync(dev)
+    per_seg = (time.perf_counter() - t_w) / n_warm
+    if dev.type == "cuda":  # (CPU stub runs measure the harness: no minimum duration)
+        n_timed = int(_max_over_ranks(float(max(n_timed, math.ceil(args.min_seconds / max(per_seg, 1e-6)))),
+                                      world, dev))
     barrier(world)
     _sync(dev)
     ev0, ev1 = _Clock(dev), _Clock(dev)
@@ -1016,7 +1027,8 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
         "warmup": n_warm * SEG,
         "requested": {"steps": args.steps, "warmup": args.warmup,
                       "rule": f"rounded up to whole {SEG}-step segments (each ends with its refill); "
-                              f"at least {MIN_TIMED_SEGS * SEG} timed and {MIN_WARMUP_SEGS * SEG} warm-up steps"},
+                              f"at least {MIN_TIMED_SEGS * SEG} timed and {MIN_WARMUP_SEGS * SEG} warm-up steps, "
+                              f"and timed segments for at least ~{args.min_seconds:g} s at the warm-up's rate"},
         "setup": {"graph_first_replays": run.first_replays,
                   "note": "steps of the first pass over the action table (a captured graph's first "
                           "replay carries its device upload), run before the warm-up, untimed"},

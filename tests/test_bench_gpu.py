@@ -26,7 +26,9 @@ def test_driver_bench_command():
     assert r.returncode == 0, r.stderr[-3000:]
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
     d = json.loads(line)
-    assert d["steps"] == 8 * 256 and d["warmup"] == 512 and d["n_gpus"] == 1   # >= 8 timed, 2 warm-up segments
+    # >= 8 timed segments, 2 warm-up segments, and the timed region lasts ~1 s (bench.MIN_TIMED_SECONDS)
+    assert d["steps"] % 256 == 0 and d["steps"] >= 8 * 256 and d["warmup"] == 512 and d["n_gpus"] == 1
+    assert d["ms_per_step"] * d["steps"] * 1e-3 >= 0.5
     assert d["value"] > 0 and d["unit"] == "env-steps/s"
     assert d["ms_per_step"] * d["steps"] * 1e-3 <= wall
     # every captured graph (4 action-table segments) ran once before the warm-up
@@ -71,12 +73,12 @@ def test_bench_two_ranks_gloo_on_one_device():
                        capture_output=True, text=True, timeout=600, cwd=ROOT, env=_two_rank_env())
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
-    assert d["n_gpus"] == 2 and d["steps"] == 8 * 256 and d["value"] > 0
+    assert d["n_gpus"] == 2 and d["steps"] % 256 == 0 and d["steps"] >= 8 * 256 and d["value"] > 0
     assert d["config"]["global_envs"] == 2 * 8192
     c = d["config"]["collective"]
-    assert "gloo SUM all_reduce" in c and "(8 in the timed region)" in c and "StagedReplay" in c
+    assert "gloo SUM all_reduce" in c and f"({d['steps'] // 256} in the timed region)" in c and "StagedReplay" in c
     po = d["pooling"]
-    assert po["mode"] == "sharded" and po["exchanges_timed"] == 8
+    assert po["mode"] == "sharded" and po["exchanges_timed"] == d["steps"] // 256
     assert po["all_gather"]["value"] > 0 and po["no_exchange"]["value"] > 0
 
 
