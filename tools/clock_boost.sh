@@ -1,3 +1,6 @@
+#!/bin/bash
+# The segment kernel's effective clock per dispatch over a default bench run (GRBM_GUI_ACTIVE / 8 XCDs /
+# duration): profiles/r05_clock_boost.txt
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -s KILL 200 rocprofv3 --pmc GRBM_GUI_ACTIVE -d gpurun_out/clk20 -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-every-output > gpurun_out/clk20.json 2> gpurun_out/clk20.log || { tail -5 gpurun_out/clk20.log; exit 1; }
