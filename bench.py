@@ -92,7 +92,8 @@ def parse(argv=None):
                     help="total CPU-baseline budget (4 C1 legs + the vectorised port)")
     ap.add_argument("--kernel-launches", type=int, default=256)
     ap.add_argument("--test-mode", type=int, default=0, help="1 = rudder frozen (no terminations)")
-    ap.add_argument("--helpers", type=int, default=8192, help="workgroups of a refill draw launch")
+    ap.add_argument("--helpers", type=int, default=None,
+                    help="workgroups of a refill draw launch (default: VecBoatEnv's, 3/16 of the envs)")
     ap.add_argument("--mixed", action="store_true",
                     help="BASELINE configs[4]: boat exp-6 + toy_parachute + toy_car in one launch")
     ap.add_argument("--mixed-envs", type=int, default=32768, help="envs per type per GPU (--mixed)")

@@ -1,7 +1,7 @@
 """The bench's exact timed path under parity.
 
 ``bench.py`` times 128-step segments of the BASELINE config (exp 6, 65 536
-envs, 500-step episodes, in-kernel auto-reset, 8 192 refill helpers,
+envs, 500-step episodes, in-kernel auto-reset, the default refill helpers (12 288),
 ``auto_refill=False`` with the refill placed after every segment), each one
 persistent ``sacenv_boat_segment`` launch (the default ``--launch segment``) or
 one hipGraph replay of 128 ``k_step`` launches (``--launch step``). This test
@@ -65,7 +65,7 @@ def test_bench_timed_path_equals_eager_and_oracle(gpu, built_lib):
     args_g = bench.parse(["--no-cpu-baseline", "--launch", "step"])
     args_e = bench.parse(["--no-cpu-baseline", "--no-graph"])
     assert args_q.launch == "segment" and args_q.refill_overlap == 0   # the default the driver times
-    assert (args_s.envs, args_s.experiment, args_s.episode_steps, args_s.helpers) == (65536, 6, 500, 8192)
+    assert (args_s.envs, args_s.experiment, args_s.episode_steps, args_s.helpers) == (65536, 6, 500, None)
     wls = [bench.make_workload(a, 0, gpu) for a in (args_s, args_q, args_g, args_e)]
     wl_e = wls[-1]
     envs = [w.envs[0] for w in wls]
