@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SACENV_ABI_VERSION 17
+#define SACENV_ABI_VERSION 18
 #define SACENV_OBS_DIM 11      /* Boat.return_state, boat_env.py:308-323 */
 #define SACENV_MT_N 624        /* MT19937 words per env (numpy legacy RNG) */
 #define SACENV_MAX_KNOTS 16    /* wind.fixed_points upper bound */
@@ -131,7 +131,9 @@ typedef struct SacenvBoatLayout {
   int64_t index;              /* i32 [n_pad] steps since reset; fuel = fuel0 - index */
   int64_t cons;               /* i32 [n_pad] episodes started (active slot = cons % SLOTS) */
   int64_t fill;               /* i32 [n_pad] episodes drawn (autoreset; cons < fill <= cons + SLOTS) */
-  int64_t mt_pos;             /* i32 [n_pad] next MT word index, 624 => twist first */
+  int64_t mt_pos;             /* i32 [n_pad] bits 0..15: next MT word index (624 => twist first; after
+                                 a refill's draw launch up to 1 248, past 624 in mt_next); bit 16: mt_next
+                                 holds the block after mt_key. A host write stores the index plain. */
   int64_t start_y;            /* i32 [SLOTS][n_pad] Boat.s_y_start per slot */
   int64_t counters;           /* u32 [5][n_pad] cumulative termination counters */
   int64_t refill_list;        /* i32 [3][n_pad] by refill rank: env, first and end episode number drawn
@@ -143,7 +145,7 @@ typedef struct SacenvBoatLayout {
   int64_t knots_raw;          /* f64 [n_pad][SLOTS][2][n_knots] drawn knot values, only with
                                  SACENV_OUT_KNOTS (else -1: no storage; a refill's fit reads the drawn
                                  knots from the slot's own wind_knots y fields) */
-  int64_t mt_key;             /* u32 [n_pad][624] per-env MT19937 state */
+  int64_t mt_key;             /* u32 [n_pad][624] per-env MT19937 state (the current block) */
   int64_t record;             /* u8 [50 n_pad]: obs f32 [n_pad][11] | reward f32 [n_pad]
                                  | done u8 [n_pad] | term u8 [n_pad]  (the all-gather payload) */
   int64_t obs, reward, done, term; /* the four parts of `record` */
@@ -161,6 +163,8 @@ typedef struct SacenvBoatLayout {
                                  the env's last termination code 1..5 (0: none yet); every step
                                  updates it, resets never clear it (boat_env.py:24-32,84-105,120-126;
                                  main.py:83 reads it) */
+  int64_t mt_next;            /* u32 [n_pad][624] the block after mt_key, twisted ahead by the refill's
+                                 fit launch (valid while mt_pos bit 16 is set) */
 } SacenvBoatLayout;
 
 /* status bits (layout.status[1]); sticky until the arena is re-initialised */

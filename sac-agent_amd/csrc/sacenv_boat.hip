@@ -59,6 +59,13 @@ constexpr int U_SX = 0, U_SY = 8, U_SR = 16, U_VX = 24, U_VY = 32, U_VR = 40, U_
               U_LIST = U_CNT + 4 * SACENV_N_COUNTERS, U_CSNAP = U_LIST + 12, U_LTERM = U_CSNAP + 4,
               U_WIND = U_LTERM + 4;
 constexpr int U_MT_BYTES = 4 * kMtN;
+// U_MTPOS holds the MT word index (bits 0..15, up to 2 x 624) and kMtNextOk:
+// mt_next holds the block after mt_key (twisted ahead by the refill's fit
+// launch), so a draw window may run past the block end without a twist; an
+// index past 624 then reads mt_next, and the fit launch makes it current.
+// Every other writer of the index (the wave-path draws, seeding, the host)
+// stores it plain, which withdraws the pre-twisted block.
+constexpr int kMtPosMask = 0xFFFF, kMtNextOk = 1 << 16;
 // The f64 fields below U_PAIRED are stored as 16-B pairs per env, [n_pad][2]:
 // (s_x, s_y) (s_r, v_x) (v_y, v_r) (rudder, ep_reward), the spline piece as
 // (y0, m0) (y1, m1) per curve, and the two next-episode y0. A field's pair
@@ -101,7 +108,8 @@ __host__ __device__ inline void compute_layout(int n, int nk, int L, int use_tab
   o->wind_knots = uw * np;
   o->knots_raw = raw_knots ? (uw + 2 * wk) * np : -1;
   o->mt_key = (uw + (2 + rk) * wk) * np;
-  const int64_t ur = uw + (2 + rk) * wk + U_MT_BYTES;
+  o->mt_next = o->mt_key + U_MT_BYTES * np;
+  const int64_t ur = uw + (2 + rk) * wk + 2 * U_MT_BYTES;
   o->record = ur * np;
   o->obs = ur * np;
   o->reward = (ur + 44) * np;
@@ -141,7 +149,8 @@ struct Arena {
   __device__ __forceinline__ double* wind_knots() const { return at<double>(U_WIND); }
   __device__ __forceinline__ double* knots_raw() const { return at<double>(U_WIND + 2 * wk()); }
   __device__ __forceinline__ uint32_t* mt_key() const { return at<uint32_t>(U_WIND + (2 + rk) * wk()); }
-  __device__ __forceinline__ int64_t ur() const { return U_WIND + (2 + rk) * wk() + U_MT_BYTES; }
+  __device__ __forceinline__ uint32_t* mt_next() const { return mt_key() + kMtN * np; }
+  __device__ __forceinline__ int64_t ur() const { return U_WIND + (2 + rk) * wk() + 2 * U_MT_BYTES; }
   __device__ __forceinline__ float* obs() const { return at<float>(ur()); }
   __device__ __forceinline__ float* reward() const { return at<float>(ur() + 44); }
   __device__ __forceinline__ uint8_t* done() const { return at<uint8_t>(ur() + 48); }
@@ -777,7 +786,9 @@ __device__ int32_t draw_knots_wave(const SacenvBoatParams& p, const Arena& A, Rn
   }
   MtStream st;
   st.gkey = A.mt_key() + (int64_t)e * kMtN;
-  st.pos = pos0 >= 0 ? pos0 : A.i32(U_MTPOS)[e];  // pos0: prefetched by the caller
+  st.pos = pos0 >= 0 ? pos0 : A.i32(U_MTPOS)[e] & kMtPosMask;  // pos0: prefetched by the caller
+  // (a pos0 past 624 lies in the block after mt_key: mt_fetch twists mt_key to it;
+  // mt_finish stores the index plain, withdrawing mt_next)
   st.cur = 0;
   st.loaded = false;
   st.nxt_valid = false;
@@ -1024,7 +1035,7 @@ __global__ void __launch_bounds__(kWave) k_seed(SacenvBoatParams p, Arena A, con
     key[i] = x;
     x = 1812433253u * (x ^ (x >> 30)) + (uint32_t)(i + 1);
   }
-  A.i32(U_MTPOS)[e] = kMtN;
+  A.i32(U_MTPOS)[e] = kMtN;  // (plain: mt_next not twisted yet)
   A.i32(U_CONS)[e] = 0;
   A.i32(U_FILL)[e] = 0;
 }
@@ -1159,9 +1170,10 @@ constexpr int kRefillStamps = 24;  // per refill wave: start, total read, fast p
 // (masked rejection, numpy legacy) and turns the following word pairs into the
 // knots (genrand_res53), lane = (curve, knot): one wave instruction serves four
 // envs, where the wave-per-env draw spent ~330 wave instructions on each (the
-// refill was VALU-bound). The rest -- windows that cross the block end (the
-// twist), a randint rejected 16 times, more than 8 knots, further episodes of
-// an env that consumed several -- goes through the wave-per-env draw
+// refill was VALU-bound). A window that crosses the block end reads on in
+// mt_next when the last fit launch twisted it ahead (kMtNextOk). The rest --
+// a crossing without mt_next (a second one since the last refill), a randint
+// rejected 16 times, more than 8 knots -- goes through the wave-per-env draw
 // (draw_knots_wave), env by env. Block 0 counts the refill.
 constexpr int kGroupLanes = 16;
 constexpr int kGroups = kWave / kGroupLanes;
@@ -1203,7 +1215,8 @@ __global__ void __launch_bounds__(kWave) k_refill(SacenvBoatParams p, Arena A) {
     const int e = ok ? e_n : 0;
     const int c = ok ? c_n : 0;
     const int f0 = ok ? f_n : 0;
-    const int pos = ok ? p_n : kMtN;
+    const int pos = ok ? (p_n & kMtPosMask) : kMtN;
+    const bool nx = ok && (p_n & kMtNextOk) != 0;  // mt_next holds the next block
     if (r0 + kGroups * G < total) {  // the next iteration's rank, in flight with this one
       rq = rr + kGroups * G < np_ ? rr + kGroups * G : 0;
       e_n = A.refill_list(0)[rq], f_n = A.refill_list(1)[rq], c_n = A.refill_list(2)[rq], p_n = A.cons_snap()[rq];
@@ -1219,13 +1232,18 @@ __global__ void __launch_bounds__(kWave) k_refill(SacenvBoatParams p, Arena A) {
     uint32_t* const gw = lds.blk[0] + g * 3 * kGroupLanes;
 #pragma unroll 1
     while (__ballot(live) != 0ull) {  // uniform: until every group left the fast path
-      bool fast = live && pos_next + nwords <= kMtN;
-      // the group's words pos_next .. pos_next + nwords - 1 (raw, key order), tempered
-      const uint32_t* key = A.mt_key() + (int64_t)e * kMtN + pos_next;
+      // (with the next block pre-twisted, a window may cross the block end)
+      bool fast = live && pos_next + nwords <= (nx ? 2 * kMtN : kMtN);
+      // the group's words pos_next .. pos_next + nwords - 1 (raw, key order), tempered;
+      // index 624 on from mt_next
+      const int64_t eo = (int64_t)e * kMtN;
       uint32_t w[3];
 #pragma unroll
-      for (int q = 0; q < 3; ++q)
-        w[q] = fast && gl + kGroupLanes * q < nwords ? mt_temper(key[gl + kGroupLanes * q]) : 0u;
+      for (int q = 0; q < 3; ++q) {
+        const int i = pos_next + gl + kGroupLanes * q;
+        const uint32_t* src = i < kMtN ? A.mt_key() + eo + i : A.mt_next() + eo + (i - kMtN);
+        w[q] = fast && gl + kGroupLanes * q < nwords ? mt_temper(*src) : 0u;
+      }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the last pass's reads of gw are done
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1252,7 +1270,7 @@ __global__ void __launch_bounds__(kWave) k_refill(SacenvBoatParams p, Arena A) {
         }
         if (gl == 0) {
           A.i32(U_STARTY)[(int64_t)slot * A.np + e] = -p.start_y_half + (int32_t)(gw[k] & mask);
-          A.i32(U_MTPOS)[e] = pos_next + k + 1 + need;
+          A.i32(U_MTPOS)[e] = (pos_next + k + 1 + need) | (nx ? kMtNextOk : 0);
         }
         f_next = f_next + 1;
         pos_next = pos_next + k + 1 + need;
@@ -1371,11 +1389,106 @@ __device__ __forceinline__ void fit_group(const SacenvBoatParams& p, const Arena
   }
 }
 
+// The fit launch's first np/kAheadEnvs workgroups twist each env's next MT
+// block ahead (mt_next, flagged kMtNextOk in U_MTPOS), so k_refill's 16-lane
+// groups draw windows that cross a block end from memory instead of leaving
+// the fast path for a wave-per-env draw with its twist (one in ~13 episodes).
+// An env whose draws ran into mt_next (index past 624) first gets it as its
+// current block. Needed by the envs that crossed or went through a wave draw
+// since the last refill (all of them after seeding); the rest are skipped.
+constexpr int kAheadEnvs = 8;
+// mt19937_gen of one block by one wave, from memory and in registers: word i
+// needs old[i], old[i+1] and old[i+397] (i < 227) or new[i-227], so lane l
+// forms the chains c, c+227, c+454 for c = l, l+64, l+128, l+192 (< 227) and
+// every dependency but word 623's (new[0], new[396]: two readlanes) stays in
+// the lane -- no LDS, no barriers. All loads complete before the first store,
+// so o may be n (the block made current is twisted in place); with `cur`, the
+// old block is also copied there.
+__device__ __forceinline__ void mt_twist_regs(const uint32_t* o, uint32_t* n, uint32_t* cur, int lane) {
+  constexpr int kD = kMtN - kMtM;  // 227
+  uint32_t a0[4], a1[4], a2[4], b0[4], b1[4], c0[4], c1[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int c = lane + kWave * k;
+    const bool ok = c < kD, okc = c < kMtN - 1 - 2 * kD;  // (c + 454 < 623)
+    a0[k] = ok ? o[c] : 0u;
+    a1[k] = ok ? o[c + 1] : 0u;
+    a2[k] = ok ? o[c + kMtM] : 0u;
+    b0[k] = ok ? o[c + kD] : 0u;
+    b1[k] = ok ? o[c + kD + 1] : 0u;
+    c0[k] = okc ? o[c + 2 * kD] : 0u;
+    c1[k] = okc ? o[c + 2 * kD + 1] : 0u;
+  }
+  const uint32_t last = o[kMtN - 1];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  uint32_t nb2 = 0u, na0 = 0u;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int c = lane + kWave * k;
+    if (c < kD) {
+      const uint32_t na = mt_mix(a0[k], a1[k], a2[k]);
+      const uint32_t nb = mt_mix(b0[k], b1[k], na);
+      n[c] = na;
+      n[c + kD] = nb;
+      if (cur) cur[c] = a0[k], cur[c + kD] = b0[k];
+      if (c < kMtN - 1 - 2 * kD) {
+        n[c + 2 * kD] = mt_mix(c0[k], c1[k], nb);
+        if (cur) cur[c + 2 * kD] = c0[k];
+      }
+      if (k == 0) na0 = na;
+      if (k == 2) nb2 = nb;
+    }
+  }
+  // word 623: mix(old[623], new[0], new[396]); new[396] = chain 169 = lane 41, k = 2
+  const uint32_t n0 = (uint32_t)__builtin_amdgcn_readlane((int)na0, 0);
+  const uint32_t n396 = (uint32_t)__builtin_amdgcn_readlane((int)nb2, kMtM - 1 - kD - 2 * kWave);
+  if (lane == 0) {
+    n[kMtN - 1] = mt_mix(last, n0, n396);
+    if (cur) cur[kMtN - 1] = last;
+  }
+}
+
+// The fit launch's first np/kAheadEnvs workgroups twist each env's next MT
+// block ahead (mt_next, flagged kMtNextOk in U_MTPOS), so k_refill's 16-lane
+// groups draw windows that cross a block end from memory instead of leaving
+// the fast path for a wave-per-env draw with its twist (one in ~13 episodes).
+// An env whose draws ran into mt_next (index past 624) first gets it as its
+// current block. Needed by the envs that crossed or went through a wave draw
+// since the last refill (all of them after seeding); the rest are skipped.
+__device__ __forceinline__ void mt_ahead(const SacenvBoatParams& p, const Arena& A, int b, int lane) {
+  const int e0 = b * kAheadEnvs;
+  int v = 0;
+  bool need = false;
+  if (lane < kAheadEnvs && e0 + lane < p.n_envs) {
+    v = A.i32(U_MTPOS)[e0 + lane];
+    need = (v & kMtNextOk) == 0 || (v & kMtPosMask) > kMtN;
+  }
+  unsigned long long m = __ballot(need);
+#pragma unroll 1
+  while (m != 0ull) {  // uniform
+    const int j = __ffsll((long long)m) - 1;
+    m &= m - 1ull;
+    const int e = e0 + j;
+    const int vj = __builtin_amdgcn_readlane(v, j);
+    const bool adv = (vj & kMtNextOk) != 0 && (vj & kMtPosMask) > kMtN;
+    uint32_t* const key = A.mt_key() + (int64_t)e * kMtN;
+    uint32_t* const nxt = A.mt_next() + (int64_t)e * kMtN;
+    mt_twist_regs(adv ? nxt : key, nxt, adv ? key : nullptr, lane);
+    if (lane == 0) A.i32(U_MTPOS)[e] = ((vj & kMtPosMask) - (adv ? kMtN : 0)) | kMtNextOk;
+  }
+}
+
 // GS lanes per (env, curve): 8 for up to 8 knots, else 16; one instantiation
 // per width, so the 8-knot launch carries no 16-knot registers
 template <int GS, bool kFull>
 __global__ void __launch_bounds__(kWave) k_refill_fit(SacenvBoatParams p, Arena A, Tail T) {
   const int lane = threadIdx.x;
+  const int ahead = (int)(A.np / kAheadEnvs);
+  if ((int)blockIdx.x < ahead) {
+    mt_ahead(p, A, (int)blockIdx.x, lane);
+    return;
+  }
+  const int fb = (int)blockIdx.x - ahead, fgrid = (int)gridDim.x - ahead;
   const int nc = p.use_wind_table ? 0 : n_curves(p.experiment);
   const int nk = kFull ? GS : p.n_knots;
   const int items = A.status()[2] * nc;  // (env, curve) groups
@@ -1385,7 +1498,7 @@ __global__ void __launch_bounds__(kWave) k_refill_fit(SacenvBoatParams p, Arena 
   const bool fst_ok = lane == 0 && (int64_t)(blockIdx.x + 1) * 16 <= 8 * A.np;
   if (fst_ok) fst[0] = st0, fst[1] = 0;
 #endif
-  if (items == 0 || (int)blockIdx.x * (kWave / GS) >= items) return;  // uniform
+  if (items == 0 || fb * (kWave / GS) >= items) return;  // uniform
   const int j = lane & (GS - 1);
   const int jj = j < nk ? j : nk - 1, j1 = jj + 1 < nk ? jj + 1 : jj;
   double gr[GS];
@@ -1394,7 +1507,7 @@ __global__ void __launch_bounds__(kWave) k_refill_fit(SacenvBoatParams p, Arena 
   IvGrid ig = interval_grid(p, j < nk - 1 ? j : 0);
   ig.valid = ig.valid && j < nk - 1;
   const int per = kWave / GS;
-  for (int base = blockIdx.x * per; base < items; base += gridDim.x * per) {
+  for (int base = fb * per; base < items; base += fgrid * per) {
     const int item = base + lane / GS;
     if (item >= items) break;
     fit_group<GS, kFull>(p, A, gr, ig, item, j, jj, j1, nc);
@@ -2891,7 +3004,9 @@ int sacenv_boat_refill(const SacenvBoatParams* p, void* arena, void* stream) {
   // that covers a typical refill in one pass (8 groups per block: 65 536
   // (episode, curve) items), grid-stride beyond it; blocks past the count exit
   // at once. Measured 0.12 us/step better than one block per owner wave.
-  constexpr int fit_blocks = 8192;
+  // (+ the twist-ahead workgroups first, np / kAheadEnvs: measured ahead of
+  // twisting in the fit blocks, before or after their fits)
+  const int fit_blocks = 8192 + (int)(A.np / kAheadEnvs);
   const Tail T = make_tail(*p, arena);
   if (p->n_knots == 8)
     hipLaunchKernelGGL((k_refill_fit<8, true>), dim3(fit_blocks), dim3(kWave), 0, (hipStream_t)stream, *p, A, T);

@@ -14,7 +14,7 @@ PKG_ROOT = _build.PKG_ROOT
 LIB_PATH = os.environ.get("SACENV_LIB", _build.LIB)
 LOADED_DIGEST = None  # source digest of the loaded library (the in-tree build)
 
-ABI_VERSION = 17
+ABI_VERSION = 18
 OBS_DIM = 11
 MT_N = 624
 MAX_KNOTS = 16
@@ -72,7 +72,7 @@ LAYOUT_FIELDS = (
     "refill_list",
     "wind_knots", "knots_raw", "mt_key", "record", "obs", "reward", "done", "term",
     "final_obs", "final_ep_reward", "accel", "reward64", "refill_mask", "status",
-    "spline_g", "wind_table", "last_term")
+    "spline_g", "wind_table", "last_term", "mt_next")
 
 
 class BoatLayout(C.Structure):

@@ -134,7 +134,7 @@ class BoatEnv:
             return
         torch.cuda.synchronize(self._vec.device)
         key = self._vec.mt_key[0].cpu().numpy().view(np.uint32).copy()
-        pos = int(self._vec.mt_pos[0].item())
+        pos = int(self._vec.mt_pos[0].item()) & 0xFFFF   # (bit 16: the refill's pre-twisted block)
         np.random.set_state((st[0], key, pos, st[3], st[4]))
 
     def _new_boat(self):

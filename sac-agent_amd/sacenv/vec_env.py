@@ -113,6 +113,8 @@ class VecBoatEnv:
         # the drawn knots per slot exist only with record_knots (SACENV_OUT_KNOTS)
         self.knots_raw_slots = view(L.knots_raw, f64, NP, _lib.SLOTS, 2, nk) if record_knots else None
         self.mt_key = view(L.mt_key, i32, NP, _lib.MT_N)[:N]
+        # the block after mt_key, twisted ahead by each refill (valid while mt_pos bit 16 is set)
+        self.mt_next = view(L.mt_next, i32, NP, _lib.MT_N)[:N]
         self.spline_g = view(L.spline_g, f64, nk, nk)
         # outputs: the packed record (the all-gather payload) and extras
         self.record = self.arena[L.record: L.record + RECORD_BYTES * NP]

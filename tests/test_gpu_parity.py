@@ -173,11 +173,42 @@ def test_rng_draws_bit_exact_across_many_resets(autoreset, gpu, built_lib):
         key = env.mt_key.cpu().numpy().view(np.uint32)
         for e, g in enumerate(rs):
             st = g.get_state()
-            pos = int(env.mt_pos[e])
+            pos = int(env.mt_pos[e]) & 0xFFFF
             if pos == st[2]:
                 assert np.array_equal(key[e], st[1])
             else:   # block exhausted: numpy twists lazily, the device may have already
                 assert pos == 0 and st[2] == 624
+
+
+def test_refill_twists_the_next_mt_block_ahead(gpu, built_lib):
+    """After every refill each env's mt_next is the block numpy's MT19937 generates after
+    mt_key (mt_pos bit 16 set, the index back inside the current block), including envs
+    whose draws ran past the block end into mt_next (the refill's draw launch reads on
+    there; its fit launch makes it current and twists the next). The draws themselves
+    are pinned by test_rng_draws_bit_exact_across_many_resets and the bench-path tests."""
+    from sacenv import VecBoatEnv
+    n = 512
+    env = VecBoatEnv({"base_settings": {"experiment": 6}}, n, seed=11, device=gpu, autoreset=True)
+    g = torch.Generator(device="cpu").manual_seed(3)
+    acts = (torch.rand(256, n, generator=g) * 2 - 1).to(gpu)
+    wrapped = 0
+    for seg in range(8):
+        p0 = env.mt_pos.clone() & 0xFFFF
+        env.segment_async(acts, 256)
+        env.refill()
+        torch.cuda.synchronize()
+        mp = env.mt_pos.clone()
+        pos = mp & 0xFFFF
+        assert bool(((mp >> 16) & 1).all()) and int(pos.max()) <= 624, seg
+        wrapped += int((pos < p0).sum())
+        key = env.mt_key.cpu().numpy().view(np.uint32)
+        nxt = env.mt_next.cpu().numpy().view(np.uint32)
+        for e in range(seg, n, 29):
+            rs = np.random.RandomState()
+            rs.set_state(("MT19937", key[e].copy(), 624, 0, 0.0))
+            rs.bytes(4)   # one word: numpy twists the block first
+            assert np.array_equal(rs.get_state()[1], nxt[e]), (seg, e)
+    assert wrapped > 0   # some envs' draws did cross into mt_next
 
 
 def test_spline_g_on_device(gpu, built_lib):

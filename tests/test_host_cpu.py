@@ -180,7 +180,7 @@ def test_arena_layout(built_lib, n, knots):
              "wind_coef": 64, "wind0_next": 16, "start_y_next": 4,
              "index": 4, "cons": 4, "fill": 4, "mt_pos": 4,
              "start_y": 4 * S, "counters": 20, "refill_list": 12, "wind_knots": 32 * S * nk,
-             "mt_key": 2496, "obs": 44, "reward": 4, "done": 1, "term": 1,
+             "mt_key": 2496, "mt_next": 2496, "obs": 44, "reward": 4, "done": 1, "term": 1,
              "final_obs": 44, "final_ep_reward": 8, "accel": 24, "reward64": 8, "last_term": 4}
     if knots:
         sizes["knots_raw"] = 16 * S * nk
@@ -202,7 +202,7 @@ def test_arena_layout(built_lib, n, knots):
     assert end <= L.total_bytes
     if n == 65536:   # per env: the wind slots dominate (<= 75 KB without recorded knots)
         per_env = (L.total_bytes - 16 * 10000) / n
-        assert per_env <= (103 * 1024 if knots else 70 * 1024), per_env
+        assert per_env <= (106 * 1024 if knots else 73 * 1024), per_env
 
 
 # ---------------------------------------------------------------- MT19937
