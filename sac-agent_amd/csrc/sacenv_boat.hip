@@ -1389,14 +1389,7 @@ __device__ __forceinline__ void fit_group(const SacenvBoatParams& p, const Arena
   }
 }
 
-// The fit launch's first np/kAheadEnvs workgroups twist each env's next MT
-// block ahead (mt_next, flagged kMtNextOk in U_MTPOS), so k_refill's 16-lane
-// groups draw windows that cross a block end from memory instead of leaving
-// the fast path for a wave-per-env draw with its twist (one in ~13 episodes).
-// An env whose draws ran into mt_next (index past 624) first gets it as its
-// current block. Needed by the envs that crossed or went through a wave draw
-// since the last refill (all of them after seeding); the rest are skipped.
-constexpr int kAheadEnvs = 8;
+constexpr int kAheadEnvs = 8;  // envs per twist-ahead workgroup of the fit launch (mt_ahead)
 // mt19937_gen of one block by one wave, from memory and in registers: word i
 // needs old[i], old[i+1] and old[i+397] (i < 227) or new[i-227], so lane l
 // forms the chains c, c+227, c+454 for c = l, l+64, l+128, l+192 (< 227) and
@@ -1459,7 +1452,8 @@ __device__ __forceinline__ void mt_ahead(const SacenvBoatParams& p, const Arena&
   const int e0 = b * kAheadEnvs;
   int v = 0;
   bool need = false;
-  if (lane < kAheadEnvs && e0 + lane < p.n_envs) {
+  // (past 8 knots every draw is a wave draw, which withdraws mt_next: nothing to gain)
+  if (lane < kAheadEnvs && e0 + lane < p.n_envs && p.n_knots <= 8) {
     v = A.i32(U_MTPOS)[e0 + lane];
     need = (v & kMtNextOk) == 0 || (v & kMtPosMask) > kMtN;
   }
