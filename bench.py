@@ -106,6 +106,22 @@ def parse(argv=None):
                          "segments, one SUM all-reduce of the segment's learn() batches (StagedReplay; the "
                          "all-gather rate is measured beside it); gather = all-gather every transition per "
                          "256-step segment (configs[3]'s literal exchange); none = no exchange")
+    ap.add_argument("--sampler", choices=("philox", "mt"), default="philox",
+                    help="the staged replay's index draws: philox = counter-based (np.random.choice's "
+                         "distribution per learn, every draw independent: one parallel launch per segment); "
+                         "mt = the reference stream's exact draws (one MT19937 chain per segment)")
+    ap.add_argument("--exchange", choices=("allgather", "allreduce"), default="allgather",
+                    help="N>1 --pooling sharded: allgather = each rank's own sampled rows packed with their "
+                         "slots, one all_gather of the chunks; allreduce = one SUM all-reduce of the "
+                         "1/N-dense batches (twice the bytes per rank)")
+    ap.add_argument("--channels", type=int, default=16,
+                    help="RCCL channel cap for N>1 (NCCL_MAX_NCHANNELS unless set): the collective's "
+                         "workgroups sharing CUs with the segment launch; also the stand-in's workgroups")
+    ap.add_argument("--standin-gbps", type=float, default=250.0,
+                    help="N=1 collective stand-in: the per-rank rate its transfer is modelled at (it stays "
+                         "resident for bytes / rate)")
+    ap.add_argument("--standin-world", type=int, default=8,
+                    help="N=1 collective stand-in: the world size whose per-rank traffic it moves")
     ap.add_argument("--replay-mem", type=int, default=1_000_000,
                     help="pooled ReplayBuffer(max_size) (configs/original_config.yaml: 1 000 000)")
     ap.add_argument("--replay-batch", type=int, default=1024, help="learn() batch (agent.batch_size: 1024)")
@@ -114,9 +130,6 @@ def parse(argv=None):
     ap.add_argument("--stub", action="store_true",
                     help="CPU control-flow rehearsal: a stub workload, no kernels (tools/bench_stub.py); "
                          "the line says data: stub")
-    ap.add_argument("--refill-overlap", type=int, default=0, choices=(0, 1),
-                    help="--launch segment: two 64-step launches per segment, each refill on a side "
-                         "stream concurrent with the next launch (1), or the refill between launches (0)")
     ap.add_argument("--pool-every", type=int, default=SEG,
                     help="N>1 gather pooling: steps per all-gather (1 = one all-gather per step, "
                          "SURVEY.md §8(e); 256 = one per segment, overlapped with the next)")
@@ -142,6 +155,10 @@ MIN_TIMED_SEGS = 8   # the timed region holds at least 2 048 steps (VERDICT r3 n
 MIN_TIMED_SECONDS = 1.0  # and lasts at least ~1 s (whole segments, sized from the warm-up's rate), so
                          # an outside sampler of GPU activity sees the timed phase
                          # (--min-seconds)
+TIMED_MARGIN = 1.15  # segments for 1.15 x --min-seconds at the warm-up's post-boost rate: the timed region
+                     # lasts >= --min-seconds (round 5 sized it from the whole warm-up, pre-boost, and
+                     # timed 0.83 s)
+WARM_BOOST_SEGS = 24  # GPU warm-up: the clock boosts after ~20 launches
 MIN_WARMUP_SEGS = 2  # and at least 512 warm-up steps: the driver's --steps 20 --warmup 5 then
                      # times the default line's region (the episode-length transient of the
                      # first ~1 000 steps -- every env starts at step 0 -- is behind it)
@@ -165,7 +182,7 @@ def timed_segs(n_steps: int) -> int:
 
 
 # ---------------------------------------------------------------- distributed
-def init_dist(n_gpus: int, stub: bool = False):
+def init_dist(n_gpus: int, stub: bool = False, channels: int = 16):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -183,6 +200,9 @@ def init_dist(n_gpus: int, stub: bool = False):
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         backend = "gloo" if stub else os.environ.get("SACENV_BENCH_BACKEND", "nccl")  # gloo: rehearsal
         if backend == "nccl":
+            # the collective's workgroups share CUs with the persistent segment launch's owner
+            # waves (one per SIMD): cap its channels (read by RCCL at communicator creation)
+            os.environ.setdefault("NCCL_MAX_NCHANNELS", str(int(channels)))
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
@@ -257,7 +277,8 @@ def dist_info(world: int, dev) -> dict | None:
         except Exception as exc:  # noqa: BLE001
             ver = f"unavailable: {exc}"
     return {"world_size": world, "backend": "RCCL (nccl)" if backend == "nccl" else backend,
-            "rccl_version": ver, "ranks": ranks}
+            "rccl_version": ver, "rccl_max_channels": os.environ.get("NCCL_MAX_NCHANNELS") if backend == "nccl"
+            else None, "ranks": ranks}
 
 
 def barrier(world):
@@ -561,16 +582,6 @@ class SegmentRunner:
                                  and (pool is None or pool_every == SEG))
                      else "eager")
         self.use_graph = self.mode == "graph"
-        # segment mode, refill overlap: launches of HALF steps; the refill after
-        # launch h runs on a side stream concurrently with launch h+1 and must be
-        # done before launch h+2. Safe with the 129-slot ring: launch h+1 reads
-        # episodes <= cons_h + 64 < the fill of the refill before (cons + 129),
-        # and the refill draws from the cons snapshot k_need_masks took.
-        self.overlap = (self.mode == "segment" and bool(getattr(args, "refill_overlap", 0))
-                        and pool is None)
-        if self.overlap:
-            self.rs = torch.cuda.Stream(device=dev, priority=0)
-            self.refill_done = [None, None]   # events of the last two refills (h-1, h-2)
         self.st = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
         self.graphs = None
         self.first_replays = 0
@@ -585,33 +596,6 @@ class SegmentRunner:
 
     def _clock_pair(self):
         return self._clocks.pop() if self._clocks else (_Clock(self.dev), _Clock(self.dev))
-
-    def _launch_overlapped(self, k0: int, n: int, timed: bool = False) -> None:
-        """One persistent launch of n steps, its refill on the side stream."""
-        wl, st, rs = self.wl, self.st, self.rs
-        ev = self.refill_done[1]          # the refill after launch h-2
-        if ev is not None:
-            st.wait_event(ev)
-        if timed:  # the launch alone (not the wait before it)
-            ea, eb = self._clock_pair()
-            ea.record(st)
-        wl.segment_step(k0, n)
-        if timed:
-            eb.record(st)
-            self.seg_events.append((ea, eb, n))
-        rs.wait_stream(st)
-        with torch.cuda.stream(rs):
-            wl.refill()
-            done = torch.cuda.Event()
-            done.record(rs)
-        self.refill_done = [done, self.refill_done[0]]
-
-    def drain_refills(self) -> None:
-        """The stepping stream waits for every refill in flight (overlap mode)."""
-        if self.overlap:
-            for ev in self.refill_done:
-                if ev is not None:
-                    self.st.wait_event(ev)
 
     def _steps(self, k0: int, with_pool: bool, buf=None, on_step=None, timed: bool = False) -> None:
         """The SEG steps of one segment, enqueued (captured, eager or persistent)."""
@@ -629,10 +613,6 @@ class SegmentRunner:
                     on_step(k)
             return
         if self.mode == "segment":
-            if p is None and self.overlap:
-                for j0 in range(0, SEG, SEG // 2):
-                    self._launch_overlapped(k0 + j0, SEG // 2, timed)
-                return
             if p is None:
                 wl.segment_step(k0, SEG)
                 return
@@ -687,13 +667,9 @@ class SegmentRunner:
             wl.segment_step(0, 3)
             wl.refill()
             for base in range(0, ACTION_STEPS, SEG):
-                if self.overlap:
-                    self._steps(base, False)
-                else:
-                    wl.segment_step(base, SEG)
-                    wl.refill()
+                wl.segment_step(base, SEG)
+                wl.refill()
                 self.first_replays += SEG
-            self.drain_refills()
             _sync(dev)
             return
         if self.use_graph:
@@ -728,12 +704,11 @@ class SegmentRunner:
 
     def finish(self) -> None:
         """The stepping stream waits for everything a segment left in flight (the last
-        all-gathers / replay exchanges, overlapped refills)."""
+        all-gathers / replay exchanges)."""
         if self.pool is not None:
             self.pool.wait()
         if self.exchange is not None:
             self.exchange.wait()
-        self.drain_refills()
 
     def segment(self, k0: int, timed: bool = False, with_pool: bool = True, on_step=None) -> int:
         """Steps k0 .. k0+SEG-1 (k0 % SEG == 0), then the refill, then the pooling
@@ -750,7 +725,7 @@ class SegmentRunner:
             buf = p.buf
         else:
             buf = None
-        own = timed and not (self.overlap and p is None)  # overlap: events per launch
+        own = timed
         if timed:  # every event_every-th timed segment (the first always)
             own = own and self.timed_segments % self.event_every == 0
             self.timed_segments += 1
@@ -765,8 +740,7 @@ class SegmentRunner:
         if own:
             eb.record(self.st)
             self.seg_events.append((ea, eb, SEG))
-        if not self.overlap:
-            self.wl.refill()
+        self.wl.refill()
         if p is not None and self.pool_every == SEG:
             p.fill = SEG
             p.flush()
@@ -785,22 +759,41 @@ def _max_over_ranks(x: float, world: int, dev) -> float:
     return float(t.item())
 
 
-def make_exchange(args, wl: Workload, rank: int, world: int, dev):
+def make_exchange(args, wl: Workload, rank: int, world: int, dev, standin: dict | None = None):
     """The sharded pooling's replay exchange: a StagedReplay over this rank's envs (the
     pooled ReplayBuffer(--replay-mem) of every rank's envs, one learn() of
-    --replay-batch per step) behind a SegmentExchange (its side stream)."""
+    --replay-batch per step; --sampler, --exchange) behind a SegmentExchange (its side
+    stream). ``standin`` (N=1): the collective's kernel stood in for (StagedReplay)."""
     from sacenv.dist import SegmentExchange
     if args.stub:
         sys.path.insert(0, os.path.join(ROOT, "tools"))
         from bench_stub import StubSampler
-        sampler = StubSampler(wl.row_bytes(), SEG, args.replay_batch, world)
+        sampler = StubSampler(wl.row_bytes(), SEG, args.replay_batch, world, exchange=args.exchange)
     else:
         from sacenv.replay import StagedReplay
         env = wl.envs[0]
         sampler = StagedReplay(env.num_envs, env.n_pad, args.experiment, env.first_obs_template(), rank=rank,
                                world=world, mem_size=args.replay_mem, batch=args.replay_batch, seg=SEG, seed=0,
-                               device=dev)
+                               device=dev, sampler=args.sampler, exchange=args.exchange, standin=standin)
     return SegmentExchange(sampler, dev)
+
+
+def collective_standin(args, wl: Workload) -> dict:
+    """The N=1 stand-in for the N>1 line's collective kernel: the bytes
+    one rank moves per segment at --standin-world ranks (the all-gather's (W-1) chunks, or
+    the ring all-reduce's 2 (W-1)/W payload), on --channels workgroups, resident for
+    bytes / --standin-gbps."""
+    W = max(2, int(args.standin_world))
+    env = wl.envs[0]
+    if args.exchange == "allgather":
+        from sacenv.replay import staged_chunk
+        _, chunk = staged_chunk(env.num_envs, env.n_pad, W, args.replay_mem, args.replay_batch, SEG,
+                                args.experiment)
+        nbytes = (W - 1) * chunk
+    else:
+        nbytes = 2 * (W - 1) / W * SEG * args.replay_batch * 26 * 4
+    us = nbytes / (args.standin_gbps * 1e9) * 1e6
+    return {"bytes": int(nbytes), "workgroups": int(args.channels), "us": us, "world": W}
 
 
 def timed_rate(run: "SegmentRunner", k: int, n_segs: int, world: int, dev, wl: Workload):
@@ -818,6 +811,8 @@ def timed_rate(run: "SegmentRunner", k: int, n_segs: int, world: int, dev, wl: W
     _sync(dev)
     barrier(world)
     el = _max_over_ranks(time.perf_counter() - t0, world, dev)
+    if run.exchange is not None:
+        run.exchange.check()
     steps = n_segs * SEG
     return ({"value": world * wl.per_gpu_envs * steps / el, "unit": "env-steps/s", "steps": steps,
              "ms_per_step": el / steps * 1e3}, k, el)
@@ -831,6 +826,21 @@ def _xgmi(bytes_per_rank: float, seconds: float, links: int) -> dict:
             "per_link_GBps": per_link, "per_link_frac": per_link / XGMI_LINK_GBPS}
 
 
+def pooling_mode(args, world: int, wl: Workload) -> str:
+    """The N>1 exchange this run can time: --pooling, except that the staged replay
+    (sharded) needs the persistent segment launch -- it writes the staged rows -- and a
+    boat-only workload; otherwise every transition is all-gathered (the
+    sharded exchange under --launch step / --no-graph read rows no launch wrote). The
+    CPU stub's sampler takes rows from any runner mode."""
+    pooling = args.pooling if world > 1 else "none"
+    if pooling == "sharded" and (args.mixed or not wl.segment_pools):
+        return "gather"   # the toys of the mixed batch have no staged replay: their rows are gathered
+    if pooling == "sharded" and not args.stub and (args.launch != "segment" or args.no_graph
+                                                   or wl.segment_step is None):
+        return "gather"
+    return pooling
+
+
 def run_bench(args, rank: int, world: int, dev, wl: Workload):
     """Warm up, time whole segments, measure the kernel; rank 0 returns the JSON dict.
 
@@ -842,9 +852,7 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
     exchange at all. N=1: the replay path without a collective is measured the same
     way (``replay_path``), so the per-GPU cost of the exchange is on the N=1 line."""
     pool_every = int(getattr(args, "pool_every", SEG))
-    pooling = args.pooling if world > 1 else "none"
-    if pooling == "sharded" and (args.mixed or not wl.segment_pools):
-        pooling = "gather"   # the toys of the mixed batch have no staged replay: their rows are gathered
+    pooling = pooling_mode(args, world, wl)
     pool = exchange = None
     if pooling == "gather":
         from sacenv.dist import SegmentPool
@@ -861,16 +869,23 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
     seg_events = run.seg_events
     segment = run.segment
     n_warm, n_timed = warm_segs(args.warmup), timed_segs(args.steps)
+    if dev.type == "cuda":  # past the clock boost (~20 launches) before the rate is sized
+        n_warm = max(n_warm, WARM_BOOST_SEGS)
     k = 0
+    half = n_warm // 2
     t_w = time.perf_counter()
-    for _ in range(n_warm):
+    for i in range(n_warm):
+        if i == half:  # the rate of the warm-up's second half: after the boost
+            run.finish()
+            _sync(dev)
+            t_w = time.perf_counter()
         k = segment(k, False)
     run.finish()
     _sync(dev)
-    per_seg = (time.perf_counter() - t_w) / n_warm
+    per_seg = (time.perf_counter() - t_w) / (n_warm - half)
     if dev.type == "cuda":  # (CPU stub runs measure the harness: no minimum duration)
-        n_timed = int(_max_over_ranks(float(max(n_timed, math.ceil(args.min_seconds / max(per_seg, 1e-6)))),
-                                      world, dev))
+        want = math.ceil(args.min_seconds * TIMED_MARGIN / max(per_seg, 1e-6))
+        n_timed = int(_max_over_ranks(float(max(n_timed, want)), world, dev))
     barrier(world)
     _sync(dev)
     ev0, ev1 = _Clock(dev), _Clock(dev)
@@ -890,6 +905,8 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
     el = time.perf_counter() - t0
     steps = n_timed * SEG
     el_max = _max_over_ranks(el, world, dev)
+    if exchange is not None:  # (after the timed region: it synchronises)
+        exchange.check()
 
     # the kernel's average launch duration from events on the stream it runs on,
     # refills excluded. N=1: the launches of the timed region itself. N>1 (the
@@ -945,7 +962,7 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
     kern_s = sum(a.ms_to(b) for a, b, _ in seg_events) * 1e-3 / sum(n for _, _, n in seg_events)
     step_s = ev0.ms_to(ev1) * 1e-3 / steps
 
-    every = replay_path = None
+    every = replay_path = standin_path = None
     if (world == 1 and run.mode == "segment" and not args.mixed and not args.no_autoreset
             and not args.no_every_output):
         every = every_output_rate(wl, dev, k0=k)
@@ -953,14 +970,30 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
             run.mode == "segment" or args.stub):
         # the sharded pooling's replay path on one GPU (no collective): rows staged, the
         # segment's learns sampled on a side stream overlapped with the next segment
+        n_x = max(1, args.exchange_segs)
         xrun = SegmentRunner(args, wl, dev, None, SEG, make_exchange(args, wl, rank, 1, dev))
-        rate, k, _ = timed_rate(xrun, k, max(1, args.exchange_segs), world, dev, wl)
-        replay_path = dict(rate, note=(
+        rate, k, _ = timed_rate(xrun, k, n_x, world, dev, wl)
+        replay_path = dict(rate, sampler=args.sampler, exchange=args.exchange, note=(
             f"the N>1 line's replay path at one GPU (--pooling sharded without the collective): each "
-            f"segment's {SEG} learn() batches of {args.replay_batch} drawn ahead from the pooled "
-            f"ReplayBuffer({args.replay_mem})'s sampling stream, the segment launch writing the 64-B rows they "
-            "read, the batches gathered on a side stream overlapped with the next segment (StagedReplay), "
-            "after the timed region, wall time"))
+            f"segment's {SEG} learn() batches of {args.replay_batch} drawn ahead ("
+            + ("counter-based: Philox4x64-10, np.random.choice's distribution per learn, one parallel "
+               "launch that also marks the rows" if args.sampler == "philox" else
+               "the pooled buffer's MT19937 stream, exact") +
+            f") from the pooled ReplayBuffer({args.replay_mem}), the segment launch writing the 64-B rows they "
+            "read, the batches " + ("packed per rank and unpacked (the all-gather's two kernels)"
+                                    if args.exchange == "allgather" else "gathered") +
+            " on a side stream overlapped with the next segment (StagedReplay), after the timed region, "
+            "wall time"))
+        if not args.stub:
+            sd = collective_standin(args, wl)
+            srun = SegmentRunner(args, wl, dev, None, SEG, make_exchange(args, wl, rank, 1, dev, standin=sd))
+            rate, k, _ = timed_rate(srun, k, n_x, world, dev, wl)
+            standin_path = dict(rate, standin=sd, frac_of_replay_path=rate["value"] / replay_path["value"], note=(
+                f"replay_path with the collective's kernel stood in for: between the pack and the unpack, "
+                f"{sd['workgroups']} workgroups (the RCCL channel cap the N>1 line sets, NCCL_MAX_NCHANNELS) copy "
+                f"the {sd['bytes']} B one rank moves per segment at {sd['world']} ranks and stay resident for "
+                f"{sd['us']:.1f} us (those bytes at {args.standin_gbps:g} GB/s per rank), on the side stream "
+                "beside the next segment's owner waves; no xGMI traffic"))
     dinfo = dist_info(world, dev)
     if rank != 0:
         return None
@@ -983,11 +1016,17 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
         backend = "RCCL" if dist.get_backend() == "nccl" else dist.get_backend()
     if exchange is not None:
         payload = exchange.sampler.bytes_per_segment
-        collective = (f"{backend} SUM all_reduce of each {SEG}-step segment's {SEG} learn() batches ({args.replay_batch} "
-                      f"rows, {payload} B) of the pooled ReplayBuffer({args.replay_mem}) of every rank's envs, "
+        what_x = (f"{backend} all_gather of each rank's packed rows of each {SEG}-step segment's {SEG} learn() "
+                  f"batches ({args.replay_batch} rows; {payload} B gathered: 100-B records with their slot, "
+                  "unpacked into the batches on every rank)" if args.exchange == "allgather" else
+                  f"{backend} SUM all_reduce of each {SEG}-step segment's {SEG} learn() batches ({args.replay_batch} "
+                  f"rows, {payload} B)")
+        collective = (f"{what_x} of the pooled ReplayBuffer({args.replay_mem}) of every rank's envs, "
                       "gathered from the rows each rank's segment launch staged (sacenv.replay.StagedReplay: the "
-                      "index draws made ahead, only the rows they read written; the pooled buffer's batches bit "
-                      f"for bit): one per segment on a side stream, overlapped with the next segment "
+                      "index draws made ahead, only the rows they read written; "
+                      + ("counter-based draws (Philox4x64-10, np.random.choice's distribution per learn)"
+                         if args.sampler == "philox" else "the reference stream's exact draws (MT19937)") +
+                      f"): one per segment on a side stream, overlapped with the next segment "
                       f"({exchanges_timed} in the timed region)")
     elif pool is not None:
         collective = (f"all_gather of each step's full transitions (the {TRANS_ROW} written by the step kernel, "
@@ -1002,11 +1041,11 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
         pooling_out = {"mode": pooling, "no_exchange": no_exchange}
         if exchange is not None:
             payload = exchange.sampler.bytes_per_segment
-            bus = 2 * (world - 1) / world * payload * exchanges_timed  # a ring all-reduce's bytes per rank
+            bus = exchange.sampler.bus_bytes_per_segment * exchanges_timed  # a ring schedule's bytes per rank
             pooling_out.update({
                 "exchanges_timed": exchanges_timed, "bytes_per_segment": payload,
-                "staged_row_bytes": 64,
-                "allreduce_bus_bytes_per_rank": bus, "xgmi": _xgmi(bus, el_max, world - 1),
+                "staged_row_bytes": 64, "sampler": args.sampler, "exchange": args.exchange,
+                "bus_bytes_per_rank": bus, "xgmi": _xgmi(bus, el_max, world - 1),
                 "all_gather": all_gather,
                 "note": "value = the timed region with this exchange; all_gather and no_exchange are the same "
                         "segments with the other exchanges, after the timed region"})
@@ -1049,9 +1088,7 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
                    "global_envs": world * wl.per_gpu_envs,
                    "episode_steps": args.episode_steps, "parallelism": f"env-dp{world}",
                    "collective": collective,
-                   "launch": ((f"two persistent sacenv_boat_segment launches of {SEG // 2} steps per {SEG}-step "
-                               "segment" if run.overlap else
-                               f"one persistent sacenv_mixed_segment launch per {SEG} steps (the boat's owner "
+                   "launch": ((f"one persistent sacenv_mixed_segment launch per {SEG} steps (the boat's owner "
                                "waves and every toy wave, state in registers)" if args.mixed else
                                f"one persistent sacenv_boat_segment launch per {SEG} steps") +
                               " (k_rollout: the carried state in registers; each owner wave checks its "
@@ -1067,9 +1104,6 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
                                 " (+ the pooled-row copies per step)" if pool is not None else "") +
                                " + the 3 refill launches" if use_graph else "eager")),
                    "refill": None if args.no_autoreset else (
-                       f"k_need_masks + k_refill + k_refill_fit after every {SEG // 2}-step launch on a side "
-                       "stream, concurrent with the next launch and done before the one after, inside the "
-                       "timed region" if run.overlap else
                        f"k_need_masks + k_refill + k_refill_fit after every {SEG}-step segment, inside the "
                        "timed region")},
         "roofline": {"bound": "fp64-issue" if compute is not None else "hbm",
@@ -1119,6 +1153,7 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
                                  "instruction issue (one owner wave per SIMD), not by HBM"}},
         "every_output": every,
         "replay_path": replay_path,
+        "replay_path_collective_standin": standin_path,
         "cpu_baseline": None,
         "dist": dinfo,
         "pooling": pooling_out,
@@ -1433,7 +1468,7 @@ def main(argv=None):
         # before anything touches the GPU: the C1 legs are child processes, and an
         # idle host keeps them from competing with the timed region's launches
         cpu = cpu_baseline(args, args.mixed_envs if args.mixed else args.envs)
-    rank, world, dev = init_dist(args.gpus, args.stub)
+    rank, world, dev = init_dist(args.gpus, args.stub, args.channels)
     if args.stub:
         sys.path.insert(0, os.path.join(ROOT, "tools"))
         import bench_stub

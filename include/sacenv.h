@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SACENV_ABI_VERSION 18
+#define SACENV_ABI_VERSION 19
 #define SACENV_OBS_DIM 11      /* Boat.return_state, boat_env.py:308-323 */
 #define SACENV_MT_N 624        /* MT19937 words per env (numpy legacy RNG) */
 #define SACENV_MAX_KNOTS 16    /* wind.fixed_points upper bound */
@@ -296,7 +296,8 @@ int sacenv_boat_rollout(const SacenvBoatParams *p, void *arena, const float *act
  * action f32, u32 term | last_term << 8 (last_term: layout.last_term after the
  * step), obs3_next f32 (experiment 2), 0 -- written only where bit e % 64 of
  * stage_marks[ks * n_pad / 64 + e / 64] is set (sacenv_replay_stage_mark: the rows
- * a learn will sample; stage_marks == NULL: every row). Counts as n_steps step
+ * a learn will sample; stage_marks == NULL: every row; with stage_marks, n_steps <=
+ * SACENV_REFILL_PERIOD in any mode, else SACENV_E_SIZE). Counts as n_steps step
  * launches for the refill contract (autoreset: n_steps <= SACENV_REFILL_PERIOD). */
 int sacenv_boat_segment(const SacenvBoatParams *p, void *arena, const float *actions, int64_t action_stride,
                         int32_t n_steps, const uint32_t *act_ready, uint32_t *step_done, uint32_t seq0,
@@ -568,6 +569,56 @@ int sacenv_replay_stage_mark(const SacenvReplayParams *p, const SacenvStagedPara
 int sacenv_replay_sample_staged(const SacenvReplayParams *p, const SacenvStagedParams *sp, int64_t g,
                                 const void *stage_cur, const void *stage_prev, const int64_t *idx, int32_t batch,
                                 int32_t n_batches, uint32_t *words, void *stream);
+
+/* The rows of a replay arena at given indices (idx: i64 [batch], device): the
+ * gather half of sacenv_replay_sample (buffer.py:28-33) without the draw; an
+ * index outside [0, mem_size) gives zero bits. Any output may be NULL. */
+int sacenv_replay_gather(const SacenvReplayParams *p, void *arena, int32_t batch, const int64_t *idx,
+                         float *state, float *action, double *reward, float *new_state, uint8_t *terminal,
+                         void *stream);
+
+/* The COUNTER-BASED sampler of the staged replay (round 6): the
+ * draws of sacenv_replay_stage_draw with the same distribution per learn --
+ * np.random.choice(min(c_k, mem_size), batch): uniform with replacement over
+ * the rows stored, learns with c_k < batch skipped (idx -1) -- from
+ * Philox4x64-10 (numpy's np.random.Philox generator function) instead of one
+ * MT19937 stream: draw i of global learn L = g*seg + k is the first of the
+ * four 64-bit words of Philox4x64-10(counter (i, L, j, 0), key (seed, 0)),
+ * j = 0, 1, ..., whose bits under numpy's mask (the smallest 2^b - 1 >= range
+ * - 1) are <= range - 1. Every draw is independent, so a segment's draws are
+ * one parallel launch with no sequential chain, in any order, for any g. The
+ * same thread marks the rows it draws on this rank and their predecessors:
+ * rows of segment g in marks_cur, of segment g - 1 in marks_prev (u64
+ * [seg][n_pad/64] each, nullable, NOT cleared: the caller clears a segment's
+ * marks before the first draw that marks it). Drawing segments g and g + 1
+ * completes segment g's marks (sacenv_replay_stage_mark's set). */
+int sacenv_replay_stage_draw_ctr(const SacenvReplayParams *p, const SacenvStagedParams *sp, int64_t g,
+                                 int32_t batch, int32_t n_batches, uint64_t seed, int64_t *idx,
+                                 uint64_t *marks_prev, uint64_t *marks_cur, void *stream);
+/* The ALL-GATHER form of the staged exchange. stage_chunk: the record capacity
+ * of one rank's chunk (the most records any rank packs in expectation over any
+ * segment + 8 standard deviations + 64; every slot at one rank) and the chunk's
+ * bytes (a 16-B header, 100 B per record, 256-B multiple). stage_pack: this
+ * rank's rows of segment g's learns (as sacenv_replay_sample_staged reads
+ * them) as 25-word records -- slot (learn x batch + draw) | terminal << 31,
+ * reward f32, state [11], new_state [11], action -- behind the count; rank 0
+ * (offset 0) also packs the skipped learns' all-zero rows. stage_unpack: the
+ * world chunks of an all-gather (rank r's at r x chunk_bytes) into
+ * sacenv_replay_sample_staged's words, bit for bit; a count above cap sets
+ * bit 0 of *status_word (device i32). */
+int sacenv_replay_stage_chunk(const SacenvReplayParams *p, const SacenvStagedParams *sp, int32_t batch,
+                              int32_t n_batches, int64_t *cap_rows, int64_t *chunk_bytes);
+int sacenv_replay_stage_pack(const SacenvReplayParams *p, const SacenvStagedParams *sp, int64_t g,
+                             const void *stage_cur, const void *stage_prev, const int64_t *idx, int32_t batch,
+                             int32_t n_batches, int64_t cap, void *chunk, void *stream);
+int sacenv_replay_stage_unpack(int32_t world, int64_t chunk_bytes, int64_t cap, int32_t batch, int32_t n_batches,
+                               const void *gathered, uint32_t *words, int32_t *status_word, void *stream);
+/* A collective's kernel stood in for on one GPU (bench.py's N = 1 replay path):
+ * `workgroups` workgroups of 256 threads copy `bytes` (16-B multiple, aligned)
+ * from src to dst and stay resident until min_us have passed since each
+ * started (<= 1e5). No reference counterpart. */
+int sacenv_copy_standin(const void *src, void *dst, int64_t bytes, int32_t workgroups, double min_us,
+                        void *stream);
 
 /* ------------------------------------------------------------------------
  * SAC agent on the device: the batched

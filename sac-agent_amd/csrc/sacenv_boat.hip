@@ -2924,6 +2924,9 @@ int sacenv_boat_segment(const SacenvBoatParams* p, void* arena, const float* act
     return SACENV_E_RANGE;  // float4 row stores
   if (stage != nullptr && (trans != nullptr || (reinterpret_cast<uintptr_t>(stage) & 15u) != 0u))
     return SACENV_E_RANGE;  // one kind of rows per launch; float4 stores
+  // the marks are staged into the wave's LDS (OwnerLds::mk: one word per step, REFILL_PERIOD
+  // entries), whatever the autoreset setting
+  if (stage_marks != nullptr && n_steps > SACENV_REFILL_PERIOD) return SACENV_E_SIZE;
   const Arena A = make_arena(*p, arena);
   RollArgs ra{};
   ra.rec = static_cast<char*>(arena) + A_ur_bytes(*p);

@@ -174,17 +174,18 @@ __global__ void __launch_bounds__(256) k_rb_gather(SacenvReplayParams p, RB r, i
   const int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int64_t nd = (int64_t)batch * D, na = (int64_t)batch * A;
   const int64_t cnt = *r.cntr(), M = p.mem_size;
+  // (an index outside the ring -- a caller's, sacenv_replay_gather -- reads nothing: zero bits)
   if (q < nd) {
     const int64_t i = q / D, k = q - i * D, row = idx[i];
-    const bool own = owns(sh, cnt, M, row);
+    const bool own = row >= 0 && row < M && owns(sh, cnt, M, row);
     if (st) st[q] = own ? r.state()[row * D + k] : 0.f;
     if (ns) ns[q] = own ? r.new_state()[row * D + k] : 0.f;
   } else if (q < nd + na) {
     const int64_t qq = q - nd, i = qq / A, k = qq - i * A, row = idx[i];
-    if (ac) ac[qq] = owns(sh, cnt, M, row) ? r.action()[row * A + k] : 0.f;
+    if (ac) ac[qq] = row >= 0 && row < M && owns(sh, cnt, M, row) ? r.action()[row * A + k] : 0.f;
   } else if (q < nd + na + batch) {
     const int64_t i = q - nd - na, row = idx[i];
-    const bool own = owns(sh, cnt, M, row);
+    const bool own = row >= 0 && row < M && owns(sh, cnt, M, row);
     if (rw) rw[i] = own ? r.reward()[row] : 0.0;
     if (tm) tm[i] = own ? r.terminal()[row] : (uint8_t)0;
   }
@@ -260,8 +261,12 @@ __global__ void __launch_bounds__(kDrawThreads) k_rb_draw_many(SacenvReplayParam
   __shared__ int s_end;
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
   constexpr int kWaves = kDrawThreads / kWave;
-  for (int i = tid; i < kMtN; i += kDrawThreads) blk[0][i] = r.key()[i];
   int cur = 0, pos = *r.pos();
+  if (pos < 0) {  // a poisoned stream (a staged draw ran short): draw nothing, keep the poison
+    for (int64_t i = tid; i < (int64_t)nb * batch; i += kDrawThreads) idx[i] = -1;
+    return;
+  }
+  for (int i = tid; i < kMtN; i += kDrawThreads) blk[0][i] = r.key()[i];
   bool advanced = false;
   __syncthreads();
   int k = 0, filled = 0;
@@ -348,8 +353,9 @@ __global__ void __launch_bounds__(kChainThreads) k_mt_chain(RB r, uint32_t* __re
   const int pos = *r.pos();
   if (l == 0) {
     ctrl[2] = 0;                          // no shortfall yet
-    ctrl[3] = pos >= kMtN ? 0 : pos;      // p0: the next word's position in block 0
+    ctrl[3] = pos >= kMtN ? 0 : pos;      // p0: the next word's position in block 0 (-1: poisoned)
   }
+  if (pos < 0) return;  // a poisoned stream: nothing generated, the draws below draw nothing
   for (int i = l; i < kMtN; i += kChainThreads) {
     const uint32_t v = r.key()[i];
     buf[0][i] = v;
@@ -417,6 +423,10 @@ __global__ void __launch_bounds__(kTileThreads) k_draw_count(DrawPlan d, int64_t
   plan_start(d, n_blocks);
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
   const int64_t t0 = (int64_t)blockIdx.x * kTile;
+  if (d.p0 < 0) {  // a poisoned stream: no words (the scan then finds too few, the emit draws nothing)
+    if (tid == 0) d.tile_cnt[blockIdx.x] = 0;
+    return;
+  }
   int c = 0;
 #pragma unroll
   for (int q = 0; q < kTile / kTileThreads; ++q) {
@@ -617,6 +627,212 @@ __global__ void __launch_bounds__(256) k_rb_gather_staged(SacenvReplayParams p, 
   }
   W[2 * batch + 2 * (int64_t)batch * D + i] = __float_as_uint(sn[12]);
   W[2 * batch + 2 * (int64_t)batch * D + batch + i] = tm;
+}
+
+// ---------------------------------------------------------------------------
+// The counter-based sampler (sacenv_replay_stage_draw_ctr). Each learn still
+// samples np.random.choice(min(c, M), batch)'s distribution -- `batch` rows
+// uniform with replacement over the rows stored -- but from Philox4x64-10
+// (Salmon, Moraes, Dror, Shaw, SC'11; numpy ships it as np.random.Philox)
+// keyed by the seed and counted by (draw, learn, attempt) instead of one
+// MT19937 stream: every draw of every learn is independent of the others, so a
+// segment's seg x batch draws run at once -- no 624-word chain that one
+// workgroup has to walk -- and the thread that draws a row also marks it.
+__device__ __forceinline__ void philox4x64_10(uint64_t c[4], uint64_t k0, uint64_t k1) {
+  constexpr uint64_t kM0 = 0xD2E7470EE14C6C93ull, kM1 = 0xCA5A826395121157ull;  // multipliers
+  constexpr uint64_t kW0 = 0x9E3779B97F4A7C15ull, kW1 = 0xBB67AE8584CAA73Bull;  // Weyl key bumps
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t hi0 = __umul64hi(kM0, c[0]), lo0 = kM0 * c[0];
+    const uint64_t hi1 = __umul64hi(kM1, c[2]), lo1 = kM1 * c[2];
+    const uint64_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+    c[0] = n0;
+    c[1] = lo1;
+    c[2] = n2;
+    c[3] = lo0;
+    k0 += kW0;
+    k1 += kW1;
+  }
+}
+
+// draw i of global learn L over [0, rng]: Philox4x64-10 of counter (i, L, attempt, 0)
+// under key (seed, 0); its four words in order, the first whose bits under `mask`
+// (the smallest 2^k - 1 >= rng) are <= rng -- numpy's masked rejection -- else the
+// next attempt (each attempt fails with probability < 2^-4 at any range)
+__device__ __forceinline__ int64_t ctr_draw(uint64_t seed, int64_t L, int i, uint64_t rng, uint64_t mask) {
+  if (rng == 0) return 0;  // numpy's off + 0: no words
+  for (uint64_t j = 0; j < 64; ++j) {
+    uint64_t c[4] = {(uint64_t)i, (uint64_t)L, j, 0ull};
+    philox4x64_10(c, seed, 0ull);
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+      if ((c[w] & mask) <= rng) return (int64_t)(c[w] & mask);
+  }
+  return 0;  // (256 failed words: probability < 2^-256; bounded so no wave can spin)
+}
+
+__device__ __forceinline__ uint64_t range_mask(uint64_t rng) {
+  uint64_t m = rng;
+  m |= m >> 1;
+  m |= m >> 2;
+  m |= m >> 4;
+  m |= m >> 8;
+  m |= m >> 16;
+  m |= m >> 32;
+  return m;
+}
+
+// Segment G.g's learns: idx[k][i] (-1: the learn is skipped, fewer than `batch`
+// rows stored) and the marks of the rows they read on this rank -- the row and
+// its predecessor (its s) -- in segment G.g (marks_cur) or G.g - 1 (marks_prev;
+// with M <= seg x period a row lies in one of the two). One thread per draw.
+__global__ void __launch_bounds__(256) k_rb_draw_ctr(SacenvReplayParams p, StagedGeom G, uint64_t seed, int batch,
+                                                     int nb, int64_t* __restrict__ idx,
+                                                     unsigned long long* __restrict__ marks_prev,
+                                                     unsigned long long* __restrict__ marks_cur) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t >= (int64_t)batch * nb) return;
+  const int k = (int)(t / batch), i = (int)(t - (int64_t)k * batch);
+  const int64_t L = G.g * G.seg + k, cntr = (L + 1) * G.period, M = p.mem_size;
+  if (cntr < batch) {  // continuous_agent.py:97-98: learn() returns before sampling
+    idx[t] = -1;
+    return;
+  }
+  const uint64_t rng = (uint64_t)((cntr < M ? cntr : M) - 1);
+  const int64_t row = ctr_draw(seed, L, i, rng, range_mask(rng));
+  idx[t] = row;
+  int64_t q, u;
+  resolve(row, cntr, M, G, &q, &u);
+  if (u < G.offset || u >= G.offset + G.n) return;
+  const int e = (int)(u - G.offset);
+  const int nw = G.n_pad / kWave;
+#pragma unroll
+  for (int d = 0; d < 2; ++d) {  // the row, and its predecessor (s)
+    const int64_t qq = q - d;
+    if (qq < 0) continue;        // step -1: the reset obs begin() staged
+    int64_t j = qq - G.g * G.seg;
+    unsigned long long* const mk = j >= 0 ? marks_cur : marks_prev;
+    j = j >= 0 ? j : j + G.seg;
+    if (mk != nullptr) atomicOr(&mk[j * nw + e / kWave], 1ull << (e % kWave));
+  }
+}
+
+// The all-gather form of the exchange. Each rank packs the rows IT owns of the
+// segment's learns -- one 25-word record per sampled row: slot (learn x batch +
+// draw) | terminal << 31, reward f32, state [11], new_state [11], action -- into
+// a chunk of `cap` records behind a 4-word header (record count); rank 0 also
+// packs the rows of skipped learns (all zero). One all-gather of the chunks and
+// an unpack on every rank rebuild sacenv_replay_sample_staged's `words`, bit for
+// bit: every slot comes from exactly one rank. Record order inside a chunk
+// follows the atomic count (not deterministic); the slot makes it irrelevant.
+constexpr int kRecWords = 2 + 2 * SACENV_OBS_DIM + 1;  // 25
+constexpr int kChunkHdr = 4;
+
+__global__ void __launch_bounds__(256) k_rb_pack_staged(SacenvReplayParams p, StagedGeom G, StagedRows S, int batch,
+                                                        int nb, const int64_t* __restrict__ idx,
+                                                        uint32_t* __restrict__ chunk, int64_t cap, int skip_owner) {
+  constexpr int D = SACENV_OBS_DIM;
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const bool live = t < (int64_t)batch * nb;
+  const int b = live ? (int)(t / batch) : 0;
+  const int64_t row = live ? idx[t] : -2;
+  int64_t q = 0, u = -1;
+  if (row >= 0) resolve(row, (G.g * G.seg + b + 1) * G.period, p.mem_size, G, &q, &u);
+  const bool own = u >= G.offset && u < G.offset + G.n;
+  const bool take = own || (row == -1 && skip_owner);
+  float sn[16], sv[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) sn[k] = sv[k] = 0.f;
+  uint32_t tm = 0u;
+  if (own) {  // (as k_rb_gather_staged)
+    const int e = (int)(u - G.offset);
+    int64_t j = q - G.g * G.seg;
+    const bool in_cur = j >= 0;
+    j = in_cur ? j : j + G.seg;
+    const float4* R = reinterpret_cast<const float4*>((in_cur ? S.cur : S.prev) + (j * G.n_pad + e) * 64);
+    const float4* P = j > 0 ? reinterpret_cast<const float4*>((in_cur ? S.cur : S.prev) + ((j - 1) * G.n_pad + e) * 64)
+                            : reinterpret_cast<const float4*>(S.prev + ((int64_t)(G.seg - 1) * G.n_pad + e) * 64);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float4 x = R[k], y = P[k];
+      sn[4 * k] = x.x, sn[4 * k + 1] = x.y, sn[4 * k + 2] = x.z, sn[4 * k + 3] = x.w;
+      sv[4 * k] = y.x, sv[4 * k + 1] = y.y, sv[4 * k + 2] = y.z, sv[4 * k + 3] = y.w;
+    }
+    const bool pdone = (__float_as_uint(sv[13]) & 0xFFu) != 0u;
+    const float o3 = sv[14];
+#pragma unroll
+    for (int k = 0; k < D; ++k) sv[k] = pdone ? S.first[k] : sv[k];
+    if (G.exp2 && pdone) sv[3] = o3;
+    tm = (p.terminal_mask >> ((__float_as_uint(sn[13]) >> 8) & 0xFFu)) & 1u;
+  }
+  // one count atomic per wave: the wave's taken records are contiguous
+  const unsigned long long bal = __ballot(take);
+  const int lane = threadIdx.x & (kWave - 1);
+  const int lead = bal != 0ull ? __ffsll((long long)bal) - 1 : 0;
+  uint32_t base = 0u;
+  if (lane == lead && bal != 0ull) base = atomicAdd(chunk, (uint32_t)__popcll(bal));
+  base = (uint32_t)__shfl((int)base, lead);
+  if (!take) return;
+  const int64_t pos = (int64_t)base + __popcll(bal & ((1ull << lane) - 1ull));
+  if (pos >= cap) return;  // (the header's count says so; the unpack flags it)
+  uint32_t* const rec = chunk + kChunkHdr + pos * kRecWords;
+  rec[0] = (uint32_t)t | (tm << 31);
+  rec[1] = __float_as_uint(sn[11]);
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    rec[2 + k] = __float_as_uint(sv[k]);
+    rec[2 + D + k] = __float_as_uint(sn[k]);
+  }
+  rec[2 + 2 * D] = __float_as_uint(sn[12]);
+}
+
+// world chunks of chunk_words each -> sacenv_replay_sample_staged's words. One
+// thread per record slot of every chunk; a count above cap sets status bit 0.
+__global__ void __launch_bounds__(256) k_rb_unpack_staged(const uint32_t* __restrict__ gathered, int world,
+                                                          int64_t chunk_words, int64_t cap, int batch,
+                                                          uint32_t* __restrict__ words, int64_t per,
+                                                          int32_t* __restrict__ status) {
+  constexpr int D = SACENV_OBS_DIM;
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t >= (int64_t)world * cap) return;
+  const int r = (int)(t / cap);
+  const int64_t j = t - (int64_t)r * cap;
+  const uint32_t* const hdr = gathered + (int64_t)r * chunk_words;
+  const int64_t cnt = hdr[0];
+  if (j == 0 && cnt > cap) atomicOr(status, 1);
+  if (j >= cnt) return;
+  const uint32_t* const rec = hdr + kChunkHdr + j * kRecWords;
+  const uint32_t s0 = rec[0], slot = s0 & 0x7FFFFFFFu;
+  const int b = (int)(slot / (uint32_t)batch), i = (int)(slot - (uint32_t)b * (uint32_t)batch);
+  uint32_t* const W = words + (int64_t)b * per;
+  const double r64 = (double)__uint_as_float(rec[1]);
+  uint64_t rb;
+  __builtin_memcpy(&rb, &r64, 8);
+  W[2 * i] = (uint32_t)rb;
+  W[2 * i + 1] = (uint32_t)(rb >> 32);
+  uint32_t* const st = W + 2 * batch + (int64_t)i * D;
+  uint32_t* const ns = W + 2 * batch + (int64_t)batch * D + (int64_t)i * D;
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    st[k] = rec[2 + k];
+    ns[k] = rec[2 + D + k];
+  }
+  W[2 * batch + 2 * (int64_t)batch * D + i] = rec[2 + 2 * D];
+  W[2 * batch + 2 * (int64_t)batch * D + batch + i] = s0 >> 31;
+}
+
+// A stand-in for a collective's kernel on one GPU (bench.py's replay_path at N =
+// 1): `workgroups` workgroups of 256 threads -- the channels of an RCCL kernel --
+// copy `n16` 16-B units and then stay resident until `min_ticks` of the 100-MHz
+// realtime clock have passed since they started (an RCCL kernel lives as long as
+// its transfer over the links, not as long as a local copy): what the owner waves
+// of a segment launch share their CUs with while the exchange runs beside them.
+__global__ void __launch_bounds__(256) k_copy_standin(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                      int64_t n16, uint64_t min_ticks) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n16; q += (int64_t)gridDim.x * blockDim.x)
+    dst[q] = src[q];
+  while (__builtin_amdgcn_s_memrealtime() - t0 < min_ticks) __builtin_amdgcn_s_sleep(8);
 }
 
 int check_replay(const SacenvReplayParams* p) {
@@ -896,6 +1112,146 @@ int sacenv_replay_sample_staged(const SacenvReplayParams* p, const SacenvStagedP
   const int64_t per = (int64_t)batch * (2 * SACENV_OBS_DIM + 1 + 3);
   hipLaunchKernelGGL(k_rb_gather_staged, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      *p, geom(p, sp, g), S, batch, n_batches, idx, words, per);
+  return status();
+}
+
+int sacenv_replay_gather(const SacenvReplayParams* p, void* arena, int32_t batch, const int64_t* idx, float* state,
+                         float* action, double* reward, float* new_state, uint8_t* terminal, void* stream) {
+  int rc = check_replay(p);
+  if (rc) return rc;
+  if (batch < 0) return SACENV_E_SIZE;
+  if (arena == nullptr || idx == nullptr) return SACENV_E_NULL;
+  if (batch == 0) return SACENV_OK;
+  const int64_t total = (int64_t)batch * (p->obs_dim + p->act_dim + 1);
+  hipLaunchKernelGGL(k_rb_gather, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *p,
+                     make_rb(*p, arena), batch, idx, state, action, reward, new_state, terminal, Shard{0, 0, 0});
+  return status();
+}
+
+static int check_ctr_shape(const SacenvReplayParams* p, const SacenvStagedParams* sp, int64_t g, int32_t batch,
+                           int32_t n_batches) {
+  const int rc = check_staged(p, sp);
+  if (rc) return rc;
+  if (g < 0 || batch < 0 || n_batches < 0 || n_batches > sp->seg) return SACENV_E_SIZE;
+  if ((int64_t)batch * n_batches >= ((int64_t)1 << 31)) return SACENV_E_SIZE;  // slot numbers: 31 bits
+  if (!staged_range_ok(sp, g)) return SACENV_E_RANGE;
+  return SACENV_OK;
+}
+
+int sacenv_replay_stage_draw_ctr(const SacenvReplayParams* p, const SacenvStagedParams* sp, int64_t g,
+                                 int32_t batch, int32_t n_batches, uint64_t seed, int64_t* idx, uint64_t* marks_prev,
+                                 uint64_t* marks_cur, void* stream) {
+  const int rc = check_ctr_shape(p, sp, g, batch, n_batches);
+  if (rc) return rc;
+  if (idx == nullptr) return SACENV_E_NULL;
+  const int64_t total = (int64_t)batch * n_batches;
+  if (total == 0) return SACENV_OK;
+  hipLaunchKernelGGL(k_rb_draw_ctr, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *p,
+                     geom(p, sp, g), seed, batch, n_batches, idx, reinterpret_cast<unsigned long long*>(marks_prev),
+                     reinterpret_cast<unsigned long long*>(marks_cur));
+  return status();
+}
+
+// rows of the window [c - W, c) of sequence numbers whose (s mod period) lies in [o, o + n)
+static double window_rows(int64_t c, int64_t W, int64_t period, int64_t o, int64_t n) {
+  auto F = [&](int64_t x) {
+    int64_t r = x % period - o;
+    r = r < 0 ? 0 : (r > n ? n : r);
+    return (x / period) * n + r;
+  };
+  return (double)(F(c) - F(c - W));
+}
+
+// The chunk of sacenv_replay_stage_pack for this shape, the same on every rank: the
+// most records any rank packs in expectation over any segment (each learn's rows
+// owned in proportion to the rank's share of the ring window; rank 0 also the
+// skipped learns' rows), + 8 standard deviations (the count is a sum of
+// independent draws: variance <= mean) + 64, at most every slot.
+static int64_t chunk_cap(const SacenvReplayParams* p, const SacenvStagedParams* sp, int32_t batch, int32_t nb) {
+  const int64_t P = sp->period, n = sp->n, M = p->mem_size, world = P / n, total = (int64_t)batch * nb;
+  if (world == 1) return total;
+  // after the first learn whose window is the whole ring, every learn's window has the
+  // same alignment (c is a multiple of period): the rank shares repeat
+  const int64_t g_last = (M / P) / sp->seg + 2;
+  double worst = 0.0;
+  for (int64_t g = 0; g <= g_last; ++g)
+    for (int64_t r = 0; r < world; ++r) {
+      double e = 0.0;
+      for (int k = 0; k < nb; ++k) {
+        const int64_t c = (g * sp->seg + k + 1) * P;
+        if (c < batch) {
+          e += r == 0 ? batch : 0;
+          continue;
+        }
+        const int64_t W = c < M ? c : M;
+        e += (double)batch * window_rows(c, W, P, r * n, n) / (double)W;
+      }
+      worst = e > worst ? e : worst;
+    }
+  const int64_t cap = (int64_t)(worst + 8.0 * sqrt(worst) + 64.0) + 1;
+  return cap < total ? cap : total;
+}
+
+int sacenv_replay_stage_chunk(const SacenvReplayParams* p, const SacenvStagedParams* sp, int32_t batch,
+                              int32_t n_batches, int64_t* cap_rows, int64_t* chunk_bytes) {
+  const int rc = check_ctr_shape(p, sp, 0, batch, n_batches);
+  if (rc) return rc;
+  if (cap_rows == nullptr || chunk_bytes == nullptr) return SACENV_E_NULL;
+  if (sp->period % sp->n != 0) return SACENV_E_RANGE;  // every rank holds n envs
+  const int64_t cap = chunk_cap(p, sp, batch, n_batches);
+  *cap_rows = cap;
+  *chunk_bytes = align256(4 * (kChunkHdr + cap * kRecWords));
+  return SACENV_OK;
+}
+
+int sacenv_replay_stage_pack(const SacenvReplayParams* p, const SacenvStagedParams* sp, int64_t g,
+                             const void* stage_cur, const void* stage_prev, const int64_t* idx, int32_t batch,
+                             int32_t n_batches, int64_t cap, void* chunk, void* stream) {
+  int rc = check_ctr_shape(p, sp, g, batch, n_batches);
+  if (rc) return rc;
+  if (!stage_cur || !stage_prev || !idx || !chunk) return SACENV_E_NULL;
+  if (((reinterpret_cast<uintptr_t>(stage_cur) | reinterpret_cast<uintptr_t>(stage_prev)) & 15u) != 0u ||
+      (reinterpret_cast<uintptr_t>(chunk) & 3u) != 0u || cap < 0)
+    return SACENV_E_RANGE;
+  const hipError_t e = hipMemsetAsync(chunk, 0, 4 * kChunkHdr, (hipStream_t)stream);  // the record count
+  if (e != hipSuccess) return (int)e;
+  const int64_t total = (int64_t)batch * n_batches;
+  if (total == 0) return SACENV_OK;
+  StagedRows S;
+  S.cur = static_cast<const char*>(stage_cur);
+  S.prev = static_cast<const char*>(stage_prev);
+  for (int k = 0; k < SACENV_OBS_DIM; ++k) S.first[k] = sp->first_obs[k];
+  hipLaunchKernelGGL(k_rb_pack_staged, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     *p, geom(p, sp, g), S, batch, n_batches, idx, static_cast<uint32_t*>(chunk), cap,
+                     sp->offset == 0 ? 1 : 0);
+  return status();
+}
+
+int sacenv_replay_stage_unpack(int32_t world, int64_t chunk_bytes, int64_t cap, int32_t batch, int32_t n_batches,
+                               const void* gathered, uint32_t* words, int32_t* status_word, void* stream) {
+  if (world < 1 || cap < 0 || batch < 0 || n_batches < 0) return SACENV_E_SIZE;
+  if ((int64_t)batch * n_batches >= ((int64_t)1 << 31) || (int64_t)world * cap >= ((int64_t)1 << 31))
+    return SACENV_E_SIZE;
+  if (chunk_bytes < 4 * (kChunkHdr + cap * kRecWords) || (chunk_bytes & 3) != 0) return SACENV_E_SIZE;
+  if (!gathered || !words || !status_word) return SACENV_E_NULL;
+  const int64_t n = (int64_t)world * cap;
+  if (n == 0 || batch == 0) return SACENV_OK;
+  const int64_t per = (int64_t)batch * (2 * SACENV_OBS_DIM + 1 + 3);
+  hipLaunchKernelGGL(k_rb_unpack_staged, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     static_cast<const uint32_t*>(gathered), world, chunk_bytes / 4, cap, batch, words, per,
+                     status_word);
+  return status();
+}
+
+int sacenv_copy_standin(const void* src, void* dst, int64_t bytes, int32_t workgroups, double min_us, void* stream) {
+  if (bytes < 0 || (bytes & 15) != 0 || workgroups < 1 || workgroups > 4096 || !(min_us >= 0.0) || min_us > 1e5)
+    return SACENV_E_SIZE;
+  if ((bytes > 0 && (!src || !dst)) ||
+      ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15u) != 0u)
+    return bytes > 0 && (!src || !dst) ? SACENV_E_NULL : SACENV_E_RANGE;
+  hipLaunchKernelGGL(k_copy_standin, dim3((unsigned)workgroups), dim3(256), 0, (hipStream_t)stream,
+                     static_cast<const uint4*>(src), static_cast<uint4*>(dst), bytes / 16,
+                     (uint64_t)(min_us * 100.0));
   return status();
 }
 

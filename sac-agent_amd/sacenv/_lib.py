@@ -14,7 +14,7 @@ PKG_ROOT = _build.PKG_ROOT
 LIB_PATH = os.environ.get("SACENV_LIB", _build.LIB)
 LOADED_DIGEST = None  # source digest of the loaded library (the in-tree build)
 
-ABI_VERSION = 18
+ABI_VERSION = 19
 OBS_DIM = 11
 MT_N = 624
 MAX_KNOTS = 16
@@ -145,7 +145,9 @@ EXPORTS = ("sacenv_abi_version", "sacenv_error_string", "sacenv_boat_layout",
            "sacenv_mixed_segment", "sacenv_replay_layout",
            "sacenv_replay_init", "sacenv_replay_store", "sacenv_replay_store_env", "sacenv_replay_store_env_at", "sacenv_replay_sample", "sacenv_replay_store_shard",
            "sacenv_replay_sample_shard", "sacenv_replay_stage_scratch_bytes", "sacenv_replay_stage_draw",
-           "sacenv_replay_stage_mark", "sacenv_replay_sample_staged",
+           "sacenv_replay_stage_mark", "sacenv_replay_sample_staged", "sacenv_replay_gather",
+           "sacenv_replay_stage_draw_ctr", "sacenv_replay_stage_chunk", "sacenv_replay_stage_pack",
+           "sacenv_replay_stage_unpack", "sacenv_copy_standin",
            "sacenv_compact_done", "sacenv_boat_reset_list", "sacenv_sac_layout", "sacenv_sac_sync",
            "sacenv_sac_act", "sacenv_sac_act_handoff", "sacenv_sac_act_occupancy", "sacenv_sac_learn")
 
@@ -224,6 +226,12 @@ def load(path: str | None = None):
         "sacenv_replay_stage_draw": (C.c_int, [RP, _p, SP, _i64, _i32, _i32, _p, _p, _i64, _p]),
         "sacenv_replay_stage_mark": (C.c_int, [RP, SP, _i64, _p, _p, _i32, _i32, _p, _p]),
         "sacenv_replay_sample_staged": (C.c_int, [RP, SP, _i64, _p, _p, _p, _i32, _i32, _p, _p]),
+        "sacenv_replay_gather": (C.c_int, [RP, _p, _i32, _p, _p, _p, _p, _p, _p, _p]),
+        "sacenv_replay_stage_draw_ctr": (C.c_int, [RP, SP, _i64, _i32, _i32, C.c_uint64, _p, _p, _p, _p]),
+        "sacenv_replay_stage_chunk": (C.c_int, [RP, SP, _i32, _i32, C.POINTER(_i64), C.POINTER(_i64)]),
+        "sacenv_replay_stage_pack": (C.c_int, [RP, SP, _i64, _p, _p, _p, _i32, _i32, _i64, _p, _p]),
+        "sacenv_replay_stage_unpack": (C.c_int, [_i32, _i64, _i64, _i32, _i32, _p, _p, _p, _p]),
+        "sacenv_copy_standin": (C.c_int, [_p, _p, _i64, _i32, C.c_double, _p]),
         "sacenv_sac_layout": (C.c_int, [C.POINTER(SacParams), C.POINTER(SacLayout)]),
         "sacenv_sac_sync": (C.c_int, [C.POINTER(SacParams), _p, _p]),
         "sacenv_sac_act": (C.c_int, [C.POINTER(SacParams), _p, _p, _i32, _p, _p, _p, _p]),

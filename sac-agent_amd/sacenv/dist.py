@@ -289,7 +289,8 @@ class SegmentExchange:
     (``prepare(g + 1)``), then -- behind the launch -- the segment's batches: the gather
     and the one SUM all-reduce over the ranks. So the draws, the gather and the
     collective all overlap the next segment. Segments are counted from ``start`` (the
-    replay buffer starts empty there)."""
+    replay buffer starts empty there). ``check()`` after a timed region raises on a
+    segment the sampler flagged invalid."""
 
     def __init__(self, sampler, device):
         self.sampler = sampler
@@ -352,3 +353,10 @@ class SegmentExchange:
                 self._cur().wait_event(ev)
         self._done.clear()
         self._ready.clear()
+
+    def check(self) -> None:
+        """Raise if the sampler reported an invalid segment (a poisoned MT stream, an
+        overflowed all-gather chunk). Synchronises: call it outside a timed region."""
+        chk = getattr(self.sampler, "check", None)
+        if chk is not None:
+            chk()

@@ -147,6 +147,22 @@ class DeviceReplayBuffer:
             ac.data_ptr(), rw.data_ptr(), ns.data_ptr(), tm.data_ptr(), self.stream))
         return st, ac, rw, ns, (tm.bool() if as_bool else tm), idx
 
+    def gather(self, idx: torch.Tensor, as_bool: bool = True):
+        """The rows at the given ring indices (buffer.py:28-33 without the draw):
+        (states, actions, rewards f64, states_, dones); an index outside the ring gives
+        zeros (``sacenv_replay_gather``)."""
+        idx = idx.to(device=self.device, dtype=torch.int64).contiguous().reshape(-1)
+        B = idx.numel()
+        st = torch.empty((B, *self.input_shape), dtype=torch.float32, device=self.device)
+        ns = torch.empty_like(st)
+        ac = torch.empty((B, self.n_actions), dtype=torch.float32, device=self.device)
+        rw = torch.empty(B, dtype=torch.float64, device=self.device)
+        tm = torch.empty(B, dtype=torch.uint8, device=self.device)
+        _lib.check(self.lib.sacenv_replay_gather(
+            self._pp, self.arena.data_ptr(), B, idx.data_ptr(), st.data_ptr(), ac.data_ptr(), rw.data_ptr(),
+            ns.data_ptr(), tm.data_ptr(), self.stream))
+        return st, ac, rw, ns, (tm.bool() if as_bool else tm)
+
 
 class ShardedReplayBuffer(DeviceReplayBuffer):
     """The replay buffer pooled over ``world`` ranks (main.py:81-88 with every rank's
@@ -269,22 +285,48 @@ class StagedReplay:
     ``stage_args(g)`` -> the launch -> ``prepare(g + 1)`` -> ``sample_segment(g)``.
     Buffers: the staged rows of segment g are read by ``sample_segment(g)`` and
     ``(g + 1)``, so the launch of segment g + 2 (3 buffers) must follow
-    ``sample_segment(g)`` in stream order (``sacenv.dist.SegmentExchange`` arranges it)."""
+    ``sample_segment(g)`` in stream order (``sacenv.dist.SegmentExchange`` arranges it).
+
+    ``sampler``: ``"mt"`` (default) draws every learn from the buffer's one MT19937
+    stream exactly as the reference's ``np.random.choice`` would (the parity mode:
+    the batches equal a DeviceReplayBuffer's bit for bit); ``"philox"`` draws the
+    same distribution -- uniform with replacement over the rows stored, the same
+    skip rule -- from a counter-based generator (Philox4x64-10 keyed by the seed,
+    counted by (draw, learn)), so a segment's draws are one parallel launch that
+    also marks the rows (``sacenv_replay_stage_draw_ctr``; oracle/ctr_sampler.py).
+    ``exchange``: ``"allreduce"`` (default) assembles the batches with one SUM
+    all-reduce of the 1/world-dense packed batches; ``"allgather"`` packs each
+    rank's own rows (100-B records with their slot) into a fixed chunk and
+    all-gathers the chunks (about half the bytes per rank of the ring all-reduce),
+    then unpacks them into the same words on every rank. Both are bit-exact.
+    ``standin`` (world 1 only; bench.py's replay path): a dict(bytes, workgroups, us)
+    -- a copy kernel of that many bytes on that many workgroups, resident for that
+    long, between the pack and the unpack: the collective's kernel stood in for."""
 
     N_BUFFERS = 3
 
     def __init__(self, n: int, n_pad: int, experiment: int, first_obs, *, rank: int = 0, world: int = 1,
                  mem_size: int = 1_000_000, batch: int = 1024, seg: int = 256, seed: int = 0,
-                 device=None, group=None, terminal_mask: int = TERMINAL_GOAL):
+                 device=None, group=None, terminal_mask: int = TERMINAL_GOAL, sampler: str = "mt",
+                 exchange: str = "allreduce", standin: dict | None = None):
         self.lib = _lib.load()
         self.device = torch.device(device if device is not None else "cuda")
         if self.device.type != "cuda":
             raise RuntimeError("StagedReplay runs on a GPU (HIP); no CPU path")
         if self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
+        if sampler not in ("mt", "philox") or exchange not in ("allreduce", "allgather"):
+            raise ValueError("sampler is 'mt' or 'philox'; exchange is 'allreduce' or 'allgather'")
+        self.sampler, self.exchange = sampler, exchange
         self.n, self.n_pad, self.seg, self.batch = int(n), int(n_pad), int(seg), int(batch)
+        if not 1 <= self.seg <= _lib.REFILL_PERIOD:
+            # the segment launch stages one mark word per step in LDS (REFILL_PERIOD of them)
+            raise ValueError(f"seg must be in [1, {_lib.REFILL_PERIOD}]")
         self.rank, self.world, self.group = int(rank), int(world), group
+        if standin is not None and self.world != 1:
+            raise ValueError("the collective stand-in is a one-GPU measurement (world 1)")
         self.mem_size = int(mem_size)
+        self.seed = int(seed)
         sp = _lib.StagedParams()
         sp.period, sp.offset = self.world * self.n, self.rank * self.n
         sp.n, sp.n_pad, sp.seg, sp.experiment = self.n, self.n_pad, self.seg, int(experiment)
@@ -297,9 +339,19 @@ class StagedReplay:
                              "reach rows older than the previous segment")
         self.sp, self._spp = sp, C.byref(sp)
         self.period = int(sp.period)
-        # the sampling stream lives in a replay arena (its key / pos fields)
-        self._rb = DeviceReplayBuffer(self.mem_size, (_lib.OBS_DIM,), 1, device=self.device, seed=seed,
-                                      reward_f32=True, terminal_mask=terminal_mask)
+        if sampler == "mt":
+            # the sampling stream lives in a replay arena (its key / pos fields)
+            self._rb = DeviceReplayBuffer(self.mem_size, (_lib.OBS_DIM,), 1, device=self.device, seed=seed,
+                                          reward_f32=True, terminal_mask=terminal_mask)
+            self._pp = self._rb._pp
+        else:  # (no stream: only the buffer's shape)
+            self._rb = None
+            p = _lib.ReplayParams()
+            p.mem_size, p.obs_dim, p.act_dim = self.mem_size, _lib.OBS_DIM, 1
+            p.reward_f32, p.terminal_mask = 1, int(terminal_mask)
+            self._params = p
+            self._pp = C.byref(p)
+        self._status = torch.zeros(4, dtype=torch.int32, device=self.device)
         nb = self.N_BUFFERS
         self.stage = [torch.zeros(self.seg * self.n_pad * 64, dtype=torch.uint8, device=self.device)
                       for _ in range(nb)]
@@ -316,9 +368,22 @@ class StagedReplay:
             for ii, idx in enumerate(self._idx):
                 self._batches[wi, ii] = [(st, ac, rw, ns, tm32, idx[i * B: (i + 1) * B])
                                          for i, (st, ac, rw, ns, tm32, _) in enumerate(views)]
-        nbytes = C.c_int64()
-        _lib.check(self.lib.sacenv_replay_stage_scratch_bytes(self._rb._pp, self.batch, self.seg, C.byref(nbytes)))
-        self._scratch = torch.empty(int(nbytes.value), dtype=torch.uint8, device=self.device)
+        if sampler == "mt":
+            nbytes = C.c_int64()
+            _lib.check(self.lib.sacenv_replay_stage_scratch_bytes(self._pp, self.batch, self.seg, C.byref(nbytes)))
+            self._scratch = torch.empty(int(nbytes.value), dtype=torch.uint8, device=self.device)
+        if exchange == "allgather":
+            self.cap, self.chunk_bytes = staged_chunk(self.n, self.n_pad, self.world, self.mem_size, self.batch,
+                                                      self.seg, experiment)
+            self._chunks = [torch.empty(self.chunk_bytes, dtype=torch.uint8, device=self.device) for _ in range(2)]
+            self._gathered = ([torch.empty(self.world * self.chunk_bytes, dtype=torch.uint8, device=self.device)
+                               for _ in range(2)] if self.world > 1 else self._chunks)
+        self.standin = dict(standin) if standin is not None else None
+        if self.standin is not None:
+            nb16 = -(-int(self.standin["bytes"]) // 16) * 16
+            self.standin["bytes"] = nb16
+            self._standin_src = torch.zeros(nb16, dtype=torch.uint8, device=self.device)
+            self._standin_dst = torch.empty(nb16, dtype=torch.uint8, device=self.device)
         self.drawn = 0   # segments whose learns are drawn
 
     @property
@@ -327,14 +392,26 @@ class StagedReplay:
 
     def _draw(self) -> None:
         g = self.drawn
-        _lib.check(self.lib.sacenv_replay_stage_draw(
-            self._rb._pp, self._rb.arena.data_ptr(), self._spp, g, self.batch, self.seg,
-            self._idx[g % 4].data_ptr(), self._scratch.data_ptr(), self._scratch.numel(), self.stream))
+        if self.sampler == "philox":
+            # segment g's draws, marking its rows in segments g - 1 and g: segment g's marks
+            # start here (cleared), segment g - 1's are complete after it
+            nb = self.N_BUFFERS
+            self.marks[g % nb].zero_()
+            _lib.check(self.lib.sacenv_replay_stage_draw_ctr(
+                self._pp, self._spp, g, self.batch, self.seg, self.seed & 0xFFFFFFFFFFFFFFFF,
+                self._idx[g % 4].data_ptr(), self.marks[(g - 1) % nb].data_ptr() if g > 0 else None,
+                self.marks[g % nb].data_ptr(), self.stream))
+        else:
+            _lib.check(self.lib.sacenv_replay_stage_draw(
+                self._pp, self._rb.arena.data_ptr(), self._spp, g, self.batch, self.seg,
+                self._idx[g % 4].data_ptr(), self._scratch.data_ptr(), self._scratch.numel(), self.stream))
         self.drawn += 1
 
     def _mark(self, g: int) -> None:
+        if self.sampler == "philox":  # (the draws marked the rows)
+            return
         _lib.check(self.lib.sacenv_replay_stage_mark(
-            self._rb._pp, self._spp, g, self._idx[g % 4].data_ptr(), self._idx[(g + 1) % 4].data_ptr(),
+            self._pp, self._spp, g, self._idx[g % 4].data_ptr(), self._idx[(g + 1) % 4].data_ptr(),
             self.batch, self.seg, self.marks[g % self.N_BUFFERS].data_ptr(), self.stream))
 
     def begin(self, obs: torch.Tensor) -> None:
@@ -371,23 +448,85 @@ class StagedReplay:
         words = self._words[g % 2][0]
         idx = self._idx[g % 4]
         nb = self.N_BUFFERS
+        if self.exchange == "allgather":
+            chunk = self._chunks[g % 2]
+            _lib.check(self.lib.sacenv_replay_stage_pack(
+                self._pp, self._spp, g, self.stage[g % nb].data_ptr(), self.stage[(g - 1) % nb].data_ptr(),
+                idx.data_ptr(), self.batch, self.seg, self.cap, chunk.data_ptr(), self.stream))
+            gathered = self._gathered[g % 2]
+            if self.world > 1:
+                all_gather_bytes(gathered, chunk, self.group)
+            elif self.standin is not None:
+                sd = self.standin
+                _lib.check(self.lib.sacenv_copy_standin(
+                    self._standin_src.data_ptr(), self._standin_dst.data_ptr(), sd["bytes"], int(sd["workgroups"]),
+                    float(sd["us"]), self.stream))
+            _lib.check(self.lib.sacenv_replay_stage_unpack(
+                self.world, self.chunk_bytes, self.cap, self.batch, self.seg, gathered.data_ptr(), words.data_ptr(),
+                self._status.data_ptr(), self.stream))
+            return self._batches[g % 2, g % 4]
         _lib.check(self.lib.sacenv_replay_sample_staged(
-            self._rb._pp, self._spp, g, self.stage[g % nb].data_ptr(), self.stage[(g - 1) % nb].data_ptr(),
+            self._pp, self._spp, g, self.stage[g % nb].data_ptr(), self.stage[(g - 1) % nb].data_ptr(),
             idx.data_ptr(), self.batch, self.seg, words.data_ptr(), self.stream))
         if self.world > 1:
             dist.all_reduce(words, op=dist.ReduceOp.SUM, group=self.group)
+        elif self.standin is not None:
+            sd = self.standin
+            _lib.check(self.lib.sacenv_copy_standin(
+                self._standin_src.data_ptr(), self._standin_dst.data_ptr(), sd["bytes"], int(sd["workgroups"]),
+                float(sd["us"]), self.stream))
         return self._batches[g % 2, g % 4]
 
     @property
     def bytes_per_segment(self) -> int:
-        """The all-reduce payload of one segment's batches."""
+        """The collective's payload of one segment: the all-reduced words, or the
+        all-gathered chunks (world x chunk)."""
+        if self.exchange == "allgather":
+            return self.world * self.chunk_bytes
         return int(self._words[0][0].numel()) * 4
+
+    @property
+    def bus_bytes_per_segment(self) -> float:
+        """Bytes one rank sends per segment in a ring schedule: 2 (W-1)/W x payload for the
+        all-reduce, (W-1) chunks for the all-gather."""
+        w = self.world
+        if self.exchange == "allgather":
+            return float((w - 1) * self.chunk_bytes)
+        return 2.0 * (w - 1) / w * self.bytes_per_segment
 
     def check(self) -> None:
         """Synchronise and raise if a draw ran short of generated MT words (the planned
-        5 % margin is > 100 standard deviations of the count at the bench's shape)."""
-        if int(self._rb.mt_pos.item()) < 0:
+        5 % margin is > 100 standard deviations of the count at the bench's shape) or a
+        rank's packed rows overflowed its chunk (8 standard deviations)."""
+        if self._rb is not None and int(self._rb.mt_pos.item()) < 0:
             raise _lib.SacenvError("staged draw: too few MT words generated; the sampling stream is invalid")
+        if int(self._status[0].item()) != 0:
+            raise _lib.SacenvError("staged all-gather: a rank's rows overflowed its chunk; batches are invalid")
+
+
+def staged_chunk(n: int, n_pad: int, world: int, mem_size: int, batch: int, seg: int,
+                 experiment: int = 6) -> tuple[int, int]:
+    """(records, bytes) of one rank's all-gather chunk for this shape
+    (``sacenv_replay_stage_chunk``): the same on every rank."""
+    lib = _lib.load()
+    p = _lib.ReplayParams()
+    p.mem_size, p.obs_dim, p.act_dim, p.reward_f32, p.terminal_mask = int(mem_size), _lib.OBS_DIM, 1, 1, 2
+    sp = _lib.StagedParams()
+    sp.period, sp.offset, sp.n, sp.n_pad, sp.seg, sp.experiment = world * n, 0, n, n_pad, seg, experiment
+    cap, nbytes = C.c_int64(), C.c_int64()
+    _lib.check(lib.sacenv_replay_stage_chunk(C.byref(p), C.byref(sp), int(batch), int(seg), C.byref(cap),
+                                             C.byref(nbytes)))
+    return int(cap.value), int(nbytes.value)
+
+
+def all_gather_bytes(out: torch.Tensor, chunk: torch.Tensor, group=None) -> None:
+    """out [world x chunk] = every rank's chunk in rank order: all_gather_into_tensor over
+    RCCL; gloo (rehearsals) through the list form."""
+    import torch.distributed as dist
+    if dist.get_backend(group) == "nccl":
+        dist.all_gather_into_tensor(out, chunk, group=group)
+    else:
+        dist.all_gather(list(out.chunk(dist.get_world_size(group))), chunk, group=group)
 
 
 class ReplayBuffer:
@@ -425,4 +564,5 @@ class ReplayBuffer:
                 rewards.cpu().numpy(), states_.cpu().numpy().astype(np.float64), dones.cpu().numpy())
 
 
-__all__ = ["DeviceReplayBuffer", "ReplayBuffer", "ShardedReplayBuffer", "StagedReplay", "TERMINAL_GOAL"]
+__all__ = ["DeviceReplayBuffer", "ReplayBuffer", "ShardedReplayBuffer", "StagedReplay", "TERMINAL_GOAL",
+           "staged_chunk", "all_gather_bytes"]

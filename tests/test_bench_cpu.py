@@ -123,19 +123,55 @@ def test_driver_command_world2_gloo_segment_gather():
 
 def test_driver_command_world2_gloo_sharded_exchange():
     """The default N>1 pooling: each segment's rows staged per rank and the segment's
-    learn() batches exchanged with one all-reduce, inside the timed region; the
-    all-gather and no-exchange rates measured beside it."""
+    learn() batches exchanged with one all-gather of each rank's packed rows, inside the
+    timed region; the all-gather of every transition and no exchange measured beside it."""
     out = _world2([])
     assert out["steps"] == 8 * 256 and out["n_gpus"] == 2 and out["value"] > 0
     po = out["pooling"]
     assert po["mode"] == "sharded" and po["exchanges_timed"] == 8
-    assert po["bytes_per_segment"] == 256 * 64 * 26 * 4
-    assert "8 in the timed region" in out["config"]["collective"] and "all_reduce" in out["config"]["collective"]
+    assert po["exchange"] == "allgather" and po["sampler"] == "philox"
+    chunk = (-(-256 * 64 // 2) * 25 + 4) * 4
+    assert po["bytes_per_segment"] == 2 * chunk and po["bus_bytes_per_rank"] == 8 * chunk
+    assert "8 in the timed region" in out["config"]["collective"] and "all_gather" in out["config"]["collective"]
+    assert "Philox" in out["config"]["collective"]
     assert po["xgmi"]["GBps_per_rank"] > 0
     ag = po["all_gather"]
     assert ag["value"] > 0 and ag["received_bytes_per_rank"] == 53 * N_PAD * ag["steps"]
     assert po["no_exchange"]["value"] > 0
     assert out["data"].startswith("stub")
+
+
+def test_driver_command_world2_gloo_sharded_allreduce():
+    """--exchange allreduce: the SUM all-reduce of the 1/N-dense batch words."""
+    out = _world2(["--exchange", "allreduce", "--sampler", "mt"])
+    po = out["pooling"]
+    assert po["mode"] == "sharded" and po["exchange"] == "allreduce" and po["sampler"] == "mt"
+    assert po["bytes_per_segment"] == 256 * 64 * 26 * 4
+    assert po["bus_bytes_per_rank"] == 8 * 2 * (2 - 1) / 2 * 256 * 64 * 26 * 4
+    assert "all_reduce" in out["config"]["collective"]
+
+
+@pytest.mark.parametrize("argv,mode", [([], "sharded"), (["--launch", "step"], "gather"),
+                                       (["--no-graph"], "gather"), (["--pooling", "none"], "none"),
+                                       (["--mixed"], "gather")])
+def test_sharded_pooling_needs_the_segment_launch(argv, mode):
+    """ADVICE r5: the staged replay's rows are written by the persistent segment launch;
+    --launch step / --no-graph at N>1 time the all-gather pooling instead (a KeyError in
+    the timed loop before)."""
+    import bench
+    args = bench.parse(["--gpus", "2", *argv])
+    _, wl = _workload(bench, 0)
+    wl.segment_step = lambda *a, **k: None   # (a GPU workload has one)
+    wl.segment_pools = not args.mixed
+    assert bench.pooling_mode(args, 2, wl) == mode
+    assert bench.pooling_mode(args, 1, wl) == "none"
+
+
+def test_driver_command_world2_gloo_launch_step():
+    """--gpus 2 --launch step: the runner steps k_step launches and the rows pooled
+    (stub: the control flow of that combination end to end)."""
+    out = _world2(["--launch", "step"])
+    assert out["n_gpus"] == 2 and out["value"] > 0 and out["pooling"]["exchanges_timed"] == 8
 
 
 def test_bench_self_launches_its_ranks():

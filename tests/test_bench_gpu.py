@@ -26,9 +26,11 @@ def test_driver_bench_command():
     assert r.returncode == 0, r.stderr[-3000:]
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
     d = json.loads(line)
-    # >= 8 timed segments, 2 warm-up segments, and the timed region lasts ~1 s (bench.MIN_TIMED_SECONDS)
-    assert d["steps"] % 256 == 0 and d["steps"] >= 8 * 256 and d["warmup"] == 512 and d["n_gpus"] == 1
-    assert d["ms_per_step"] * d["steps"] * 1e-3 >= 0.5
+    # >= 8 timed segments, the warm-up past the clock boost, and the timed region lasts >= 1 s
+    # (bench.MIN_TIMED_SECONDS, sized at the warm-up's post-boost rate)
+    assert d["steps"] % 256 == 0 and d["steps"] >= 8 * 256 and d["n_gpus"] == 1
+    assert d["warmup"] == 256 * 24
+    assert d["ms_per_step"] * d["steps"] * 1e-3 >= 1.0
     assert d["value"] > 0 and d["unit"] == "env-steps/s"
     assert d["ms_per_step"] * d["steps"] * 1e-3 <= wall
     # every captured graph (4 action-table segments) ran once before the warm-up
@@ -39,8 +41,12 @@ def test_driver_bench_command():
     assert rf["bound"] == "fp64-issue" and rf["unit"] == "TFLOP/s" and 0 < rf["frac"] < 1
     assert 0 < rf["issue_floor_frac"] <= 1.05 and rf["kernel_avg_us"] > 0
     assert 0 < rf["hbm"]["frac"] < 1 and rf["hbm"]["unit"] == "GB/s"
-    # the N>1 replay path at one GPU, measured on the same line
-    assert d["replay_path"]["value"] > 0 and d["every_output"]["value"] > 0
+    # the N>1 replay path at one GPU, measured on the same line, with the sampler it timed, and
+    # the same with the collective's kernel stood in for
+    rp, sd = d["replay_path"], d["replay_path_collective_standin"]
+    assert rp["value"] > 0 and d["every_output"]["value"] > 0
+    assert rp["sampler"] == "philox" and rp["exchange"] == "allgather"
+    assert sd["value"] > 0 and sd["standin"]["workgroups"] == 16 and sd["standin"]["bytes"] > 20e6
     if rf["kernel"].startswith("k_rollout"):  # the persistent launch: resident-state bytes headline
         assert abs(rf["bytes_per_env_step"] - (70 + 152 / 256)) < 1e-9
         assert rf["survey_222B"]["bytes_per_env_step"] == 222
@@ -76,7 +82,7 @@ def test_bench_two_ranks_gloo_on_one_device():
     assert d["n_gpus"] == 2 and d["steps"] % 256 == 0 and d["steps"] >= 8 * 256 and d["value"] > 0
     assert d["config"]["global_envs"] == 2 * 8192
     c = d["config"]["collective"]
-    assert "gloo SUM all_reduce" in c and f"({d['steps'] // 256} in the timed region)" in c and "StagedReplay" in c
+    assert "gloo all_gather" in c and f"({d['steps'] // 256} in the timed region)" in c and "StagedReplay" in c
     po = d["pooling"]
     assert po["mode"] == "sharded" and po["exchanges_timed"] == d["steps"] // 256
     assert po["all_gather"]["value"] > 0 and po["no_exchange"]["value"] > 0
@@ -94,3 +100,16 @@ def test_bench_self_launch_two_ranks_on_one_device():
     assert len(lines) == 1
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["pooling"]["mode"] == "sharded" and d["value"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_allreduce_exact_sampler():
+    """The previous default, kept as options: the MT-exact draws and the SUM all-reduce."""
+    env = {k: v for k, v in _two_rank_env().items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "20",
+                        "--warmup", "5", "--envs", "4096", "--exchange-segs", "1", "--sampler", "mt",
+                        "--exchange", "allreduce"],
+                       capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert d["pooling"]["exchange"] == "allreduce" and "gloo SUM all_reduce" in d["config"]["collective"]

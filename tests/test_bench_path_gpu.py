@@ -1,10 +1,10 @@
 """The bench's exact timed path under parity.
 
-``bench.py`` times 128-step segments of the BASELINE config (exp 6, 65 536
+``bench.py`` times 256-step segments of the BASELINE config (exp 6, 65 536
 envs, 500-step episodes, in-kernel auto-reset, the default refill helpers (12 288),
 ``auto_refill=False`` with the refill placed after every segment), each one
 persistent ``sacenv_boat_segment`` launch (the default ``--launch segment``) or
-one hipGraph replay of 128 ``k_step`` launches (``--launch step``). This test
+one hipGraph replay of 256 ``k_step`` launches (``--launch step``). This test
 builds that workload with bench's own ``make_workload`` and drives it with
 bench's own ``SegmentRunner`` -- ``prepare()`` (warm-up, capture, the first
 pass over the action table) and five timed-path segments -- in both modes,
@@ -42,38 +42,25 @@ def _picked(t, pick_d):
     return t.index_select(0, pick_d).cpu().numpy()
 
 
-def _same(env, ref, bookkeeping: bool) -> bool:
-    """Arena equality; without ``bookkeeping`` the refill's own scratch (which envs
-    the LAST refill ranked: masks, rank list, cons snapshot, refill count) is left
-    out -- it depends on how often the refill ran, not on what the envs did."""
-    if bookkeeping:
-        return torch.equal(env.arena, ref.arena)
-    L = env.layout
-    cut = [(int(L.refill_list), int(L.refill_list) + 16 * env.n_pad), (int(L.refill_mask), int(L.spline_g))]
-    a, b, o = env.arena, ref.arena, 0
-    for lo, hi in cut:
-        if not torch.equal(a[o:lo], b[o:lo]):
-            return False
-        o = hi
-    return torch.equal(a[o:], b[o:])
+def _same(env, ref) -> bool:
+    return torch.equal(env.arena, ref.arena)
 
 
 def test_bench_timed_path_equals_eager_and_oracle(gpu, built_lib):
     import bench
-    args_s = bench.parse(["--no-cpu-baseline", "--refill-overlap", "1"])
     args_q = bench.parse(["--no-cpu-baseline"])
     args_g = bench.parse(["--no-cpu-baseline", "--launch", "step"])
     args_e = bench.parse(["--no-cpu-baseline", "--no-graph"])
-    assert args_q.launch == "segment" and args_q.refill_overlap == 0   # the default the driver times
-    assert (args_s.envs, args_s.experiment, args_s.episode_steps, args_s.helpers) == (65536, 6, 500, None)
-    wls = [bench.make_workload(a, 0, gpu) for a in (args_s, args_q, args_g, args_e)]
+    assert args_q.launch == "segment"   # the default the driver times
+    assert (args_q.envs, args_q.experiment, args_q.episode_steps, args_q.helpers) == (65536, 6, 500, None)
+    wls = [bench.make_workload(a, 0, gpu) for a in (args_q, args_g, args_e)]
     wl_e = wls[-1]
     envs = [w.envs[0] for w in wls]
-    env_g, env_e = envs[2], envs[3]
+    env_g, env_e = envs[1], envs[2]
     assert not env_g.auto_refill and env_g.autoreset
     torch.cuda.synchronize()
     for w, env in zip(wls, envs):
-        assert torch.equal(w.actions, wl_e.actions) and _same(env, env_e, True)
+        assert torch.equal(w.actions, wl_e.actions) and _same(env, env_e)
 
     N = env_e.num_envs
     pick = np.sort(np.random.default_rng(7).choice(N, 256, replace=False))
@@ -108,38 +95,36 @@ def test_bench_timed_path_equals_eager_and_oracle(gpu, built_lib):
         if seen["phase"] == "segments":
             seen["trunc_in_segments"] += n_tr
 
-    runs = [bench.SegmentRunner(a, w, gpu) for a, w in zip((args_s, args_q, args_g, args_e), wls)]
-    names = ("segment+overlap", "segment", "graph")
-    assert [r.mode for r in runs] == ["segment", "segment", "graph", "eager"]
-    assert runs[0].overlap and not runs[1].overlap
-    for r in runs[:3]:
+    runs = [bench.SegmentRunner(a, w, gpu) for a, w in zip((args_q, args_g, args_e), wls)]
+    names = ("segment", "graph")
+    assert [r.mode for r in runs] == ["segment", "graph", "eager"]
+    for r in runs[:2]:
         r.prepare()
-    runs[3].prepare(on_step=on_step)
+    runs[2].prepare(on_step=on_step)
     torch.cuda.synchronize()
     assert all(r.first_replays == 512 for r in runs)
     for name, env in zip(names, envs):
-        assert _same(env, env_e, name != "segment+overlap"), f"{name} arena differs after prepare()"
+        assert _same(env, env_e), f"{name} arena differs after prepare()"
 
     seen["phase"] = "segments"
     refills0 = [int(env.status[0].item()) for env in envs]
     k = 0
     for s in range(N_SEGMENTS):
-        ks = [r.segment(k) for r in runs[:3]]
-        ke = runs[3].segment(k, on_step=on_step)
-        assert ks == [ke] * 3 and ke == k + bench.SEG
+        ks = [r.segment(k) for r in runs[:2]]
+        ke = runs[2].segment(k, on_step=on_step)
+        assert ks == [ke] * 2 and ke == k + bench.SEG
         k = ke
-        runs[0].drain_refills()
         torch.cuda.synchronize()
         for name, env in zip(names, envs):
-            if not _same(env, env_e, name != "segment+overlap"):
+            if not _same(env, env_e):
                 diff = torch.nonzero(env.arena != env_e.arena)[:8, 0].tolist()
                 raise AssertionError(f"{name} arena differs after segment {s} at bytes {diff}")
             for f in STATE:  # the timed-path env itself, at the segment boundary
                 assert np.abs(_picked(getattr(env, f), pick_d) - getattr(ora, f)).max() <= STATE_TOL, f
     for env in envs:
         env.check_status()
-    assert int(env_g.status[0].item()) - refills0[2] == N_SEGMENTS   # one refill per segment
-    assert int(envs[0].status[0].item()) - refills0[0] == 2 * N_SEGMENTS  # overlap: one per 64 steps
+    for r0, env in zip(refills0, envs):
+        assert int(env.status[0].item()) - r0 == N_SEGMENTS   # one refill per segment
     np.testing.assert_array_equal(_picked(env_g.counters.t().contiguous(), pick_d), ora.counters)
     assert seen["steps"] == 3 + 512 + N_SEGMENTS * bench.SEG
     assert seen["trunc_in_segments"] > 0 and seen["ended"] > 256, seen

@@ -34,7 +34,7 @@ def declared_functions():
 def test_library_exports_header(built_lib):
     from sacenv import _lib
     names = declared_functions()
-    assert len(names) == 42
+    assert len(names) == 48
     assert set(names) == set(_lib.EXPORTS)
     for n in names:
         assert hasattr(built_lib, n), n
@@ -69,6 +69,48 @@ def test_staged_sampler_argument_errors_without_gpu(built_lib):
     assert built_lib.sacenv_replay_stage_scratch_bytes(R, 1024, 256, ctypes.byref(need)) == 0
     assert need.value > 4 * 624 * 256 * 1024 / 0.95 / 624
     assert built_lib.sacenv_replay_stage_draw(R, 1, S, 300, 1024, 256, 1, 1, need.value - 1, None) == -4
+
+
+def test_counter_sampler_and_allgather_argument_errors_without_gpu(built_lib):
+    """The round-6 entry points (counter-based draws, the all-gather's pack / unpack, the
+    collective stand-in, the gather at given indices) validate on the host, never launching."""
+    from sacenv import _lib
+    rp = _lib.ReplayParams(mem_size=1_000_000, obs_dim=11, act_dim=1, reward_f32=1, terminal_mask=2)
+    sp = _lib.StagedParams(period=4096, offset=0, n=4096, n_pad=4096, seg=256, experiment=6)
+    R, S = ctypes.byref(rp), ctypes.byref(sp)
+    assert built_lib.sacenv_replay_stage_draw_ctr(R, S, 0, 1024, 256, 0, None, None, None, None) == -1
+    assert built_lib.sacenv_replay_stage_draw_ctr(R, S, 0, 1024, 257, 0, 1, None, None, None) == -4
+    assert built_lib.sacenv_replay_stage_draw_ctr(R, S, -1, 1024, 256, 0, 1, None, None, None) == -4
+    sp.period = sp.n = sp.n_pad = 64      # mem_size > seg * period
+    assert built_lib.sacenv_replay_stage_draw_ctr(R, S, 0, 1024, 256, 0, 1, None, None, None) == -5
+    sp.period = sp.n = sp.n_pad = 4096
+    assert built_lib.sacenv_replay_stage_pack(R, S, 0, 16, 16, 8, 1024, 256, 10, None, None) == -1
+    assert built_lib.sacenv_replay_stage_pack(R, S, 0, 24, 16, 8, 1024, 256, 10, 16, None) == -5  # stage align
+    cap, nb = ctypes.c_int64(), ctypes.c_int64()
+    assert built_lib.sacenv_replay_stage_chunk(R, S, 1024, 256, ctypes.byref(cap), ctypes.byref(nb)) == 0
+    assert cap.value == 1024 * 256 and nb.value >= 16 + 100 * cap.value
+    sp.period = 3 * 4096 - 1              # not world x n
+    assert built_lib.sacenv_replay_stage_chunk(R, S, 1024, 256, ctypes.byref(cap), ctypes.byref(nb)) == -5
+    assert built_lib.sacenv_replay_stage_unpack(2, 16 + 100 * 10 - 4, 10, 64, 4, 16, 16, 16, None) == -4
+    assert built_lib.sacenv_replay_stage_unpack(2, 16 + 100 * 10, 10, 64, 4, None, 16, 16, None) == -1
+    assert built_lib.sacenv_replay_stage_unpack(0, 16 + 100 * 10, 10, 64, 4, 16, 16, 16, None) == -4
+    assert built_lib.sacenv_copy_standin(16, 32, 17, 16, 0.0, None) == -4        # 16-B multiple
+    assert built_lib.sacenv_copy_standin(16, 32, 32, 0, 0.0, None) == -4         # workgroups
+    assert built_lib.sacenv_copy_standin(16, 32, 32, 16, 2e5, None) == -4        # resident time bound
+    assert built_lib.sacenv_copy_standin(None, 32, 32, 16, 1.0, None) == -1
+    assert built_lib.sacenv_copy_standin(8, 32, 32, 16, 1.0, None) == -5         # alignment
+    assert built_lib.sacenv_replay_gather(R, 1, 4, None, None, None, None, None, None, None) == -1
+
+
+def test_segment_marks_are_bounded_without_autoreset(built_lib):
+    """the segment launch stages one mark word per step in LDS (256 of them): with
+    stage marks, n_steps > SACENV_REFILL_PERIOD is refused in any autoreset mode."""
+    from sacenv.config import BoatConfig, make_params
+    p = make_params(BoatConfig(experiment=6), 64)
+    p.autoreset = 0
+    seg = built_lib.sacenv_boat_segment
+    assert seg(ctypes.byref(p), 1, 1, 64, 257, None, None, 0, None, 0, 4096, 8, None) == -4
+    assert seg(ctypes.byref(p), None, 1, 64, 256, None, None, 0, None, 0, 4096, 8, None) == -1
 
 
 def test_argument_errors_without_gpu(built_lib):

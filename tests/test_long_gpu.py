@@ -206,7 +206,7 @@ def test_long_fixture_bench_segment_runner(name, gpu, built_lib):
 
     wl = bench.Workload([env], env.step_async, env.refill, table, None, 0, E, 0, segment_step)
     run = bench.SegmentRunner(bench.parse(["--no-cpu-baseline"]), wl, gpu)
-    assert run.mode == "segment" and not run.overlap
+    assert run.mode == "segment"
     seg_state = torch.empty((n_seg, E, len(CARRIED)), dtype=torch.float64, device=gpu)
     k = 0
     for s in range(n_seg):

@@ -42,15 +42,22 @@ def _cfg(exp):
     return {"base_settings": {"experiment": exp, "test_mode": 0}, "boat_env": {"track_width": 30}}
 
 
-def _run(rank, world, exp, N, M, B, n_segs, dev, group=None):
-    """Returns (n learns checked, n skipped) on rank 0 (None elsewhere)."""
+def _run(rank, world, exp, N, M, B, n_segs, dev, group=None, sampler="mt", exchange="allreduce"):
+    """Returns (n learns checked, n skipped) on rank 0 (None elsewhere).
+
+    sampler "mt": the indices equal the reference stream's (DeviceReplayBuffer.sample
+    after every step). sampler "philox": the indices equal the CPU oracle's
+    counter-based draws (oracle/ctr_sampler.py, pinned to numpy's Philox), lie in
+    [0, min(cntr, M)), and the batch equals DeviceReplayBuffer.gather of the same
+    indices from the buffer fed every step."""
     from sacenv import VecBoatEnv
     from sacenv.replay import DeviceReplayBuffer, StagedReplay
+    import ctr_sampler
     kw = dict(seed=3, device=dev, max_episode_steps=40, n_helpers=64, auto_refill=False)
     env = VecBoatEnv(_cfg(exp), N, env_id_offset=rank * N, **kw)
     obs0 = env.reset().clone()
     rep = StagedReplay(N, env.n_pad, exp, env.first_obs_template(), rank=rank, world=world, mem_size=M,
-                       batch=B, seg=SEG, seed=5, device=dev, group=group)
+                       batch=B, seg=SEG, seed=5, device=dev, group=group, sampler=sampler, exchange=exchange)
     rep.begin(obs0)
     assert bool((env.last_term == 0).all())
     ref = ref_rb = None
@@ -82,9 +89,16 @@ def _run(rank, world, exp, N, M, B, n_segs, dev, group=None):
                 assert bool((idx == -1).all()) and not bool(st.any()), (s, k)
                 skipped += 1
                 continue
-            want = ref_rb.sample(B)
-            torch.cuda.synchronize()
-            assert torch.equal(idx, want[5]), f"segment {s} learn {k}: indices"
+            if sampler == "mt":
+                want = ref_rb.sample(B)
+                torch.cuda.synchronize()
+                assert torch.equal(idx, want[5]), f"segment {s} learn {k}: indices"
+            else:
+                drawn = ctr_sampler.draw_learn(5, s * SEG + k, B, world * N, M)
+                assert torch.equal(idx.cpu(), torch.from_numpy(drawn)), f"segment {s} learn {k}: indices"
+                assert int(idx.min()) >= 0 and int(idx.max()) < min(ref_rb.mem_cntr, M)
+                want = ref_rb.gather(idx)
+                torch.cuda.synchronize()
             for i, (x, y) in enumerate(zip((st, ac, rw, ns, tm), want[:5])):
                 assert torch.equal(x.reshape(-1), y.reshape(-1).to(x.dtype)), (s, k, i)
             checked += 1
@@ -112,6 +126,19 @@ def test_staged_replay_equals_per_step_learns(exp, N, M, B, gpu, built_lib):
     assert skipped == (1 if N < B else 0)
 
 
+@pytest.mark.parametrize("sampler,exchange,exp,N,M,B", [
+    ("philox", "allgather", 6, 3000, 50_021, 256), ("philox", "allgather", 2, 2000, 40_000, 511),
+    ("philox", "allgather", 6, 700, 20_000, 1024), ("philox", "allreduce", 5, 1500, 30_011, 300),
+    ("mt", "allgather", 6, 3000, 50_021, 256), ("philox", "allgather", 1, 300, 19_000, 700)])
+def test_staged_replay_counter_sampler_and_allgather(sampler, exchange, exp, N, M, B, gpu, built_lib):
+    """The counter-based sampler (range, skip rule, rows and terminals assembled as the
+    buffer fed every step holds them at the same indices) and the packed all-gather
+    exchange (at world 1: pack + unpack) against the literal loop."""
+    checked, skipped = _run(0, 1, exp, N, M, B, 4, gpu, sampler=sampler, exchange=exchange)
+    assert checked + skipped == 4 * SEG
+    assert skipped == -(-B // N) - 1  # learns while fewer than B rows are stored
+
+
 def test_staged_replay_refuses_a_ring_older_than_one_segment(gpu, built_lib):
     from sacenv.replay import StagedReplay
     with pytest.raises(ValueError):
@@ -126,13 +153,15 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, sampler="mt", exchange="allreduce"):
     import sys
     sys.path.insert(0, os.path.join(ROOT, "sac-agent_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        q.put((rank, _run(rank, world, 6, 1000, 30_011, 333, 3, torch.device("cuda", 0))))
+        q.put((rank, _run(rank, world, 6, 1000, 30_011, 333, 3, torch.device("cuda", 0), sampler=sampler,
+                          exchange=exchange)))
     except Exception:  # noqa: BLE001
         import traceback
         q.put((rank, traceback.format_exc()))
@@ -140,12 +169,13 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_staged_replay_two_ranks_equal_pooled_buffer(gpu, built_lib):
+@pytest.mark.parametrize("sampler,exchange", [("mt", "allreduce"), ("philox", "allgather")])
+def test_staged_replay_two_ranks_equal_pooled_buffer(sampler, exchange, gpu, built_lib):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, sampler, exchange)) for r in range(world)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=240) for _ in ps)

@@ -36,12 +36,16 @@ class StubEnv:
 
 
 class StubSampler:
-    """Stands in for StagedReplay: three row buffers, one all-reduce per segment."""
+    """Stands in for StagedReplay: three row buffers, one collective per segment (the
+    all-gather of a fixed chunk per rank, or the SUM all-reduce of the batch words)."""
 
-    def __init__(self, row_bytes, seg, batch, world, n_buffers=3):
+    def __init__(self, row_bytes, seg, batch, world, n_buffers=3, exchange="allgather"):
         self.row_bytes, self.seg, self.batch, self.world = row_bytes, seg, batch, world
+        self.exchange = exchange
         self.buffers = [torch.zeros(seg * row_bytes, dtype=torch.uint8) for _ in range(n_buffers)]
         self.words = torch.zeros(seg * batch * 26, dtype=torch.int32)
+        self.chunk = torch.zeros(-(-seg * batch // world) * 25 + 4, dtype=torch.int32)
+        self.gathered = torch.zeros(world * self.chunk.numel(), dtype=torch.int32)
         self.sampled = []
 
     def stage_args(self, g):
@@ -55,15 +59,30 @@ class StubSampler:
 
     def sample_segment(self, g):
         import torch.distributed as dist
-        self.words.fill_(g)
-        if self.world > 1:
-            dist.all_reduce(self.words)
+        if self.exchange == "allgather":
+            self.chunk.fill_(g)
+            if self.world > 1:
+                dist.all_gather(list(self.gathered.chunk(self.world)), self.chunk)
+        else:
+            self.words.fill_(g)
+            if self.world > 1:
+                dist.all_reduce(self.words)
         self.sampled.append(g)
         return []
 
     @property
     def bytes_per_segment(self):
-        return self.words.numel() * 4
+        return (self.gathered.numel() if self.exchange == "allgather" else self.words.numel()) * 4
+
+    @property
+    def bus_bytes_per_segment(self):
+        w = self.world
+        if self.exchange == "allgather":
+            return float((w - 1) * self.chunk.numel() * 4)
+        return 2.0 * (w - 1) / w * self.bytes_per_segment
+
+    def check(self):
+        pass
 
 
 def workload(bench, rank):

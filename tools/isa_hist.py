@@ -28,7 +28,7 @@ def asm_text(src=None):
     return open(out).read()
 
 
-def kernel(text, name="k_rolloutILi2ELb1ELb0E"):
+def kernel(text, name="k_rolloutILi2ELb1ELi0E"):
     lines = text.split("\n")
     start = next(i for i, l in enumerate(lines) if re.match(r"^_Z\w*%s\w*:" % name, l))
     end = next(i for i in range(start, len(lines)) if lines[i].startswith(".Lfunc_end"))
