@@ -80,12 +80,15 @@ class DeviceReplayBuffer:
         return t.to(dtype).contiguous() if t.dtype != dtype else t.contiguous()
 
     def store_batch(self, state, action, reward, new_state, code, final_state=None,
-                    last_term=None) -> None:
+                    last_term=None, graph_safe: bool = False) -> None:
         """Append n transitions (rows in order, buffer.py:13-22). ``code`` is u8:
         terminal = (terminal_mask >> code) & 1; rows with code != 0 take new_state
         from ``final_state`` if it is given. ``last_term`` (u8 [n] device tensor, in/out):
         row i's terminal follows env i's persistent last termination instead
-        (``sacenv_replay_store_env``; see ``store_env_step``)."""
+        (``sacenv_replay_store_env``; see ``store_env_step``). By default the host's
+        count goes into the launch (one launch, ``sacenv_replay_store_env_at``), which a
+        captured graph would freeze; ``graph_safe=True`` reads and advances the device
+        count instead (``sacenv_replay_store_env``: a store and an advance launch)."""
         s = self._dev(state, torch.float32)
         n = s.shape[0]
         a = self._dev(action, torch.float32).reshape(n, -1)
@@ -101,11 +104,16 @@ class DeviceReplayBuffer:
             if (lt.dtype != torch.uint8 or lt.device != self.device or lt.numel() != n
                     or not lt.is_contiguous()):
                 raise ValueError("last_term must be a contiguous u8 device tensor with one byte per row")
-        # the host issues every store, so it knows the count: one launch (sacenv.h)
-        _lib.check(self.lib.sacenv_replay_store_env_at(
-            self._pp, self.arena.data_ptr(), self.mem_cntr, n, s.data_ptr(), a.data_ptr(), r.data_ptr(),
-            ns.data_ptr(), None if fs is None else fs.data_ptr(), c.data_ptr(),
-            None if lt is None else lt.data_ptr(), self.stream))
+        if graph_safe:  # the device count, read and advanced on the device
+            _lib.check(self.lib.sacenv_replay_store_env(
+                self._pp, self.arena.data_ptr(), n, s.data_ptr(), a.data_ptr(), r.data_ptr(), ns.data_ptr(),
+                None if fs is None else fs.data_ptr(), c.data_ptr(), None if lt is None else lt.data_ptr(),
+                self.stream))
+        else:  # the host issues every store, so it knows the count: one launch (sacenv.h)
+            _lib.check(self.lib.sacenv_replay_store_env_at(
+                self._pp, self.arena.data_ptr(), self.mem_cntr, n, s.data_ptr(), a.data_ptr(), r.data_ptr(),
+                ns.data_ptr(), None if fs is None else fs.data_ptr(), c.data_ptr(),
+                None if lt is None else lt.data_ptr(), self.stream))
         self._keep = (s, a, r, ns, c, fs)
         self.mem_cntr += n
 

@@ -104,6 +104,9 @@ class VecBoatEnv:
         self._t_from_index = t_from_index(float(self.cfg.dt))
         self.index = view(L.index, i32, NP)[:N]
         self.cons = view(L.cons, i32, NP)[:N]
+        # RAW arena words (ABI 18+): bits 0..15 the MT word index, bit 16 the refill's
+        # pre-twisted mt_next flag; between a refill's draw and fit launches the index can
+        # point past 623 into mt_next. `mt_index` is the stream position a host should read.
         self.mt_pos = view(L.mt_pos, i32, NP)[:N]
         self.start_y_slots = view(L.start_y, i32, _lib.SLOTS, NP)[:, :N]
         self.counters = view(L.counters, i32, _lib.N_COUNTERS, NP)[:, :N]
@@ -155,6 +158,15 @@ class VecBoatEnv:
                                              self.stream))
 
     # ------------------------------------------------------------------ plumbing
+    @property
+    def mt_index(self) -> torch.Tensor:
+        """Each env's MT19937 stream position: the raw ``mt_pos`` word without its flag bit
+        -- the next word's index in ``mt_key``, 0..624 as numpy's ``get_state()[2]`` (624:
+        twist first). Only between a refill's draw and fit launches can it exceed 624 (the
+        draws went on into the pre-twisted ``mt_next``; the fit makes that block current).
+        Synchronise before reading it on the host."""
+        return self.mt_pos & 0xFFFF
+
     @property
     def _ptr(self) -> int:
         return self.arena.data_ptr()

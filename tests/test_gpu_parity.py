@@ -200,6 +200,7 @@ def test_refill_twists_the_next_mt_block_ahead(gpu, built_lib):
         mp = env.mt_pos.clone()
         pos = mp & 0xFFFF
         assert bool(((mp >> 16) & 1).all()) and int(pos.max()) <= 624, seg
+        assert torch.equal(env.mt_index, pos)   # the masked accessor (mt_pos is the raw word)
         wrapped += int((pos < p0).sum())
         key = env.mt_key.cpu().numpy().view(np.uint32)
         nxt = env.mt_next.cpu().numpy().view(np.uint32)

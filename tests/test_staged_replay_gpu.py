@@ -200,7 +200,8 @@ def test_bench_runner_exchange_equals_direct_staged_replay(gpu, built_lib):
     env_b = wl_b.envs[0]
     rep = StagedReplay(env_b.num_envs, env_b.n_pad, args.experiment, env_b.first_obs_template(), rank=0,
                        world=1, mem_size=args.replay_mem, batch=args.replay_batch, seg=bench.SEG, seed=0,
-                       device=gpu)
+                       device=gpu, sampler=args.sampler, exchange=args.exchange)
+    assert (args.sampler, args.exchange) == ("philox", "allgather")   # bench's defaults
     rep.begin(env_b.obs)
     k = 0
     for g in range(3):

@@ -1,10 +1,11 @@
 """Measurement for the §8(f) replay buffer: one JSON line.
 
 * store: one VecBoatEnv step's transitions (65 536 envs) appended per launch
-  pair (k_rb_store + k_rb_advance), graph-replayed; algorithmic bytes per
+  pair (k_rb_store + k_rb_advance: store_batch(graph_safe=True), the device-count
+  form a captured graph can replay -- each replay appends), graph-replayed; algorithmic bytes per
   transition = read (s 44 + a 4 + r 4 + s' 44 (+ final-obs select) + code 1)
   + write (s 44 + s' 44 + a 4 + r 8 + terminal 1) = 198 B.
-* sample: batch 1024 (original_config.yaml:20): the one-wave MT draw + gather.
+* sample: batch 1024 (original_config.yaml:20): the 1 024-thread MT draw + gather.
 Timed with HIP events on the launch stream.
 """
 import json
@@ -35,12 +36,12 @@ def main():
     side = torch.cuda.Stream()
     side.wait_stream(st)
     with torch.cuda.stream(side):
-        rb.store_batch(s, a, r, s2, code, final_state=fin)
+        rb.store_batch(s, a, r, s2, code, final_state=fin, graph_safe=True)
     st.wait_stream(side)
     torch.cuda.synchronize()
     with torch.cuda.graph(g):
         for _ in range(10):
-            rb.store_batch(s, a, r, s2, code, final_state=fin)
+            rb.store_batch(s, a, r, s2, code, final_state=fin, graph_safe=True)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     g.replay()
     torch.cuda.synchronize()
