@@ -601,8 +601,10 @@ int sacenv_replay_stage_draw_ctr(const SacenvReplayParams *p, const SacenvStaged
  * bytes (a 16-B header, 100 B per record, 256-B multiple). stage_pack: this
  * rank's rows of segment g's learns (as sacenv_replay_sample_staged reads
  * them) as 25-word records -- slot (learn x batch + draw) | terminal << 31,
- * reward f32, state [11], new_state [11], action -- behind the count; rank 0
- * (offset 0) also packs the skipped learns' all-zero rows. stage_unpack: the
+ * reward f32, state [11], new_state [11], action -- behind the count, in slot
+ * order (no atomics: the chunk's bytes are the same run to run); rank 0
+ * (offset 0) also packs the skipped learns' all-zero rows; `tiles` is device
+ * scratch of ceil(n_batches x batch / 1024) i32. stage_unpack: the
  * world chunks of an all-gather (rank r's at r x chunk_bytes) into
  * sacenv_replay_sample_staged's words, bit for bit; a count above cap sets
  * bit 0 of *status_word (device i32). */
@@ -610,7 +612,7 @@ int sacenv_replay_stage_chunk(const SacenvReplayParams *p, const SacenvStagedPar
                               int32_t n_batches, int64_t *cap_rows, int64_t *chunk_bytes);
 int sacenv_replay_stage_pack(const SacenvReplayParams *p, const SacenvStagedParams *sp, int64_t g,
                              const void *stage_cur, const void *stage_prev, const int64_t *idx, int32_t batch,
-                             int32_t n_batches, int64_t cap, void *chunk, void *stream);
+                             int32_t n_batches, int64_t cap, void *chunk, int32_t *tiles, void *stream);
 int sacenv_replay_stage_unpack(int32_t world, int64_t chunk_bytes, int64_t cap, int32_t batch, int32_t n_batches,
                                const void *gathered, uint32_t *words, int32_t *status_word, void *stream);
 /* A collective's kernel stood in for on one GPU (bench.py's N = 1 replay path):

@@ -723,23 +723,78 @@ __global__ void __launch_bounds__(256) k_rb_draw_ctr(SacenvReplayParams p, Stage
 // a chunk of `cap` records behind a 4-word header (record count); rank 0 also
 // packs the rows of skipped learns (all zero). One all-gather of the chunks and
 // an unpack on every rank rebuild sacenv_replay_sample_staged's `words`, bit for
-// bit: every slot comes from exactly one rank. Record order inside a chunk
-// follows the atomic count (not deterministic); the slot makes it irrelevant.
+// bit: every slot comes from exactly one rank. The records sit in slot order (a
+// count pass per 1 024-slot tile, then each tile's prefix over the tiles before
+// it: no atomics -- one count word taking every wave's atomic cost ~100 us a
+// segment -- and the chunk is the same bytes run to run).
 constexpr int kRecWords = 2 + 2 * SACENV_OBS_DIM + 1;  // 25
 constexpr int kChunkHdr = 4;
+constexpr int kPackTile = 1024;
 
-__global__ void __launch_bounds__(256) k_rb_pack_staged(SacenvReplayParams p, StagedGeom G, StagedRows S, int batch,
-                                                        int nb, const int64_t* __restrict__ idx,
-                                                        uint32_t* __restrict__ chunk, int64_t cap, int skip_owner) {
+// does this rank pack slot t (its row, or rank 0 a skipped learn's zero row)?
+__device__ __forceinline__ bool pack_takes(const SacenvReplayParams& p, const StagedGeom& G, int batch, int64_t t,
+                                           int64_t row, int skip_owner, int64_t* q, int64_t* u) {
+  *q = 0;
+  *u = -1;
+  if (row >= 0) resolve(row, (G.g * G.seg + t / batch + 1) * G.period, p.mem_size, G, q, u);
+  return (*u >= G.offset && *u < G.offset + G.n) || (row == -1 && skip_owner);
+}
+
+// the tile's records before this thread's (the block's waves in order): returns the
+// exclusive rank, *tile_total the tile's count
+__device__ __forceinline__ int tile_rank(bool take, int* wcnt, int* tile_total) {
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
+  const unsigned long long bal = __ballot(take);
+  if (lane == 0) wcnt[wv] = __popcll(bal);
+  __syncthreads();
+  int before = 0, total = 0;
+#pragma unroll
+  for (int w = 0; w < kPackTile / kWave; ++w) {
+    const int c = wcnt[w];
+    before += w < wv ? c : 0;
+    total += c;
+  }
+  *tile_total = total;
+  return before + __popcll(bal & ((1ull << lane) - 1ull));
+}
+
+__global__ void __launch_bounds__(kPackTile) k_rb_pack_count(SacenvReplayParams p, StagedGeom G, int batch, int nb,
+                                                             const int64_t* __restrict__ idx, int skip_owner,
+                                                             int* __restrict__ tile_cnt) {
+  __shared__ int wcnt[kPackTile / kWave];
+  const int64_t t = blockIdx.x * (int64_t)kPackTile + threadIdx.x;
+  int64_t q, u;
+  const bool take = t < (int64_t)batch * nb && pack_takes(p, G, batch, t, idx[t], skip_owner, &q, &u);
+  int total;
+  tile_rank(take, wcnt, &total);
+  if (threadIdx.x == 0) tile_cnt[blockIdx.x] = total;
+}
+
+__global__ void __launch_bounds__(kPackTile) k_rb_pack_staged(SacenvReplayParams p, StagedGeom G, StagedRows S, int batch,
+                                                              int nb, const int64_t* __restrict__ idx,
+                                                              uint32_t* __restrict__ chunk, int64_t cap, int skip_owner,
+                                                              const int* __restrict__ tile_cnt) {
   constexpr int D = SACENV_OBS_DIM;
-  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  __shared__ int wcnt[kPackTile / kWave];
+  __shared__ int s_base;
+  const int tid = threadIdx.x;
+  // this tile's first record: the counts of the tiles before it
+  if (tid < kWave) {
+    int s = 0;
+    for (int i = tid; i < (int)blockIdx.x; i += kWave) s += tile_cnt[i];
+    for (int o = kWave / 2; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (tid == 0) s_base = s;
+  }
+  const int64_t t = blockIdx.x * (int64_t)kPackTile + tid;
   const bool live = t < (int64_t)batch * nb;
-  const int b = live ? (int)(t / batch) : 0;
   const int64_t row = live ? idx[t] : -2;
-  int64_t q = 0, u = -1;
-  if (row >= 0) resolve(row, (G.g * G.seg + b + 1) * G.period, p.mem_size, G, &q, &u);
-  const bool own = u >= G.offset && u < G.offset + G.n;
-  const bool take = own || (row == -1 && skip_owner);
+  int64_t q, u;
+  const bool take = live && pack_takes(p, G, batch, t, row, skip_owner, &q, &u);
+  const bool own = take && row >= 0;
+  int tile_total;
+  const int rank = tile_rank(take, wcnt, &tile_total);  // (its barrier also publishes s_base)
+  const int64_t pos = (int64_t)s_base + rank;
+  if (blockIdx.x == gridDim.x - 1 && tid == 0) chunk[0] = (uint32_t)(s_base + tile_total);  // the record count
   float sn[16], sv[16];
 #pragma unroll
   for (int k = 0; k < 16; ++k) sn[k] = sv[k] = 0.f;
@@ -765,16 +820,7 @@ __global__ void __launch_bounds__(256) k_rb_pack_staged(SacenvReplayParams p, St
     if (G.exp2 && pdone) sv[3] = o3;
     tm = (p.terminal_mask >> ((__float_as_uint(sn[13]) >> 8) & 0xFFu)) & 1u;
   }
-  // one count atomic per wave: the wave's taken records are contiguous
-  const unsigned long long bal = __ballot(take);
-  const int lane = threadIdx.x & (kWave - 1);
-  const int lead = bal != 0ull ? __ffsll((long long)bal) - 1 : 0;
-  uint32_t base = 0u;
-  if (lane == lead && bal != 0ull) base = atomicAdd(chunk, (uint32_t)__popcll(bal));
-  base = (uint32_t)__shfl((int)base, lead);
-  if (!take) return;
-  const int64_t pos = (int64_t)base + __popcll(bal & ((1ull << lane) - 1ull));
-  if (pos >= cap) return;  // (the header's count says so; the unpack flags it)
+  if (!take || pos >= cap) return;  // (past cap: the header's count says so; the unpack flags it)
   uint32_t* const rec = chunk + kChunkHdr + pos * kRecWords;
   rec[0] = (uint32_t)t | (tm << 31);
   rec[1] = __float_as_uint(sn[11]);
@@ -1206,24 +1252,30 @@ int sacenv_replay_stage_chunk(const SacenvReplayParams* p, const SacenvStagedPar
 
 int sacenv_replay_stage_pack(const SacenvReplayParams* p, const SacenvStagedParams* sp, int64_t g,
                              const void* stage_cur, const void* stage_prev, const int64_t* idx, int32_t batch,
-                             int32_t n_batches, int64_t cap, void* chunk, void* stream) {
+                             int32_t n_batches, int64_t cap, void* chunk, int32_t* tiles, void* stream) {
   int rc = check_ctr_shape(p, sp, g, batch, n_batches);
   if (rc) return rc;
-  if (!stage_cur || !stage_prev || !idx || !chunk) return SACENV_E_NULL;
+  if (!stage_cur || !stage_prev || !idx || !chunk || !tiles) return SACENV_E_NULL;
   if (((reinterpret_cast<uintptr_t>(stage_cur) | reinterpret_cast<uintptr_t>(stage_prev)) & 15u) != 0u ||
       (reinterpret_cast<uintptr_t>(chunk) & 3u) != 0u || cap < 0)
     return SACENV_E_RANGE;
-  const hipError_t e = hipMemsetAsync(chunk, 0, 4 * kChunkHdr, (hipStream_t)stream);  // the record count
-  if (e != hipSuccess) return (int)e;
   const int64_t total = (int64_t)batch * n_batches;
-  if (total == 0) return SACENV_OK;
+  if (total == 0) {  // no records: only the count
+    const hipError_t e = hipMemsetAsync(chunk, 0, 4 * kChunkHdr, (hipStream_t)stream);
+    return e == hipSuccess ? SACENV_OK : (int)e;
+  }
   StagedRows S;
   S.cur = static_cast<const char*>(stage_cur);
   S.prev = static_cast<const char*>(stage_prev);
   for (int k = 0; k < SACENV_OBS_DIM; ++k) S.first[k] = sp->first_obs[k];
-  hipLaunchKernelGGL(k_rb_pack_staged, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                     *p, geom(p, sp, g), S, batch, n_batches, idx, static_cast<uint32_t*>(chunk), cap,
-                     sp->offset == 0 ? 1 : 0);
+  const StagedGeom G = geom(p, sp, g);
+  const int skip_owner = sp->offset == 0 ? 1 : 0;
+  const unsigned T = (unsigned)((total + kPackTile - 1) / kPackTile);
+  hipLaunchKernelGGL(k_rb_pack_count, dim3(T), dim3(kPackTile), 0, (hipStream_t)stream, *p, G, batch, n_batches, idx,
+                     skip_owner, tiles);
+  if ((rc = status())) return rc;
+  hipLaunchKernelGGL(k_rb_pack_staged, dim3(T), dim3(kPackTile), 0, (hipStream_t)stream, *p, G, S, batch, n_batches,
+                     idx, static_cast<uint32_t*>(chunk), cap, skip_owner, tiles);
   return status();
 }
 

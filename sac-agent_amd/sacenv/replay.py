@@ -384,6 +384,7 @@ class StagedReplay:
             self.cap, self.chunk_bytes = staged_chunk(self.n, self.n_pad, self.world, self.mem_size, self.batch,
                                                       self.seg, experiment)
             self._chunks = [torch.empty(self.chunk_bytes, dtype=torch.uint8, device=self.device) for _ in range(2)]
+            self._tiles = torch.empty(-(-self.seg * self.batch // 1024), dtype=torch.int32, device=self.device)
             self._gathered = ([torch.empty(self.world * self.chunk_bytes, dtype=torch.uint8, device=self.device)
                                for _ in range(2)] if self.world > 1 else self._chunks)
         self.standin = dict(standin) if standin is not None else None
@@ -460,7 +461,7 @@ class StagedReplay:
             chunk = self._chunks[g % 2]
             _lib.check(self.lib.sacenv_replay_stage_pack(
                 self._pp, self._spp, g, self.stage[g % nb].data_ptr(), self.stage[(g - 1) % nb].data_ptr(),
-                idx.data_ptr(), self.batch, self.seg, self.cap, chunk.data_ptr(), self.stream))
+                idx.data_ptr(), self.batch, self.seg, self.cap, chunk.data_ptr(), self._tiles.data_ptr(), self.stream))
             gathered = self._gathered[g % 2]
             if self.world > 1:
                 all_gather_bytes(gathered, chunk, self.group)

@@ -84,8 +84,9 @@ def test_counter_sampler_and_allgather_argument_errors_without_gpu(built_lib):
     sp.period = sp.n = sp.n_pad = 64      # mem_size > seg * period
     assert built_lib.sacenv_replay_stage_draw_ctr(R, S, 0, 1024, 256, 0, 1, None, None, None) == -5
     sp.period = sp.n = sp.n_pad = 4096
-    assert built_lib.sacenv_replay_stage_pack(R, S, 0, 16, 16, 8, 1024, 256, 10, None, None) == -1
-    assert built_lib.sacenv_replay_stage_pack(R, S, 0, 24, 16, 8, 1024, 256, 10, 16, None) == -5  # stage align
+    assert built_lib.sacenv_replay_stage_pack(R, S, 0, 16, 16, 8, 1024, 256, 10, None, 4, None) == -1
+    assert built_lib.sacenv_replay_stage_pack(R, S, 0, 16, 16, 8, 1024, 256, 10, 16, None, None) == -1
+    assert built_lib.sacenv_replay_stage_pack(R, S, 0, 24, 16, 8, 1024, 256, 10, 16, 4, None) == -5  # stage align
     cap, nb = ctypes.c_int64(), ctypes.c_int64()
     assert built_lib.sacenv_replay_stage_chunk(R, S, 1024, 256, ctypes.byref(cap), ctypes.byref(nb)) == 0
     assert cap.value == 1024 * 256 and nb.value >= 16 + 100 * cap.value
