@@ -740,6 +740,8 @@ class SegmentRunner:
         if own:
             eb.record(self.st)
             self.seg_events.append((ea, eb, SEG))
+        if x is not None:
+            x.launched()
         self.wl.refill()
         if p is not None and self.pool_every == SEG:
             p.fill = SEG

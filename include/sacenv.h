@@ -297,11 +297,14 @@ int sacenv_boat_rollout(const SacenvBoatParams *p, void *arena, const float *act
  * step), obs3_next f32 (experiment 2), 0 -- written only where bit e % 64 of
  * stage_marks[ks * n_pad / 64 + e / 64] is set (sacenv_replay_stage_mark: the rows
  * a learn will sample; stage_marks == NULL: every row; with stage_marks, n_steps <=
- * SACENV_REFILL_PERIOD in any mode, else SACENV_E_SIZE). Counts as n_steps step
+ * SACENV_REFILL_PERIOD in any mode, else SACENV_E_SIZE). The launch CONSUMES the
+ * marks: it clears the words it read (steps 0..n_steps-1), so the next draws into
+ * the buffer start from zero (round 6; a stale mark would only write one more
+ * row). Counts as n_steps step
  * launches for the refill contract (autoreset: n_steps <= SACENV_REFILL_PERIOD). */
 int sacenv_boat_segment(const SacenvBoatParams *p, void *arena, const float *actions, int64_t action_stride,
                         int32_t n_steps, const uint32_t *act_ready, uint32_t *step_done, uint32_t seq0,
-                        void *trans, int64_t trans_stride, void *stage, const uint64_t *stage_marks,
+                        void *trans, int64_t trans_stride, void *stage, uint64_t *stage_marks,
                         void *stream);
 
 /* Co-residency data for the closed loop (main.py:70-91 on the device): the
@@ -589,9 +592,10 @@ int sacenv_replay_gather(const SacenvReplayParams *p, void *arena, int32_t batch
  * one parallel launch with no sequential chain, in any order, for any g. The
  * same thread marks the rows it draws on this rank and their predecessors:
  * rows of segment g in marks_cur, of segment g - 1 in marks_prev (u64
- * [seg][n_pad/64] each, nullable, NOT cleared: the caller clears a segment's
- * marks before the first draw that marks it). Drawing segments g and g + 1
- * completes segment g's marks (sacenv_replay_stage_mark's set). */
+ * [seg][n_pad/64] each, nullable, NOT cleared: a segment's marks start from zero --
+ * cleared by the caller, or by the sacenv_boat_segment launch that consumed them
+ * last). Drawing segments g and g + 1 completes segment g's marks
+ * (sacenv_replay_stage_mark's set). */
 int sacenv_replay_stage_draw_ctr(const SacenvReplayParams *p, const SacenvStagedParams *sp, int64_t g,
                                  int32_t batch, int32_t n_batches, uint64_t seed, int64_t *idx,
                                  uint64_t *marks_prev, uint64_t *marks_cur, void *stream);
@@ -604,7 +608,7 @@ int sacenv_replay_stage_draw_ctr(const SacenvReplayParams *p, const SacenvStaged
  * reward f32, state [11], new_state [11], action -- behind the count, in slot
  * order (no atomics: the chunk's bytes are the same run to run); rank 0
  * (offset 0) also packs the skipped learns' all-zero rows; `tiles` is device
- * scratch of ceil(n_batches x batch / 1024) i32. stage_unpack: the
+ * scratch of ceil(n_batches x batch / 256) i32. stage_unpack: the
  * world chunks of an all-gather (rank r's at r x chunk_bytes) into
  * sacenv_replay_sample_staged's words, bit for bit; a count above cap sets
  * bit 0 of *status_word (device i32). */

@@ -1875,7 +1875,7 @@ struct RollArgs {
   // staged replay rows (kRows == 2): env e's 64-B row of step ks at stage + (ks * n_pad + e) * 64,
   // written where bit (e % 64) of marks[ks * n_pad / 64 + e / 64] is set (marks == null: every row)
   char* stage;
-  const unsigned long long* marks;
+  unsigned long long* marks;  // (consumed: the launch clears the words it read)
   int64_t act_stride;     // floats between consecutive action rows
   // Action hand-off (sacenv_boat_segment): owner wave w steps ks only once
   // ready[w] >= seq0 + ks + 1, and publishes done[w] = seq0 + ks + 1 once step
@@ -2059,7 +2059,13 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   // LDS once (a per-step global load would sit in the loop's vmcnt accounting, and the
   // step's first full wait would expose its ~1-us latency every step)
   if (kRoll && kRows == 2 && ra->marks != nullptr) {
-    for (int q = lane; q < n_steps; q += kWave) l.mk[q] = ra->marks[(int64_t)q * A.nwaves() + ob];
+    // the launch consumes its marks: each word is read by this wave alone and cleared, so
+    // the staged replay's next draws into this buffer start from zero (no fill kernel)
+    for (int q = lane; q < n_steps; q += kWave) {
+      unsigned long long* const w = ra->marks + (int64_t)q * A.nwaves() + ob;
+      l.mk[q] = *w;
+      *w = 0ull;
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -2920,7 +2926,7 @@ int sacenv_boat_rollout(const SacenvBoatParams* p, void* arena, const float* act
 
 int sacenv_boat_segment(const SacenvBoatParams* p, void* arena, const float* actions, int64_t action_stride,
                         int32_t n_steps, const uint32_t* act_ready, uint32_t* step_done, uint32_t seq0,
-                        void* trans, int64_t trans_stride, void* stage, const uint64_t* stage_marks,
+                        void* trans, int64_t trans_stride, void* stage, uint64_t* stage_marks,
                         void* stream) {
   int rc = check_params(p);
   if (rc) return rc;
@@ -2945,7 +2951,7 @@ int sacenv_boat_segment(const SacenvBoatParams* p, void* arena, const float* act
   ra.trans = static_cast<char*>(trans);
   ra.trans_stride = trans_stride;
   ra.stage = static_cast<char*>(stage);
-  ra.marks = reinterpret_cast<const unsigned long long*>(stage_marks);
+  ra.marks = reinterpret_cast<unsigned long long*>(stage_marks);
   ra.act_stride = action_stride;
   ra.ready = act_ready;
   ra.done = step_done;

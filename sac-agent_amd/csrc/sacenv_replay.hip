@@ -729,7 +729,14 @@ __global__ void __launch_bounds__(256) k_rb_draw_ctr(SacenvReplayParams p, Stage
 // segment -- and the chunk is the same bytes run to run).
 constexpr int kRecWords = 2 + 2 * SACENV_OBS_DIM + 1;  // 25
 constexpr int kChunkHdr = 4;
-constexpr int kPackTile = 1024;
+constexpr int kPackTile = 256;
+// The side kernels of the staged exchange (draws, marks, pack, unpack, gather) run
+// beside a persistent segment launch, whose owner waves each need ~336 of a SIMD's
+// 512 VGPRs: a side kernel holding a SIMD when the launch dispatches would delay that
+// owner wave, and the launch ends with its slowest wave. Each side workgroup (256
+// threads: one wave per SIMD, <= 88 VGPRs) reserves this much LDS, so a CU holds at
+// most two of them -- and the owner waves fit beside them whatever the dispatch order.
+constexpr size_t kSideLds = 64 * 1024;
 
 // does this rank pack slot t (its row, or rank 0 a skipped learn's zero row)?
 __device__ __forceinline__ bool pack_takes(const SacenvReplayParams& p, const StagedGeom& G, int batch, int64_t t,
@@ -1133,7 +1140,7 @@ int sacenv_replay_stage_mark(const SacenvReplayParams* p, const SacenvStagedPara
   if (per == 0) return SACENV_OK;
   // without the next segment's draws, only this segment's learns mark
   const int64_t total = idx_next != nullptr ? 2 * per : per;
-  hipLaunchKernelGGL(k_rb_stage_mark, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(k_rb_stage_mark, dim3((unsigned)((total + 255) / 256)), dim3(256), kSideLds, (hipStream_t)stream,
                      *p, geom(p, sp, g), idx_g, idx_next != nullptr ? idx_next : idx_g, batch, n_batches,
                      reinterpret_cast<unsigned long long*>(marks), total);
   return status();
@@ -1156,7 +1163,7 @@ int sacenv_replay_sample_staged(const SacenvReplayParams* p, const SacenvStagedP
   for (int k = 0; k < SACENV_OBS_DIM; ++k) S.first[k] = sp->first_obs[k];
   const int64_t total = (int64_t)batch * n_batches;
   const int64_t per = (int64_t)batch * (2 * SACENV_OBS_DIM + 1 + 3);
-  hipLaunchKernelGGL(k_rb_gather_staged, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(k_rb_gather_staged, dim3((unsigned)((total + 255) / 256)), dim3(256), kSideLds, (hipStream_t)stream,
                      *p, geom(p, sp, g), S, batch, n_batches, idx, words, per);
   return status();
 }
@@ -1192,7 +1199,7 @@ int sacenv_replay_stage_draw_ctr(const SacenvReplayParams* p, const SacenvStaged
   if (idx == nullptr) return SACENV_E_NULL;
   const int64_t total = (int64_t)batch * n_batches;
   if (total == 0) return SACENV_OK;
-  hipLaunchKernelGGL(k_rb_draw_ctr, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *p,
+  hipLaunchKernelGGL(k_rb_draw_ctr, dim3((unsigned)((total + 255) / 256)), dim3(256), kSideLds, (hipStream_t)stream, *p,
                      geom(p, sp, g), seed, batch, n_batches, idx, reinterpret_cast<unsigned long long*>(marks_prev),
                      reinterpret_cast<unsigned long long*>(marks_cur));
   return status();
@@ -1271,10 +1278,10 @@ int sacenv_replay_stage_pack(const SacenvReplayParams* p, const SacenvStagedPara
   const StagedGeom G = geom(p, sp, g);
   const int skip_owner = sp->offset == 0 ? 1 : 0;
   const unsigned T = (unsigned)((total + kPackTile - 1) / kPackTile);
-  hipLaunchKernelGGL(k_rb_pack_count, dim3(T), dim3(kPackTile), 0, (hipStream_t)stream, *p, G, batch, n_batches, idx,
+  hipLaunchKernelGGL(k_rb_pack_count, dim3(T), dim3(kPackTile), kSideLds, (hipStream_t)stream, *p, G, batch, n_batches, idx,
                      skip_owner, tiles);
   if ((rc = status())) return rc;
-  hipLaunchKernelGGL(k_rb_pack_staged, dim3(T), dim3(kPackTile), 0, (hipStream_t)stream, *p, G, S, batch, n_batches,
+  hipLaunchKernelGGL(k_rb_pack_staged, dim3(T), dim3(kPackTile), kSideLds, (hipStream_t)stream, *p, G, S, batch, n_batches,
                      idx, static_cast<uint32_t*>(chunk), cap, skip_owner, tiles);
   return status();
 }
@@ -1289,7 +1296,7 @@ int sacenv_replay_stage_unpack(int32_t world, int64_t chunk_bytes, int64_t cap, 
   const int64_t n = (int64_t)world * cap;
   if (n == 0 || batch == 0) return SACENV_OK;
   const int64_t per = (int64_t)batch * (2 * SACENV_OBS_DIM + 1 + 3);
-  hipLaunchKernelGGL(k_rb_unpack_staged, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(k_rb_unpack_staged, dim3((unsigned)((n + 255) / 256)), dim3(256), kSideLds, (hipStream_t)stream,
                      static_cast<const uint32_t*>(gathered), world, chunk_bytes / 4, cap, batch, words, per,
                      status_word);
   return status();

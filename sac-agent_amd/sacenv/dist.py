@@ -278,80 +278,121 @@ def shard_owner(rows, cntr: int, mem_size: int, period: int, n_per_rank: int):
 
 
 class SegmentExchange:
-    """The replay exchange of a segment, run on a side stream while the next segment steps.
+    """The replay exchange of the persistent segments (StagedReplay), run beside them.
 
-    ``sampler`` is a ``sacenv.replay.StagedReplay`` (or anything with ``begin(obs)``,
-    ``stage_args(g)``, ``prepare(g)`` and ``sample_segment(g)``). Per segment g:
-    ``before()`` makes the stepping stream wait for the marks of segment g's rows and
-    for ``sample_segment(g - 2)`` (its gather still reads the buffer segment g is about
-    to overwrite); the launch writes its rows (``stage_args()``); ``after()`` enqueues on
-    the side stream, without waiting for the launch, the next segment's draws and marks
-    (``prepare(g + 1)``), then -- behind the launch -- the segment's batches: the gather
-    and the one SUM all-reduce over the ranks. So the draws, the gather and the
-    collective all overlap the next segment. Segments are counted from ``start`` (the
-    replay buffer starts empty there). ``check()`` after a timed region raises on a
-    segment the sampler flagged invalid."""
+    A segment launch's owner waves need ~336 VGPRs each, one per SIMD: a side kernel
+    holding a SIMD when the launch dispatches delays that owner wave, and the launch ends
+    with its slowest wave; a side chain the launch must wait for sits on the critical
+    path (round 6 measured both). So the side work of segment g runs in a WINDOW that
+    no launch waits for until segment g + 2:
+
+    - ``side`` (high priority, behind launch g's END -- ``launched()``'s event -- so
+      beside refill g and launch g + 1): the unpack of segment g - 1 (its collective is
+      done), the pack of segment g's share (``pack_segment``), and ``prepare(g + 2)``:
+      the draws of segment g + 3 and segment g + 2's marks. Its end event is what launch
+      g + 2 waits for (``before()``): the marks it reads, and the pack of segment g that
+      read the stage buffer launch g + 2 overwrites. The side kernels reserve LDS so a
+      CU holds at most two of their workgroups (the owner waves always fit beside them);
+    - ``coll`` (high priority): the collective of segment g behind its pack
+      (``collect_segment``: the all-gather or the all-reduce; at one rank the stand-in,
+      if any), overlapped with launch g + 1.
+
+    Segment g's batches (``last``) land in the next window (``wait()`` unpacks the one
+    still pending). The high-priority streams come from a separate pool of hardware
+    queues, so no side kernel queues behind a launch in the stepping stream's queue.
+    ``sampler`` is a ``sacenv.replay.StagedReplay`` or anything with its methods; on the
+    CPU (no streams) everything runs in order. ``check()`` after a timed region raises on
+    a segment the sampler flagged invalid."""
 
     def __init__(self, sampler, device):
         self.sampler = sampler
         self.device = torch.device(device)
         self.cuda = self.device.type == "cuda"
-        self.side = torch.cuda.Stream(device=self.device) if self.cuda else None
+        if self.cuda:
+            hi = torch.cuda.Stream.priority_range()[1]   # (low, high): the highest priority
+            self.side = torch.cuda.Stream(device=self.device, priority=hi)
+            self.coll = torch.cuda.Stream(device=self.device, priority=hi)
         self.g = 0               # segments exchanged so far
         self.started = False
-        self._done = {}
-        self._ready = {}
+        self._ready = {}         # segment -> events its launch waits for
+        self._pending = None     # (segment, its collective's event): packed, not unpacked yet
+        self._launched = None
         self.exchanges = 0
-        self.last = None         # the batches of the latest segment
+        self.last = None         # the batches of the latest unpacked segment
 
     def _cur(self):
         return torch.cuda.current_stream(self.device) if self.cuda else None
+
+    def _record(self, stream):
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        return ev
 
     def start(self, obs: torch.Tensor) -> None:
         """The obs every env starts from (the s of the first stored transition); the
         first segments' draws and marks, on the stepping stream."""
         self.sampler.begin(obs)
         if self.cuda:
-            # the side stream's first prepare() continues the sampling stream begin()'s
-            # draws advance on this stream: it must not run ahead of them
-            self.side.wait_stream(self._cur())
-        self.started, self.g = True, 0
+            # the side streams continue the sampling stream begin()'s draws advance on this
+            # stream: they must not run ahead of them
+            for st in (self.side, self.coll):
+                st.wait_stream(self._cur())
+        self.started, self.g, self._pending = True, 0, None
 
     def stage_args(self) -> dict:
         """The row arguments of the segment about to be stepped."""
         return self.sampler.stage_args(self.g)
 
     def before(self) -> None:
-        for ev in (self._done.pop(self.g - 2, None), self._ready.pop(self.g, None)):
-            if ev is not None:
-                self._cur().wait_event(ev)
+        """The stepping stream waits for the window of segment g - 2 (the next launch's
+        marks; the pack that read the stage buffer it overwrites)."""
+        for ev in self._ready.pop(self.g, ()):
+            self._cur().wait_event(ev)
+
+    def launched(self) -> None:
+        """Right after the segment launch was enqueued (before its refill)."""
+        if self.cuda:
+            self._launched = self._record(self._cur())
+
+    def _unpack_pending(self) -> None:
+        g, ev_c = self._pending
+        if self.cuda:
+            self.side.wait_event(ev_c)
+        self.last = self.sampler.unpack_segment(g)
+        self._pending = None
 
     def after(self) -> None:
         g = self.g
-        if self.cuda:
-            with torch.cuda.stream(self.side):
-                self.sampler.prepare(g + 1)       # independent of the launch: overlaps it
-                ev = torch.cuda.Event()
-                ev.record(self.side)
-            self._ready[g + 1] = ev
-            self.side.wait_stream(self._cur())
-            with torch.cuda.stream(self.side):
-                self.last = self.sampler.sample_segment(g)
-                ev = torch.cuda.Event()
-                ev.record(self.side)
-            self._done[g] = ev
-        else:
-            self.sampler.prepare(g + 1)
+        if not self.cuda:
+            self.sampler.prepare(g + 2)
             self.last = self.sampler.sample_segment(g)
+        else:
+            launched = self._launched if self._launched is not None else self._record(self._cur())
+            self._launched = None
+            with torch.cuda.stream(self.side):
+                self.side.wait_event(launched)
+                if self._pending is not None:
+                    self._unpack_pending()
+                self.sampler.pack_segment(g)
+                packed = self._record(self.side)
+                self.sampler.prepare(g + 2)
+                self._ready[g + 2] = [self._record(self.side)]
+            with torch.cuda.stream(self.coll):
+                self.coll.wait_event(packed)
+                self.sampler.collect_segment(g)
+                self._pending = (g, self._record(self.coll))
         self.g += 1
         self.exchanges += 1
 
     def wait(self) -> None:
-        """The stepping stream waits for every exchange in flight."""
+        """Unpack the segment still pending; the stepping stream waits for every exchange
+        in flight."""
         if self.cuda:
-            for ev in list(self._done.values()) + list(self._ready.values()):
-                self._cur().wait_event(ev)
-        self._done.clear()
+            if self._pending is not None:
+                with torch.cuda.stream(self.side):
+                    self._unpack_pending()
+            for st in (self.side, self.coll):
+                self._cur().wait_stream(st)
         self._ready.clear()
 
     def check(self) -> None:

@@ -289,11 +289,12 @@ class StagedReplay:
     bit, on every rank (tests/test_staged_replay_gpu.py). ~27 MB cross the links per
     256-step segment at batch 1 024, whatever the world size.
 
-    Order per segment g (``begin`` did draws 0 and 1 and the marks of segment 0):
-    ``stage_args(g)`` -> the launch -> ``prepare(g + 1)`` -> ``sample_segment(g)``.
-    Buffers: the staged rows of segment g are read by ``sample_segment(g)`` and
-    ``(g + 1)``, so the launch of segment g + 2 (3 buffers) must follow
-    ``sample_segment(g)`` in stream order (``sacenv.dist.SegmentExchange`` arranges it).
+    Order per segment g (``begin`` did the draws of segments 0-2 and the marks of 0 and
+    1): ``stage_args(g)`` -> the launch -> ``prepare(g + 1)`` (or up to ``g + 2``) ->
+    ``sample_segment(g)``. Buffers: the staged rows of segment g are read by
+    ``sample_segment(g)`` and ``(g + 1)``, so the launch of segment g + 2 (3 buffers)
+    must follow ``sample_segment(g)`` in stream order; a launch consumes (clears) its
+    marks (``sacenv.dist.SegmentExchange`` arranges the streams).
 
     ``sampler``: ``"mt"`` (default) draws every learn from the buffer's one MT19937
     stream exactly as the reference's ``np.random.choice`` would (the parity mode:
@@ -384,7 +385,7 @@ class StagedReplay:
             self.cap, self.chunk_bytes = staged_chunk(self.n, self.n_pad, self.world, self.mem_size, self.batch,
                                                       self.seg, experiment)
             self._chunks = [torch.empty(self.chunk_bytes, dtype=torch.uint8, device=self.device) for _ in range(2)]
-            self._tiles = torch.empty(-(-self.seg * self.batch // 1024), dtype=torch.int32, device=self.device)
+            self._tiles = torch.empty(-(-self.seg * self.batch // 256), dtype=torch.int32, device=self.device)
             self._gathered = ([torch.empty(self.world * self.chunk_bytes, dtype=torch.uint8, device=self.device)
                                for _ in range(2)] if self.world > 1 else self._chunks)
         self.standin = dict(standin) if standin is not None else None
@@ -402,10 +403,10 @@ class StagedReplay:
     def _draw(self) -> None:
         g = self.drawn
         if self.sampler == "philox":
-            # segment g's draws, marking its rows in segments g - 1 and g: segment g's marks
-            # start here (cleared), segment g - 1's are complete after it
+            # segment g's draws, marking its rows in segments g - 1 and g (segment g - 1's
+            # marks are complete after it). The buffer is zero: the launch that read it last
+            # (segment g - 3) cleared it, and begin() clears all three
             nb = self.N_BUFFERS
-            self.marks[g % nb].zero_()
             _lib.check(self.lib.sacenv_replay_stage_draw_ctr(
                 self._pp, self._spp, g, self.batch, self.seg, self.seed & 0xFFFFFFFFFFFFFFFF,
                 self._idx[g % 4].data_ptr(), self.marks[(g - 1) % nb].data_ptr() if g > 0 else None,
@@ -431,10 +432,11 @@ class StagedReplay:
         last = self.stage[(-1) % nb][(self.seg - 1) * self.n_pad * 64:].view(torch.float32).view(self.n_pad, 16)
         last.zero_()
         last[: self.n, : _lib.OBS_DIM].copy_(obs.to(device=self.device, dtype=torch.float32))
+        for m in self.marks:
+            m.zero_()
         self.drawn = 0
-        self._draw()
-        self._draw()
-        self._mark(0)
+        self.prepare(0)
+        self.prepare(1)   # (segment 1's marks too: its launch may follow before another prepare)
 
     def stage_args(self, g: int) -> dict:
         """The staged-row arguments of segment g's launch (VecBoatEnv.segment_async /
@@ -442,8 +444,9 @@ class StagedReplay:
         return {"stage": self.stage[g % self.N_BUFFERS], "marks": self.marks[g % self.N_BUFFERS]}
 
     def prepare(self, g: int) -> None:
-        """Before segment g steps (after segment g - 1 was launched): draw segment g+1's
-        learns and mark segment g's rows."""
+        """Any time before segment g's launch (after segment g - 3's, whose buffers it
+        reuses): draw the learns up to segment g + 1 and complete segment g's marks.
+        ``sacenv.dist.SegmentExchange`` calls ``prepare(g + 2)`` after launch g."""
         while self.drawn < g + 2:
             self._draw()
         self._mark(g)
@@ -451,39 +454,54 @@ class StagedReplay:
     def sample_segment(self, g: int):
         """Enqueue segment g's learns' batches (after its launch, on this stream); returns
         [(state, action, reward f64, new_state, terminal int32 0/1, idx)], one per learn,
-        views valid until ``sample_segment(g + 2)``."""
-        import torch.distributed as dist
+        views valid until ``sample_segment(g + 2)``. = ``pack_segment(g)``,
+        ``collect_segment(g)``, ``unpack_segment(g)`` on one stream."""
+        self.pack_segment(g)
+        self.collect_segment(g)
+        return self.unpack_segment(g)
+
+    def pack_segment(self, g: int) -> None:
+        """This rank's share of segment g's batches, from the staged rows of segments g
+        and g - 1 (after segment g's launch): the packed chunk of its rows (all-gather), or
+        its rows in the batch words with the others' zero (all-reduce)."""
         g = int(g)
-        words = self._words[g % 2][0]
         idx = self._idx[g % 4]
         nb = self.N_BUFFERS
+        cur, prev = self.stage[g % nb].data_ptr(), self.stage[(g - 1) % nb].data_ptr()
         if self.exchange == "allgather":
-            chunk = self._chunks[g % 2]
             _lib.check(self.lib.sacenv_replay_stage_pack(
-                self._pp, self._spp, g, self.stage[g % nb].data_ptr(), self.stage[(g - 1) % nb].data_ptr(),
-                idx.data_ptr(), self.batch, self.seg, self.cap, chunk.data_ptr(), self._tiles.data_ptr(), self.stream))
-            gathered = self._gathered[g % 2]
-            if self.world > 1:
-                all_gather_bytes(gathered, chunk, self.group)
-            elif self.standin is not None:
-                sd = self.standin
-                _lib.check(self.lib.sacenv_copy_standin(
-                    self._standin_src.data_ptr(), self._standin_dst.data_ptr(), sd["bytes"], int(sd["workgroups"]),
-                    float(sd["us"]), self.stream))
-            _lib.check(self.lib.sacenv_replay_stage_unpack(
-                self.world, self.chunk_bytes, self.cap, self.batch, self.seg, gathered.data_ptr(), words.data_ptr(),
-                self._status.data_ptr(), self.stream))
-            return self._batches[g % 2, g % 4]
-        _lib.check(self.lib.sacenv_replay_sample_staged(
-            self._pp, self._spp, g, self.stage[g % nb].data_ptr(), self.stage[(g - 1) % nb].data_ptr(),
-            idx.data_ptr(), self.batch, self.seg, words.data_ptr(), self.stream))
+                self._pp, self._spp, g, cur, prev, idx.data_ptr(), self.batch, self.seg, self.cap,
+                self._chunks[g % 2].data_ptr(), self._tiles.data_ptr(), self.stream))
+        else:
+            _lib.check(self.lib.sacenv_replay_sample_staged(
+                self._pp, self._spp, g, cur, prev, idx.data_ptr(), self.batch, self.seg,
+                self._words[g % 2][0].data_ptr(), self.stream))
+
+    def collect_segment(self, g: int) -> None:
+        """The collective over the ranks of segment g's packed share (world > 1): the
+        all-gather of the chunks or the SUM all-reduce of the words; at world 1 the
+        stand-in for it, if one was asked for."""
+        import torch.distributed as dist
+        g = int(g)
         if self.world > 1:
-            dist.all_reduce(words, op=dist.ReduceOp.SUM, group=self.group)
+            if self.exchange == "allgather":
+                all_gather_bytes(self._gathered[g % 2], self._chunks[g % 2], self.group)
+            else:
+                dist.all_reduce(self._words[g % 2][0], op=dist.ReduceOp.SUM, group=self.group)
         elif self.standin is not None:
             sd = self.standin
             _lib.check(self.lib.sacenv_copy_standin(
                 self._standin_src.data_ptr(), self._standin_dst.data_ptr(), sd["bytes"], int(sd["workgroups"]),
                 float(sd["us"]), self.stream))
+
+    def unpack_segment(self, g: int):
+        """Segment g's batches from the collected chunks (all-gather; the all-reduce's words
+        are the batches already): the views ``sample_segment`` returns."""
+        g = int(g)
+        if self.exchange == "allgather":
+            _lib.check(self.lib.sacenv_replay_stage_unpack(
+                self.world, self.chunk_bytes, self.cap, self.batch, self.seg, self._gathered[g % 2].data_ptr(),
+                self._words[g % 2][0].data_ptr(), self._status.data_ptr(), self.stream))
         return self._batches[g % 2, g % 4]
 
     @property

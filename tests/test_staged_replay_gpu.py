@@ -72,11 +72,12 @@ def _run(rank, world, exp, N, M, B, n_segs, dev, group=None, sampler="mt", excha
         acts = torch.rand((SEG, world * N), generator=g, device=dev) * 2 - 1
         mine = acts[:, rank * N:(rank + 1) * N].contiguous()
         sa = rep.stage_args(s)
+        written += _popcount(sa["marks"])   # (complete before the launch, which consumes them)
         env.segment_async(mine, SEG, stage=sa["stage"], stage_marks=sa["marks"])
         env.refill()
         rep.prepare(s + 1)
         got = rep.sample_segment(s)
-        written += _popcount(sa["marks"])
+        assert _popcount(rep.stage_args(s)["marks"]) == 0   # the launch cleared the marks it read
         if ref is None:
             continue
         for k in range(SEG):
