@@ -595,10 +595,13 @@ int sacenv_replay_gather(const SacenvReplayParams *p, void *arena, int32_t batch
  * [seg][n_pad/64] each, nullable, NOT cleared: a segment's marks start from zero --
  * cleared by the caller, or by the sacenv_boat_segment launch that consumed them
  * last). Drawing segments g and g + 1 completes segment g's marks
- * (sacenv_replay_stage_mark's set). */
+ * (sacenv_replay_stage_mark's set). tiles (nullable, i32 [ceil(n_batches x
+ * batch / 256)]): the records per 256-slot tile this rank's
+ * sacenv_replay_stage_pack of segment g will write (pass them there with
+ * counted = 1: no count pass). */
 int sacenv_replay_stage_draw_ctr(const SacenvReplayParams *p, const SacenvStagedParams *sp, int64_t g,
                                  int32_t batch, int32_t n_batches, uint64_t seed, int64_t *idx,
-                                 uint64_t *marks_prev, uint64_t *marks_cur, void *stream);
+                                 uint64_t *marks_prev, uint64_t *marks_cur, int32_t *tiles, void *stream);
 /* The ALL-GATHER form of the staged exchange. stage_chunk: the record capacity
  * of one rank's chunk (the most records any rank packs in expectation over any
  * segment + 8 standard deviations + 64; every slot at one rank) and the chunk's
@@ -608,7 +611,8 @@ int sacenv_replay_stage_draw_ctr(const SacenvReplayParams *p, const SacenvStaged
  * reward f32, state [11], new_state [11], action -- behind the count, in slot
  * order (no atomics: the chunk's bytes are the same run to run); rank 0
  * (offset 0) also packs the skipped learns' all-zero rows; `tiles` is device
- * scratch of ceil(n_batches x batch / 256) i32. stage_unpack: the
+ * scratch of ceil(n_batches x batch / 256) i32 (counted = 1: it holds the tile
+ * counts sacenv_replay_stage_draw_ctr wrote for segment g). stage_unpack: the
  * world chunks of an all-gather (rank r's at r x chunk_bytes) into
  * sacenv_replay_sample_staged's words, bit for bit; a count above cap sets
  * bit 0 of *status_word (device i32). */
@@ -616,7 +620,8 @@ int sacenv_replay_stage_chunk(const SacenvReplayParams *p, const SacenvStagedPar
                               int32_t n_batches, int64_t *cap_rows, int64_t *chunk_bytes);
 int sacenv_replay_stage_pack(const SacenvReplayParams *p, const SacenvStagedParams *sp, int64_t g,
                              const void *stage_cur, const void *stage_prev, const int64_t *idx, int32_t batch,
-                             int32_t n_batches, int64_t cap, void *chunk, int32_t *tiles, void *stream);
+                             int32_t n_batches, int64_t cap, void *chunk, int32_t *tiles, int32_t counted,
+                             void *stream);
 int sacenv_replay_stage_unpack(int32_t world, int64_t chunk_bytes, int64_t cap, int32_t batch, int32_t n_batches,
                                const void *gathered, uint32_t *words, int32_t *status_word, void *stream);
 /* A collective's kernel stood in for on one GPU (bench.py's N = 1 replay path):

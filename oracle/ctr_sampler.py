@@ -8,11 +8,12 @@ i.e. `batch` ring rows uniform with replacement, and skips the learn while fewer
 than `batch` rows are stored (agent/continuous_agent.py:97-98). The counter-based
 sampler keeps that distribution and that skip rule but takes its words from
 Philox4x64-10 instead of the one MT19937 stream: draw i of global learn L (after
-L + 1 pooled steps, c = (L + 1) x period rows stored) is the first of the four
-64-bit words of Philox4x64-10(counter (i, L, j, 0), key (seed, 0)), j = 0, 1, ...,
-whose bits under numpy's mask (the smallest 2^b - 1 >= range - 1) are <= range - 1
--- the masked rejection numpy's legacy bounded draw applies to MT words
-(numpy/random/src/distributions: random_bounded_uint64 with use_masked).
+L + 1 pooled steps, c = (L + 1) x period rows stored) takes word i mod 4 of the
+Philox4x64-10 blocks at counters (i div 4, L, j, 0), key (seed, 0), j = 0, 1, ...:
+the first whose bits under numpy's mask (the smallest 2^b - 1 >= range - 1) are
+<= range - 1 -- the masked rejection numpy's legacy bounded draw applies to MT words
+(numpy/random/src/distributions: random_bounded_uint64 with use_masked). One block
+serves four draws (the device draws a segment with a quarter of the Philox work).
 
 Pinning. ``philox4x64_10`` is this file's own restatement of the published
 generator (Salmon, Moraes, Dror, Shaw, "Parallel random numbers: as easy as 1,
@@ -81,20 +82,19 @@ def draw_learn(seed: int, L: int, batch: int, period: int, mem_size: int) -> np.
         return np.zeros(batch, np.int64)
     mask = np.uint64(range_mask(rng))
     out = np.full(batch, -1, np.int64)
-    todo = np.arange(batch, dtype=np.uint64)
+    todo = np.arange(batch, dtype=np.int64)
     for j in range(64):
         ctr = np.zeros((todo.size, 4), np.uint64)
-        ctr[:, 0] = todo
+        ctr[:, 0] = (todo // 4).astype(np.uint64)
         ctr[:, 1] = np.uint64(L)
         ctr[:, 2] = np.uint64(j)
-        words = philox4x64_10(ctr, np.uint64(seed), np.uint64(0)) & mask
-        ok = words <= np.uint64(rng)
-        first = np.where(ok.any(axis=1), ok.argmax(axis=1), -1)
-        hit = first >= 0
-        out[todo[hit].astype(np.int64)] = words[hit, first[hit]].astype(np.int64)
+        words = philox4x64_10(ctr, np.uint64(seed), np.uint64(0))[np.arange(todo.size), todo % 4] & mask
+        hit = words <= np.uint64(rng)
+        out[todo[hit]] = words[hit].astype(np.int64)
         todo = todo[~hit]
         if todo.size == 0:
             break
+    out[todo] = 0   # (64 rejected words in a row: probability < 2^-64; the device's bound)
     return out
 
 

@@ -655,20 +655,22 @@ __device__ __forceinline__ void philox4x64_10(uint64_t c[4], uint64_t k0, uint64
   }
 }
 
-// draw i of global learn L over [0, rng]: Philox4x64-10 of counter (i, L, attempt, 0)
-// under key (seed, 0); its four words in order, the first whose bits under `mask`
-// (the smallest 2^k - 1 >= rng) are <= rng -- numpy's masked rejection -- else the
-// next attempt (each attempt fails with probability < 2^-4 at any range)
-__device__ __forceinline__ int64_t ctr_draw(uint64_t seed, int64_t L, int i, uint64_t rng, uint64_t mask) {
+// Draw i of global learn L over [0, rng]: word i % 4 of the Philox4x64-10 blocks at
+// counters (i / 4, L, j, 0) under key (seed, 0), j = 0, 1, ...: the first whose bits
+// under `mask` (the smallest 2^k - 1 >= rng) are <= rng -- numpy's masked rejection.
+// One block serves four draws (`blk`, the block at j = 0 of counter c): a retry (each
+// word fails with probability < 1/2) takes the draw's word of the next block.
+__device__ __forceinline__ int64_t ctr_draw4(uint64_t seed, int64_t L, int i, uint64_t rng, uint64_t mask,
+                                             const uint64_t blk[4]) {
   if (rng == 0) return 0;  // numpy's off + 0: no words
-  for (uint64_t j = 0; j < 64; ++j) {
-    uint64_t c[4] = {(uint64_t)i, (uint64_t)L, j, 0ull};
+  const int w = i & 3;
+  uint64_t v = (w == 0 ? blk[0] : w == 1 ? blk[1] : w == 2 ? blk[2] : blk[3]) & mask;
+  for (uint64_t j = 1; v > rng && j < 64; ++j) {  // (64 failed words: probability < 2^-64)
+    uint64_t c[4] = {(uint64_t)(i >> 2), (uint64_t)L, j, 0ull};
     philox4x64_10(c, seed, 0ull);
-#pragma unroll
-    for (int w = 0; w < 4; ++w)
-      if ((c[w] & mask) <= rng) return (int64_t)(c[w] & mask);
+    v = (w == 0 ? c[0] : w == 1 ? c[1] : w == 2 ? c[2] : c[3]) & mask;
   }
-  return 0;  // (256 failed words: probability < 2^-256; bounded so no wave can spin)
+  return v <= rng ? (int64_t)v : 0;
 }
 
 __device__ __forceinline__ uint64_t range_mask(uint64_t rng) {
@@ -682,70 +684,7 @@ __device__ __forceinline__ uint64_t range_mask(uint64_t rng) {
   return m;
 }
 
-// Segment G.g's learns: idx[k][i] (-1: the learn is skipped, fewer than `batch`
-// rows stored) and the marks of the rows they read on this rank -- the row and
-// its predecessor (its s) -- in segment G.g (marks_cur) or G.g - 1 (marks_prev;
-// with M <= seg x period a row lies in one of the two). One thread per draw.
-__global__ void __launch_bounds__(256) k_rb_draw_ctr(SacenvReplayParams p, StagedGeom G, uint64_t seed, int batch,
-                                                     int nb, int64_t* __restrict__ idx,
-                                                     unsigned long long* __restrict__ marks_prev,
-                                                     unsigned long long* __restrict__ marks_cur) {
-  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (t >= (int64_t)batch * nb) return;
-  const int k = (int)(t / batch), i = (int)(t - (int64_t)k * batch);
-  const int64_t L = G.g * G.seg + k, cntr = (L + 1) * G.period, M = p.mem_size;
-  if (cntr < batch) {  // continuous_agent.py:97-98: learn() returns before sampling
-    idx[t] = -1;
-    return;
-  }
-  const uint64_t rng = (uint64_t)((cntr < M ? cntr : M) - 1);
-  const int64_t row = ctr_draw(seed, L, i, rng, range_mask(rng));
-  idx[t] = row;
-  int64_t q, u;
-  resolve(row, cntr, M, G, &q, &u);
-  if (u < G.offset || u >= G.offset + G.n) return;
-  const int e = (int)(u - G.offset);
-  const int nw = G.n_pad / kWave;
-#pragma unroll
-  for (int d = 0; d < 2; ++d) {  // the row, and its predecessor (s)
-    const int64_t qq = q - d;
-    if (qq < 0) continue;        // step -1: the reset obs begin() staged
-    int64_t j = qq - G.g * G.seg;
-    unsigned long long* const mk = j >= 0 ? marks_cur : marks_prev;
-    j = j >= 0 ? j : j + G.seg;
-    if (mk != nullptr) atomicOr(&mk[j * nw + e / kWave], 1ull << (e % kWave));
-  }
-}
-
-// The all-gather form of the exchange. Each rank packs the rows IT owns of the
-// segment's learns -- one 25-word record per sampled row: slot (learn x batch +
-// draw) | terminal << 31, reward f32, state [11], new_state [11], action -- into
-// a chunk of `cap` records behind a 4-word header (record count); rank 0 also
-// packs the rows of skipped learns (all zero). One all-gather of the chunks and
-// an unpack on every rank rebuild sacenv_replay_sample_staged's `words`, bit for
-// bit: every slot comes from exactly one rank. The records sit in slot order (a
-// count pass per 1 024-slot tile, then each tile's prefix over the tiles before
-// it: no atomics -- one count word taking every wave's atomic cost ~100 us a
-// segment -- and the chunk is the same bytes run to run).
-constexpr int kRecWords = 2 + 2 * SACENV_OBS_DIM + 1;  // 25
-constexpr int kChunkHdr = 4;
 constexpr int kPackTile = 256;
-// The side kernels of the staged exchange (draws, marks, pack, unpack, gather) run
-// beside a persistent segment launch, whose owner waves each need ~336 of a SIMD's
-// 512 VGPRs: a side kernel holding a SIMD when the launch dispatches would delay that
-// owner wave, and the launch ends with its slowest wave. Each side workgroup (256
-// threads: one wave per SIMD, <= 88 VGPRs) reserves this much LDS, so a CU holds at
-// most two of them -- and the owner waves fit beside them whatever the dispatch order.
-constexpr size_t kSideLds = 64 * 1024;
-
-// does this rank pack slot t (its row, or rank 0 a skipped learn's zero row)?
-__device__ __forceinline__ bool pack_takes(const SacenvReplayParams& p, const StagedGeom& G, int batch, int64_t t,
-                                           int64_t row, int skip_owner, int64_t* q, int64_t* u) {
-  *q = 0;
-  *u = -1;
-  if (row >= 0) resolve(row, (G.g * G.seg + t / batch + 1) * G.period, p.mem_size, G, q, u);
-  return (*u >= G.offset && *u < G.offset + G.n) || (row == -1 && skip_owner);
-}
 
 // the tile's records before this thread's (the block's waves in order): returns the
 // exclusive rank, *tile_total the tile's count
@@ -763,6 +702,87 @@ __device__ __forceinline__ int tile_rank(bool take, int* wcnt, int* tile_total) 
   }
   *tile_total = total;
   return before + __popcll(bal & ((1ull << lane) - 1ull));
+}
+
+// Segment G.g's learns: idx[k][i] (-1: the learn is skipped, fewer than `batch`
+// rows stored) and the marks of the rows they read on this rank -- the row and
+// its predecessor (its s) -- in segment G.g (marks_cur) or G.g - 1 (marks_prev;
+// with M <= seg x period a row lies in one of the two). Four consecutive draws per
+// thread (one Philox block for an aligned four; a wave covers one 256-slot tile);
+// with tile_cnt, also the records per 256-slot tile the all-gather's pack of this
+// segment will write (so the pack needs no count pass).
+constexpr int kDrawThreads4 = 256;  // x 4 draws
+__global__ void __launch_bounds__(kDrawThreads4) k_rb_draw_ctr(SacenvReplayParams p, StagedGeom G, uint64_t seed,
+                                                               int batch, int nb, int64_t* __restrict__ idx,
+                                                               unsigned long long* __restrict__ marks_prev,
+                                                               unsigned long long* __restrict__ marks_cur,
+                                                               int* __restrict__ tile_cnt, int skip_owner) {
+  const int64_t total = (int64_t)batch * nb;
+  const int64_t t0 = (blockIdx.x * (int64_t)kDrawThreads4 + threadIdx.x) * 4;
+  const int64_t M = p.mem_size;
+  const int nw = G.n_pad / kWave;
+  int takes = 0;  // (slots the all-gather's pack of this segment takes on this rank)
+  uint64_t blk[4] = {0ull, 0ull, 0ull, 0ull};
+  int64_t blk_c = -1, blk_L = -1;
+  for (int s4 = 0; s4 < 4; ++s4) {
+    const int64_t t = t0 + s4;
+    if (t >= total) break;
+    const int k = (int)(t / batch), i = (int)(t - (int64_t)k * batch);
+    const int64_t L = G.g * G.seg + k, cntr = (L + 1) * G.period;
+    if (cntr < batch) {  // continuous_agent.py:97-98: learn() returns before sampling
+      idx[t] = -1;
+      takes += skip_owner != 0 ? 1 : 0;
+      continue;
+    }
+    const uint64_t rng = (uint64_t)((cntr < M ? cntr : M) - 1);
+    if ((int64_t)(i >> 2) != blk_c || L != blk_L) {  // the block of this draw's four
+      blk[0] = (uint64_t)(i >> 2), blk[1] = (uint64_t)L, blk[2] = 0ull, blk[3] = 0ull;
+      philox4x64_10(blk, seed, 0ull);
+      blk_c = i >> 2, blk_L = L;
+    }
+    const int64_t row = ctr_draw4(seed, L, i, rng, range_mask(rng), blk);
+    idx[t] = row;
+    int64_t q, u;
+    resolve(row, cntr, M, G, &q, &u);
+    if (u < G.offset || u >= G.offset + G.n) continue;
+    ++takes;
+    const int e = (int)(u - G.offset);
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {  // the row, and its predecessor (s)
+      const int64_t qq = q - d;
+      if (qq < 0) continue;        // step -1: the reset obs begin() staged
+      int64_t j = qq - G.g * G.seg;
+      unsigned long long* const mk = j >= 0 ? marks_cur : marks_prev;
+      j = j >= 0 ? j : j + G.seg;
+      if (mk != nullptr) atomicOr(&mk[j * nw + e / kWave], 1ull << (e % kWave));
+    }
+  }
+  if (tile_cnt != nullptr) {  // the pack's per-tile record counts, drawn ahead: a wave = one tile
+    for (int o = kWave / 2; o > 0; o >>= 1) takes += __shfl_xor(takes, o);
+    const int64_t tile = (blockIdx.x * (int64_t)kDrawThreads4 + threadIdx.x) / kWave;
+    if ((threadIdx.x & (kWave - 1)) == 0 && tile * kPackTile < total) tile_cnt[tile] = takes;
+  }
+}
+
+// The all-gather form of the exchange. Each rank packs the rows IT owns of the
+// segment's learns -- one 25-word record per sampled row: slot (learn x batch +
+// draw) | terminal << 31, reward f32, state [11], new_state [11], action -- into
+// a chunk of `cap` records behind a 4-word header (record count); rank 0 also
+// packs the rows of skipped learns (all zero). One all-gather of the chunks and
+// an unpack on every rank rebuild sacenv_replay_sample_staged's `words`, bit for
+// bit: every slot comes from exactly one rank. The records sit in slot order (a
+// count pass per 1 024-slot tile, then each tile's prefix over the tiles before
+// it: no atomics -- one count word taking every wave's atomic cost ~100 us a
+// segment -- and the chunk is the same bytes run to run).
+constexpr int kRecWords = 2 + 2 * SACENV_OBS_DIM + 1;  // 25
+constexpr int kChunkHdr = 4;
+// does this rank pack slot t (its row, or rank 0 a skipped learn's zero row)?
+__device__ __forceinline__ bool pack_takes(const SacenvReplayParams& p, const StagedGeom& G, int batch, int64_t t,
+                                           int64_t row, int skip_owner, int64_t* q, int64_t* u) {
+  *q = 0;
+  *u = -1;
+  if (row >= 0) resolve(row, (G.g * G.seg + t / batch + 1) * G.period, p.mem_size, G, q, u);
+  return (*u >= G.offset && *u < G.offset + G.n) || (row == -1 && skip_owner);
 }
 
 __global__ void __launch_bounds__(kPackTile) k_rb_pack_count(SacenvReplayParams p, StagedGeom G, int batch, int nb,
@@ -1140,7 +1160,7 @@ int sacenv_replay_stage_mark(const SacenvReplayParams* p, const SacenvStagedPara
   if (per == 0) return SACENV_OK;
   // without the next segment's draws, only this segment's learns mark
   const int64_t total = idx_next != nullptr ? 2 * per : per;
-  hipLaunchKernelGGL(k_rb_stage_mark, dim3((unsigned)((total + 255) / 256)), dim3(256), kSideLds, (hipStream_t)stream,
+  hipLaunchKernelGGL(k_rb_stage_mark, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      *p, geom(p, sp, g), idx_g, idx_next != nullptr ? idx_next : idx_g, batch, n_batches,
                      reinterpret_cast<unsigned long long*>(marks), total);
   return status();
@@ -1163,7 +1183,7 @@ int sacenv_replay_sample_staged(const SacenvReplayParams* p, const SacenvStagedP
   for (int k = 0; k < SACENV_OBS_DIM; ++k) S.first[k] = sp->first_obs[k];
   const int64_t total = (int64_t)batch * n_batches;
   const int64_t per = (int64_t)batch * (2 * SACENV_OBS_DIM + 1 + 3);
-  hipLaunchKernelGGL(k_rb_gather_staged, dim3((unsigned)((total + 255) / 256)), dim3(256), kSideLds, (hipStream_t)stream,
+  hipLaunchKernelGGL(k_rb_gather_staged, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      *p, geom(p, sp, g), S, batch, n_batches, idx, words, per);
   return status();
 }
@@ -1193,15 +1213,17 @@ static int check_ctr_shape(const SacenvReplayParams* p, const SacenvStagedParams
 
 int sacenv_replay_stage_draw_ctr(const SacenvReplayParams* p, const SacenvStagedParams* sp, int64_t g,
                                  int32_t batch, int32_t n_batches, uint64_t seed, int64_t* idx, uint64_t* marks_prev,
-                                 uint64_t* marks_cur, void* stream) {
+                                 uint64_t* marks_cur, int32_t* tiles, void* stream) {
   const int rc = check_ctr_shape(p, sp, g, batch, n_batches);
   if (rc) return rc;
   if (idx == nullptr) return SACENV_E_NULL;
   const int64_t total = (int64_t)batch * n_batches;
   if (total == 0) return SACENV_OK;
-  hipLaunchKernelGGL(k_rb_draw_ctr, dim3((unsigned)((total + 255) / 256)), dim3(256), kSideLds, (hipStream_t)stream, *p,
-                     geom(p, sp, g), seed, batch, n_batches, idx, reinterpret_cast<unsigned long long*>(marks_prev),
-                     reinterpret_cast<unsigned long long*>(marks_cur));
+  hipLaunchKernelGGL(k_rb_draw_ctr, dim3((unsigned)((total + 4 * kDrawThreads4 - 1) / (4 * kDrawThreads4))),
+                     dim3(kDrawThreads4), 0,
+                     (hipStream_t)stream, *p, geom(p, sp, g), seed, batch, n_batches, idx,
+                     reinterpret_cast<unsigned long long*>(marks_prev), reinterpret_cast<unsigned long long*>(marks_cur),
+                     tiles, sp->offset == 0 ? 1 : 0);
   return status();
 }
 
@@ -1259,7 +1281,8 @@ int sacenv_replay_stage_chunk(const SacenvReplayParams* p, const SacenvStagedPar
 
 int sacenv_replay_stage_pack(const SacenvReplayParams* p, const SacenvStagedParams* sp, int64_t g,
                              const void* stage_cur, const void* stage_prev, const int64_t* idx, int32_t batch,
-                             int32_t n_batches, int64_t cap, void* chunk, int32_t* tiles, void* stream) {
+                             int32_t n_batches, int64_t cap, void* chunk, int32_t* tiles, int32_t counted,
+                             void* stream) {
   int rc = check_ctr_shape(p, sp, g, batch, n_batches);
   if (rc) return rc;
   if (!stage_cur || !stage_prev || !idx || !chunk || !tiles) return SACENV_E_NULL;
@@ -1278,10 +1301,12 @@ int sacenv_replay_stage_pack(const SacenvReplayParams* p, const SacenvStagedPara
   const StagedGeom G = geom(p, sp, g);
   const int skip_owner = sp->offset == 0 ? 1 : 0;
   const unsigned T = (unsigned)((total + kPackTile - 1) / kPackTile);
-  hipLaunchKernelGGL(k_rb_pack_count, dim3(T), dim3(kPackTile), kSideLds, (hipStream_t)stream, *p, G, batch, n_batches, idx,
-                     skip_owner, tiles);
-  if ((rc = status())) return rc;
-  hipLaunchKernelGGL(k_rb_pack_staged, dim3(T), dim3(kPackTile), kSideLds, (hipStream_t)stream, *p, G, S, batch, n_batches,
+  if (!counted) {  // (the counter-based draw wrote the tile counts already)
+    hipLaunchKernelGGL(k_rb_pack_count, dim3(T), dim3(kPackTile), 0, (hipStream_t)stream, *p, G, batch, n_batches,
+                       idx, skip_owner, tiles);
+    if ((rc = status())) return rc;
+  }
+  hipLaunchKernelGGL(k_rb_pack_staged, dim3(T), dim3(kPackTile), 0, (hipStream_t)stream, *p, G, S, batch, n_batches,
                      idx, static_cast<uint32_t*>(chunk), cap, skip_owner, tiles);
   return status();
 }
@@ -1296,7 +1321,7 @@ int sacenv_replay_stage_unpack(int32_t world, int64_t chunk_bytes, int64_t cap, 
   const int64_t n = (int64_t)world * cap;
   if (n == 0 || batch == 0) return SACENV_OK;
   const int64_t per = (int64_t)batch * (2 * SACENV_OBS_DIM + 1 + 3);
-  hipLaunchKernelGGL(k_rb_unpack_staged, dim3((unsigned)((n + 255) / 256)), dim3(256), kSideLds, (hipStream_t)stream,
+  hipLaunchKernelGGL(k_rb_unpack_staged, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      static_cast<const uint32_t*>(gathered), world, chunk_bytes / 4, cap, batch, words, per,
                      status_word);
   return status();

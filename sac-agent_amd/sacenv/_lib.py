@@ -227,9 +227,9 @@ def load(path: str | None = None):
         "sacenv_replay_stage_mark": (C.c_int, [RP, SP, _i64, _p, _p, _i32, _i32, _p, _p]),
         "sacenv_replay_sample_staged": (C.c_int, [RP, SP, _i64, _p, _p, _p, _i32, _i32, _p, _p]),
         "sacenv_replay_gather": (C.c_int, [RP, _p, _i32, _p, _p, _p, _p, _p, _p, _p]),
-        "sacenv_replay_stage_draw_ctr": (C.c_int, [RP, SP, _i64, _i32, _i32, C.c_uint64, _p, _p, _p, _p]),
+        "sacenv_replay_stage_draw_ctr": (C.c_int, [RP, SP, _i64, _i32, _i32, C.c_uint64, _p, _p, _p, _p, _p]),
         "sacenv_replay_stage_chunk": (C.c_int, [RP, SP, _i32, _i32, C.POINTER(_i64), C.POINTER(_i64)]),
-        "sacenv_replay_stage_pack": (C.c_int, [RP, SP, _i64, _p, _p, _p, _i32, _i32, _i64, _p, _p, _p]),
+        "sacenv_replay_stage_pack": (C.c_int, [RP, SP, _i64, _p, _p, _p, _i32, _i32, _i64, _p, _p, _i32, _p]),
         "sacenv_replay_stage_unpack": (C.c_int, [_i32, _i64, _i64, _i32, _i32, _p, _p, _p, _p]),
         "sacenv_copy_standin": (C.c_int, [_p, _p, _i64, _i32, C.c_double, _p]),
         "sacenv_sac_layout": (C.c_int, [C.POINTER(SacParams), C.POINTER(SacLayout)]),

@@ -278,45 +278,49 @@ def shard_owner(rows, cntr: int, mem_size: int, period: int, n_per_rank: int):
 
 
 class SegmentExchange:
-    """The replay exchange of the persistent segments (StagedReplay), run beside them.
+    """The replay exchange of the persistent segments (StagedReplay), on the stepping
+    stream after each segment's refill.
 
-    A segment launch's owner waves need ~336 VGPRs each, one per SIMD: a side kernel
-    holding a SIMD when the launch dispatches delays that owner wave, and the launch ends
-    with its slowest wave; a side chain the launch must wait for sits on the critical
-    path (round 6 measured both). So the side work of segment g runs in a WINDOW that
-    no launch waits for until segment g + 2:
+    Measured on the box (round 6, kernel traces, ``tools/prof_staged3.py``): a segment
+    launch's owner waves are one per SIMD and bound by their own instruction issue, so a
+    kernel co-running with a launch slows the owner waves it shares SIMDs with and the
+    launch ends with its slowest wave (300 -> 360-440 us with the pack, the draws or a
+    16-workgroup collective stand-in beside it); side kernels co-running with the refill
+    slow its latency chain as much (k_need_masks 6 -> 85-95 us, k_refill_fit 28 -> 90-115
+    us); and every wait of the stepping stream on another stream's event cost ~20-40 us.
+    So the exchange's local work runs on the stepping stream, after refill g:
 
-    - ``side`` (high priority, behind launch g's END -- ``launched()``'s event -- so
-      beside refill g and launch g + 1): the unpack of segment g - 1 (its collective is
-      done), the pack of segment g's share (``pack_segment``), and ``prepare(g + 2)``:
-      the draws of segment g + 3 and segment g + 2's marks. Its end event is what launch
-      g + 2 waits for (``before()``): the marks it reads, and the pack of segment g that
-      read the stage buffer launch g + 2 overwrites. The side kernels reserve LDS so a
-      CU holds at most two of their workgroups (the owner waves always fit beside them);
-    - ``coll`` (high priority): the collective of segment g behind its pack
-      (``collect_segment``: the all-gather or the all-reduce; at one rank the stand-in,
-      if any), overlapped with launch g + 1.
+    - the unpack of segment g - 1 (at N > 1: behind its collective, which ran beside
+      launch g), the pack of segment g's share (``pack_segment``), at one rank with no
+      collective the unpack of segment g at once, and ``prepare(g + 1)``: the
+      counter-based draws of segment g + 2, which also mark segment g + 1's rows and
+      count segment g + 2's pack tiles;
+    - ``coll``: the collective of segment g behind its pack (``collect_segment``: the
+      all-gather or the all-reduce; at one rank the stand-in, if any), overlapped with
+      launch g + 1 -- the one piece that cannot wait;
+    - MT-exact draws (one workgroup walking the MT chain, ~140 us) run on ``sd`` as soon as
+      they are enqueued, beside launch g, and launch g + 1 waits for them.
 
-    Segment g's batches (``last``) land in the next window (``wait()`` unpacks the one
-    still pending). The high-priority streams come from a separate pool of hardware
-    queues, so no side kernel queues behind a launch in the stepping stream's queue.
-    ``sampler`` is a ``sacenv.replay.StagedReplay`` or anything with its methods; on the
-    CPU (no streams) everything runs in order. ``check()`` after a timed region raises on
-    a segment the sampler flagged invalid."""
+    ``last`` holds the batches of the latest unpacked segment (``wait()`` unpacks one
+    still pending). ``sampler`` is a ``sacenv.replay.StagedReplay`` or anything with its
+    methods; on the CPU (no streams) everything runs in order. ``check()`` after a timed
+    region raises on a segment the sampler flagged invalid."""
 
     def __init__(self, sampler, device):
         self.sampler = sampler
         self.device = torch.device(device)
         self.cuda = self.device.type == "cuda"
         if self.cuda:
-            hi = torch.cuda.Stream.priority_range()[1]   # (low, high): the highest priority
-            self.side = torch.cuda.Stream(device=self.device, priority=hi)
-            self.coll = torch.cuda.Stream(device=self.device, priority=hi)
+            self.sd = torch.cuda.Stream(device=self.device)
+            self.coll = torch.cuda.Stream(device=self.device)
+        self.mt = getattr(sampler, "sampler", None) == "mt"
+        # a collective (or its stand-in) runs between the pack and the unpack
+        self.collective = (getattr(sampler, "world", 1) > 1 or getattr(sampler, "standin", None) is not None)
         self.g = 0               # segments exchanged so far
         self.started = False
         self._ready = {}         # segment -> events its launch waits for
         self._pending = None     # (segment, its collective's event): packed, not unpacked yet
-        self._launched = None
+        self._launched = None    # (MT-exact draws) the last two launches' end events
         self.exchanges = 0
         self.last = None         # the batches of the latest unpacked segment
 
@@ -335,7 +339,7 @@ class SegmentExchange:
         if self.cuda:
             # the side streams continue the sampling stream begin()'s draws advance on this
             # stream: they must not run ahead of them
-            for st in (self.side, self.coll):
+            for st in (self.sd, self.coll):
                 st.wait_stream(self._cur())
         self.started, self.g, self._pending = True, 0, None
 
@@ -344,43 +348,50 @@ class SegmentExchange:
         return self.sampler.stage_args(self.g)
 
     def before(self) -> None:
-        """The stepping stream waits for the window of segment g - 2 (the next launch's
-        marks; the pack that read the stage buffer it overwrites)."""
+        """(MT-exact draws) the stepping stream waits for the draws and marks of the
+        segment about to be launched."""
         for ev in self._ready.pop(self.g, ()):
             self._cur().wait_event(ev)
 
     def launched(self) -> None:
-        """Right after the segment launch was enqueued (before its refill)."""
-        if self.cuda:
-            self._launched = self._record(self._cur())
+        """Right after the segment launch was enqueued (before its refill): the MT-exact
+        draws after segment g's launch wait for launch g - 1's end (the buffers they
+        rewrite)."""
+        if self.cuda and self.mt:
+            self._launched = (self._launched or [])[-1:] + [self._record(self._cur())]
 
     def _unpack_pending(self) -> None:
         g, ev_c = self._pending
-        if self.cuda:
-            self.side.wait_event(ev_c)
+        if self.cuda and ev_c is not None:
+            self._cur().wait_event(ev_c)
         self.last = self.sampler.unpack_segment(g)
         self._pending = None
 
     def after(self) -> None:
         g = self.g
         if not self.cuda:
-            self.sampler.prepare(g + 2)
+            self.sampler.prepare(g + 1)
             self.last = self.sampler.sample_segment(g)
         else:
-            launched = self._launched if self._launched is not None else self._record(self._cur())
-            self._launched = None
-            with torch.cuda.stream(self.side):
-                self.side.wait_event(launched)
-                if self._pending is not None:
-                    self._unpack_pending()
-                self.sampler.pack_segment(g)
-                packed = self._record(self.side)
-                self.sampler.prepare(g + 2)
-                self._ready[g + 2] = [self._record(self.side)]
-            with torch.cuda.stream(self.coll):
-                self.coll.wait_event(packed)
-                self.sampler.collect_segment(g)
-                self._pending = (g, self._record(self.coll))
+            if self._pending is not None:
+                self._unpack_pending()
+            self.sampler.pack_segment(g)
+            if self.collective:
+                packed = self._record(self._cur())
+                with torch.cuda.stream(self.coll):
+                    self.coll.wait_event(packed)
+                    self.sampler.collect_segment(g)
+                    self._pending = (g, self._record(self.coll))
+            else:
+                self.last = self.sampler.unpack_segment(g)
+            if self.mt:  # beside launch g (after launch g - 1's end); launch g + 1 waits for it
+                with torch.cuda.stream(self.sd):
+                    if self._launched and len(self._launched) == 2:
+                        self.sd.wait_event(self._launched[0])
+                    self.sampler.prepare(g + 1)
+                    self._ready[g + 1] = [self._record(self.sd)]
+            else:
+                self.sampler.prepare(g + 1)
         self.g += 1
         self.exchanges += 1
 
@@ -389,9 +400,8 @@ class SegmentExchange:
         in flight."""
         if self.cuda:
             if self._pending is not None:
-                with torch.cuda.stream(self.side):
-                    self._unpack_pending()
-            for st in (self.side, self.coll):
+                self._unpack_pending()
+            for st in (self.sd, self.coll):
                 self._cur().wait_stream(st)
         self._ready.clear()
 

@@ -289,9 +289,8 @@ class StagedReplay:
     bit, on every rank (tests/test_staged_replay_gpu.py). ~27 MB cross the links per
     256-step segment at batch 1 024, whatever the world size.
 
-    Order per segment g (``begin`` did the draws of segments 0-2 and the marks of 0 and
-    1): ``stage_args(g)`` -> the launch -> ``prepare(g + 1)`` (or up to ``g + 2``) ->
-    ``sample_segment(g)``. Buffers: the staged rows of segment g are read by
+    Order per segment g (``begin`` did draws 0 and 1 and the marks of segment 0):
+    ``stage_args(g)`` -> the launch -> ``prepare(g + 1)`` -> ``sample_segment(g)``. Buffers: the staged rows of segment g are read by
     ``sample_segment(g)`` and ``(g + 1)``, so the launch of segment g + 2 (3 buffers)
     must follow ``sample_segment(g)`` in stream order; a launch consumes (clears) its
     marks (``sacenv.dist.SegmentExchange`` arranges the streams).
@@ -385,7 +384,11 @@ class StagedReplay:
             self.cap, self.chunk_bytes = staged_chunk(self.n, self.n_pad, self.world, self.mem_size, self.batch,
                                                       self.seg, experiment)
             self._chunks = [torch.empty(self.chunk_bytes, dtype=torch.uint8, device=self.device) for _ in range(2)]
-            self._tiles = torch.empty(-(-self.seg * self.batch // 256), dtype=torch.int32, device=self.device)
+            # the pack's per-tile record counts: written by the counter-based draw of each segment
+            # (a buffer per drawn segment, as idx), or by the pack's own count pass (MT draws)
+            nt = -(-self.seg * self.batch // 256)
+            self._tiles = [torch.empty(nt, dtype=torch.int32, device=self.device)
+                           for _ in range(4 if sampler == "philox" else 1)]
             self._gathered = ([torch.empty(self.world * self.chunk_bytes, dtype=torch.uint8, device=self.device)
                                for _ in range(2)] if self.world > 1 else self._chunks)
         self.standin = dict(standin) if standin is not None else None
@@ -407,10 +410,11 @@ class StagedReplay:
             # marks are complete after it). The buffer is zero: the launch that read it last
             # (segment g - 3) cleared it, and begin() clears all three
             nb = self.N_BUFFERS
+            tiles = self._tiles[g % 4].data_ptr() if self.exchange == "allgather" else None
             _lib.check(self.lib.sacenv_replay_stage_draw_ctr(
                 self._pp, self._spp, g, self.batch, self.seg, self.seed & 0xFFFFFFFFFFFFFFFF,
                 self._idx[g % 4].data_ptr(), self.marks[(g - 1) % nb].data_ptr() if g > 0 else None,
-                self.marks[g % nb].data_ptr(), self.stream))
+                self.marks[g % nb].data_ptr(), tiles, self.stream))
         else:
             _lib.check(self.lib.sacenv_replay_stage_draw(
                 self._pp, self._rb.arena.data_ptr(), self._spp, g, self.batch, self.seg,
@@ -436,7 +440,6 @@ class StagedReplay:
             m.zero_()
         self.drawn = 0
         self.prepare(0)
-        self.prepare(1)   # (segment 1's marks too: its launch may follow before another prepare)
 
     def stage_args(self, g: int) -> dict:
         """The staged-row arguments of segment g's launch (VecBoatEnv.segment_async /
@@ -444,9 +447,8 @@ class StagedReplay:
         return {"stage": self.stage[g % self.N_BUFFERS], "marks": self.marks[g % self.N_BUFFERS]}
 
     def prepare(self, g: int) -> None:
-        """Any time before segment g's launch (after segment g - 3's, whose buffers it
-        reuses): draw the learns up to segment g + 1 and complete segment g's marks.
-        ``sacenv.dist.SegmentExchange`` calls ``prepare(g + 2)`` after launch g."""
+        """Before segment g's launch (after segment g - 1's, whose pack reads the buffers
+        it reuses): draw the learns up to segment g + 1 and complete segment g's marks."""
         while self.drawn < g + 2:
             self._draw()
         self._mark(g)
@@ -469,9 +471,11 @@ class StagedReplay:
         nb = self.N_BUFFERS
         cur, prev = self.stage[g % nb].data_ptr(), self.stage[(g - 1) % nb].data_ptr()
         if self.exchange == "allgather":
+            counted = self.sampler == "philox"   # (the draw of segment g counted its tiles)
             _lib.check(self.lib.sacenv_replay_stage_pack(
                 self._pp, self._spp, g, cur, prev, idx.data_ptr(), self.batch, self.seg, self.cap,
-                self._chunks[g % 2].data_ptr(), self._tiles.data_ptr(), self.stream))
+                self._chunks[g % 2].data_ptr(), self._tiles[g % 4 if counted else 0].data_ptr(), int(counted),
+                self.stream))
         else:
             _lib.check(self.lib.sacenv_replay_sample_staged(
                 self._pp, self._spp, g, cur, prev, idx.data_ptr(), self.batch, self.seg,

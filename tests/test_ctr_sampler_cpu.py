@@ -25,17 +25,22 @@ def test_philox_matches_numpy(seed):
 
 
 def test_draw_rule_is_the_first_accepted_word():
-    seed, L, B, period, M = 9, 40, 64, 1000, 30_011
-    idx = cs.draw_learn(seed, L, B, period, M)
-    rng = min((L + 1) * period, M) - 1
-    mask = cs.range_mask(rng)
-    for i in range(B):
-        for j in range(4):
-            w = cs.philox4x64_10(np.array([[i, L, j, 0]], np.uint64), seed, 0)[0] & np.uint64(mask)
-            acc = [int(x) for x in w if int(x) <= rng]
-            if acc:
-                assert idx[i] == acc[0]
-                break
+    """draw i takes word i % 4 of the blocks at counters (i // 4, L, j, 0), j = 0, 1, ...:
+    the first accepted one (a range with a 50 % rejection rate exercises the retries)."""
+    for seed, L, B, period, M in ((9, 40, 64, 1000, 30_011), (3, 2, 200, 1000, 1025)):
+        idx = cs.draw_learn(seed, L, B, period, M)
+        rng = min((L + 1) * period, M) - 1
+        mask = cs.range_mask(rng)
+        retried = 0
+        for i in range(B):
+            for j in range(64):
+                w = int(cs.philox4x64_10(np.array([[i // 4, L, j, 0]], np.uint64), seed, 0)[0][i % 4]) & mask
+                if w <= rng:
+                    assert idx[i] == w, (seed, i, j)
+                    retried += j > 0
+                    break
+        if M == 1025:
+            assert retried > 20
 
 
 def test_draw_range_and_skip_rule():

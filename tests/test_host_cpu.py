@@ -78,15 +78,15 @@ def test_counter_sampler_and_allgather_argument_errors_without_gpu(built_lib):
     rp = _lib.ReplayParams(mem_size=1_000_000, obs_dim=11, act_dim=1, reward_f32=1, terminal_mask=2)
     sp = _lib.StagedParams(period=4096, offset=0, n=4096, n_pad=4096, seg=256, experiment=6)
     R, S = ctypes.byref(rp), ctypes.byref(sp)
-    assert built_lib.sacenv_replay_stage_draw_ctr(R, S, 0, 1024, 256, 0, None, None, None, None) == -1
-    assert built_lib.sacenv_replay_stage_draw_ctr(R, S, 0, 1024, 257, 0, 1, None, None, None) == -4
-    assert built_lib.sacenv_replay_stage_draw_ctr(R, S, -1, 1024, 256, 0, 1, None, None, None) == -4
+    assert built_lib.sacenv_replay_stage_draw_ctr(R, S, 0, 1024, 256, 0, None, None, None, None, None) == -1
+    assert built_lib.sacenv_replay_stage_draw_ctr(R, S, 0, 1024, 257, 0, 1, None, None, None, None) == -4
+    assert built_lib.sacenv_replay_stage_draw_ctr(R, S, -1, 1024, 256, 0, 1, None, None, None, None) == -4
     sp.period = sp.n = sp.n_pad = 64      # mem_size > seg * period
-    assert built_lib.sacenv_replay_stage_draw_ctr(R, S, 0, 1024, 256, 0, 1, None, None, None) == -5
+    assert built_lib.sacenv_replay_stage_draw_ctr(R, S, 0, 1024, 256, 0, 1, None, None, None, None) == -5
     sp.period = sp.n = sp.n_pad = 4096
-    assert built_lib.sacenv_replay_stage_pack(R, S, 0, 16, 16, 8, 1024, 256, 10, None, 4, None) == -1
-    assert built_lib.sacenv_replay_stage_pack(R, S, 0, 16, 16, 8, 1024, 256, 10, 16, None, None) == -1
-    assert built_lib.sacenv_replay_stage_pack(R, S, 0, 24, 16, 8, 1024, 256, 10, 16, 4, None) == -5  # stage align
+    assert built_lib.sacenv_replay_stage_pack(R, S, 0, 16, 16, 8, 1024, 256, 10, None, 4, 0, None) == -1
+    assert built_lib.sacenv_replay_stage_pack(R, S, 0, 16, 16, 8, 1024, 256, 10, 16, None, 0, None) == -1
+    assert built_lib.sacenv_replay_stage_pack(R, S, 0, 24, 16, 8, 1024, 256, 10, 16, 4, 0, None) == -5
     cap, nb = ctypes.c_int64(), ctypes.c_int64()
     assert built_lib.sacenv_replay_stage_chunk(R, S, 1024, 256, ctypes.byref(cap), ctypes.byref(nb)) == 0
     assert cap.value == 1024 * 256 and nb.value >= 16 + 100 * cap.value

@@ -35,6 +35,36 @@ def main():
     for _ in range(24):   # past the clock boost
         k = run0.segment(k, False)
     torch.cuda.synchronize()
+    # the staged launch alone (no side work): marks all zero, and a real segment's marks
+    # (the philox draws' density, re-copied before each launch: the launch consumes them)
+    from sacenv.replay import StagedReplay
+    env = wl.envs[0]
+    rep = StagedReplay(env.num_envs, env.n_pad, base.experiment, env.first_obs_template(), mem_size=base.replay_mem,
+                       batch=base.replay_batch, seg=bench.SEG, device=dev, sampler="philox", exchange="allgather")
+    rep.begin(env.obs)
+    real = rep.marks[0].clone()
+    stage = rep.stage[0]
+    marks = torch.zeros_like(real)
+    st = torch.cuda.current_stream(dev)
+    for name, src in (("plain", None), ("staged-0", "zero"), ("staged-real", real)):
+        evs = []
+        for _ in range(n):
+            if src is not None and name == "staged-real":
+                marks.copy_(src)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(st)
+            if src is None:
+                wl.segment_step(k % bench.ACTION_STEPS, bench.SEG)
+            else:
+                wl.segment_step(k % bench.ACTION_STEPS, bench.SEG, stage=stage, marks=marks)
+            b.record(st)
+            wl.refill()
+            k += bench.SEG
+            evs.append((a, b))
+        torch.cuda.synchronize()
+        ms = [a.elapsed_time(b) * 1e3 for a, b in evs[2:]]
+        print(f"launch only {name:12s} median {statistics.median(ms):6.1f} us (min {min(ms):6.1f})", flush=True)
+    del rep
     confs = [("none", None, None, False), ("mt", "mt", "allreduce", False), ("philox-ar", "philox", "allreduce", False),
              ("philox-ag", "philox", "allgather", False), ("standin", "philox", "allgather", True)]
     for rnd in range(2):
