@@ -984,8 +984,8 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
             f") from the pooled ReplayBuffer({args.replay_mem}), the segment launch writing the 64-B rows they "
             "read, the batches " + ("packed per rank and unpacked (the all-gather's two kernels)"
                                     if args.exchange == "allgather" else "gathered") +
-            " on a side stream overlapped with the next segment (StagedReplay), after the timed region, "
-            "wall time"))
+            " on the stepping stream after each segment's refill (sacenv.dist.SegmentExchange: kernels beside a "
+            "launch or a refill slowed them more than they overlapped), after the timed region, wall time"))
         if not args.stub:
             sd = collective_standin(args, wl)
             srun = SegmentRunner(args, wl, dev, None, SEG, make_exchange(args, wl, rank, 1, dev, standin=sd))
@@ -994,8 +994,9 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
                 f"replay_path with the collective's kernel stood in for: between the pack and the unpack, "
                 f"{sd['workgroups']} workgroups (the RCCL channel cap the N>1 line sets, NCCL_MAX_NCHANNELS) copy "
                 f"the {sd['bytes']} B one rank moves per segment at {sd['world']} ranks and stay resident for "
-                f"{sd['us']:.1f} us (those bytes at {args.standin_gbps:g} GB/s per rank), on the side stream "
-                "beside the next segment's owner waves; no xGMI traffic"))
+                f"{sd['us']:.1f} us (those bytes at {args.standin_gbps:g} GB/s per rank), on a side stream "
+                "beside the next segment's launch, as the N>1 collective runs; the unpack waits for it; no xGMI "
+                "traffic"))
     dinfo = dist_info(world, dev)
     if rank != 0:
         return None

@@ -8,10 +8,12 @@
 #   the training loop (--train),
 #   then tools/pmc.sh (kernel trace + calibrated PMC
 #   passes of the persistent segment kernel).
+# PART=1: tests, smoke and the bench lines; PART=2: the rest (two gpurun calls).
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-if [ -z "$SKIP_TESTS" ]; then
+P=${PART:-all}
+if [ "$P" != 2 ] && [ -z "$SKIP_TESTS" ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread \
     -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
   rc=$?; echo "pytest rc=$rc"; tail -4 gpurun_out/pytest_gpu.log
@@ -20,6 +22,7 @@ if [ -z "$SKIP_TESTS" ]; then
   tail -1 gpurun_out/smoke.log
 fi
 B="timeout -k 10 300 python bench.py"
+if [ "$P" != 2 ]; then
 $B --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_driver.json 2> gpurun_out/bench_driver.log || exit 1
 $B > gpurun_out/bench_default.json 2> gpurun_out/bench_default.log || exit 1
 $B --launch step --no-cpu-baseline > gpurun_out/bench_step.json 2> gpurun_out/bench_step.log || exit 1
@@ -36,7 +39,14 @@ for f in ("driver", "default", "step", "c2", "c5", "rollout_k128", "131k", "clos
     k = r.get("kernel_avg_us", r.get("kernel_avg_us_per_step")) or 0.0
     print(f"{f:13s} {d['value']/1e9:7.3f} G/s {d['ms_per_step']*1e3:6.2f} us/step kernel {k:5.2f} us "
           f"frac {r.get('frac', 0):.3f} cpu {c and round(c['value'])}")
+d = json.load(open("gpurun_out/bench_default.json"))
+rp, sd, ev = d["replay_path"], d["replay_path_collective_standin"], d["every_output"]
+print(f"default: replay_path {rp['value']/1e9:.3f} ({rp['value']/d['value']:.3f}), standin {sd['value']/1e9:.3f} "
+      f"({sd['value']/d['value']:.3f}), every_output {ev['value']/1e9:.3f} ({ev['value']/d['value']:.3f}), "
+      f"timed {d['steps'] * d['ms_per_step'] * 1e-3:.3f} s")
 PY
+fi
+[ "$P" = 1 ] && { echo final_check part 1 done; exit 0; }
 # N=2 rehearsals over gloo on the one GPU: the default sharded exchange (bench starting its
 # own ranks, no launcher), and the all-gather under torch.distributed.run
 SACENV_BENCH_BACKEND=gloo SACENV_BENCH_ONE_DEVICE=1 timeout -k 10 400 python bench.py --gpus 2 --envs 65536 \
