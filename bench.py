@@ -520,7 +520,7 @@ def make_workload(args, rank: int, dev) -> Workload:
         assert r0 + n <= ACTION_STEPS
         if trans is not None and trans.numel() < (n - 1) * row_bytes + lay.nbytes:
             raise ValueError("pooled rows buffer too small")
-        if stage is not None and (stage.numel() < n * 64 * env.n_pad or (marks is not None and marks.numel() < n * env.n_pad // 64)):
+        if stage is not None and (stage.numel() < n * 64 * env.n_pad or (marks is not None and marks.numel() < env.n_pad * -(-n // 64))):
             raise ValueError("staged rows / marks buffer too small")
         _lib.check(seg_fn(env._pp, env._ptr, C.c_void_p(a0 + 4 * r0 * astride), astride, n, ready.data_ptr(),
                           None, 0, None if trans is None else trans.data_ptr(),

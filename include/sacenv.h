@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SACENV_ABI_VERSION 19
+#define SACENV_ABI_VERSION 20
 #define SACENV_OBS_DIM 11      /* Boat.return_state, boat_env.py:308-323 */
 #define SACENV_MT_N 624        /* MT19937 words per env (numpy legacy RNG) */
 #define SACENV_MAX_KNOTS 16    /* wind.fixed_points upper bound */
@@ -291,11 +291,12 @@ int sacenv_boat_rollout(const SacenvBoatParams *p, void *arena, const float *act
  * trans (nullable, 16-B aligned, trans_stride a multiple of 16): step ks's
  * pooled transition row (sacenv_boat_step_pooled's format) at trans + ks *
  * trans_stride. stage (nullable, 16-B aligned, not with trans): the staged
- * replay rows of sacenv_replay_sample_staged -- step ks, env e at stage + (ks *
- * n_pad + e) * 64: s' f32 [11] (the obs before any auto-reset), reward f32,
- * action f32, u32 term | last_term << 8 (last_term: layout.last_term after the
- * step), obs3_next f32 (experiment 2), 0 -- written only where bit e % 64 of
- * stage_marks[ks * n_pad / 64 + e / 64] is set (sacenv_replay_stage_mark: the rows
+ * replay rows of sacenv_replay_sample_staged -- ENV-MAJOR (ABI 20): env e, step
+ * ks at stage + (e * n_steps + ks) * 64: s' f32 [11] (the obs before any
+ * auto-reset), reward f32, action f32, u32 term | last_term << 8 (last_term:
+ * layout.last_term after the step), obs3_next f32 (experiment 2), 0 -- written
+ * only where bit ks % 64 of stage_marks[e * ceil(n_steps / 64) + ks / 64] is set
+ * (u64 [n_pad][ceil(n_steps / 64)]; sacenv_replay_stage_mark: the rows
  * a learn will sample; stage_marks == NULL: every row; with stage_marks, n_steps <=
  * SACENV_REFILL_PERIOD in any mode, else SACENV_E_SIZE). The launch CONSUMES the
  * marks: it clears the words it read (steps 0..n_steps-1), so the next draws into
@@ -549,8 +550,9 @@ int sacenv_replay_stage_scratch_bytes(const SacenvReplayParams *p, int32_t batch
 int sacenv_replay_stage_draw(const SacenvReplayParams *p, void *arena, const SacenvStagedParams *sp, int64_t g,
                              int32_t batch, int32_t n_batches, int64_t *idx, void *scratch, int64_t scratch_bytes,
                              void *stream);
-/* The rows of segment g some learn will read (u64 [seg][n_pad/64], one bit per
- * env; cleared first): every row the draws of segment g (idx_g) and g + 1
+/* The rows of segment g some learn will read (u64 [n_pad][ceil(seg / 64)], bit
+ * j % 64 of env e's word j / 64 for step j, as sacenv_boat_segment reads them;
+ * cleared first): every row the draws of segment g (idx_g) and g + 1
  * (idx_next, nullable) sample that lies in segment g on this rank, and the row
  * before it (its s). sacenv_boat_segment writes exactly these (stage_marks). */
 int sacenv_replay_stage_mark(const SacenvReplayParams *p, const SacenvStagedParams *sp, int64_t g,
@@ -592,7 +594,7 @@ int sacenv_replay_gather(const SacenvReplayParams *p, void *arena, int32_t batch
  * one parallel launch with no sequential chain, in any order, for any g. The
  * same thread marks the rows it draws on this rank and their predecessors:
  * rows of segment g in marks_cur, of segment g - 1 in marks_prev (u64
- * [seg][n_pad/64] each, nullable, NOT cleared: a segment's marks start from zero --
+ * [n_pad][ceil(seg / 64)] each, nullable, NOT cleared: a segment's marks start from zero --
  * cleared by the caller, or by the sacenv_boat_segment launch that consumed them
  * last). Drawing segments g and g + 1 completes segment g's marks
  * (sacenv_replay_stage_mark's set). tiles (nullable, i32 [ceil(n_batches x
@@ -624,6 +626,38 @@ int sacenv_replay_stage_pack(const SacenvReplayParams *p, const SacenvStagedPara
                              void *stream);
 int sacenv_replay_stage_unpack(int32_t world, int64_t chunk_bytes, int64_t cap, int32_t batch, int32_t n_batches,
                                const void *gathered, uint32_t *words, int32_t *status_word, void *stream);
+/* One segment's side work of the counter-based, all-gather staged exchange in ONE
+ * launch (ABI 20): sacenv_replay_stage_draw_ctr of segment draw_g (draw_g < 0:
+ * none), sacenv_replay_stage_pack of segment pack_g with counted tiles (pack_g <
+ * 0: none) and sacenv_replay_stage_unpack of `gathered` (NULL: none), each
+ * bit-identical to its own entry point. The three run side by side, so their
+ * buffers must be disjoint: the pack's idx / tiles are not the draws' (ring them,
+ * as sacenv.replay.StagedReplay does: draws of g + 2 beside the pack of g), and
+ * the chunk the pack writes is not in the gathered range the unpack reads
+ * (SACENV_E_RANGE). cap is the chunk's record capacity (pack and unpack). */
+typedef struct SacenvStageSide {
+  int64_t draw_g;           /* segment whose learns are drawn; < 0: no draws */
+  uint64_t seed;
+  int64_t *draw_idx;        /* i64 [n_batches x batch] */
+  uint64_t *marks_prev;     /* nullable (draw_g == 0) */
+  uint64_t *marks_cur;
+  int32_t *draw_tiles;      /* i32 [ceil(n_batches x batch / 256)] */
+  int64_t pack_g;           /* segment packed; < 0: no pack */
+  const void *stage_cur;
+  const void *stage_prev;
+  const int64_t *pack_idx;  /* segment pack_g's draws */
+  const int32_t *pack_tiles;/* and their tile counts */
+  int64_t cap;
+  void *chunk;
+  const void *gathered;     /* world chunks to unpack; NULL: no unpack */
+  int64_t chunk_bytes;
+  uint32_t *words;
+  int32_t *status_word;
+  int32_t world;
+  int32_t reserved;
+} SacenvStageSide;
+int sacenv_replay_stage_side(const SacenvReplayParams *p, const SacenvStagedParams *sp, int32_t batch,
+                             int32_t n_batches, const SacenvStageSide *work, void *stream);
 /* A collective's kernel stood in for on one GPU (bench.py's N = 1 replay path):
  * `workgroups` workgroups of 256 threads copy `bytes` (16-B multiple, aligned)
  * from src to dst and stay resident until min_us have passed since each

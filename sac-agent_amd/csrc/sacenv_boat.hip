@@ -1806,9 +1806,12 @@ struct MixedToys {
 // soon as they are final (EARLY_STORE); the obs rows go out through LDS as
 // float4 (64 rows x 44 B = 176 float4).
 constexpr int kCoef = 8;  // wind_coef fields: 2 curves x (y0, y1, m0, m1)
+constexpr int kMkWords = SACENV_REFILL_PERIOD / 32;  // 32-bit mark words per env (one bit per step)
 struct OwnerLds {
   float obs[kWave * SACENV_OBS_DIM];  // the wave's obs rows, stored as float4
-  unsigned long long mk[SACENV_REFILL_PERIOD];  // staged replay rows: the wave's mark word per step
+  // staged replay rows: bit (ks % 32) of mk[ks / 32][lane] marks lane's row of step ks
+  // (word-major: the 64 lanes of one read hit 64 consecutive words, no bank conflict)
+  uint32_t mk[kMkWords][kWave];
 };
 
 // t += dt (boat_env.py:69) accumulates exactly when dt = m * 2^e with m < 2^22:
@@ -1872,8 +1875,9 @@ struct RollArgs {
   int64_t fin_stride;     // floats
   char* trans;            // pooled transition row of step ks at trans + ks * trans_stride (or null)
   int64_t trans_stride;   // bytes
-  // staged replay rows (kRows == 2): env e's 64-B row of step ks at stage + (ks * n_pad + e) * 64,
-  // written where bit (e % 64) of marks[ks * n_pad / 64 + e / 64] is set (marks == null: every row)
+  // staged replay rows (kRows == 2): env e's 64-B row of step ks at stage + (e * K + ks) * 64
+  // (K = n_steps: env-major, an env's rows of consecutive steps adjacent), written where bit
+  // (ks % 64) of marks[e * ceil(K / 64) + ks / 64] is set (marks == null: every row)
   char* stage;
   unsigned long long* marks;  // (consumed: the launch clears the words it read)
   int64_t act_stride;     // floats between consecutive action rows
@@ -2055,16 +2059,28 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   const int slot0 = cons % kSlots;
   int nslot = slot0 + 1 == kSlots ? 0 : slot0 + 1;
   uint32_t so = lane_ring + (uint32_t)slot0 * slot_bytes, sno = lane_ring + (uint32_t)nslot * slot_bytes;
-  // staged replay rows: the wave's mark words of every step of the launch, staged in
-  // LDS once (a per-step global load would sit in the loop's vmcnt accounting, and the
-  // step's first full wait would expose its ~1-us latency every step)
-  if (kRoll && kRows == 2 && ra->marks != nullptr) {
-    // the launch consumes its marks: each word is read by this wave alone and cleared, so
-    // the staged replay's next draws into this buffer start from zero (no fill kernel)
-    for (int q = lane; q < n_steps; q += kWave) {
-      unsigned long long* const w = ra->marks + (int64_t)q * A.nwaves() + ob;
-      l.mk[q] = *w;
-      *w = 0ull;
+  // staged replay rows: each lane's mark bits of every step of the launch (its env's
+  // ceil(n_steps / 64) words, env-major), staged in LDS once (a per-step global load
+  // would sit in the loop's vmcnt accounting, and the step's first full wait would
+  // expose its ~1-us latency every step)
+  if (kRoll && kRows == 2) {
+    // the launch consumes its marks: each env's words are read by its lane alone and
+    // cleared, so the staged replay's next draws into this buffer start from zero (no
+    // fill kernel). No marks: every row, all bits set (the loop reads mk[(ks / 32) % 8]
+    // with no per-step branch on the pointer)
+    static_assert((kMkWords & (kMkWords - 1)) == 0, "l.mk is indexed (ks / 32) % kMkWords");
+    if (ra->marks != nullptr) {
+      const int W = (n_steps + 63) / 64;  // (n_steps <= 256 with marks: sacenv_boat_segment)
+      unsigned long long* const w = ra->marks + (int64_t)e * W;
+      for (int q = 0; q < W; ++q) {
+        const unsigned long long m = w[q];
+        w[q] = 0ull;
+        l.mk[2 * q][lane] = (uint32_t)m;
+        l.mk[2 * q + 1][lane] = (uint32_t)(m >> 32);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < kMkWords; ++q) l.mk[q][lane] = ~0u;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -2282,9 +2298,9 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   bool staged = false;
   float4* stage_row = nullptr;
   if (kRoll && kRows == 2) {
-    const unsigned long long mk = ra->marks != nullptr ? l.mk[ks] : ~0ull;
-    staged = ((mk >> lane) & 1ull) != 0ull;
-    stage_row = reinterpret_cast<float4*>(ra->stage + ((int64_t)ks * A.np + e) * 64);
+    const uint32_t mk = l.mk[(ks >> 5) & (kMkWords - 1)][lane];  // (n_steps <= 256 with marks)
+    staged = ((mk >> (ks & 31)) & 1u) != 0u;
+    stage_row = reinterpret_cast<float4*>(ra->stage + ((int64_t)e * n_steps + ks) * 64);
     if (staged) {
       stage_row[0] = make_float4(o.v[0], o.v[1], o.v[2], o.v[3]);
       stage_row[1] = make_float4(o.v[4], o.v[5], o.v[6], o.v[7]);

@@ -219,6 +219,19 @@ __device__ __forceinline__ int64_t div_floor(int64_t x, int64_t d, double rd) {
   return q;
 }
 
+// The staged segment buffers are ENV-MAJOR (round 6): env e's 64-B row of step j of a
+// segment at (e x seg + j) x 64, its mark bits in the ceil(seg / 64) words from e x
+// that, bit j % 64 -- a row and its predecessor (the row before it: its s) share a
+// mark word (one atomic) and mostly a 128-B line.
+__device__ __forceinline__ int64_t stage_row(const StagedGeom& G, int e, int64_t j) {
+  return ((int64_t)e * G.seg + j) * 64;
+}
+__device__ __forceinline__ void mark_rows(unsigned long long* __restrict__ marks, const StagedGeom& G, int e,
+                                          int64_t j, unsigned long long bits) {
+  const int W = (G.seg + 63) / 64;
+  atomicOr(&marks[(int64_t)e * W + (j >> 6)], bits << (j & 63));
+}
+
 // ring row `row` at learn time (cntr rows stored) -> (global step q, global env u)
 __device__ __forceinline__ void resolve(int64_t row, int64_t cntr, int64_t M, const StagedGeom& G, int64_t* q,
                                         int64_t* u) {
@@ -553,17 +566,18 @@ __global__ void __launch_bounds__(256) k_rb_stage_mark(SacenvReplayParams p, Sta
   resolve(row, cntr, p.mem_size, G, &q, &u);
   if (u < G.offset || u >= G.offset + G.n) return;
   const int e = (int)(u - G.offset);
-  const int nw = G.n_pad / kWave;
-#pragma unroll
-  for (int d = 0; d < 2; ++d) {  // the row, and its predecessor (s)
-    const int64_t j = q - d - G.g * G.seg;
-    if (j >= 0 && j < G.seg)
-      atomicOr(&marks[j * nw + e / kWave], 1ull << (e % kWave));
+  const int64_t j = q - G.g * G.seg;  // the row's step in segment g (or outside it)
+  if (j >= 1 && j < G.seg && (j & 63) != 0) {  // row and predecessor in one word
+    mark_rows(marks, G, e, j - 1, 3ull);
+    return;
   }
+#pragma unroll
+  for (int d = 0; d < 2; ++d)  // the row, and its predecessor (s)
+    if (j - d >= 0 && j - d < G.seg) mark_rows(marks, G, e, j - d, 1ull);
 }
 
 struct StagedRows {
-  const char* cur;   // segment g's 64-B rows [seg][n_pad]
+  const char* cur;   // segment g's 64-B rows [n_pad][seg] (env-major)
   const char* prev;  // segment g - 1's (g = 0: its last row holds the reset obs, term 0)
   float first[SACENV_OBS_DIM];
 };
@@ -597,9 +611,8 @@ __global__ void __launch_bounds__(256) k_rb_gather_staged(SacenvReplayParams p, 
     int64_t j = q - G.g * G.seg;  // > -seg (M <= seg * period)
     const bool in_cur = j >= 0;
     j = in_cur ? j : j + G.seg;
-    const float4* R = reinterpret_cast<const float4*>((in_cur ? S.cur : S.prev) + (j * G.n_pad + e) * 64);
-    const float4* P = j > 0 ? reinterpret_cast<const float4*>((in_cur ? S.cur : S.prev) + ((j - 1) * G.n_pad + e) * 64)
-                            : reinterpret_cast<const float4*>(S.prev + ((int64_t)(G.seg - 1) * G.n_pad + e) * 64);
+    const float4* R = reinterpret_cast<const float4*>((in_cur ? S.cur : S.prev) + stage_row(G, e, j));
+    const float4* P = j > 0 ? R - 4 : reinterpret_cast<const float4*>(S.prev + stage_row(G, e, G.seg - 1));
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const float4 x = R[k], y = P[k];
@@ -704,66 +717,6 @@ __device__ __forceinline__ int tile_rank(bool take, int* wcnt, int* tile_total) 
   return before + __popcll(bal & ((1ull << lane) - 1ull));
 }
 
-// Segment G.g's learns: idx[k][i] (-1: the learn is skipped, fewer than `batch`
-// rows stored) and the marks of the rows they read on this rank -- the row and
-// its predecessor (its s) -- in segment G.g (marks_cur) or G.g - 1 (marks_prev;
-// with M <= seg x period a row lies in one of the two). Four consecutive draws per
-// thread (one Philox block for an aligned four; a wave covers one 256-slot tile);
-// with tile_cnt, also the records per 256-slot tile the all-gather's pack of this
-// segment will write (so the pack needs no count pass).
-constexpr int kDrawThreads4 = 256;  // x 4 draws
-__global__ void __launch_bounds__(kDrawThreads4) k_rb_draw_ctr(SacenvReplayParams p, StagedGeom G, uint64_t seed,
-                                                               int batch, int nb, int64_t* __restrict__ idx,
-                                                               unsigned long long* __restrict__ marks_prev,
-                                                               unsigned long long* __restrict__ marks_cur,
-                                                               int* __restrict__ tile_cnt, int skip_owner) {
-  const int64_t total = (int64_t)batch * nb;
-  const int64_t t0 = (blockIdx.x * (int64_t)kDrawThreads4 + threadIdx.x) * 4;
-  const int64_t M = p.mem_size;
-  const int nw = G.n_pad / kWave;
-  int takes = 0;  // (slots the all-gather's pack of this segment takes on this rank)
-  uint64_t blk[4] = {0ull, 0ull, 0ull, 0ull};
-  int64_t blk_c = -1, blk_L = -1;
-  for (int s4 = 0; s4 < 4; ++s4) {
-    const int64_t t = t0 + s4;
-    if (t >= total) break;
-    const int k = (int)(t / batch), i = (int)(t - (int64_t)k * batch);
-    const int64_t L = G.g * G.seg + k, cntr = (L + 1) * G.period;
-    if (cntr < batch) {  // continuous_agent.py:97-98: learn() returns before sampling
-      idx[t] = -1;
-      takes += skip_owner != 0 ? 1 : 0;
-      continue;
-    }
-    const uint64_t rng = (uint64_t)((cntr < M ? cntr : M) - 1);
-    if ((int64_t)(i >> 2) != blk_c || L != blk_L) {  // the block of this draw's four
-      blk[0] = (uint64_t)(i >> 2), blk[1] = (uint64_t)L, blk[2] = 0ull, blk[3] = 0ull;
-      philox4x64_10(blk, seed, 0ull);
-      blk_c = i >> 2, blk_L = L;
-    }
-    const int64_t row = ctr_draw4(seed, L, i, rng, range_mask(rng), blk);
-    idx[t] = row;
-    int64_t q, u;
-    resolve(row, cntr, M, G, &q, &u);
-    if (u < G.offset || u >= G.offset + G.n) continue;
-    ++takes;
-    const int e = (int)(u - G.offset);
-#pragma unroll
-    for (int d = 0; d < 2; ++d) {  // the row, and its predecessor (s)
-      const int64_t qq = q - d;
-      if (qq < 0) continue;        // step -1: the reset obs begin() staged
-      int64_t j = qq - G.g * G.seg;
-      unsigned long long* const mk = j >= 0 ? marks_cur : marks_prev;
-      j = j >= 0 ? j : j + G.seg;
-      if (mk != nullptr) atomicOr(&mk[j * nw + e / kWave], 1ull << (e % kWave));
-    }
-  }
-  if (tile_cnt != nullptr) {  // the pack's per-tile record counts, drawn ahead: a wave = one tile
-    for (int o = kWave / 2; o > 0; o >>= 1) takes += __shfl_xor(takes, o);
-    const int64_t tile = (blockIdx.x * (int64_t)kDrawThreads4 + threadIdx.x) / kWave;
-    if ((threadIdx.x & (kWave - 1)) == 0 && tile * kPackTile < total) tile_cnt[tile] = takes;
-  }
-}
-
 // The all-gather form of the exchange. Each rank packs the rows IT owns of the
 // segment's learns -- one 25-word record per sampled row: slot (learn x batch +
 // draw) | terminal << 31, reward f32, state [11], new_state [11], action -- into
@@ -771,18 +724,237 @@ __global__ void __launch_bounds__(kDrawThreads4) k_rb_draw_ctr(SacenvReplayParam
 // packs the rows of skipped learns (all zero). One all-gather of the chunks and
 // an unpack on every rank rebuild sacenv_replay_sample_staged's `words`, bit for
 // bit: every slot comes from exactly one rank. The records sit in slot order (a
-// count pass per 1 024-slot tile, then each tile's prefix over the tiles before
-// it: no atomics -- one count word taking every wave's atomic cost ~100 us a
-// segment -- and the chunk is the same bytes run to run).
+// count per 256-slot tile, then each tile's prefix over the tiles before it: no
+// atomics -- one count word taking every wave's atomic cost ~100 us a segment --
+// and the chunk is the same bytes run to run).
 constexpr int kRecWords = 2 + 2 * SACENV_OBS_DIM + 1;  // 25
 constexpr int kChunkHdr = 4;
-// does this rank pack slot t (its row, or rank 0 a skipped learn's zero row)?
+
+// One 256-slot tile of side work in LDS: the tile's records (the pack assembles them
+// here and writes them out as one contiguous run; the unpack reads its run in here:
+// coalesced dwords instead of a 100-B stride per lane), the per-wave counts, the
+// tile's first record.
+struct SideLds {
+  uint32_t rec[kPackTile * kRecWords];  // the tile's records
+  uint32_t meta[kPackTile];             // unpack: the record's learn's words offset
+  uint32_t meta2[kPackTile];            // unpack: the record's draw within its learn
+  int wcnt[kPackTile / kWave];
+  int base;
+};
+
+// Segment G.g's learns, slots [tile x 256, tile x 256 + 256): idx[k][i] (-1: the
+// learn is skipped, fewer than `batch` rows stored) and the marks of the rows they
+// read on this rank -- the row and its predecessor (its s) -- in segment G.g
+// (marks_cur) or G.g - 1 (marks_prev; with M <= seg x period a row lies in one of
+// the two). One draw per thread (the four threads of an aligned four compute their
+// shared Philox block each: ~200 integer ops, cheaper than any exchange); with
+// tile_cnt, also the records this tile's pack will write (so the pack needs no
+// count pass).
+__device__ __forceinline__ void draw_ctr_tile(const SacenvReplayParams& p, const StagedGeom& G, uint64_t seed,
+                                              int batch, int nb, int64_t* __restrict__ idx,
+                                              unsigned long long* __restrict__ marks_prev,
+                                              unsigned long long* __restrict__ marks_cur, int* __restrict__ tile_cnt,
+                                              int skip_owner, int64_t tile, int* wcnt) {
+  const int total = batch * nb;  // (< 2^31: check_ctr_shape)
+  const int t = (int)(tile * kPackTile) + (int)threadIdx.x;
+  const int64_t M = p.mem_size;
+  bool take = false;  // (a slot the all-gather's pack of this segment takes on this rank)
+  if (t < total) {
+    const int k = t / batch, i = t - k * batch;
+    const int64_t L = G.g * G.seg + k, cntr = (L + 1) * G.period;
+    if (cntr < batch) {  // continuous_agent.py:97-98: learn() returns before sampling
+      idx[t] = -1;
+      take = skip_owner != 0;
+    } else {
+      const uint64_t rng = (uint64_t)((cntr < M ? cntr : M) - 1);
+      uint64_t blk[4] = {(uint64_t)(i >> 2), (uint64_t)L, 0ull, 0ull};  // the block of this draw's four
+      philox4x64_10(blk, seed, 0ull);
+      const int64_t row = ctr_draw4(seed, L, i, rng, range_mask(rng), blk);
+      idx[t] = row;
+      int64_t q, u;
+      resolve(row, cntr, M, G, &q, &u);
+      if (u >= G.offset && u < G.offset + G.n) {
+        take = true;
+        const int e = (int)(u - G.offset);
+        // the row and its predecessor (s); the predecessor of segment g's first row is
+        // segment g - 1's last (a learn of segment g reaches no row before step 1 of
+        // segment g - 1: M <= seg x period); step -1 is the reset obs begin() staged
+        int64_t j = q - G.g * G.seg;
+        unsigned long long* const mk = j >= 0 ? marks_cur : marks_prev;
+        j = j >= 0 ? j : j + G.seg;
+        if (j >= 1 && (j & 63) != 0) {  // both in one word: one atomic
+          if (mk != nullptr) mark_rows(mk, G, e, j - 1, 3ull);
+        } else {
+          if (mk != nullptr) mark_rows(mk, G, e, j, 1ull);
+          if (q >= 1) {
+            unsigned long long* const mp = j >= 1 ? mk : marks_prev;  // (j = 0: segment g - 1's last)
+            if (mp != nullptr) mark_rows(mp, G, e, j >= 1 ? j - 1 : G.seg - 1, 1ull);
+          }
+        }
+      }
+    }
+  }
+  if (tile_cnt != nullptr) {  // the pack's per-tile record counts, drawn ahead
+    int tile_total;
+    tile_rank(take, wcnt, &tile_total);
+    if (threadIdx.x == 0 && (int64_t)tile * kPackTile < total) tile_cnt[tile] = tile_total;
+  }
+}
+
+// do this rank's records include slot t (its row, or rank 0 a skipped learn's zero row)?
 __device__ __forceinline__ bool pack_takes(const SacenvReplayParams& p, const StagedGeom& G, int batch, int64_t t,
                                            int64_t row, int skip_owner, int64_t* q, int64_t* u) {
   *q = 0;
   *u = -1;
   if (row >= 0) resolve(row, (G.g * G.seg + t / batch + 1) * G.period, p.mem_size, G, q, u);
   return (*u >= G.offset && *u < G.offset + G.n) || (row == -1 && skip_owner);
+}
+
+// The records of tile `tile` (slots tile x 256 ...): each taking thread forms its
+// record in LDS at its rank within the tile, then the block writes the tile's run
+// [base, base + count) of the chunk with coalesced dword stores (records past `cap`
+// are dropped: the header's count says so and the unpack flags it). The last tile
+// writes the header's count.
+__device__ __forceinline__ void pack_tile(const SacenvReplayParams& p, const StagedGeom& G, const StagedRows& S,
+                                          int batch, int nb, const int64_t* __restrict__ idx,
+                                          uint32_t* __restrict__ chunk, int64_t cap, int skip_owner,
+                                          const int* __restrict__ tile_cnt, int64_t tile, int64_t n_tiles,
+                                          SideLds& l) {
+  constexpr int D = SACENV_OBS_DIM;
+  const int tid = threadIdx.x;
+  if (tid < kWave) {  // this tile's first record: the counts of the tiles before it (8 loads in flight per lane)
+    int s = 0;
+    for (int64_t b0 = 0; b0 < tile; b0 += 8 * kWave) {
+      int v[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int64_t i = b0 + r * kWave + tid;
+        v[r] = i < tile ? tile_cnt[i] : 0;
+      }
+#pragma unroll
+      for (int r = 0; r < 8; ++r) s += v[r];
+    }
+    for (int o = kWave / 2; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (tid == 0) l.base = s;
+  }
+  const int64_t t = tile * kPackTile + tid;
+  const bool live = t < (int64_t)batch * nb;
+  const int64_t row = live ? idx[t] : -2;
+  int64_t q = 0, u = -1;
+  const bool take = live && pack_takes(p, G, batch, t, row, skip_owner, &q, &u);
+  const bool own = take && row >= 0;
+  int tile_total;
+  const int rank = tile_rank(take, l.wcnt, &tile_total);  // (its barrier also publishes l.base)
+  const int64_t base = l.base;
+  if (tile == n_tiles - 1 && tid == 0) chunk[0] = (uint32_t)(base + tile_total);  // the record count
+  float sn[16], sv[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) sn[k] = sv[k] = 0.f;
+  uint32_t tm = 0u;
+  if (own) {  // (as k_rb_gather_staged)
+    const int e = (int)(u - G.offset);
+    int64_t j = q - G.g * G.seg;
+    const bool in_cur = j >= 0;
+    j = in_cur ? j : j + G.seg;
+    const float4* R = reinterpret_cast<const float4*>((in_cur ? S.cur : S.prev) + stage_row(G, e, j));
+    const float4* P = j > 0 ? R - 4 : reinterpret_cast<const float4*>(S.prev + stage_row(G, e, G.seg - 1));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float4 x = R[k], y = P[k];
+      sn[4 * k] = x.x, sn[4 * k + 1] = x.y, sn[4 * k + 2] = x.z, sn[4 * k + 3] = x.w;
+      sv[4 * k] = y.x, sv[4 * k + 1] = y.y, sv[4 * k + 2] = y.z, sv[4 * k + 3] = y.w;
+    }
+    const bool pdone = (__float_as_uint(sv[13]) & 0xFFu) != 0u;
+    const float o3 = sv[14];
+#pragma unroll
+    for (int k = 0; k < D; ++k) sv[k] = pdone ? S.first[k] : sv[k];
+    if (G.exp2 && pdone) sv[3] = o3;
+    tm = (p.terminal_mask >> ((__float_as_uint(sn[13]) >> 8) & 0xFFu)) & 1u;
+  }
+  if (take) {
+    uint32_t* const rec = l.rec + rank * kRecWords;
+    rec[0] = (uint32_t)t | (tm << 31);
+    rec[1] = __float_as_uint(sn[11]);
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      rec[2 + k] = __float_as_uint(sv[k]);
+      rec[2 + D + k] = __float_as_uint(sn[k]);
+    }
+    rec[2 + 2 * D] = __float_as_uint(sn[12]);
+  }
+  __syncthreads();
+  int64_t nrec = tile_total;
+  if (base + nrec > cap) nrec = cap - base;  // (past cap: dropped; the count tells the unpack)
+  if (nrec <= 0) return;
+  uint32_t* const dst = chunk + kChunkHdr + base * kRecWords;
+  const int nw = (int)nrec * kRecWords;
+  for (int w = tid; w < nw; w += kPackTile) dst[w] = l.rec[w];
+}
+
+// Records [j0, j0 + 256) of chunk r -> sacenv_replay_sample_staged's words: the run
+// is read into LDS with coalesced dwords, then one thread per record scatters it to
+// its slot. A count above cap sets status bit 0 (the first tile of the chunk).
+__device__ __forceinline__ void unpack_tile(const uint32_t* __restrict__ gathered, int64_t chunk_words, int64_t cap,
+                                            int batch, uint32_t* __restrict__ words, int64_t per,
+                                            int32_t* __restrict__ status, int64_t blk, int64_t tiles_per_chunk,
+                                            SideLds& l) {
+  constexpr int D = SACENV_OBS_DIM;
+  const int tid = threadIdx.x;
+  const int64_t r = blk / tiles_per_chunk;
+  const int64_t j0 = (blk - r * tiles_per_chunk) * kPackTile;
+  const uint32_t* const hdr = gathered + r * chunk_words;
+  int64_t cnt = hdr[0];
+  if (j0 == 0 && tid == 0 && cnt > cap) atomicOr(status, 1);
+  cnt = cnt < cap ? cnt : cap;
+  const int nrec = (int)(cnt - j0 < kPackTile ? cnt - j0 : kPackTile);
+  if (nrec <= 0) return;  // (uniform over the block)
+  const uint32_t* const src = hdr + kChunkHdr + j0 * kRecWords;
+  for (int w = tid; w < nrec * kRecWords; w += kPackTile) l.rec[w] = src[w];
+  __syncthreads();
+  if (tid < nrec) {  // the record's batch: words offset of learn b, draw i (i < 2^31 / 26)
+    const uint32_t slot = l.rec[tid * kRecWords] & 0x7FFFFFFFu;
+    const uint32_t b = slot / (uint32_t)batch, i = slot - b * (uint32_t)batch;
+    l.meta[tid] = (uint32_t)(b * per);  // (n_batches x per < 2^32: the host's size checks)
+    l.meta2[tid] = i;
+  }
+  __syncthreads();
+  // one output word per thread, so consecutive lanes write consecutive words where the
+  // records' slots are consecutive (a 100-B record per lane scattered 26 partial lines)
+  const int64_t B = batch;
+  for (int w = tid; w < nrec * 2; w += kPackTile) {  // reward f64: two words each
+    const int q = w >> 1;
+    const uint32_t m = l.meta[q], i = l.meta2[q];
+    const double r64 = (double)__uint_as_float(l.rec[q * kRecWords + 1]);
+    uint64_t rb;
+    __builtin_memcpy(&rb, &r64, 8);
+    words[(int64_t)m + 2 * (int64_t)i + (w & 1)] = (w & 1) ? (uint32_t)(rb >> 32) : (uint32_t)rb;
+  }
+  for (int w = tid; w < nrec * D; w += kPackTile) {  // state
+    const int q = w / D, k = w - q * D;
+    const uint32_t m = l.meta[q], i = l.meta2[q];
+    words[(int64_t)m + 2 * B + (int64_t)i * D + k] = l.rec[q * kRecWords + 2 + k];
+  }
+  for (int w = tid; w < nrec * D; w += kPackTile) {  // new_state
+    const int q = w / D, k = w - q * D;
+    const uint32_t m = l.meta[q], i = l.meta2[q];
+    words[(int64_t)m + 2 * B + B * D + (int64_t)i * D + k] = l.rec[q * kRecWords + 2 + D + k];
+  }
+  if (tid < nrec) {  // action, terminal
+    const uint32_t m = l.meta[tid], i = l.meta2[tid];
+    const uint32_t* const rec = l.rec + tid * kRecWords;
+    uint32_t* const W = words + (int64_t)m;
+    W[2 * B + 2 * B * D + i] = rec[2 + 2 * D];
+    W[2 * B + 2 * B * D + B + i] = rec[0] >> 31;
+  }
+}
+
+__global__ void __launch_bounds__(kPackTile) k_rb_draw_ctr(SacenvReplayParams p, StagedGeom G, uint64_t seed,
+                                                           int batch, int nb, int64_t* __restrict__ idx,
+                                                           unsigned long long* __restrict__ marks_prev,
+                                                           unsigned long long* __restrict__ marks_cur,
+                                                           int* __restrict__ tile_cnt, int skip_owner) {
+  __shared__ int wcnt[kPackTile / kWave];
+  draw_ctr_tile(p, G, seed, batch, nb, idx, marks_prev, marks_cur, tile_cnt, skip_owner, blockIdx.x, wcnt);
 }
 
 __global__ void __launch_bounds__(kPackTile) k_rb_pack_count(SacenvReplayParams p, StagedGeom G, int batch, int nb,
@@ -801,97 +973,65 @@ __global__ void __launch_bounds__(kPackTile) k_rb_pack_staged(SacenvReplayParams
                                                               int nb, const int64_t* __restrict__ idx,
                                                               uint32_t* __restrict__ chunk, int64_t cap, int skip_owner,
                                                               const int* __restrict__ tile_cnt) {
-  constexpr int D = SACENV_OBS_DIM;
-  __shared__ int wcnt[kPackTile / kWave];
-  __shared__ int s_base;
-  const int tid = threadIdx.x;
-  // this tile's first record: the counts of the tiles before it
-  if (tid < kWave) {
-    int s = 0;
-    for (int i = tid; i < (int)blockIdx.x; i += kWave) s += tile_cnt[i];
-    for (int o = kWave / 2; o > 0; o >>= 1) s += __shfl_xor(s, o);
-    if (tid == 0) s_base = s;
-  }
-  const int64_t t = blockIdx.x * (int64_t)kPackTile + tid;
-  const bool live = t < (int64_t)batch * nb;
-  const int64_t row = live ? idx[t] : -2;
-  int64_t q, u;
-  const bool take = live && pack_takes(p, G, batch, t, row, skip_owner, &q, &u);
-  const bool own = take && row >= 0;
-  int tile_total;
-  const int rank = tile_rank(take, wcnt, &tile_total);  // (its barrier also publishes s_base)
-  const int64_t pos = (int64_t)s_base + rank;
-  if (blockIdx.x == gridDim.x - 1 && tid == 0) chunk[0] = (uint32_t)(s_base + tile_total);  // the record count
-  float sn[16], sv[16];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) sn[k] = sv[k] = 0.f;
-  uint32_t tm = 0u;
-  if (own) {  // (as k_rb_gather_staged)
-    const int e = (int)(u - G.offset);
-    int64_t j = q - G.g * G.seg;
-    const bool in_cur = j >= 0;
-    j = in_cur ? j : j + G.seg;
-    const float4* R = reinterpret_cast<const float4*>((in_cur ? S.cur : S.prev) + (j * G.n_pad + e) * 64);
-    const float4* P = j > 0 ? reinterpret_cast<const float4*>((in_cur ? S.cur : S.prev) + ((j - 1) * G.n_pad + e) * 64)
-                            : reinterpret_cast<const float4*>(S.prev + ((int64_t)(G.seg - 1) * G.n_pad + e) * 64);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float4 x = R[k], y = P[k];
-      sn[4 * k] = x.x, sn[4 * k + 1] = x.y, sn[4 * k + 2] = x.z, sn[4 * k + 3] = x.w;
-      sv[4 * k] = y.x, sv[4 * k + 1] = y.y, sv[4 * k + 2] = y.z, sv[4 * k + 3] = y.w;
-    }
-    const bool pdone = (__float_as_uint(sv[13]) & 0xFFu) != 0u;
-    const float o3 = sv[14];
-#pragma unroll
-    for (int k = 0; k < D; ++k) sv[k] = pdone ? S.first[k] : sv[k];
-    if (G.exp2 && pdone) sv[3] = o3;
-    tm = (p.terminal_mask >> ((__float_as_uint(sn[13]) >> 8) & 0xFFu)) & 1u;
-  }
-  if (!take || pos >= cap) return;  // (past cap: the header's count says so; the unpack flags it)
-  uint32_t* const rec = chunk + kChunkHdr + pos * kRecWords;
-  rec[0] = (uint32_t)t | (tm << 31);
-  rec[1] = __float_as_uint(sn[11]);
-#pragma unroll
-  for (int k = 0; k < D; ++k) {
-    rec[2 + k] = __float_as_uint(sv[k]);
-    rec[2 + D + k] = __float_as_uint(sn[k]);
-  }
-  rec[2 + 2 * D] = __float_as_uint(sn[12]);
+  __shared__ SideLds l;
+  pack_tile(p, G, S, batch, nb, idx, chunk, cap, skip_owner, tile_cnt, blockIdx.x, gridDim.x, l);
 }
 
-// world chunks of chunk_words each -> sacenv_replay_sample_staged's words. One
-// thread per record slot of every chunk; a count above cap sets status bit 0.
-__global__ void __launch_bounds__(256) k_rb_unpack_staged(const uint32_t* __restrict__ gathered, int world,
-                                                          int64_t chunk_words, int64_t cap, int batch,
-                                                          uint32_t* __restrict__ words, int64_t per,
-                                                          int32_t* __restrict__ status) {
-  constexpr int D = SACENV_OBS_DIM;
-  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (t >= (int64_t)world * cap) return;
-  const int r = (int)(t / cap);
-  const int64_t j = t - (int64_t)r * cap;
-  const uint32_t* const hdr = gathered + (int64_t)r * chunk_words;
-  const int64_t cnt = hdr[0];
-  if (j == 0 && cnt > cap) atomicOr(status, 1);
-  if (j >= cnt) return;
-  const uint32_t* const rec = hdr + kChunkHdr + j * kRecWords;
-  const uint32_t s0 = rec[0], slot = s0 & 0x7FFFFFFFu;
-  const int b = (int)(slot / (uint32_t)batch), i = (int)(slot - (uint32_t)b * (uint32_t)batch);
-  uint32_t* const W = words + (int64_t)b * per;
-  const double r64 = (double)__uint_as_float(rec[1]);
-  uint64_t rb;
-  __builtin_memcpy(&rb, &r64, 8);
-  W[2 * i] = (uint32_t)rb;
-  W[2 * i + 1] = (uint32_t)(rb >> 32);
-  uint32_t* const st = W + 2 * batch + (int64_t)i * D;
-  uint32_t* const ns = W + 2 * batch + (int64_t)batch * D + (int64_t)i * D;
-#pragma unroll
-  for (int k = 0; k < D; ++k) {
-    st[k] = rec[2 + k];
-    ns[k] = rec[2 + D + k];
+__global__ void __launch_bounds__(kPackTile) k_rb_unpack_staged(const uint32_t* __restrict__ gathered,
+                                                                int64_t chunk_words, int64_t cap, int batch,
+                                                                uint32_t* __restrict__ words, int64_t per,
+                                                                int32_t* __restrict__ status, int64_t tiles_per_chunk) {
+  __shared__ SideLds l;
+  unpack_tile(gathered, chunk_words, cap, batch, words, per, status, blockIdx.x, tiles_per_chunk, l);
+}
+
+// A segment's side work in ONE launch (sacenv_replay_stage_side): the unpack of one
+// segment's collected chunks, the pack of the next segment's rows and the draws of a
+// later segment, on disjoint buffers (the host checks) -- three launches, their
+// boundaries and their tails become one, and the three kinds of blocks share the GPU
+// (each alone leaves it mostly idle: ~1 000 short-lived blocks bound by latency).
+// Block ranges: the draws' tiles first (their Philox and atomics are the longest
+// chains), then the pack's tiles, then the unpack's.
+struct SideArgs {
+  SacenvReplayParams p;
+  int batch, nb, skip_owner, world;
+  // draws
+  StagedGeom Gd;
+  uint64_t seed;
+  int64_t* d_idx;
+  unsigned long long* marks_prev;
+  unsigned long long* marks_cur;
+  int* d_tiles;
+  int64_t n_draw;
+  // pack
+  StagedGeom Gp;
+  StagedRows S;
+  const int64_t* p_idx;
+  const int* p_tiles;
+  uint32_t* chunk;
+  int64_t cap, n_pack;
+  // unpack
+  const uint32_t* gathered;
+  uint32_t* words;
+  int32_t* status;
+  int64_t chunk_words, per, u_tiles, n_unpack;
+};
+
+__global__ void __launch_bounds__(kPackTile) k_rb_side(SideArgs a) {
+  __shared__ SideLds l;
+  int64_t b = blockIdx.x;
+  if (b < a.n_draw) {
+    draw_ctr_tile(a.p, a.Gd, a.seed, a.batch, a.nb, a.d_idx, a.marks_prev, a.marks_cur, a.d_tiles, a.skip_owner, b,
+                  l.wcnt);
+    return;
   }
-  W[2 * batch + 2 * (int64_t)batch * D + i] = rec[2 + 2 * D];
-  W[2 * batch + 2 * (int64_t)batch * D + batch + i] = s0 >> 31;
+  b -= a.n_draw;
+  if (b < a.n_pack) {
+    pack_tile(a.p, a.Gp, a.S, a.batch, a.nb, a.p_idx, a.chunk, a.cap, a.skip_owner, a.p_tiles, b, a.n_pack, l);
+    return;
+  }
+  b -= a.n_pack;
+  unpack_tile(a.gathered, a.chunk_words, a.cap, a.batch, a.words, a.per, a.status, b, a.u_tiles, l);
 }
 
 // A stand-in for a collective's kernel on one GPU (bench.py's replay_path at N =
@@ -907,6 +1047,9 @@ __global__ void __launch_bounds__(256) k_copy_standin(const uint4* __restrict__ 
     dst[q] = src[q];
   while (__builtin_amdgcn_s_memrealtime() - t0 < min_ticks) __builtin_amdgcn_s_sleep(8);
 }
+
+// 32-bit words of one learn's batch in sacenv_replay_sample_staged's packing
+int64_t words_per_batch(int32_t batch) { return (int64_t)batch * (2 * SACENV_OBS_DIM + 1 + 3); }
 
 int check_replay(const SacenvReplayParams* p) {
   if (p == nullptr) return SACENV_E_NULL;
@@ -1154,7 +1297,7 @@ int sacenv_replay_stage_mark(const SacenvReplayParams* p, const SacenvStagedPara
   if (g < 0 || batch < 0 || n_batches < 0 || n_batches > sp->seg) return SACENV_E_SIZE;
   if (!idx_g || !marks) return SACENV_E_NULL;
   if (!staged_range_ok(sp, g)) return SACENV_E_RANGE;
-  const hipError_t e = hipMemsetAsync(marks, 0, (size_t)sp->seg * (sp->n_pad / kWave) * 8, (hipStream_t)stream);
+  const hipError_t e = hipMemsetAsync(marks, 0, (size_t)sp->n_pad * ((sp->seg + 63) / 64) * 8, (hipStream_t)stream);
   if (e != hipSuccess) return (int)e;
   const int64_t per = (int64_t)batch * n_batches;
   if (per == 0) return SACENV_OK;
@@ -1219,8 +1362,7 @@ int sacenv_replay_stage_draw_ctr(const SacenvReplayParams* p, const SacenvStaged
   if (idx == nullptr) return SACENV_E_NULL;
   const int64_t total = (int64_t)batch * n_batches;
   if (total == 0) return SACENV_OK;
-  hipLaunchKernelGGL(k_rb_draw_ctr, dim3((unsigned)((total + 4 * kDrawThreads4 - 1) / (4 * kDrawThreads4))),
-                     dim3(kDrawThreads4), 0,
+  hipLaunchKernelGGL(k_rb_draw_ctr, dim3((unsigned)((total + kPackTile - 1) / kPackTile)), dim3(kPackTile), 0,
                      (hipStream_t)stream, *p, geom(p, sp, g), seed, batch, n_batches, idx,
                      reinterpret_cast<unsigned long long*>(marks_prev), reinterpret_cast<unsigned long long*>(marks_cur),
                      tiles, sp->offset == 0 ? 1 : 0);
@@ -1317,13 +1459,88 @@ int sacenv_replay_stage_unpack(int32_t world, int64_t chunk_bytes, int64_t cap, 
   if ((int64_t)batch * n_batches >= ((int64_t)1 << 31) || (int64_t)world * cap >= ((int64_t)1 << 31))
     return SACENV_E_SIZE;
   if (chunk_bytes < 4 * (kChunkHdr + cap * kRecWords) || (chunk_bytes & 3) != 0) return SACENV_E_SIZE;
+  if ((int64_t)n_batches * words_per_batch(batch) >= ((int64_t)1 << 32)) return SACENV_E_SIZE;  // 32-bit offsets
   if (!gathered || !words || !status_word) return SACENV_E_NULL;
-  const int64_t n = (int64_t)world * cap;
-  if (n == 0 || batch == 0) return SACENV_OK;
-  const int64_t per = (int64_t)batch * (2 * SACENV_OBS_DIM + 1 + 3);
-  hipLaunchKernelGGL(k_rb_unpack_staged, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                     static_cast<const uint32_t*>(gathered), world, chunk_bytes / 4, cap, batch, words, per,
-                     status_word);
+  const int64_t tiles = (cap + kPackTile - 1) / kPackTile;
+  if (tiles == 0 || batch == 0) return SACENV_OK;
+  hipLaunchKernelGGL(k_rb_unpack_staged, dim3((unsigned)(world * tiles)), dim3(kPackTile), 0, (hipStream_t)stream,
+                     static_cast<const uint32_t*>(gathered), chunk_bytes / 4, cap, batch, words, words_per_batch(batch),
+                     status_word, tiles);
+  return status();
+}
+
+int sacenv_replay_stage_side(const SacenvReplayParams* p, const SacenvStagedParams* sp, int32_t batch,
+                             int32_t n_batches, const SacenvStageSide* w, void* stream) {
+  if (w == nullptr) return SACENV_E_NULL;
+  const bool draw = w->draw_g >= 0, pack = w->pack_g >= 0, unpack = w->gathered != nullptr;
+  int rc = check_ctr_shape(p, sp, draw ? w->draw_g : 0, batch, n_batches);
+  if (rc) return rc;
+  if (pack && (rc = check_ctr_shape(p, sp, w->pack_g, batch, n_batches))) return rc;
+  const int64_t total = (int64_t)batch * n_batches;
+  const int64_t tiles = (total + kPackTile - 1) / kPackTile;
+  SideArgs a = {};
+  a.p = *p;
+  a.batch = batch;
+  a.nb = n_batches;
+  a.skip_owner = sp->offset == 0 ? 1 : 0;
+  if (draw) {
+    if (!w->draw_idx || !w->marks_cur || !w->draw_tiles) return SACENV_E_NULL;
+    a.Gd = geom(p, sp, w->draw_g);
+    a.seed = w->seed;
+    a.d_idx = w->draw_idx;
+    a.marks_prev = reinterpret_cast<unsigned long long*>(w->marks_prev);
+    a.marks_cur = reinterpret_cast<unsigned long long*>(w->marks_cur);
+    a.d_tiles = w->draw_tiles;
+    a.n_draw = tiles;
+  }
+  if (pack || unpack) {
+    if (w->cap < 0 || w->cap > total) return SACENV_E_SIZE;
+    if ((int64_t)w->world * w->cap >= ((int64_t)1 << 31)) return SACENV_E_SIZE;
+    a.cap = w->cap;
+  }
+  if (pack) {
+    if (!w->stage_cur || !w->stage_prev || !w->pack_idx || !w->pack_tiles || !w->chunk) return SACENV_E_NULL;
+    if (((reinterpret_cast<uintptr_t>(w->stage_cur) | reinterpret_cast<uintptr_t>(w->stage_prev)) & 15u) != 0u ||
+        (reinterpret_cast<uintptr_t>(w->chunk) & 3u) != 0u)
+      return SACENV_E_RANGE;
+    // the roles run side by side: the pack must not read what the draws write
+    if (draw && (w->pack_idx == w->draw_idx || w->pack_tiles == w->draw_tiles)) return SACENV_E_RANGE;
+    a.Gp = geom(p, sp, w->pack_g);
+    a.S.cur = static_cast<const char*>(w->stage_cur);
+    a.S.prev = static_cast<const char*>(w->stage_prev);
+    for (int k = 0; k < SACENV_OBS_DIM; ++k) a.S.first[k] = sp->first_obs[k];
+    a.p_idx = w->pack_idx;
+    a.p_tiles = w->pack_tiles;
+    a.chunk = static_cast<uint32_t*>(w->chunk);
+    a.n_pack = tiles;
+  }
+  if (unpack) {
+    if (w->world < 1) return SACENV_E_SIZE;
+    if (w->chunk_bytes < 4 * (kChunkHdr + w->cap * kRecWords) || (w->chunk_bytes & 3) != 0) return SACENV_E_SIZE;
+    if ((int64_t)n_batches * words_per_batch(batch) >= ((int64_t)1 << 32)) return SACENV_E_SIZE;  // 32-bit offsets
+    if (!w->words || !w->status_word) return SACENV_E_NULL;
+    // nor the unpack read the chunk the pack writes
+    if (pack && static_cast<const char*>(w->gathered) < static_cast<const char*>(w->chunk) + w->chunk_bytes &&
+        static_cast<const char*>(w->chunk) < static_cast<const char*>(w->gathered) + w->world * w->chunk_bytes)
+      return SACENV_E_RANGE;
+    a.gathered = static_cast<const uint32_t*>(w->gathered);
+    a.words = w->words;
+    a.status = w->status_word;
+    a.world = w->world;
+    a.chunk_words = w->chunk_bytes / 4;
+    a.per = words_per_batch(batch);
+    a.u_tiles = (w->cap + kPackTile - 1) / kPackTile;
+    a.n_unpack = w->world * a.u_tiles;
+  }
+  const int64_t blocks = a.n_draw + a.n_pack + a.n_unpack;
+  if (total == 0 || blocks == 0) {
+    if (pack && w->chunk) {  // no records: only the count
+      const hipError_t e = hipMemsetAsync(w->chunk, 0, 4 * kChunkHdr, (hipStream_t)stream);
+      return e == hipSuccess ? SACENV_OK : (int)e;
+    }
+    return SACENV_OK;
+  }
+  hipLaunchKernelGGL(k_rb_side, dim3((unsigned)blocks), dim3(kPackTile), 0, (hipStream_t)stream, a);
   return status();
 }
 

@@ -14,7 +14,7 @@ PKG_ROOT = _build.PKG_ROOT
 LIB_PATH = os.environ.get("SACENV_LIB", _build.LIB)
 LOADED_DIGEST = None  # source digest of the loaded library (the in-tree build)
 
-ABI_VERSION = 19
+ABI_VERSION = 20
 OBS_DIM = 11
 MT_N = 624
 MAX_KNOTS = 16
@@ -112,6 +112,14 @@ class StagedParams(C.Structure):
                 ("experiment", _i32), ("first_obs", C.c_float * OBS_DIM)]
 
 
+class StageSide(C.Structure):
+    """SacenvStageSide (sacenv.h): one segment's draws, pack and unpack in one launch."""
+    _fields_ = [("draw_g", _i64), ("seed", C.c_uint64), ("draw_idx", _p), ("marks_prev", _p), ("marks_cur", _p),
+                ("draw_tiles", _p), ("pack_g", _i64), ("stage_cur", _p), ("stage_prev", _p), ("pack_idx", _p),
+                ("pack_tiles", _p), ("cap", _i64), ("chunk", _p), ("gathered", _p), ("chunk_bytes", _i64),
+                ("words", _p), ("status_word", _p), ("world", _i32), ("reserved", _i32)]
+
+
 REPLAY_LAYOUT_FIELDS = ("total_bytes", "state", "new_state", "action", "reward", "terminal",
                         "mem_cntr", "mt_key", "mt_pos")
 
@@ -147,7 +155,7 @@ EXPORTS = ("sacenv_abi_version", "sacenv_error_string", "sacenv_boat_layout",
            "sacenv_replay_sample_shard", "sacenv_replay_stage_scratch_bytes", "sacenv_replay_stage_draw",
            "sacenv_replay_stage_mark", "sacenv_replay_sample_staged", "sacenv_replay_gather",
            "sacenv_replay_stage_draw_ctr", "sacenv_replay_stage_chunk", "sacenv_replay_stage_pack",
-           "sacenv_replay_stage_unpack", "sacenv_copy_standin",
+           "sacenv_replay_stage_unpack", "sacenv_replay_stage_side", "sacenv_copy_standin",
            "sacenv_compact_done", "sacenv_boat_reset_list", "sacenv_sac_layout", "sacenv_sac_sync",
            "sacenv_sac_act", "sacenv_sac_act_handoff", "sacenv_sac_act_occupancy", "sacenv_sac_learn")
 
@@ -231,6 +239,7 @@ def load(path: str | None = None):
         "sacenv_replay_stage_chunk": (C.c_int, [RP, SP, _i32, _i32, C.POINTER(_i64), C.POINTER(_i64)]),
         "sacenv_replay_stage_pack": (C.c_int, [RP, SP, _i64, _p, _p, _p, _i32, _i32, _i64, _p, _p, _i32, _p]),
         "sacenv_replay_stage_unpack": (C.c_int, [_i32, _i64, _i64, _i32, _i32, _p, _p, _p, _p]),
+        "sacenv_replay_stage_side": (C.c_int, [RP, SP, _i32, _i32, C.POINTER(StageSide), _p]),
         "sacenv_copy_standin": (C.c_int, [_p, _p, _i64, _i32, C.c_double, _p]),
         "sacenv_sac_layout": (C.c_int, [C.POINTER(SacParams), C.POINTER(SacLayout)]),
         "sacenv_sac_sync": (C.c_int, [C.POINTER(SacParams), _p, _p]),

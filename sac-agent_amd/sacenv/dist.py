@@ -288,7 +288,10 @@ class SegmentExchange:
     16-workgroup collective stand-in beside it); side kernels co-running with the refill
     slow its latency chain as much (k_need_masks 6 -> 85-95 us, k_refill_fit 28 -> 90-115
     us); and every wait of the stepping stream on another stream's event cost ~20-40 us.
-    So the exchange's local work runs on the stepping stream, after refill g:
+    So the exchange's local work runs on the stepping stream, after refill g (with the
+    counter-based draws and the all-gather, ``sampler.fused``: the three as ONE launch,
+    ``side_segment``, the unpack then always one segment behind its pack, collective or
+    not):
 
     - the unpack of segment g - 1 (at N > 1: behind its collective, which ran beside
       launch g), the pack of segment g's share (``pack_segment``), at one rank with no
@@ -314,6 +317,7 @@ class SegmentExchange:
             self.sd = torch.cuda.Stream(device=self.device)
             self.coll = torch.cuda.Stream(device=self.device)
         self.mt = getattr(sampler, "sampler", None) == "mt"
+        self.fused = bool(getattr(sampler, "fused", False))
         # a collective (or its stand-in) runs between the pack and the unpack
         self.collective = (getattr(sampler, "world", 1) > 1 or getattr(sampler, "standin", None) is not None)
         self.g = 0               # segments exchanged so far
@@ -372,6 +376,20 @@ class SegmentExchange:
         if not self.cuda:
             self.sampler.prepare(g + 1)
             self.last = self.sampler.sample_segment(g)
+        elif self.fused:
+            pend = self._pending
+            if pend is not None and pend[1] is not None:
+                self._cur().wait_event(pend[1])
+            got = self.sampler.side_segment(g, pend[0] if pend is not None else None)
+            if pend is not None:
+                self.last = got
+            self._pending = (g, None)
+            if self.collective:
+                packed = self._record(self._cur())
+                with torch.cuda.stream(self.coll):
+                    self.coll.wait_event(packed)
+                    self.sampler.collect_segment(g)
+                    self._pending = (g, self._record(self.coll))
         else:
             if self._pending is not None:
                 self._unpack_pending()

@@ -363,7 +363,9 @@ class StagedReplay:
         nb = self.N_BUFFERS
         self.stage = [torch.zeros(self.seg * self.n_pad * 64, dtype=torch.uint8, device=self.device)
                       for _ in range(nb)]
-        self.marks = [torch.zeros(self.seg * self.n_pad // 64, dtype=torch.int64, device=self.device)
+        # env-major (sacenv_boat_segment): env e's row of step j at (e * seg + j) * 64, its mark
+        # bit j % 64 in word e * ceil(seg / 64) + j // 64
+        self.marks = [torch.zeros(self.n_pad * -(-self.seg // 64), dtype=torch.int64, device=self.device)
                       for _ in range(nb)]
         self._idx = [torch.empty(self.seg * self.batch, dtype=torch.int64, device=self.device) for _ in range(4)]
         self._words = [_packed_batches(self.batch, self.seg, _lib.OBS_DIM, 1, (_lib.OBS_DIM,), self.device)
@@ -433,7 +435,7 @@ class StagedReplay:
         stored transition) go into the last row of the buffer standing for segment -1,
         with term 0; segment 0 and 1's learns are drawn and segment 0's rows marked."""
         nb = self.N_BUFFERS
-        last = self.stage[(-1) % nb][(self.seg - 1) * self.n_pad * 64:].view(torch.float32).view(self.n_pad, 16)
+        last = self.stage[(-1) % nb].view(torch.float32).view(self.n_pad, self.seg, 16)[:, self.seg - 1]
         last.zero_()
         last[: self.n, : _lib.OBS_DIM].copy_(obs.to(device=self.device, dtype=torch.float32))
         for m in self.marks:
@@ -461,6 +463,49 @@ class StagedReplay:
         self.pack_segment(g)
         self.collect_segment(g)
         return self.unpack_segment(g)
+
+    @property
+    def fused(self) -> bool:
+        """A segment's side work is one launch (``side_segment``): the counter-based draws
+        and the all-gather pack/unpack (sacenv_replay_stage_side)."""
+        return self.sampler == "philox" and self.exchange == "allgather"
+
+    def side_segment(self, g: int, unpack: int | None = None):
+        """After segment g's launch, ONE launch (sacenv_replay_stage_side) doing the unpack
+        of segment ``unpack``'s collected chunks (its collective complete in stream
+        order), the pack of segment g (``pack_segment``) and ``prepare(g + 1)``'s draws
+        (segment g + 2): the same bytes as the three separate calls. Then
+        ``collect_segment(g)``; segment g's unpack goes into the next call (or
+        ``unpack_segment``). Returns segment ``unpack``'s batches (or None)."""
+        if not self.fused:
+            raise ValueError("side_segment needs sampler='philox' and exchange='allgather'")
+        g = int(g)
+        while self.drawn < g + 2:   # (begin() drew 0 and 1; each call draws one more)
+            self._draw()
+        nb = self.N_BUFFERS
+        w = _lib.StageSide()
+        d = self.drawn
+        draw = d == g + 2
+        w.draw_g = d if draw else -1
+        if draw:
+            w.seed = self.seed & 0xFFFFFFFFFFFFFFFF
+            w.draw_idx = self._idx[d % 4].data_ptr()
+            w.marks_prev = self.marks[(d - 1) % nb].data_ptr() if d > 0 else None
+            w.marks_cur = self.marks[d % nb].data_ptr()
+            w.draw_tiles = self._tiles[d % 4].data_ptr()
+        w.pack_g = g
+        w.stage_cur, w.stage_prev = self.stage[g % nb].data_ptr(), self.stage[(g - 1) % nb].data_ptr()
+        w.pack_idx, w.pack_tiles = self._idx[g % 4].data_ptr(), self._tiles[g % 4].data_ptr()
+        w.cap, w.chunk = self.cap, self._chunks[g % 2].data_ptr()
+        if unpack is not None:
+            u = int(unpack)
+            w.gathered, w.chunk_bytes = self._gathered[u % 2].data_ptr(), self.chunk_bytes
+            w.words, w.status_word, w.world = self._words[u % 2][0].data_ptr(), self._status.data_ptr(), self.world
+        _lib.check(self.lib.sacenv_replay_stage_side(self._pp, self._spp, self.batch, self.seg, C.byref(w),
+                                                     self.stream))
+        if draw:
+            self.drawn += 1
+        return self._batches[u % 2, u % 4] if unpack is not None else None
 
     def pack_segment(self, g: int) -> None:
         """This rank's share of segment g's batches, from the staged rows of segments g

@@ -324,8 +324,10 @@ class VecBoatEnv:
         with ``step_done`` it publishes ``seq0 + ks + 1`` there once step ks's outputs
         are visible. ``trans`` (u8 device, 16-B aligned): step ks's pooled transition
         row at ``trans[ks * trans_stride:]``. ``stage`` / ``stage_marks``: the staged
-        replay rows (64 B per step and env, written where the mark bit is set;
-        ``sacenv.replay.StagedReplay``)."""
+        replay rows (env-major: env e's 64-B row of step ks at ``(e * K + ks) * 64``),
+        written where bit ks % 64 of ``stage_marks[e * ceil(K / 64) + ks // 64]`` is set
+        (int64 [n_pad, ceil(K / 64)]; consumed: the launch clears them; K <= 256);
+        ``sacenv.replay.StagedReplay``."""
         K = int(actions.shape[0]) if n_steps is None else int(n_steps)
         if (not isinstance(actions, torch.Tensor) or actions.dtype != torch.float32
                 or actions.device != self.device or actions.dim() != 2
@@ -352,8 +354,8 @@ class VecBoatEnv:
                 raise ValueError("stage must be a contiguous uint8 device tensor of n_steps x 64 x n_pad bytes")
             if stage_marks is not None and (stage_marks.dtype != torch.int64 or stage_marks.device != self.device
                                             or not stage_marks.is_contiguous()
-                                            or stage_marks.numel() < K * self.n_pad // 64):
-                raise ValueError("stage_marks must be a contiguous int64 device tensor of n_steps x n_pad/64")
+                                            or stage_marks.numel() < self.n_pad * -(-K // 64)):
+                raise ValueError("stage_marks must be a contiguous int64 device tensor of n_pad x ceil(n_steps/64)")
         _lib.check(self.lib.sacenv_boat_segment(
             self._pp, self._ptr, actions.data_ptr(), int(actions.stride(0)), K,
             None if act_ready is None else act_ready.data_ptr(),

@@ -34,7 +34,7 @@ def declared_functions():
 def test_library_exports_header(built_lib):
     from sacenv import _lib
     names = declared_functions()
-    assert len(names) == 48
+    assert len(names) == 49
     assert set(names) == set(_lib.EXPORTS)
     for n in names:
         assert hasattr(built_lib, n), n
@@ -101,6 +101,43 @@ def test_counter_sampler_and_allgather_argument_errors_without_gpu(built_lib):
     assert built_lib.sacenv_copy_standin(None, 32, 32, 16, 1.0, None) == -1
     assert built_lib.sacenv_copy_standin(8, 32, 32, 16, 1.0, None) == -5         # alignment
     assert built_lib.sacenv_replay_gather(R, 1, 4, None, None, None, None, None, None, None) == -1
+
+
+def test_stage_side_argument_errors_without_gpu(built_lib):
+    """sacenv_replay_stage_side (ABI 20: one segment's draws, pack and unpack in one launch)
+    validates each role's arguments and refuses buffers the side-by-side roles would share."""
+    from sacenv import _lib
+    rp = _lib.ReplayParams(mem_size=1_000_000, obs_dim=11, act_dim=1, reward_f32=1, terminal_mask=2)
+    sp = _lib.StagedParams(period=4096, offset=0, n=4096, n_pad=4096, seg=256, experiment=6)
+    R, S = ctypes.byref(rp), ctypes.byref(sp)
+    side = built_lib.sacenv_replay_stage_side
+    assert side(R, S, 1024, 256, None, None) == -1
+    w = _lib.StageSide(draw_g=2, pack_g=-1, gathered=None)
+    assert side(R, S, 1024, 256, ctypes.byref(w), None) == -1           # draws without idx
+    w.draw_idx, w.marks_cur, w.draw_tiles = 256, 512, 768
+    w.draw_g = -3
+    w.pack_g = 0
+    assert side(R, S, 1024, 256, ctypes.byref(w), None) == -1           # pack without its buffers
+    w.stage_cur, w.stage_prev, w.pack_idx, w.pack_tiles, w.chunk = 1024, 2048, 4096, 8192, 1 << 20
+    w.cap = 1024 * 256 + 1                                              # more records than slots
+    assert side(R, S, 1024, 256, ctypes.byref(w), None) == -4
+    w.cap = 1024 * 256
+    w.draw_g, w.draw_idx = 2, 4096                                      # the pack reads what the draws write
+    assert side(R, S, 1024, 256, ctypes.byref(w), None) == -5
+    w.draw_idx = 256
+    w.stage_cur = 1032                                                  # rows not 16-B aligned
+    assert side(R, S, 1024, 256, ctypes.byref(w), None) == -5
+    w.stage_cur = 1024
+    w.gathered, w.world, w.words, w.status_word = (1 << 20) + 64, 1, 1 << 30, 64
+    w.chunk_bytes = 16 + 100 * w.cap - 4                                # chunk too small for cap
+    assert side(R, S, 1024, 256, ctypes.byref(w), None) == -4
+    w.chunk_bytes = 16 + 100 * w.cap
+    assert side(R, S, 1024, 256, ctypes.byref(w), None) == -5           # unpacks the chunk being packed
+    w.world = 0
+    assert side(R, S, 1024, 256, ctypes.byref(w), None) == -4
+    w.world, w.draw_g = 1, -1
+    sp.period = sp.n = sp.n_pad = 64                                    # mem_size > seg * period
+    assert side(R, S, 1024, 256, ctypes.byref(w), None) == -5
 
 
 def test_segment_marks_are_bounded_without_autoreset(built_lib):
@@ -182,7 +219,8 @@ def test_ctypes_structs_match_c_layout(tmp_path):
     structs = {"SacenvBoatParams": _lib.BoatParams, "SacenvBoatLayout": _lib.BoatLayout,
                "SacenvToyParams": _lib.ToyParams, "SacenvToyLayout": _lib.ToyLayout,
                "SacenvReplayParams": _lib.ReplayParams, "SacenvReplayLayout": _lib.ReplayLayout,
-               "SacenvSacParams": _lib.SacParams, "SacenvSacLayout": _lib.SacLayout}
+               "SacenvSacParams": _lib.SacParams, "SacenvSacLayout": _lib.SacLayout,
+               "SacenvStagedParams": _lib.StagedParams, "SacenvStageSide": _lib.StageSide}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "sacenv.h"', "int main(void) {"]
     for cname, py in structs.items():
         lines.append(f'printf("{cname} sizeof %zu\\n", sizeof({cname}));')

@@ -42,14 +42,17 @@ def _cfg(exp):
     return {"base_settings": {"experiment": exp, "test_mode": 0}, "boat_env": {"track_width": 30}}
 
 
-def _run(rank, world, exp, N, M, B, n_segs, dev, group=None, sampler="mt", exchange="allreduce"):
+def _run(rank, world, exp, N, M, B, n_segs, dev, group=None, sampler="mt", exchange="allreduce", fused=False):
     """Returns (n learns checked, n skipped) on rank 0 (None elsewhere).
 
     sampler "mt": the indices equal the reference stream's (DeviceReplayBuffer.sample
     after every step). sampler "philox": the indices equal the CPU oracle's
     counter-based draws (oracle/ctr_sampler.py, pinned to numpy's Philox), lie in
     [0, min(cntr, M)), and the batch equals DeviceReplayBuffer.gather of the same
-    indices from the buffer fed every step."""
+    indices from the buffer fed every step. fused (philox + allgather): each
+    segment's side work is ONE launch (side_segment: the unpack of the segment
+    before, the pack of this one, the draws of the one after next), as
+    SegmentExchange runs it."""
     from sacenv import VecBoatEnv
     from sacenv.replay import DeviceReplayBuffer, StagedReplay
     import ctr_sampler
@@ -58,6 +61,7 @@ def _run(rank, world, exp, N, M, B, n_segs, dev, group=None, sampler="mt", excha
     obs0 = env.reset().clone()
     rep = StagedReplay(N, env.n_pad, exp, env.first_obs_template(), rank=rank, world=world, mem_size=M,
                        batch=B, seg=SEG, seed=5, device=dev, group=group, sampler=sampler, exchange=exchange)
+    assert rep.fused == (sampler == "philox" and exchange == "allgather")
     rep.begin(obs0)
     assert bool((env.last_term == 0).all())
     ref = ref_rb = None
@@ -67,19 +71,30 @@ def _run(rank, world, exp, N, M, B, n_segs, dev, group=None, sampler="mt", excha
         ref_rb = DeviceReplayBuffer(M, (11,), 1, device=dev, seed=5)
     g = torch.Generator(device=dev)
     g.manual_seed(9)
-    checked = skipped = written = 0
+    written = 0
+    acts_all, gots = [], []
     for s in range(n_segs):
         acts = torch.rand((SEG, world * N), generator=g, device=dev) * 2 - 1
+        acts_all.append(acts)
         mine = acts[:, rank * N:(rank + 1) * N].contiguous()
         sa = rep.stage_args(s)
         written += _popcount(sa["marks"])   # (complete before the launch, which consumes them)
         env.segment_async(mine, SEG, stage=sa["stage"], stage_marks=sa["marks"])
         env.refill()
-        rep.prepare(s + 1)
-        got = rep.sample_segment(s)
+        if fused:
+            got = rep.side_segment(s, s - 1 if s > 0 else None)
+            rep.collect_segment(s)
+            if got is not None:
+                gots.append([tuple(x.clone() for x in b) for b in got])
+        else:
+            rep.prepare(s + 1)
+            gots.append([tuple(x.clone() for x in b) for b in rep.sample_segment(s)])
         assert _popcount(rep.stage_args(s)["marks"]) == 0   # the launch cleared the marks it read
-        if ref is None:
-            continue
+    if fused:
+        gots.append([tuple(x.clone() for x in b) for b in rep.unpack_segment(n_segs - 1)])
+    checked = skipped = 0
+    for s in range(n_segs if ref is not None else 0):
+        acts, got = acts_all[s], gots[s]
         for k in range(SEG):
             prev = ref.obs.clone()
             ref.step(acts[k].contiguous())
@@ -140,6 +155,15 @@ def test_staged_replay_counter_sampler_and_allgather(sampler, exchange, exp, N, 
     assert skipped == -(-B // N) - 1  # learns while fewer than B rows are stored
 
 
+@pytest.mark.parametrize("exp,N,M,B", [(6, 3000, 50_021, 256), (2, 2000, 40_000, 511), (6, 700, 20_000, 1024)])
+def test_staged_replay_side_launch(exp, N, M, B, gpu, built_lib):
+    """The fused side launch (sacenv_replay_stage_side: unpack g - 1, pack g, draw g + 2 in
+    one launch) against the literal loop, as the separate calls are."""
+    checked, skipped = _run(0, 1, exp, N, M, B, 5, gpu, sampler="philox", exchange="allgather", fused=True)
+    assert checked + skipped == 5 * SEG
+    assert skipped == -(-B // N) - 1
+
+
 def test_staged_replay_refuses_a_ring_older_than_one_segment(gpu, built_lib):
     from sacenv.replay import StagedReplay
     with pytest.raises(ValueError):
@@ -154,7 +178,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q, sampler="mt", exchange="allreduce"):
+def _worker(rank, world, port, q, sampler="mt", exchange="allreduce", fused=False):
     import sys
     sys.path.insert(0, os.path.join(ROOT, "sac-agent_amd"))
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -162,7 +186,7 @@ def _worker(rank, world, port, q, sampler="mt", exchange="allreduce"):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         q.put((rank, _run(rank, world, 6, 1000, 30_011, 333, 3, torch.device("cuda", 0), sampler=sampler,
-                          exchange=exchange)))
+                          exchange=exchange, fused=fused)))
     except Exception:  # noqa: BLE001
         import traceback
         q.put((rank, traceback.format_exc()))
@@ -170,13 +194,14 @@ def _worker(rank, world, port, q, sampler="mt", exchange="allreduce"):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("sampler,exchange", [("mt", "allreduce"), ("philox", "allgather")])
-def test_staged_replay_two_ranks_equal_pooled_buffer(sampler, exchange, gpu, built_lib):
+@pytest.mark.parametrize("sampler,exchange,fused", [("mt", "allreduce", False), ("philox", "allgather", False),
+                                                    ("philox", "allgather", True)])
+def test_staged_replay_two_ranks_equal_pooled_buffer(sampler, exchange, fused, gpu, built_lib):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q, sampler, exchange)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, sampler, exchange, fused)) for r in range(world)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=240) for _ in ps)
