@@ -964,7 +964,7 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
     kern_s = sum(a.ms_to(b) for a, b, _ in seg_events) * 1e-3 / sum(n for _, _, n in seg_events)
     step_s = ev0.ms_to(ev1) * 1e-3 / steps
 
-    every = replay_path = standin_path = None
+    every = replay_path = standin_path = rank_path = None
     if (world == 1 and run.mode == "segment" and not args.mixed and not args.no_autoreset
             and not args.no_every_output):
         every = every_output_rate(wl, dev, k0=k)
@@ -997,6 +997,18 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
                 f"{sd['us']:.1f} us (those bytes at {args.standin_gbps:g} GB/s per rank), on a side stream "
                 "beside the next segment's launch, as the N>1 collective runs; the unpack waits for it; no xGMI "
                 "traffic"))
+            if args.sampler == "philox" and args.exchange == "allgather":
+                W = max(2, int(args.standin_world))
+                rrun = SegmentRunner(args, wl, dev, None, SEG, make_exchange(args, wl, rank, W, dev, standin=sd))
+                rate, k, _ = timed_rate(rrun, k, n_x, world, dev, wl)
+                rank_path = dict(rate, world=W, standin=sd, note=(
+                    f"this GPU's {wl.per_gpu_envs} envs as rank 0 of a {W}-rank pooled buffer (period {W} x "
+                    f"{wl.per_gpu_envs}: the N = {W} line's per-rank work at one GPU): the draws of every learn, "
+                    "the marks, staged rows and packed chunk of its own rows, the collective stood in for as "
+                    "above (its own chunk copied into the gathered buffer, resident for the other ranks' "
+                    f"{W - 1} chunks at {args.standin_gbps:g} GB/s), the unpack of all {W} chunks; the other "
+                    "ranks' chunks were packed once, before the timed segments, from this GPU's rows under "
+                    "their env ids (their slots and counts, not their transitions: timing only)"))
     dinfo = dist_info(world, dev)
     if rank != 0:
         return None
@@ -1061,6 +1073,9 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
                 # each peer's rows arrive over its own point-to-point link
                 "xgmi": _xgmi(recv, el_max, world - 1),
                 "note": "the timed region ends when the last all_gather has landed"})
+    for fld in (every, replay_path, rank_path):   # (fractions of the headline value)
+        if fld is not None:
+            fld["frac_of_value"] = fld["value"] / (world * wl.per_gpu_envs * steps / el_max)
     return {
         "metric": metric_name(args),
         "value": world * wl.per_gpu_envs * steps / el_max,
@@ -1157,6 +1172,7 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
         "every_output": every,
         "replay_path": replay_path,
         "replay_path_collective_standin": standin_path,
+        "replay_path_rank_of_world": rank_path,
         "cpu_baseline": None,
         "dist": dinfo,
         "pooling": pooling_out,

@@ -2086,6 +2086,13 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
+  // the staged rows: the wave's rows through one buffer resource (env-major: lane's row
+  // of step ks at s_lane + ks * 64 from the wave's first env's), the step's offset in
+  // the scalar offset
+  const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
+      (kRoll && kRows == 2) ? ra->stage + (int64_t)ob * kWave * n_steps * 64 : nullptr, 0, 0x7fffffff, 0x00020000);
+  const uint32_t s_lane = (kRoll && kRows == 2) ? (uint32_t)lane * (uint32_t)n_steps * 64u : 0u;
+  uint32_t mkw = 0u;
   // every load of the launch's prologue has landed before the step loop: the waitcnt
   // pass then sees no load pending at the loop's entry, and the loop keeps no wait
   // for them -- such a wait, on later steps, also waits for the previous step's
@@ -2296,16 +2303,25 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
   // (written by a restarting lane below); stored before the restart selects, so the
   // pre-reset obs need not stay live across them
   bool staged = false;
-  float4* stage_row = nullptr;
   if (kRoll && kRows == 2) {
-    const uint32_t mk = l.mk[(ks >> 5) & (kMkWords - 1)][lane];  // (n_steps <= 256 with marks)
-    staged = ((mk >> (ks & 31)) & 1u) != 0u;
-    stage_row = reinterpret_cast<float4*>(ra->stage + ((int64_t)e * n_steps + ks) * 64);
-    if (staged) {
-      stage_row[0] = make_float4(o.v[0], o.v[1], o.v[2], o.v[3]);
-      stage_row[1] = make_float4(o.v[4], o.v[5], o.v[6], o.v[7]);
-      stage_row[2] = make_float4(o.v[8], o.v[9], o.v[10], (float)reward);
-      stage_row[3] = make_float4(act, __uint_as_float((uint32_t)term | (lt << 8)), 0.0f, 0.0f);
+    // the lane's mark bits, one LDS read per 32 steps (a per-step read waited its
+    // latency right before the test), consumed bit by bit
+    if ((ks & 31) == 0) mkw = l.mk[(ks >> 5) & (kMkWords - 1)][lane];  // (n_steps <= 256 with marks)
+    staged = (mkw & 1u) != 0u;
+    mkw >>= 1;
+    if (staged) {  // (write-through, as the record's stores: measured +70 us per launch here)
+      const uint32_t so = (uint32_t)ks * 64u;
+      __builtin_amdgcn_raw_buffer_store_b128(
+          u4v{__float_as_uint(o.v[0]), __float_as_uint(o.v[1]), __float_as_uint(o.v[2]), __float_as_uint(o.v[3])},
+          srs, s_lane, so, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(
+          u4v{__float_as_uint(o.v[4]), __float_as_uint(o.v[5]), __float_as_uint(o.v[6]), __float_as_uint(o.v[7])},
+          srs, s_lane + 16u, so, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(
+          u4v{__float_as_uint(o.v[8]), __float_as_uint(o.v[9]), __float_as_uint(o.v[10]), __float_as_uint((float)reward)},
+          srs, s_lane + 32u, so, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(u4v{__float_as_uint(act), (uint32_t)term | (lt << 8), 0u, 0u}, srs,
+                                             s_lane + 48u, so, 0);
     }
   }
   float row[SACENV_OBS_DIM];
@@ -2333,8 +2349,8 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
 #pragma unroll
       for (int k = 0; k < SACENV_OBS_DIM; ++k) row[k] = fo.v[k];
       row3_new = fo.v[3];
-      if (kRoll && kRows == 2 && p.experiment == 2 && staged)
-        reinterpret_cast<float*>(stage_row)[14] = row3_new;  // the staged row's obs3_next
+      if (kRoll && kRows == 2 && p.experiment == 2 && staged)  // the staged row's obs3_next
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(row3_new), srs, s_lane + 56u, (uint32_t)ks * 64u, 0);
       cons_out = cons + 1;
     }
   }

@@ -331,8 +331,14 @@ class StagedReplay:
             # the segment launch stages one mark word per step in LDS (REFILL_PERIOD of them)
             raise ValueError(f"seg must be in [1, {_lib.REFILL_PERIOD}]")
         self.rank, self.world, self.group = int(rank), int(world), group
-        if standin is not None and self.world != 1:
-            raise ValueError("the collective stand-in is a one-GPU measurement (world 1)")
+        if standin is not None and group is not None:
+            raise ValueError("the collective stand-in is a one-GPU measurement (no process group)")
+        # world > 1 with the stand-in and no group: ONE GPU as rank `rank` of a world-rank
+        # pooled buffer (bench.py's replay_path_rank_of_W): the collective stood in for, the
+        # other ranks' chunks packed once from this GPU's rows under their env ids
+        self.emulated = standin is not None and self.world > 1
+        if self.emulated and (exchange != "allgather" or sampler != "philox"):
+            raise ValueError("the emulated rank runs the counter-based all-gather exchange")
         self.mem_size = int(mem_size)
         self.seed = int(seed)
         sp = _lib.StagedParams()
@@ -394,11 +400,12 @@ class StagedReplay:
             self._gathered = ([torch.empty(self.world * self.chunk_bytes, dtype=torch.uint8, device=self.device)
                                for _ in range(2)] if self.world > 1 else self._chunks)
         self.standin = dict(standin) if standin is not None else None
-        if self.standin is not None:
+        if self.standin is not None and not self.emulated:
             nb16 = -(-int(self.standin["bytes"]) // 16) * 16
             self.standin["bytes"] = nb16
             self._standin_src = torch.zeros(nb16, dtype=torch.uint8, device=self.device)
             self._standin_dst = torch.empty(nb16, dtype=torch.uint8, device=self.device)
+        self._peers_filled = False
         self.drawn = 0   # segments whose learns are drawn
 
     @property
@@ -532,7 +539,15 @@ class StagedReplay:
         stand-in for it, if one was asked for."""
         import torch.distributed as dist
         g = int(g)
-        if self.world > 1:
+        if self.emulated:
+            if not self._peers_filled:
+                self._fill_peers(g)
+            sd, cb = self.standin, self.chunk_bytes
+            out = self._gathered[g % 2][self.rank * cb:(self.rank + 1) * cb]
+            _lib.check(self.lib.sacenv_copy_standin(
+                self._chunks[g % 2].data_ptr(), out.data_ptr(), cb, int(sd["workgroups"]), float(sd["us"]),
+                self.stream))
+        elif self.world > 1:
             if self.exchange == "allgather":
                 all_gather_bytes(self._gathered[g % 2], self._chunks[g % 2], self.group)
             else:
@@ -542,6 +557,26 @@ class StagedReplay:
             _lib.check(self.lib.sacenv_copy_standin(
                 self._standin_src.data_ptr(), self._standin_dst.data_ptr(), sd["bytes"], int(sd["workgroups"]),
                 float(sd["us"]), self.stream))
+
+    def _fill_peers(self, g: int) -> None:
+        """(emulated rank) The other ranks' chunks of both gathered buffers: segment g's
+        draws packed from this GPU's staged rows as if its envs were rank r's (each
+        rank's slots, counts and record layout as that rank would send them; the values
+        are this GPU's rows, not the other ranks' transitions: timing only)."""
+        nb, cb = self.N_BUFFERS, self.chunk_bytes
+        scratch = torch.empty_like(self._tiles[0])
+        for r in range(self.world):
+            if r == self.rank:
+                continue
+            sp = _lib.StagedParams.from_buffer_copy(self.sp)
+            sp.offset = r * self.n
+            for b in range(2):
+                dst = self._gathered[b][r * cb:(r + 1) * cb]
+                _lib.check(self.lib.sacenv_replay_stage_pack(
+                    self._pp, C.byref(sp), int(g), self.stage[g % nb].data_ptr(), self.stage[(g - 1) % nb].data_ptr(),
+                    self._idx[g % 4].data_ptr(), self.batch, self.seg, self.cap, dst.data_ptr(), scratch.data_ptr(),
+                    0, self.stream))
+        self._peers_filled = True
 
     def unpack_segment(self, g: int):
         """Segment g's batches from the collected chunks (all-gather; the all-reduce's words

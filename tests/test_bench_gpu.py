@@ -47,6 +47,10 @@ def test_driver_bench_command():
     assert rp["value"] > 0 and d["every_output"]["value"] > 0
     assert rp["sampler"] == "philox" and rp["exchange"] == "allgather"
     assert sd["value"] > 0 and sd["standin"]["workgroups"] == 16 and sd["standin"]["bytes"] > 20e6
+    # one GPU as rank 0 of the 8-rank pooled buffer (the N = 8 line's per-rank work)
+    rk = d["replay_path_rank_of_world"]
+    assert rk["value"] > 0 and rk["world"] == 8 and 0 < rk["frac_of_value"] < 1.05
+    assert 0 < rp["frac_of_value"] < 1.05
     if rf["kernel"].startswith("k_rollout"):  # the persistent launch: resident-state bytes headline
         assert abs(rf["bytes_per_env_step"] - (70 + 152 / 256)) < 1e-9
         assert rf["survey_222B"]["bytes_per_env_step"] == 222

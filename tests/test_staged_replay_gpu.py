@@ -42,7 +42,8 @@ def _cfg(exp):
     return {"base_settings": {"experiment": exp, "test_mode": 0}, "boat_env": {"track_width": 30}}
 
 
-def _run(rank, world, exp, N, M, B, n_segs, dev, group=None, sampler="mt", exchange="allreduce", fused=False):
+def _run(rank, world, exp, N, M, B, n_segs, dev, group=None, sampler="mt", exchange="allreduce", fused=False,
+         emulate=False):
     """Returns (n learns checked, n skipped) on rank 0 (None elsewhere).
 
     sampler "mt": the indices equal the reference stream's (DeviceReplayBuffer.sample
@@ -52,7 +53,9 @@ def _run(rank, world, exp, N, M, B, n_segs, dev, group=None, sampler="mt", excha
     indices from the buffer fed every step. fused (philox + allgather): each
     segment's side work is ONE launch (side_segment: the unpack of the segment
     before, the pack of this one, the draws of the one after next), as
-    SegmentExchange runs it."""
+    SegmentExchange runs it. emulate (rank 0 of `world`, one process): the collective
+    stood in for and the other ranks' chunks packed from this GPU's rows (timing
+    only), so only the slots this rank owns are compared."""
     from sacenv import VecBoatEnv
     from sacenv.replay import DeviceReplayBuffer, StagedReplay
     import ctr_sampler
@@ -60,7 +63,9 @@ def _run(rank, world, exp, N, M, B, n_segs, dev, group=None, sampler="mt", excha
     env = VecBoatEnv(_cfg(exp), N, env_id_offset=rank * N, **kw)
     obs0 = env.reset().clone()
     rep = StagedReplay(N, env.n_pad, exp, env.first_obs_template(), rank=rank, world=world, mem_size=M,
-                       batch=B, seg=SEG, seed=5, device=dev, group=group, sampler=sampler, exchange=exchange)
+                       batch=B, seg=SEG, seed=5, device=dev, group=group, sampler=sampler, exchange=exchange,
+                       standin=dict(bytes=0, workgroups=4, us=1.0) if emulate else None)
+    assert rep.emulated == emulate
     assert rep.fused == (sampler == "philox" and exchange == "allgather")
     rep.begin(obs0)
     assert bool((env.last_term == 0).all())
@@ -115,8 +120,19 @@ def _run(rank, world, exp, N, M, B, n_segs, dev, group=None, sampler="mt", excha
                 assert int(idx.min()) >= 0 and int(idx.max()) < min(ref_rb.mem_cntr, M)
                 want = ref_rb.gather(idx)
                 torch.cuda.synchronize()
+            own = slice(None)
+            if emulate and s > 0:   # (the other ranks' chunks are segment 0's: their records would
+                checked += 1        # overwrite this rank's slots of later segments; timing only)
+                continue
+            if emulate:   # the slots whose row lies in this rank's envs (ring row -> sequence -> env)
+                cntr = (s * SEG + k + 1) * world * N
+                row = idx.cpu().numpy()
+                seq = row + M * ((cntr - 1 - row) // M)
+                own = torch.from_numpy(seq % (world * N) < N).to(dev)
+                assert 0 < int(own.sum()) < B
             for i, (x, y) in enumerate(zip((st, ac, rw, ns, tm), want[:5])):
-                assert torch.equal(x.reshape(-1), y.reshape(-1).to(x.dtype)), (s, k, i)
+                x, y = x.reshape(B, -1)[own], y.reshape(B, -1).to(x.dtype)[own]
+                assert torch.equal(x, y), (s, k, i)
             checked += 1
         ref.refill()
         torch.cuda.synchronize()
@@ -162,6 +178,16 @@ def test_staged_replay_side_launch(exp, N, M, B, gpu, built_lib):
     checked, skipped = _run(0, 1, exp, N, M, B, 5, gpu, sampler="philox", exchange="allgather", fused=True)
     assert checked + skipped == 5 * SEG
     assert skipped == -(-B // N) - 1
+
+
+def test_staged_replay_emulated_rank_of_four(gpu, built_lib):
+    """bench.py's replay_path_rank_of_W: one GPU as rank 0 of a 4-rank pooled buffer (period
+    4 N), the collective stood in for, the other ranks' chunks packed (once, from segment
+    0) from this GPU's rows: every learn's draws equal the oracle's, segment 0's slots that
+    rank 0 owns equal the literal loop's, and no chunk overflows."""
+    checked, skipped = _run(0, 4, 6, 500, 30_011, 333, 3, gpu, sampler="philox", exchange="allgather", fused=True,
+                            emulate=True)
+    assert checked + skipped == 3 * SEG
 
 
 def test_staged_replay_refuses_a_ring_older_than_one_segment(gpu, built_lib):
