@@ -13,7 +13,9 @@ rate and the median segment launch (HIP events around every launch):
 - ag-plain: the side kernels run, the launch is the plain one (no staged rows);
 - evict: no exchange, a 96-MB fill after each refill (does an L2 / MALL sweep
   between refill and launch slow the launch?);
-- ag-draw-only: the draws run, no pack/unpack.
+- ag-draw-only: the draws run, no pack/unpack;
+- ag-corun (timing only): the side launch beside the next segment's launch on a side
+  stream (the launch does not wait for its draws: marks may race).
 
     python tools/prof_staged4.py [n_segments] [kind,kind,...]
 """
@@ -39,6 +41,11 @@ class Variant(SegmentExchange):
             self.fused = False
         self.junk = torch.empty(96 << 20, dtype=torch.uint8, device=device) if kind == "evict" else None
 
+    def wait(self):
+        if self.kind == "ag-corun":   # the pending unpack reads what the side stream packed
+            self._cur().wait_stream(self.sd)
+        super().wait()
+
     def stage_args(self):
         sa = super().stage_args()
         if self.kind == "ag-zero":
@@ -48,6 +55,19 @@ class Variant(SegmentExchange):
         return sa
 
     def after(self):
+        if self.kind == "ag-corun":
+            # TIMING ONLY: the side launch of segment g on a side stream once refill g is
+            # done, beside launch g + 1, which does not wait for it (its draws of segment
+            # g + 2 then race launch g + 1's marks: rows may be missing)
+            ev = self._record(self._cur())
+            pend = self._pending
+            with torch.cuda.stream(self.sd):
+                self.sd.wait_event(ev)
+                self.sampler.side_segment(self.g, pend[0] if pend is not None else None)
+            self._pending = (self.g, None)
+            self.g += 1
+            self.exchanges += 1
+            return
         if self.kind == "evict":
             self.junk.fill_(self.g & 0xFF)
             self.g += 1
