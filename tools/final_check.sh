@@ -41,8 +41,10 @@ for f in ("driver", "default", "step", "c2", "c5", "rollout_k128", "131k", "clos
           f"frac {r.get('frac', 0):.3f} cpu {c and round(c['value'])}")
 d = json.load(open("gpurun_out/bench_default.json"))
 rp, sd, ev = d["replay_path"], d["replay_path_collective_standin"], d["every_output"]
+rk = d["replay_path_rank_of_world"]
 print(f"default: replay_path {rp['value']/1e9:.3f} ({rp['value']/d['value']:.3f}), standin {sd['value']/1e9:.3f} "
-      f"({sd['value']/d['value']:.3f}), every_output {ev['value']/1e9:.3f} ({ev['value']/d['value']:.3f}), "
+      f"({sd['value']/d['value']:.3f}), rank_of_{rk['world']} {rk['value']/1e9:.3f} ({rk['value']/d['value']:.3f}), "
+      f"every_output {ev['value']/1e9:.3f} ({ev['value']/d['value']:.3f}), "
       f"timed {d['steps'] * d['ms_per_step'] * 1e-3:.3f} s")
 PY
 fi

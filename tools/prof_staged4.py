@@ -14,6 +14,9 @@ rate and the median segment launch (HIP events around every launch):
 - evict: no exchange, a 96-MB fill after each refill (does an L2 / MALL sweep
   between refill and launch slow the launch?);
 - ag-draw-only: the draws run, no pack/unpack;
+- rank8: one GPU as rank 0 of the 8-rank buffer (bench's replay_path_rank_of_world);
+- rank8-nowait (timing only): the same, the stepping stream not waiting for the
+  collective's event before the side launch (its unpack may race the stand-in);
 - ag-corun (timing only): the side launch beside the next segment's launch on a side
   stream (the launch does not wait for its draws: marks may race).
 
@@ -41,6 +44,10 @@ class Variant(SegmentExchange):
             self.fused = False
         self.junk = torch.empty(96 << 20, dtype=torch.uint8, device=device) if kind == "evict" else None
 
+    def check(self):
+        if self.kind != "rank8-nowait":   # (its unpacks may race the stand-in's copies)
+            super().check()
+
     def wait(self):
         if self.kind == "ag-corun":   # the pending unpack reads what the side stream packed
             self._cur().wait_stream(self.sd)
@@ -55,6 +62,9 @@ class Variant(SegmentExchange):
         return sa
 
     def after(self):
+        if self.kind == "rank8-nowait" and self._pending is not None:
+            # TIMING ONLY: the stepping stream does not wait for the collective's event
+            self._pending = (self._pending[0], None)
         if self.kind == "ag-corun":
             # TIMING ONLY: the side launch of segment g on a side stream once refill g is
             # done, beside launch g + 1, which does not wait for it (its draws of segment
@@ -100,7 +110,10 @@ def main():
             if kind == "none":
                 run = bench.SegmentRunner(base, wl, dev)
             else:
-                x = bench.make_exchange(args, wl, 0, 1, dev)
+                if kind.startswith("rank8"):   # one GPU as rank 0 of 8, the collective stood in for
+                    x = bench.make_exchange(args, wl, 0, 8, dev, standin=bench.collective_standin(args, wl))
+                else:
+                    x = bench.make_exchange(args, wl, 0, 1, dev)
                 v = Variant(x.sampler, dev, kind)
                 run = bench.SegmentRunner(args, wl, dev, None, bench.SEG, v)
             rate, k, _ = bench.timed_rate(run, k, n, 1, dev, wl)
