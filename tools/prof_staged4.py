@@ -11,12 +11,14 @@ rate and the median segment launch (HIP events around every launch):
 - ag-zero: the same, the marks zeroed right before each launch (the staged launch
   writes no row; every side kernel still runs);
 - ag-plain: the side kernels run, the launch is the plain one (no staged rows);
-- evict: no exchange, a 96-MB fill after each refill (does an L2 / MALL sweep
-  between refill and launch slow the launch?);
+- evict, evict16, evict256: no exchange, a 96-, 16- or 256-MB fill after each refill
+  (does an L2 / MALL sweep between refill and launch slow the launch, and from what
+  size?);
 - ag-draw-only: the draws run, no pack/unpack;
 - rank8: one GPU as rank 0 of the 8-rank buffer (bench's replay_path_rank_of_world);
 - rank8-nowait (timing only): the same, the stepping stream not waiting for the
   collective's event before the side launch (its unpack may race the stand-in);
+- ag-first, rank8-first: the side launch before the refill instead of after it;
 - ag-corun (timing only): the side launch beside the next segment's launch on a side
   stream (the launch does not wait for its draws: marks may race).
 
@@ -42,7 +44,8 @@ class Variant(SegmentExchange):
         self.kind = kind
         if kind == "ag-sep":   # the draws, pack and unpack as three launches (round 6's first form)
             self.fused = False
-        self.junk = torch.empty(96 << 20, dtype=torch.uint8, device=device) if kind == "evict" else None
+        mb = {"evict": 96, "evict16": 16, "evict256": 256}.get(kind)
+        self.junk = torch.empty(mb << 20, dtype=torch.uint8, device=device) if mb else None
 
     def check(self):
         if self.kind != "rank8-nowait":   # (its unpacks may race the stand-in's copies)
@@ -57,11 +60,35 @@ class Variant(SegmentExchange):
         sa = super().stage_args()
         if self.kind == "ag-zero":
             sa["marks"].zero_()
-        if self.kind in ("ag-plain", "evict"):
+        if self.kind in ("ag-plain", "evict", "evict16", "evict256"):
             return {"stage": None, "marks": None}
         return sa
 
+    def launched(self):
+        if self.kind in ("ag-first", "rank8-first"):
+            # the side launch right after the segment launch, BEFORE the refill: the refill's
+            # fresh slot-ring lines (the next episodes' wind) stay in L2 for the next launch
+            g, pend = self.g, self._pending
+            if pend is not None and pend[1] is not None:
+                self._cur().wait_event(pend[1])
+            got = self.sampler.side_segment(g, pend[0] if pend is not None else None)
+            if pend is not None:
+                self.last = got
+            self._pending = (g, None)
+            if self.collective:
+                packed = self._record(self._cur())
+                with torch.cuda.stream(self.coll):
+                    self.coll.wait_event(packed)
+                    self.sampler.collect_segment(g)
+                    self._pending = (g, self._record(self.coll))
+            return
+        super().launched()
+
     def after(self):
+        if self.kind in ("ag-first", "rank8-first"):
+            self.g += 1
+            self.exchanges += 1
+            return
         if self.kind == "rank8-nowait" and self._pending is not None:
             # TIMING ONLY: the stepping stream does not wait for the collective's event
             self._pending = (self._pending[0], None)
@@ -78,7 +105,7 @@ class Variant(SegmentExchange):
             self.g += 1
             self.exchanges += 1
             return
-        if self.kind == "evict":
+        if self.kind.startswith("evict"):
             self.junk.fill_(self.g & 0xFF)
             self.g += 1
             self.exchanges += 1
