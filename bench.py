@@ -846,13 +846,16 @@ def pooling_mode(args, world: int, wl: Workload) -> str:
 def run_bench(args, rank: int, world: int, dev, wl: Workload):
     """Warm up, time whole segments, measure the kernel; rank 0 returns the JSON dict.
 
-    N>1 (``--pooling sharded``, the default): every segment's transition rows go into
-    the rank's StagedReplay buffer and the segment's learn() batches are exchanged
-    with ONE SUM all-reduce on a side stream, overlapped with the next segment --
-    inside the timed region. Beside it (after the timed region, same segments):
+    N>1 (``--pooling sharded``, the default): the segment launch stages the rows the
+    pooled buffer's learns will read, each rank draws every learn (counter-based),
+    packs its own sampled rows and ONE all-gather per segment (a side stream,
+    overlapped with the next segment) gives every rank the segment's learn() batches
+    -- inside the timed region. Beside it (after the timed region, same segments):
     the all-gather of every transition (configs[3]'s literal exchange) and no
-    exchange at all. N=1: the replay path without a collective is measured the same
-    way (``replay_path``), so the per-GPU cost of the exchange is on the N=1 line."""
+    exchange at all. N=1: the replay path without a collective (``replay_path``),
+    with the collective's kernel stood in for (``replay_path_collective_standin``)
+    and this GPU as rank 0 of --standin-world ranks (``replay_path_rank_of_world``),
+    so the per-GPU cost of the exchange is on the N=1 line."""
     pool_every = int(getattr(args, "pool_every", SEG))
     pooling = pooling_mode(args, world, wl)
     pool = exchange = None
@@ -982,7 +985,8 @@ def run_bench(args, rank: int, world: int, dev, wl: Workload):
                "launch that also marks the rows" if args.sampler == "philox" else
                "the pooled buffer's MT19937 stream, exact") +
             f") from the pooled ReplayBuffer({args.replay_mem}), the segment launch writing the 64-B rows they "
-            "read, the batches " + ("packed per rank and unpacked (the all-gather's two kernels)"
+            "read, the batches " + ("packed per rank and unpacked (the all-gather's two roles; with the "
+                                    "draws, one side launch per segment)"
                                     if args.exchange == "allgather" else "gathered") +
             " on the stepping stream after each segment's refill (sacenv.dist.SegmentExchange: kernels beside a "
             "launch or a refill slowed them more than they overlapped), after the timed region, wall time"))
