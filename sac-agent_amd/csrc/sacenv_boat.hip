@@ -1836,6 +1836,19 @@ __host__ __device__ inline bool t_from_index(double dt) {
     if (!kRoll) st_pair(A.b, (u), (uint32_t)A.np, eo, (v0), (v1));  \
   } while (0)
 
+// (store_row with non-temporal stores: rows written once and not read back by the launch)
+template <int ROW>
+__device__ __forceinline__ void store_row_nt(float* row, const float* w) {
+  typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+  typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
+#pragma unroll
+  for (int i = 0; i + 4 <= ROW; i += 4)
+    __builtin_nontemporal_store(f4u{w[i], w[i + 1], w[i + 2], w[i + 3]}, reinterpret_cast<f4u*>(row + i));
+  constexpr int t = ROW & ~3;
+  static_assert(ROW - t == 3, "an obs row: 11 floats");
+  __builtin_nontemporal_store(f3u{w[t], w[t + 1], w[t + 2]}, reinterpret_cast<f3u*>(row + t));
+}
+
 // one env's row of ROW floats (4-B aligned) from registers: dwordx4 stores,
 // then the 1..3-float tail as one store
 template <int ROW>
@@ -2404,16 +2417,25 @@ __device__ __forceinline__ void owner_wave(const SacenvBoatParams& pin, const Ar
       kcur = knot_coord(p, 0);
     }
   }
-  st_out<kWT>(*reinterpret_cast<float*>(R + 44 * A.np + eo4), (float)reward);
-  st_out<kWT>(*reinterpret_cast<uint8_t*>(R + 48 * A.np + e), (uint8_t)(ended ? 1 : 0));
-  st_out<kWT>(*reinterpret_cast<uint8_t*>(R + 49 * A.np + e), term);
+  if (kRows == 3) {  // (fresh rows: streaming stores, as the obs row below)
+    __builtin_nontemporal_store((float)reward, reinterpret_cast<float*>(R + 44 * A.np + eo4));
+    __builtin_nontemporal_store((uint8_t)(ended ? 1 : 0), reinterpret_cast<uint8_t*>(R + 48 * A.np + e));
+    __builtin_nontemporal_store(term, reinterpret_cast<uint8_t*>(R + 49 * A.np + e));
+  } else {
+    st_out<kWT>(*reinterpret_cast<float*>(R + 44 * A.np + eo4), (float)reward);
+    st_out<kWT>(*reinterpret_cast<uint8_t*>(R + 48 * A.np + e), (uint8_t)(ended ? 1 : 0));
+    st_out<kWT>(*reinterpret_cast<uint8_t*>(R + 49 * A.np + e), term);
+  }
   // a restarting env's row is its new episode's first obs
   if (!kWT) {
     // write-back record (open-loop multi-step launch): each lane stores its own
     // 44-B row as 16 + 16 + 12 B (4-B aligned vector stores): 0.08 us/step
     // cheaper than the LDS-staged block below, whose LDS round trip and waits
     // sit on the step's path
-    store_row<SACENV_OBS_DIM>(reinterpret_cast<float*>(R) + (int64_t)e * SACENV_OBS_DIM, row);
+    if (kRows == 3)  // every step's record to fresh rows (sacenv_boat_rollout): streaming stores
+      store_row_nt<SACENV_OBS_DIM>(reinterpret_cast<float*>(R) + (int64_t)e * SACENV_OBS_DIM, row);
+    else
+      store_row<SACENV_OBS_DIM>(reinterpret_cast<float*>(R) + (int64_t)e * SACENV_OBS_DIM, row);
   } else {
     // obs rows through LDS, stored as write-through float4 (64 rows x 44 B = 176 float4)
 #pragma unroll
@@ -2912,6 +2934,9 @@ static int launch_multi(const SacenvBoatParams& p, void* arena, const float* act
                        make_arena(p, arena), make_tail(p, arena), actions, n_steps, ra);                   \
   else if (ra.trans != nullptr)                                                                            \
     hipLaunchKernelGGL((KER<NC, TI, 1>), dim3(nb_boat), dim3(kWave), 0, (hipStream_t)stream, p,            \
+                       make_arena(p, arena), make_tail(p, arena), actions, n_steps, ra);                   \
+  else if (ra.rec_stride != 0)                                                                             \
+    hipLaunchKernelGGL((KER<NC, TI, 3>), dim3(nb_boat), dim3(kWave), 0, (hipStream_t)stream, p,            \
                        make_arena(p, arena), make_tail(p, arena), actions, n_steps, ra);                   \
   else                                                                                                     \
     hipLaunchKernelGGL((KER<NC, TI, 0>), dim3(nb_boat), dim3(kWave), 0, (hipStream_t)stream, p,            \
